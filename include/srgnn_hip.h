@@ -1,0 +1,128 @@
+/*
+ * srgnn_hip.h -- C-ABI of libsrgnn_hip.so, the MI355X (gfx950) implementation of the spectral
+ * feature-propagation hot path of yyysyyy/Scalable-Roubust-GNN.
+ *
+ * Paths below are relative to "/root/reference/Scalable Spectral Robust GNN/" (SSRG/).
+ *
+ * Two groups of entry points:
+ *
+ *  (A) Drop-in replacements with the reference's exact signatures (host pointers, synchronous).
+ *      The reference binds them through numpy.ctypeslib in operators/utils.py:17-47 and :49-79;
+ *      pointing that load_library call at this library moves the product onto the GPU unchanged.
+ *
+ *  (B) Device entry points (device pointers, asynchronous on the caller's HIP stream) used by the
+ *      device-resident K-hop driver and by the row-partitioned multi-GPU path.
+ *
+ * Conventions for (B):
+ *   - Status: 0 on success, a negative SRG_ERR_* code on failure; srg_last_error() (thread-local)
+ *     then holds a message.  Nothing is launched when an argument check fails.
+ *   - Ownership: the caller owns every buffer.  The library allocates nothing on these paths.
+ *   - CSR: int64 row pointers (nnz may exceed 2^31), int32 column ids, row-major dense panels with
+ *     explicit leading dimensions (64-bit element offsets: N*d may exceed 2^31).
+ *   - Column ids are trusted on (B): validate a matrix once with srg_csr_validate() before use.
+ *   - `stream` is a hipStream_t passed as void* (NULL = the null stream).
+ */
+#ifndef SRGNN_HIP_H_
+#define SRGNN_HIP_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ---------------------------------------------------------------------------- */
+#define SRG_OK 0
+#define SRG_ERR_INVALID (-1)   /* bad argument (shape, null pointer, alignment, out-of-range id) */
+#define SRG_ERR_HIP (-2)       /* a HIP runtime call failed */
+#define SRG_ERR_ALLOC (-3)     /* device allocation failed (host-compat entries only) */
+
+/* ---- SpMM flags ------------------------------------------------------------------------------ */
+/* Default (0): every output element Y[i,c] is ONE sequential fp32 fma chain over row i's nonzeros
+ * in stored CSR order, starting from +0.0f -- bit-identical to FloatCSRMulDenseOMP
+ * (SSRG/operators/csrc/matmul.c:23-40) given a zeroed answer (SSRG/operators/utils.py:38). */
+#define SRG_SPMM_ACCUMULATE 0x1u   /* chains start from Y's current content (matmul.c contract) */
+#define SRG_SPMM_NT_STORE 0x2u     /* non-temporal stores of Y */
+
+/* =============================================================================================
+ * (A) drop-in entry points
+ * ============================================================================================= */
+
+/* Replaces FloatCSRMulDenseOMP, declared at SSRG/operators/csrc/matmul.h:5, defined at
+ * SSRG/operators/csrc/matmul.c:23-40, bound at SSRG/operators/utils.py:34-45.
+ * answer[mat_row*mat_col] += A * mat, A = CSR(data, indices, indptr) with mat_row rows; the
+ * reference's caller passes a zeroed answer.  Host pointers; the product runs on the current HIP
+ * device; returns after the result is back in `answer`.  The reference returns nothing and checks
+ * nothing; here a failed check or HIP error leaves `answer` untouched and is reported through
+ * srg_last_error_code()/srg_last_error(). */
+void FloatCSRMulDenseOMP(float answer[], float data[], int indices[], int indptr[], float mat[],
+                         int mat_row, int mat_col);
+
+/* Replaces FloatCSRMulDense, SSRG/operators/csrc/cudamatmul.c:28-146 (declared void at
+ * cudamatmul.h:4, defined int), bound at SSRG/operators/utils.py:65-77 (cuSPARSE CSR_ALG2 SpMM,
+ * alpha = 1, beta = 0).  Overwrites answer with A * mat.  Returns 0 (EXIT_SUCCESS) or 1. */
+int FloatCSRMulDense(float answer[], int data_nnz, float data[], int indices[], int indptr[],
+                     float mat[], int mat_row, int mat_col);
+
+/* =============================================================================================
+ * (B) device entry points
+ * ============================================================================================= */
+
+/* One hop: Y[r,:] = A[r,:] * X for the local rows r in [0, n_rows).
+ *   indptr[n_rows+1] int64, indices[nnz] int32 (ids into X's rows), values[nnz] fp32;
+ *   row_order: optional (NULL) int32 permutation of [0, n_rows) giving the order in which rows are
+ *              scheduled (srgnn plans pass rows by decreasing length so hubs start first);
+ *   n_heavy:   the first n_heavy rows of row_order are worked on in 32-column slices, one wave per
+ *              slice (long power-law rows); 0 without a row_order.
+ *   Neither scheduling argument changes any result: every output element is one fma chain.
+ *   X: ldx >= d; Y: ldy >= d.  Device pointers.  Replaces one call of csr_sparse_dense_matmul
+ *   (SSRG/operators/utils.py:17-47) inside GraphOp.propagate (SSRG/operators/base_operator.py:33-35). */
+int srg_spmm_csr_f32(const int64_t* indptr, const int32_t* indices, const float* values,
+                     int64_t n_rows, const int32_t* row_order, int64_t n_heavy, const float* X,
+                     int64_t ldx, float* Y, int64_t ldy, int32_t d, uint32_t flags, void* stream);
+
+/* K hops: panels[k] = A * panels[k-1] for k = 1..K, panels[0] = X (read only).  `panels` is a
+ * HOST array of K+1 device pointers, all with leading dimension ld.  Replaces the hop loop of
+ * GraphOp.propagate, SSRG/operators/base_operator.py:32-35 (with the per-hop host round trips of
+ * utils.py:38-47 removed).  A square (n_rows == rows of X). */
+int srg_propagate_khop_f32(const int64_t* indptr, const int32_t* indices, const float* values,
+                           int64_t n_rows, const int32_t* row_order, int64_t n_heavy,
+                           float* const* panels,
+                           int64_t ld, int32_t d, int32_t K, uint32_t flags, void* stream);
+
+/* Chebyshev heat-kernel filter bank (wavelet basis), SSRG/models/base_scalable/base_model.py:
+ * 184-191, 236-265 via pygsp cheby_op.  One fused launch per Chebyshev order:
+ *   mode SRG_CHEBY_INIT (order 1):  Tn = (A*Tc - a2*Tc) / a1;   R_s  = (c0_s/2)*Tc + c1_s*Tn
+ *   mode SRG_CHEBY_STEP (order k>=2): Tn = A*Tc - To;           R_s += ck_s*Tn
+ * with A = L (combinatorial Laplacian) for INIT and A = F = (2/a1)(L - a2 I) for STEP (the caller
+ * builds F's values).  R holds n_scales stacked panels: R + s*r_stride.  coef_prev (c0 per scale,
+ * INIT only) and coef (c1 or ck per scale) are HOST arrays of n_scales <= 8 values.  fp64 follows
+ * scipy's operation order (separate multiply and add, no fma); fp32 uses fma chains. */
+#define SRG_CHEBY_INIT 0
+#define SRG_CHEBY_STEP 1
+int srg_cheby_step_f64(const int64_t* indptr, const int32_t* indices, const double* values,
+                       int64_t n_rows, const int32_t* row_order, const double* Tc,
+                       const double* To, double* Tn, int64_t ld, int32_t d, int mode, double a1,
+                       double a2, const double* coef_prev, const double* coef, int32_t n_scales,
+                       double* R, int64_t r_stride, void* stream);
+int srg_cheby_step_f32(const int64_t* indptr, const int32_t* indices, const float* values,
+                       int64_t n_rows, const int32_t* row_order, const float* Tc, const float* To,
+                       float* Tn, int64_t ld, int32_t d, int mode, float a1, float a2,
+                       const float* coef_prev, const float* coef, int32_t n_scales, float* R,
+                       int64_t r_stride, void* stream);
+
+/* Checks a device CSR: indptr[0] == 0, indptr non-decreasing, indptr[n_rows] == nnz, and every
+ * column id in [0, n_cols).  Synchronous on `stream`.  Returns SRG_OK or SRG_ERR_INVALID. */
+int srg_csr_validate(const int64_t* indptr, const int32_t* indices, int64_t n_rows,
+                     int64_t nnz, int64_t n_cols, void* stream);
+
+/* ---- diagnostics ----------------------------------------------------------------------------- */
+const char* srg_last_error(void);   /* thread-local message of the last failure ("" if none) */
+int srg_last_error_code(void);      /* thread-local status of the last call (SRG_OK if fine)  */
+void srg_clear_error(void);
+const char* srg_version(void);      /* build identification, incl. the offload arch          */
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SRGNN_HIP_H_ */

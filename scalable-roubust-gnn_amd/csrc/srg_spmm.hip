@@ -1,0 +1,722 @@
+// srg_spmm.hip -- CSR x dense-panel propagation kernels for MI355X (gfx950, CDNA4).
+//
+// The hot path of the reference is FloatCSRMulDenseOMP (SSRG/operators/csrc/matmul.c:23-40): per
+// output row, for every stored nonzero in CSR order, answer[i,:] = fma(a_ij, X[j,:], answer[i,:]).
+// It is HBM-bound (~0.48 flop/B at d = 128): the work is gathering 4*d-byte rows of X, one per
+// nonzero.  The design here:
+//
+//  * One wavefront (64 lanes) owns one output row and a 64*VEC-column tile of it; each lane owns
+//    VEC consecutive columns and keeps their running sums in registers.  Every output element is
+//    therefore one sequential fp32 fma chain in CSR order -- bit-identical to the reference.
+//  * The row's (column id, value) stream is wave-uniform, so it is read with scalar loads into
+//    SGPRs (s_load_dwordx*), and each X row address is a scalar base + the lane's column offset:
+//    one vector instruction (global_load_dwordx{1,2,4}) per nonzero gathers the whole 4*d-byte row.
+//  * U nonzeros are processed per step: U independent gathers are issued back to back (U rows in
+//    flight per wave, ~U*512 B at d = 128), then consumed in order by the fma chain.  The chain is
+//    4 cycles per link; the gathers are what the wave waits on.
+//  * Rows are scheduled through an optional permutation (host plan: decreasing length), so the
+//    long power-law hub rows start first and overlap the bulk instead of forming the tail.
+//  * No atomics, no inter-workgroup communication, no LDS: each row is owned by exactly one wave.
+//
+// The Chebyshev (wavelet) kernels reuse the same row-wave gather and add a fused epilogue that
+// forms the next Chebyshev term and accumulates every scale's filter output in the same pass.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "srgnn_hip.h"
+
+#ifndef SRG_GIT_REV
+#define SRG_GIT_REV "dev"
+#endif
+
+namespace {
+
+// ------------------------------------------------------------------------------------------------
+// error handling
+// ------------------------------------------------------------------------------------------------
+thread_local char g_err_msg[512] = "";
+thread_local int g_err_code = SRG_OK;
+
+int fail(int code, const char* fmt, ...)
+{
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err_msg, sizeof(g_err_msg), fmt, ap);
+    va_end(ap);
+    g_err_code = code;
+    return code;
+}
+
+int ok()
+{
+    g_err_code = SRG_OK;
+    g_err_msg[0] = '\0';
+    return SRG_OK;
+}
+
+#define SRG_HIP_CHECK(expr)                                                                     \
+    do {                                                                                        \
+        hipError_t e_ = (expr);                                                                 \
+        if (e_ != hipSuccess)                                                                   \
+            return fail(SRG_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(e_));            \
+    } while (0)
+
+// ------------------------------------------------------------------------------------------------
+// vector helpers
+// ------------------------------------------------------------------------------------------------
+template <typename T, int VEC> struct Vec;
+template <> struct Vec<float, 1> { typedef float type; };
+template <> struct Vec<float, 2> { typedef float type __attribute__((ext_vector_type(2))); };
+template <> struct Vec<float, 4> { typedef float type __attribute__((ext_vector_type(4))); };
+template <> struct Vec<double, 1> { typedef double type; };
+template <> struct Vec<double, 2> { typedef double type __attribute__((ext_vector_type(2))); };
+
+template <typename V> __device__ __forceinline__ float& el(V& v, int i) { return v[i]; }
+
+template <typename T, int VEC>
+__device__ __forceinline__ typename Vec<T, VEC>::type vload(const T* p)
+{
+    return *reinterpret_cast<const typename Vec<T, VEC>::type*>(p);
+}
+template <typename T, int VEC>
+__device__ __forceinline__ void vstore(T* p, typename Vec<T, VEC>::type v, bool nt)
+{
+    typedef typename Vec<T, VEC>::type V;
+    if (nt)
+        __builtin_nontemporal_store(v, reinterpret_cast<V*>(p));
+    else
+        *reinterpret_cast<V*>(p) = v;
+}
+
+// One link of the reference chain: acc = fma(a, x, acc) per component (fp32), or acc + a*x without
+// contraction (fp64: scipy's csr_matvecs order, see srg_oracle.c).
+__device__ __forceinline__ float link(float a, float x, float acc) { return __builtin_fmaf(a, x, acc); }
+__device__ __forceinline__ double link(double a, double x, double acc)
+{
+    return __dadd_rn(acc, __dmul_rn(a, x));
+}
+
+template <typename T, int VEC>
+__device__ __forceinline__ void chain(typename Vec<T, VEC>::type& acc, T a,
+                                      const typename Vec<T, VEC>::type& x)
+{
+    if constexpr (VEC == 1) {
+        acc = link(a, x, acc);
+    } else {
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) acc[i] = link(a, x[i], acc[i]);
+    }
+}
+
+template <typename T, int VEC> __device__ __forceinline__ typename Vec<T, VEC>::type vzero()
+{
+    typename Vec<T, VEC>::type z;
+    if constexpr (VEC == 1) {
+        z = T(0);
+    } else {
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) z[i] = T(0);
+    }
+    return z;
+}
+
+constexpr int kWavesPerBlock = 4;   // 256-thread workgroups
+constexpr int kBlock = 64 * kWavesPerBlock;
+
+// ------------------------------------------------------------------------------------------------
+// the row-wave gather: acc (+)= A[row, :] * X[:, col .. col+VEC)
+//
+// The row's (column id, value) stream is read 64 entries at a time with one coalesced vector load
+// (lane l holds entry jb + l), prefetched one block ahead, and broadcast to the whole wave with
+// v_readlane (the lane index is wave-uniform).  Each entry's X row address is then a scalar base
+// plus the lane's column offset.  U gathers are issued back to back, then consumed in CSR order.
+// Entries past the end of the row repeat its last entry and are skipped by a wave-uniform predicate
+// (never folded in as 0*x: that would flip -0.0 sums and turn inf/nan inputs into nan).
+// FULL: every lane of the wave owns columns (d is a multiple of 64*VEC), so no lane predicates.
+// ------------------------------------------------------------------------------------------------
+template <typename T, int VEC, int U, bool FULL, typename IP>
+__device__ __forceinline__ void row_gather(typename Vec<T, VEC>::type& acc,
+                                           const IP* __restrict__ indptr,
+                                           const int32_t* __restrict__ indices,
+                                           const T* __restrict__ vals, int row,
+                                           const T* __restrict__ X, int64_t ldx, int col, bool act)
+{
+    typedef typename Vec<T, VEC>::type V;
+    const int lane = threadIdx.x & 63;
+    const int64_t beg = indptr[row];
+    const int64_t end = indptr[row + 1];
+    if (beg >= end) return;
+    // entries past the row end are clamped to its last entry (always a valid id; skipped below)
+    int64_t j0 = beg + lane;
+    j0 = j0 < end ? j0 : end - 1;
+    int c_nxt = indices[j0];
+    T a_nxt = vals[j0];
+    for (int64_t jb = beg; jb < end; jb += 64) {
+        const int c_blk = c_nxt;
+        const T a_blk = a_nxt;
+        int64_t jn = jb + 64 + lane;   // prefetch the next block of the stream
+        jn = jn < end ? jn : end - 1;
+        c_nxt = indices[jn];
+        a_nxt = vals[jn];
+        const int nblk = (end - jb) < 64 ? (int)(end - jb) : 64;   // wave-uniform
+        for (int s0 = 0; s0 < nblk; s0 += U) {
+            V x[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int c = __builtin_amdgcn_readlane(c_blk, s0 + u);
+                const T* p = X + (int64_t)c * ldx + col;
+                if (FULL || act)
+                    x[u] = vload<T, VEC>(p);
+                else
+                    x[u] = vzero<T, VEC>();
+            }
+            const int n = (nblk - s0) < U ? (nblk - s0) : U;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                T a;
+                if constexpr (sizeof(T) == 8) {
+                    const long long bits = __builtin_amdgcn_readlane(
+                        (long long)__builtin_bit_cast(long long, a_blk), s0 + u);
+                    a = __builtin_bit_cast(T, bits);
+                } else {
+                    a = __builtin_bit_cast(T, __builtin_amdgcn_readlane(__builtin_bit_cast(int, a_blk), s0 + u));
+                }
+                if (u < n) chain<T, VEC>(acc, a, x[u]);
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ int wave_slot()
+{
+    // wave-uniform by construction; readfirstlane makes that provable to the compiler so that the
+    // row's index stream goes through the scalar path.
+    return __builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)));
+}
+
+// ------------------------------------------------------------------------------------------------
+// SpMM: Y = A * X  (or Y += A * X)
+//
+// One launch, two wave roles (wave-uniform, decided by blockIdx):
+//  * blocks [0, nb_heavy): "slice" waves.  The first n_heavy rows of `order` are long rows; each is
+//    cut into 32-column slices (128 B of every X row = one cache line) and every (row, slice) pair
+//    is one wave.  Lane l gathers the 16-byte chunk (l & 7) of nonzero (l >> 3): one
+//    global_load_dwordx4 instruction brings 8 nonzeros' slices (1 KiB); UH such instructions are in
+//    flight per wave.  The 8x32 tile is transposed through a wave-private LDS slot so that lane c
+//    (c < 32) runs the sequential fma chain of column c over the nonzeros in CSR order.  A row of
+//    degree D is worked on by d/32 waves at once with UH*1 KiB in flight each, which keeps
+//    power-law hubs (D > 10^5 on the products-shaped graph) off the critical path.
+//  * blocks [nb_heavy, ...): "row" waves, one per remaining row (row_gather above).
+// Both roles produce bit-identical results (one fma chain per output element, CSR order).
+// ------------------------------------------------------------------------------------------------
+constexpr int kSliceCols = 32;
+
+template <int UH, bool SFULL, typename IP>
+__device__ __forceinline__ void slice_wave(const IP* __restrict__ indptr,
+                                           const int32_t* __restrict__ indices,
+                                           const float* __restrict__ vals, int row, int slice,
+                                           const float* __restrict__ X, int64_t ldx,
+                                           float* __restrict__ Y, int64_t ldy, int d, int accumulate,
+                                           int nt, float* __restrict__ lds)
+{
+    typedef typename Vec<float, 4>::type V4;
+    const int lane = threadIdx.x & 63;
+    const int g = lane >> 3;                 // nonzero within a group of 8
+    const int qcol = slice * kSliceCols + (lane & 7) * 4;   // gather columns of this lane
+    const bool gact = SFULL || qcol < d;
+    const int ccol = slice * kSliceCols + lane;             // chain column of this lane
+    const bool cact = lane < kSliceCols && (SFULL || ccol < d);
+    float* __restrict__ yrow = Y + (int64_t)row * ldy;
+    float acc = 0.0f;
+    if (accumulate && cact) acc = yrow[ccol];
+    const int64_t beg = indptr[row];
+    const int64_t end = indptr[row + 1];
+    for (int64_t j = beg; j < end; j += 8 * UH) {
+        V4 x[UH];
+        float av[UH];
+        int cv[UH];
+#pragma unroll
+        for (int b = 0; b < UH; ++b) {   // all index/value loads first (clamped: no branches) ...
+            int64_t jj = j + b * 8 + g;
+            jj = jj < end ? jj : end - 1;
+            cv[b] = indices[jj];
+            av[b] = vals[jj];
+        }
+        __builtin_amdgcn_sched_barrier(0);   // keep every index load ahead of the first gather
+#pragma unroll
+        for (int b = 0; b < UH; ++b)     // ... then UH dependent gathers in flight
+            x[b] = gact ? vload<float, 4>(X + (int64_t)cv[b] * ldx + qcol) : vzero<float, 4>();
+#pragma unroll
+        for (int b = 0; b < UH; ++b) {
+            const int64_t jb = j + b * 8;
+            if (jb >= end) break;                               // wave-uniform
+            const int nb = (end - jb) < 8 ? (int)(end - jb) : 8;
+            float* slot = lds + (b & 1) * 256;
+            *reinterpret_cast<V4*>(slot + lane * 4) = x[b];     // tile [g][32 cols]
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            float t[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) t[q] = slot[q * kSliceCols + (lane & 31)];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const float a = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, av[b]), q * 8));
+                if (q < nb && cact) acc = __builtin_fmaf(a, t[q], acc);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+    }
+    if (cact) {
+        if (nt)
+            __builtin_nontemporal_store(acc, yrow + ccol);
+        else
+            yrow[ccol] = acc;
+    }
+}
+
+template <int VEC, int U, int UH, bool FULL, bool SFULL, typename IP>
+__global__ void __launch_bounds__(kBlock)
+k_spmm(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
+       const float* __restrict__ vals, const int32_t* __restrict__ order, int n_rows, int n_heavy,
+       int n_slices, int nb_heavy, const float* __restrict__ X, int64_t ldx, float* __restrict__ Y,
+       int64_t ldy, int d, int accumulate, int nt)
+{
+    typedef typename Vec<float, VEC>::type V;
+    __shared__ __attribute__((aligned(16))) float lds[kWavesPerBlock * 2 * 256];
+    const int lane = threadIdx.x & 63;
+    const int wib = threadIdx.x >> 6;
+    if ((int)blockIdx.x < nb_heavy) {
+        const int item = __builtin_amdgcn_readfirstlane((int)blockIdx.x * kWavesPerBlock + wib);
+        if (item >= n_heavy * n_slices) return;
+        const int row = order[item / n_slices];
+        slice_wave<UH, SFULL, IP>(indptr, indices, vals, row, item % n_slices, X, ldx, Y, ldy, d,
+                           accumulate, nt, lds + wib * 2 * 256);
+        return;
+    }
+    const int w = __builtin_amdgcn_readfirstlane(((int)blockIdx.x - nb_heavy) * kWavesPerBlock + wib) + n_heavy;
+    if (w >= n_rows) return;
+    const int row = order ? order[w] : w;
+    float* __restrict__ yrow = Y + (int64_t)row * ldy;
+    for (int c0 = 0; c0 < d; c0 += 64 * VEC) {
+        const int col = c0 + lane * VEC;
+        const bool act = col < d;
+        V acc = vzero<float, VEC>();
+        if (accumulate && (FULL || act)) acc = vload<float, VEC>(yrow + col);
+        row_gather<float, VEC, U, FULL, IP>(acc, indptr, indices, vals, row, X, ldx, col, act);
+        if (FULL || act) vstore<float, VEC>(yrow + col, acc, nt != 0);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Chebyshev step with fused epilogue (wavelet basis)
+// ------------------------------------------------------------------------------------------------
+template <typename T> struct ChebyCoef {
+    T prev[8];   // c0_s / 2 (INIT only)
+    T cur[8];    // c1_s (INIT) or ck_s (STEP)
+};
+
+template <typename T, int VEC, int U>
+__global__ void __launch_bounds__(kBlock)
+k_cheby(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
+        const T* __restrict__ vals, const int32_t* __restrict__ order, int n_rows,
+        const T* __restrict__ Tc, const T* __restrict__ To, T* __restrict__ Tn, int64_t ld, int d,
+        int mode, T a1, T a2, ChebyCoef<T> cf, int n_scales, T* __restrict__ R, int64_t r_stride)
+{
+    typedef typename Vec<T, VEC>::type V;
+    const int w = wave_slot();
+    if (w >= n_rows) return;
+    const int row = order ? order[w] : w;
+    const int lane = threadIdx.x & 63;
+    const int64_t roff = (int64_t)row * ld;
+    for (int c0 = 0; c0 < d; c0 += 64 * VEC) {
+        const int col = c0 + lane * VEC;
+        const bool act = col < d;
+        V acc = vzero<T, VEC>();
+        row_gather<T, VEC, U, false, int64_t>(acc, indptr, indices, vals, row, Tc, ld, col, act);
+        if (!act) continue;
+        V tn;
+        if (mode == SRG_CHEBY_INIT) {
+            const V tc = vload<T, VEC>(Tc + roff + col);
+            if constexpr (VEC == 1) {
+                tn = (acc - a2 * tc) / a1;
+            } else {
+#pragma unroll
+                for (int i = 0; i < VEC; ++i) tn[i] = (acc[i] - a2 * tc[i]) / a1;
+            }
+            for (int s = 0; s < n_scales; ++s) {
+                V r;
+                if constexpr (VEC == 1) {
+                    r = cf.prev[s] * tc + cf.cur[s] * tn;
+                } else {
+#pragma unroll
+                    for (int i = 0; i < VEC; ++i) r[i] = cf.prev[s] * tc[i] + cf.cur[s] * tn[i];
+                }
+                vstore<T, VEC>(R + s * r_stride + roff + col, r, false);
+            }
+        } else {
+            const V to = vload<T, VEC>(To + roff + col);
+            tn = acc - to;
+            for (int s = 0; s < n_scales; ++s) {
+                T* rp = R + s * r_stride + roff + col;
+                V r = vload<T, VEC>(rp);
+                r = r + cf.cur[s] * tn;
+                vstore<T, VEC>(rp, r, false);
+            }
+        }
+        vstore<T, VEC>(Tn + roff + col, tn, false);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// validation kernel
+// ------------------------------------------------------------------------------------------------
+__global__ void k_validate(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
+                           int64_t n_rows, int64_t nnz, int64_t n_cols, unsigned int* __restrict__ bad)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    unsigned int b = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nnz; i += stride) {
+        const int32_t c = indices[i];
+        if (c < 0 || (int64_t)c >= n_cols) b |= 1u;
+    }
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_rows; i += stride) {
+        if (indptr[i + 1] < indptr[i]) b |= 2u;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (indptr[0] != 0) b |= 4u;
+        if (indptr[n_rows] != nnz) b |= 8u;
+    }
+    if (b) atomicOr(bad, b);
+}
+
+// ------------------------------------------------------------------------------------------------
+// launch helpers
+// ------------------------------------------------------------------------------------------------
+constexpr int kUnroll = 8;
+
+bool aligned(const void* p, size_t a) { return (reinterpret_cast<uintptr_t>(p) % a) == 0; }
+
+int pick_vec(int d, int64_t ldx, int64_t ldy, const void* X, const void* Y, size_t elem)
+{
+    // widest per-lane access whose tiles line up with every row of X and Y
+    if (elem == 4 && d >= 256 && d % 4 == 0 && ldx % 4 == 0 && ldy % 4 == 0 && aligned(X, 16) &&
+        aligned(Y, 16))
+        return 4;
+    if (d >= 128 && d % 2 == 0 && ldx % 2 == 0 && ldy % 2 == 0 && aligned(X, 2 * elem) &&
+        aligned(Y, 2 * elem))
+        return 2;
+    return 1;
+}
+
+constexpr int kUnrollHeavy = 8;
+
+template <typename IP>
+int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int64_t n_rows,
+                const int32_t* order, int64_t n_heavy, const float* X, int64_t ldx, float* Y,
+                int64_t ldy, int d, uint32_t flags, hipStream_t s)
+{
+    if (n_rows <= 0 || d <= 0) return SRG_OK;
+    if (n_heavy < 0 || n_heavy > n_rows || (n_heavy > 0 && !order))
+        return fail(SRG_ERR_INVALID, "n_heavy=%lld needs a row_order and <= n_rows", (long long)n_heavy);
+    // slice waves gather 16-byte chunks: they need d % 4 == 0 and 16-byte aligned rows
+    const bool slice_ok = d % 4 == 0 && ldx % 4 == 0 && aligned(X, 16);
+    if (!slice_ok) n_heavy = 0;
+    const int n_slices = (d + kSliceCols - 1) / kSliceCols;
+    if (n_heavy * (int64_t)n_slices > INT32_MAX - 64)
+        return fail(SRG_ERR_INVALID, "too many heavy slices");
+    const int nb_heavy = (int)((n_heavy * n_slices + kWavesPerBlock - 1) / kWavesPerBlock);
+    const int64_t n_light = n_rows - n_heavy;
+    const int64_t blocks = nb_heavy + (n_light + kWavesPerBlock - 1) / kWavesPerBlock;
+    if (blocks > INT32_MAX) return fail(SRG_ERR_INVALID, "grid too large");
+    const int vec = pick_vec(d, ldx, ldy, X, Y, sizeof(float));
+    const dim3 grid((unsigned)blocks);
+    const int acc = (flags & SRG_SPMM_ACCUMULATE) ? 1 : 0;
+    const int nt = (flags & SRG_SPMM_NT_STORE) ? 1 : 0;
+    const int nr = (int)n_rows, nh = (int)n_heavy;
+#define SRG_LAUNCH_SPMM(V, F, SF)                                                               \
+    hipLaunchKernelGGL((k_spmm<V, kUnroll, kUnrollHeavy, F, SF, IP>), grid, dim3(kBlock), 0, s,     \
+                       indptr, indices, vals, order, nr, nh, n_slices, nb_heavy, X, ldx, Y, ldy, d, \
+                       acc, nt)
+    const bool full = d % (64 * vec) == 0;        // implies d % 32 == 0
+    const bool sfull = d % kSliceCols == 0;
+    if (vec == 4) {
+        if (full) SRG_LAUNCH_SPMM(4, true, true);
+        else if (sfull) SRG_LAUNCH_SPMM(4, false, true);
+        else SRG_LAUNCH_SPMM(4, false, false);
+    } else if (vec == 2) {
+        if (full) SRG_LAUNCH_SPMM(2, true, true);
+        else if (sfull) SRG_LAUNCH_SPMM(2, false, true);
+        else SRG_LAUNCH_SPMM(2, false, false);
+    } else {
+        if (full) SRG_LAUNCH_SPMM(1, true, true);
+        else if (sfull) SRG_LAUNCH_SPMM(1, false, true);
+        else SRG_LAUNCH_SPMM(1, false, false);
+    }
+#undef SRG_LAUNCH_SPMM
+    SRG_HIP_CHECK(hipGetLastError());
+    return SRG_OK;
+}
+
+int check_spmm_args(const void* indptr, const void* indices, const void* vals, int64_t n_rows,
+                    const void* X, int64_t ldx, const void* Y, int64_t ldy, int d)
+{
+    if (n_rows < 0 || n_rows > INT32_MAX - 64)
+        return fail(SRG_ERR_INVALID, "n_rows=%lld out of range [0, 2^31-64)", (long long)n_rows);
+    if (d < 0) return fail(SRG_ERR_INVALID, "d=%d < 0", d);
+    if (ldx < d || ldy < d)
+        return fail(SRG_ERR_INVALID, "leading dimensions (ldx=%lld, ldy=%lld) < d=%d",
+                    (long long)ldx, (long long)ldy, d);
+    if (n_rows > 0 && d > 0 && (!indptr || !Y))
+        return fail(SRG_ERR_INVALID, "null indptr or Y");
+    (void)indices; (void)vals; (void)X;
+    return SRG_OK;
+}
+
+template <typename T>
+int launch_cheby(const int64_t* indptr, const int32_t* indices, const T* vals, int64_t n_rows,
+                 const int32_t* order, const T* Tc, const T* To, T* Tn, int64_t ld, int d, int mode,
+                 T a1, T a2, const T* coef_prev, const T* coef, int n_scales, T* R, int64_t r_stride,
+                 hipStream_t s)
+{
+    if (mode != SRG_CHEBY_INIT && mode != SRG_CHEBY_STEP)
+        return fail(SRG_ERR_INVALID, "cheby mode %d", mode);
+    if (n_scales < 1 || n_scales > 8) return fail(SRG_ERR_INVALID, "n_scales=%d not in [1,8]", n_scales);
+    if (!coef || (mode == SRG_CHEBY_INIT && !coef_prev))
+        return fail(SRG_ERR_INVALID, "null coefficient array");
+    if (mode == SRG_CHEBY_STEP && !To) return fail(SRG_ERR_INVALID, "null To for a step");
+    int rc = check_spmm_args(indptr, indices, vals, n_rows, Tc, ld, Tn, ld, d);
+    if (rc) return rc;
+    if (r_stride < n_rows * ld && n_scales > 1)
+        return fail(SRG_ERR_INVALID, "r_stride too small for stacked scale panels");
+    ChebyCoef<T> cf;
+    for (int i = 0; i < 8; ++i) {
+        cf.prev[i] = (mode == SRG_CHEBY_INIT && i < n_scales) ? T(0.5) * coef_prev[i] : T(0);
+        cf.cur[i] = i < n_scales ? coef[i] : T(0);
+    }
+    if (n_rows == 0 || d == 0) return ok();
+    const dim3 grid((unsigned)((n_rows + kWavesPerBlock - 1) / kWavesPerBlock));
+    const int vec = pick_vec(d, ld, ld, Tc, Tn, sizeof(T)) >= 2 && aligned(R, 2 * sizeof(T)) &&
+                            (r_stride % 2 == 0) && (To == nullptr || aligned(To, 2 * sizeof(T)))
+                        ? 2
+                        : 1;
+    const int nr = (int)n_rows;
+    if (vec == 2)
+        hipLaunchKernelGGL((k_cheby<T, 2, kUnroll>), grid, dim3(kBlock), 0, s, indptr, indices,
+                           vals, order, nr, Tc, To, Tn, ld, d, mode, a1, a2, cf, n_scales, R,
+                           r_stride);
+    else
+        hipLaunchKernelGGL((k_cheby<T, 1, kUnroll>), grid, dim3(kBlock), 0, s, indptr, indices,
+                           vals, order, nr, Tc, To, Tn, ld, d, mode, a1, a2, cf, n_scales, R,
+                           r_stride);
+    SRG_HIP_CHECK(hipGetLastError());
+    return ok();
+}
+
+// ------------------------------------------------------------------------------------------------
+// host-compat staging: grow-only device buffers reused across calls (the reference calls the
+// product once per hop from Python, utils.py:45)
+// ------------------------------------------------------------------------------------------------
+struct Staging {
+    std::mutex mu;
+    void* buf[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    size_t cap[5] = {0, 0, 0, 0, 0};
+    int device[5] = {-1, -1, -1, -1, -1};
+    hipStream_t stream = nullptr;
+    int stream_device = -1;
+};
+Staging g_stage;
+
+int stage_reserve(int slot, size_t bytes, int dev)
+{
+    if (g_stage.cap[slot] >= bytes && g_stage.device[slot] == dev) return SRG_OK;
+    if (g_stage.buf[slot]) {
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        (void)hipSetDevice(g_stage.device[slot]);
+        (void)hipFree(g_stage.buf[slot]);
+        (void)hipSetDevice(cur);
+        g_stage.buf[slot] = nullptr;
+        g_stage.cap[slot] = 0;
+    }
+    size_t want = std::max<size_t>(bytes, 256);
+    if (hipMalloc(&g_stage.buf[slot], want) != hipSuccess) {
+        g_stage.buf[slot] = nullptr;
+        (void)hipGetLastError();
+        return fail(SRG_ERR_ALLOC, "hipMalloc(%zu) failed", want);
+    }
+    g_stage.cap[slot] = want;
+    g_stage.device[slot] = dev;
+    return SRG_OK;
+}
+
+// answer (+)= A * mat on the GPU with host buffers.  overwrite: cuSPARSE beta = 0 semantics.
+int host_compat_spmm(float* answer, const float* data, const int* indices, const int* indptr,
+                     const float* mat, int mat_row, int mat_col, bool overwrite, int64_t nnz_hint)
+{
+    if (mat_row < 0 || mat_col < 0)
+        return fail(SRG_ERR_INVALID, "mat_row=%d mat_col=%d", mat_row, mat_col);
+    if (mat_row == 0 || mat_col == 0) return ok();
+    if (!answer || !indptr || !mat) return fail(SRG_ERR_INVALID, "null host pointer");
+    const int64_t nnz = indptr[mat_row];
+    if (indptr[0] != 0 || nnz < 0) return fail(SRG_ERR_INVALID, "indptr[0]=%d indptr[n]=%lld", indptr[0], (long long)nnz);
+    if (nnz_hint >= 0 && nnz_hint != nnz)
+        return fail(SRG_ERR_INVALID, "data_nnz=%lld != indptr[mat_row]=%lld", (long long)nnz_hint, (long long)nnz);
+    for (int i = 0; i < mat_row; ++i)
+        if (indptr[i + 1] < indptr[i]) return fail(SRG_ERR_INVALID, "indptr decreases at row %d", i);
+    if (nnz > 0 && (!indices || !data)) return fail(SRG_ERR_INVALID, "null indices/data");
+    for (int64_t j = 0; j < nnz; ++j)
+        if (indices[j] < 0 || indices[j] >= mat_row)
+            return fail(SRG_ERR_INVALID, "column id %d at %lld outside [0, %d)", indices[j], (long long)j, mat_row);
+
+    std::lock_guard<std::mutex> lock(g_stage.mu);
+    int dev = 0;
+    SRG_HIP_CHECK(hipGetDevice(&dev));
+    if (!g_stage.stream || g_stage.stream_device != dev) {
+        SRG_HIP_CHECK(hipStreamCreateWithFlags(&g_stage.stream, hipStreamNonBlocking));
+        g_stage.stream_device = dev;
+    }
+    hipStream_t s = g_stage.stream;
+    const size_t panel = (size_t)mat_row * (size_t)mat_col * sizeof(float);
+    int rc;
+    if ((rc = stage_reserve(0, (size_t)(mat_row + 1) * sizeof(int), dev))) return rc;
+    if ((rc = stage_reserve(1, (size_t)nnz * sizeof(int), dev))) return rc;
+    if ((rc = stage_reserve(2, (size_t)nnz * sizeof(float), dev))) return rc;
+    if ((rc = stage_reserve(3, panel, dev))) return rc;
+    if ((rc = stage_reserve(4, panel, dev))) return rc;
+    int* d_ptr = static_cast<int*>(g_stage.buf[0]);
+    int* d_idx = static_cast<int*>(g_stage.buf[1]);
+    float* d_val = static_cast<float*>(g_stage.buf[2]);
+    float* d_x = static_cast<float*>(g_stage.buf[3]);
+    float* d_y = static_cast<float*>(g_stage.buf[4]);
+    SRG_HIP_CHECK(hipMemcpyAsync(d_ptr, indptr, (size_t)(mat_row + 1) * sizeof(int), hipMemcpyHostToDevice, s));
+    if (nnz > 0) {
+        SRG_HIP_CHECK(hipMemcpyAsync(d_idx, indices, (size_t)nnz * sizeof(int), hipMemcpyHostToDevice, s));
+        SRG_HIP_CHECK(hipMemcpyAsync(d_val, data, (size_t)nnz * sizeof(float), hipMemcpyHostToDevice, s));
+    }
+    SRG_HIP_CHECK(hipMemcpyAsync(d_x, mat, panel, hipMemcpyHostToDevice, s));
+    uint32_t flags = 0;
+    if (!overwrite) {
+        SRG_HIP_CHECK(hipMemcpyAsync(d_y, answer, panel, hipMemcpyHostToDevice, s));
+        flags |= SRG_SPMM_ACCUMULATE;
+    }
+    rc = launch_spmm<int>(d_ptr, d_idx, d_val, mat_row, nullptr, 0, d_x, mat_col, d_y, mat_col, mat_col, flags, s);
+    if (rc) return rc;
+    SRG_HIP_CHECK(hipMemcpyAsync(answer, d_y, panel, hipMemcpyDeviceToHost, s));
+    SRG_HIP_CHECK(hipStreamSynchronize(s));
+    return ok();
+}
+
+}  // namespace
+
+// ================================================================================================
+// C ABI
+// ================================================================================================
+extern "C" {
+
+void FloatCSRMulDenseOMP(float answer[], float data[], int indices[], int indptr[], float mat[],
+                         int mat_row, int mat_col)
+{
+    (void)host_compat_spmm(answer, data, indices, indptr, mat, mat_row, mat_col, false, -1);
+}
+
+int FloatCSRMulDense(float answer[], int data_nnz, float data[], int indices[], int indptr[],
+                     float mat[], int mat_row, int mat_col)
+{
+    return host_compat_spmm(answer, data, indices, indptr, mat, mat_row, mat_col, true, data_nnz) == SRG_OK ? 0 : 1;
+}
+
+int srg_spmm_csr_f32(const int64_t* indptr, const int32_t* indices, const float* values,
+                     int64_t n_rows, const int32_t* row_order, int64_t n_heavy, const float* X,
+                     int64_t ldx, float* Y, int64_t ldy, int32_t d, uint32_t flags, void* stream)
+{
+    int rc = check_spmm_args(indptr, indices, values, n_rows, X, ldx, Y, ldy, d);
+    if (rc) return rc;
+    rc = launch_spmm<int64_t>(indptr, indices, values, n_rows, row_order, n_heavy, X, ldx, Y, ldy, d, flags,
+                              static_cast<hipStream_t>(stream));
+    return rc ? rc : ok();
+}
+
+int srg_propagate_khop_f32(const int64_t* indptr, const int32_t* indices, const float* values,
+                           int64_t n_rows, const int32_t* row_order, int64_t n_heavy,
+                           float* const* panels,
+                           int64_t ld, int32_t d, int32_t K, uint32_t flags, void* stream)
+{
+    if (K < 0) return fail(SRG_ERR_INVALID, "K=%d < 0", K);
+    if (K > 0 && !panels) return fail(SRG_ERR_INVALID, "null panels");
+    for (int k = 0; k <= K; ++k)
+        if (!panels[k] && n_rows > 0 && d > 0) return fail(SRG_ERR_INVALID, "panels[%d] is null", k);
+    int rc = check_spmm_args(indptr, indices, values, n_rows, panels ? panels[0] : nullptr, ld,
+                             panels ? panels[0] : nullptr, ld, d);
+    if (rc) return rc;
+    const uint32_t f = flags & ~SRG_SPMM_ACCUMULATE;
+    for (int k = 1; k <= K; ++k) {
+        rc = launch_spmm<int64_t>(indptr, indices, values, n_rows, row_order, n_heavy, panels[k - 1], ld,
+                                  panels[k], ld, d, f, static_cast<hipStream_t>(stream));
+        if (rc) return rc;
+    }
+    return ok();
+}
+
+int srg_cheby_step_f64(const int64_t* indptr, const int32_t* indices, const double* values,
+                       int64_t n_rows, const int32_t* row_order, const double* Tc,
+                       const double* To, double* Tn, int64_t ld, int32_t d, int mode, double a1,
+                       double a2, const double* coef_prev, const double* coef, int32_t n_scales,
+                       double* R, int64_t r_stride, void* stream)
+{
+    return launch_cheby<double>(indptr, indices, values, n_rows, row_order, Tc, To, Tn, ld, d, mode,
+                                a1, a2, coef_prev, coef, n_scales, R, r_stride,
+                                static_cast<hipStream_t>(stream));
+}
+
+int srg_cheby_step_f32(const int64_t* indptr, const int32_t* indices, const float* values,
+                       int64_t n_rows, const int32_t* row_order, const float* Tc, const float* To,
+                       float* Tn, int64_t ld, int32_t d, int mode, float a1, float a2,
+                       const float* coef_prev, const float* coef, int32_t n_scales, float* R,
+                       int64_t r_stride, void* stream)
+{
+    return launch_cheby<float>(indptr, indices, values, n_rows, row_order, Tc, To, Tn, ld, d, mode,
+                               a1, a2, coef_prev, coef, n_scales, R, r_stride,
+                               static_cast<hipStream_t>(stream));
+}
+
+int srg_csr_validate(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t nnz,
+                     int64_t n_cols, void* stream)
+{
+    if (n_rows < 0 || nnz < 0 || n_cols < 0) return fail(SRG_ERR_INVALID, "negative size");
+    if (!indptr) return fail(SRG_ERR_INVALID, "null indptr");
+    if (nnz > 0 && !indices) return fail(SRG_ERR_INVALID, "null indices");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    unsigned int* d_bad = nullptr;
+    SRG_HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&d_bad), sizeof(unsigned int), s));
+    SRG_HIP_CHECK(hipMemsetAsync(d_bad, 0, sizeof(unsigned int), s));
+    const int64_t work = std::max(nnz, n_rows);
+    const unsigned blocks = (unsigned)std::min<int64_t>(std::max<int64_t>((work + 255) / 256, 1), 8192);
+    hipLaunchKernelGGL(k_validate, dim3(blocks), dim3(256), 0, s, indptr, indices, n_rows, nnz, n_cols, d_bad);
+    SRG_HIP_CHECK(hipGetLastError());
+    unsigned int bad = 0;
+    SRG_HIP_CHECK(hipMemcpyAsync(&bad, d_bad, sizeof(bad), hipMemcpyDeviceToHost, s));
+    SRG_HIP_CHECK(hipFreeAsync(d_bad, s));
+    SRG_HIP_CHECK(hipStreamSynchronize(s));
+    if (bad & 1u) return fail(SRG_ERR_INVALID, "column id outside [0, %lld)", (long long)n_cols);
+    if (bad & 2u) return fail(SRG_ERR_INVALID, "indptr decreases");
+    if (bad & 4u) return fail(SRG_ERR_INVALID, "indptr[0] != 0");
+    if (bad & 8u) return fail(SRG_ERR_INVALID, "indptr[n_rows] != nnz=%lld", (long long)nnz);
+    return ok();
+}
+
+const char* srg_last_error(void) { return g_err_msg; }
+int srg_last_error_code(void) { return g_err_code; }
+void srg_clear_error(void) { (void)ok(); }
+const char* srg_version(void) { return "srgnn_hip " SRG_GIT_REV " gfx950"; }
+
+}  // extern "C"

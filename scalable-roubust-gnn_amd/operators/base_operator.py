@@ -1,0 +1,112 @@
+"""Reference-compatible operator base classes (mirror of SSRG/operators/base_operator.py).
+
+`GraphOp.propagate` keeps the reference's signature, checks, error messages and return type (a list
+of K+1 CPU float32 tensors, hop 0 being the caller's feature array) -- SSRG/operators/
+base_operator.py:19-36 -- but the K hops run back to back on the GPU: Â and X are uploaded once,
+the hop loop is `srgnn.spmm.propagate` (libsrgnn_hip.so, exact fma chains, bit-identical to the
+reference's FloatCSRMulDenseOMP), and the K result panels come back in one batch of copies.
+
+`propagate_device` is the performance entry: same computation, device tensors in and out.
+"""
+from __future__ import annotations
+
+import ctypes
+import platform
+
+import numpy as np
+import scipy.sparse as sp
+import torch
+import torch.nn as nn
+from torch import Tensor
+
+from operators.utils import csr_sparse_dense_matmul, cuda_csr_sparse_dense_matmul  # noqa: F401
+from srgnn.csr import DeviceCSR
+from srgnn.spmm import propagate as _device_propagate
+
+
+class GraphOp:
+    def __init__(self, prop_steps):
+        self.prop_steps = prop_steps
+        self.adj = None
+
+    def construct_adj(self, adj):
+        raise NotImplementedError
+
+    def _checked_inputs(self, adj, feature):
+        """The reference's checks, in its order (base_operator.py:20-30)."""
+        self.adj = self.construct_adj(adj)
+        if not isinstance(adj, sp.csr_matrix):
+            raise TypeError("The adjacency matrix must be a scipy csr sparse matrix!")
+        elif not isinstance(feature, np.ndarray):
+            if isinstance(feature, Tensor):
+                feature = feature.numpy()
+            else:
+                raise TypeError("The feature matrix must be a numpy.ndarray!")
+        elif self.adj.shape[1] != feature.shape[0]:
+            raise ValueError("Dimension mismatch detected for the adjacency and the feature matrix!")
+        if self.prop_steps > 0 and feature.dtype != np.float32:
+            # the reference's first hop hands the array to an ndpointer(float32) (utils.py:29-34)
+            raise ctypes.ArgumentError("argument 5: TypeError: array must have data type float32")
+        return feature
+
+    def _operator(self, device=None):
+        adj = self.adj if isinstance(self.adj, sp.csr_matrix) else sp.csr_matrix(self.adj)
+        return DeviceCSR.from_scipy(adj, device=device)
+
+    def propagate(self, adj, feature):
+        feature = self._checked_inputs(adj, feature)
+        if self.prop_steps <= 0:
+            return [torch.FloatTensor(feature)]
+        A = self._operator()
+        X = torch.from_numpy(np.ascontiguousarray(feature)).to(A.device)
+        panels = _device_propagate(A, X, self.prop_steps)
+        host = [torch.empty(tuple(p.shape), dtype=torch.float32, pin_memory=True) for p in panels[1:]]
+        for h, p in zip(host, panels[1:]):
+            h.copy_(p, non_blocking=True)
+        torch.cuda.current_stream(A.device).synchronize()
+        return [torch.FloatTensor(feature)] + host
+
+    def propagate_device(self, adj, feature, device=None):
+        """Same as propagate() but returns device tensors (hop 0 = the feature on the device)."""
+        if isinstance(feature, Tensor) and feature.is_cuda:
+            self.adj = self.construct_adj(adj)
+            if not isinstance(adj, sp.csr_matrix):
+                raise TypeError("The adjacency matrix must be a scipy csr sparse matrix!")
+            if self.adj.shape[1] != feature.shape[0]:
+                raise ValueError("Dimension mismatch detected for the adjacency and the feature matrix!")
+            A = self._operator(feature.device)
+            X = feature.to(torch.float32)
+        else:
+            feature = self._checked_inputs(adj, feature)
+            A = self._operator(device)
+            X = torch.from_numpy(np.ascontiguousarray(feature)).to(A.device)
+        return _device_propagate(A, X, self.prop_steps)
+
+
+# Might include training parameters
+class MessageOp(nn.Module):
+    def __init__(self, start=None, end=None):
+        super(MessageOp, self).__init__()
+        self.aggr_type = None
+        self.start, self.end = start, end
+
+    def aggr_type(self):
+        return self.aggr_type
+
+    def combine(self, feat_list):
+        return NotImplementedError
+
+    def aggregate(self, feat_list):
+        if not isinstance(feat_list, list):
+            return TypeError("The input must be a list consists of feature matrices!")
+        for feat in feat_list:
+            if not isinstance(feat, Tensor):
+                raise TypeError("The feature matrices must be tensors!")
+        return self.combine(feat_list)
+
+
+def ada_platform_one_step_propagation(adj, x):
+    """One hop with host arrays (base_operator.py:309-314): the GPU SpMM on Linux, scipy elsewhere."""
+    if platform.system() == "Linux":
+        return csr_sparse_dense_matmul(adj, x)
+    return adj.dot(x)

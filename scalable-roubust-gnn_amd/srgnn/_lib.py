@@ -1,0 +1,108 @@
+"""ctypes binding of libsrgnn_hip.so (the C-ABI declared in include/srgnn_hip.h).
+
+The library is built in-tree by scalable-roubust-gnn_amd/csrc/Makefile (or __graft_entry__.build()).
+There is no fallback: if the library is missing or fails to load, every product entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("SRGNN_HIP_LIB", os.path.join(_PKG_ROOT, "lib", "libsrgnn_hip.so"))
+
+SRG_OK = 0
+SRG_ERR_INVALID = -1
+SRG_ERR_HIP = -2
+SRG_ERR_ALLOC = -3
+
+SRG_SPMM_ACCUMULATE = 0x1
+SRG_SPMM_NT_STORE = 0x2
+
+SRG_CHEBY_INIT = 0
+SRG_CHEBY_STEP = 1
+
+# every symbol include/srgnn_hip.h declares (checked by tests/test_capi.py)
+EXPORTED_SYMBOLS = (
+    "FloatCSRMulDenseOMP",
+    "FloatCSRMulDense",
+    "srg_spmm_csr_f32",
+    "srg_propagate_khop_f32",
+    "srg_cheby_step_f64",
+    "srg_cheby_step_f32",
+    "srg_csr_validate",
+    "srg_last_error",
+    "srg_last_error_code",
+    "srg_clear_error",
+    "srg_version",
+)
+
+
+class SrgError(RuntimeError):
+    """A libsrgnn_hip entry point returned an error status."""
+
+
+_lock = threading.Lock()
+_lib = None
+
+_p = ctypes.c_void_p
+_i32 = ctypes.c_int32
+_i64 = ctypes.c_int64
+_u32 = ctypes.c_uint32
+_f32 = ctypes.c_float
+_f64 = ctypes.c_double
+
+
+def _declare(lib):
+    lib.srg_spmm_csr_f32.argtypes = [_p, _p, _p, _i64, _p, _i64, _p, _i64, _p, _i64, _i32, _u32, _p]
+    lib.srg_spmm_csr_f32.restype = ctypes.c_int
+    lib.srg_propagate_khop_f32.argtypes = [_p, _p, _p, _i64, _p, _i64, _p, _i64, _i32, _i32, _u32, _p]
+    lib.srg_propagate_khop_f32.restype = ctypes.c_int
+    lib.srg_cheby_step_f64.argtypes = [_p, _p, _p, _i64, _p, _p, _p, _p, _i64, _i32, ctypes.c_int,
+                                       _f64, _f64, _p, _p, _i32, _p, _i64, _p]
+    lib.srg_cheby_step_f64.restype = ctypes.c_int
+    lib.srg_cheby_step_f32.argtypes = [_p, _p, _p, _i64, _p, _p, _p, _p, _i64, _i32, ctypes.c_int,
+                                       _f32, _f32, _p, _p, _i32, _p, _i64, _p]
+    lib.srg_cheby_step_f32.restype = ctypes.c_int
+    lib.srg_csr_validate.argtypes = [_p, _p, _i64, _i64, _i64, _p]
+    lib.srg_csr_validate.restype = ctypes.c_int
+    lib.srg_last_error.argtypes = []
+    lib.srg_last_error.restype = ctypes.c_char_p
+    lib.srg_last_error_code.argtypes = []
+    lib.srg_last_error_code.restype = ctypes.c_int
+    lib.srg_clear_error.argtypes = []
+    lib.srg_clear_error.restype = None
+    lib.srg_version.argtypes = []
+    lib.srg_version.restype = ctypes.c_char_p
+    lib.FloatCSRMulDense.restype = ctypes.c_int
+    return lib
+
+
+def lib():
+    """The loaded library (loaded once).  Raises OSError with the build hint if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise OSError(
+                    f"libsrgnn_hip.so not found at {LIB_PATH}: build it with "
+                    f"`make -C scalable-roubust-gnn_amd/csrc` or `python -c 'import __graft_entry__ as g; g.build()'`"
+                )
+            _lib = _declare(ctypes.CDLL(LIB_PATH))
+    return _lib
+
+
+def last_error() -> str:
+    return lib().srg_last_error().decode(errors="replace")
+
+
+def check(rc: int, what: str) -> None:
+    if rc != SRG_OK:
+        raise SrgError(f"{what} failed ({rc}): {last_error()}")
+
+
+def version() -> str:
+    return lib().srg_version().decode()

@@ -1,0 +1,110 @@
+"""Device-resident CSR operand + its schedule (the "plan").
+
+A `DeviceCSR` holds the normalised adjacency Â of `GraphOp.construct_adj`
+(SSRG/operators/base_operator.py:20) in HBM, laid out for the gfx950 kernels:
+
+    indptr  int64 [n_rows + 1]     (nnz may exceed 2^31: papers100M / RMAT-26 scale)
+    indices int32 [nnz]            column ids, CSR order preserved exactly (the fma chains follow it)
+    values  fp32  [nnz]            Â values, already cast to fp32 as utils.py:39 does
+    order   int32 [n_rows]         schedule: rows with more than `heavy_threshold` nonzeros first
+                                   (decreasing length), then the rest (decreasing length)
+    n_heavy int                    those long rows are split into 32-column slices, one wave each
+
+The schedule never changes results -- every output element stays one fma chain in CSR order -- it
+only decides which wave works on what and when (power-law hubs start first).
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _lib
+
+DEFAULT_HEAVY_THRESHOLD = int(os.environ.get("SRGNN_HEAVY_THRESHOLD", "128"))
+
+
+def _dev(device):
+    if device is None:
+        device = torch.device("cuda", torch.cuda.current_device())
+    device = torch.device(device)
+    if device.type != "cuda":
+        raise RuntimeError(f"libsrgnn_hip runs on a HIP device, got {device}")
+    return device
+
+
+@dataclass
+class DeviceCSR:
+    indptr: torch.Tensor
+    indices: torch.Tensor
+    values: torch.Tensor
+    n_rows: int
+    n_cols: int
+    order: torch.Tensor
+    n_heavy: int
+
+    @property
+    def nnz(self) -> int:
+        return int(self.indices.numel())
+
+    @property
+    def device(self):
+        return self.indices.device
+
+    # ------------------------------------------------------------------------------------------
+    @classmethod
+    def from_tensors(cls, indptr, indices, values, n_cols=None, heavy_threshold=None,
+                     validate=True, device=None):
+        """Build from CSR arrays (numpy or torch, any device); copies to `device` if needed."""
+        device = _dev(device if device is not None else
+                      (indices.device if isinstance(indices, torch.Tensor) and indices.is_cuda else None))
+        ip = torch.as_tensor(indptr).to(device=device, dtype=torch.int64)
+        ix = torch.as_tensor(indices).to(device=device, dtype=torch.int32)
+        vv = torch.as_tensor(values).to(device=device, dtype=torch.float32)
+        n_rows = int(ip.numel()) - 1
+        if n_rows < 0:
+            raise ValueError("indptr must have n_rows + 1 entries")
+        if n_cols is None:
+            n_cols = n_rows
+        if ix.numel() != vv.numel():
+            raise ValueError(f"indices ({ix.numel()}) and values ({vv.numel()}) differ in length")
+        ip, ix, vv = ip.contiguous(), ix.contiguous(), vv.contiguous()
+        if validate:
+            stream = torch.cuda.current_stream(device).cuda_stream
+            _lib.check(_lib.lib().srg_csr_validate(ip.data_ptr(), ix.data_ptr(), n_rows, ix.numel(),
+                                                   n_cols, stream), "srg_csr_validate")
+        order, n_heavy = make_schedule(ip, heavy_threshold)
+        return cls(ip, ix, vv, n_rows, int(n_cols), order, n_heavy)
+
+    @classmethod
+    def from_scipy(cls, adj, heavy_threshold=None, device=None):
+        """From a scipy.sparse.csr_matrix (values cast to fp32 like SSRG/operators/utils.py:39)."""
+        return cls.from_tensors(np.asarray(adj.indptr, dtype=np.int64),
+                                np.asarray(adj.indices, dtype=np.int32),
+                                np.asarray(adj.data).astype(np.float32),
+                                n_cols=adj.shape[1], heavy_threshold=heavy_threshold, device=device)
+
+    def rows(self, r0: int, r1: int, heavy_threshold=None) -> "DeviceCSR":
+        """Row block [r0, r1) with rebased row pointers (global column ids kept)."""
+        ip = self.indptr[r0:r1 + 1]
+        base = int(ip[0].item())
+        end = int(ip[-1].item())
+        ip = ip - base
+        order, n_heavy = make_schedule(ip, heavy_threshold)
+        return DeviceCSR(ip.contiguous(), self.indices[base:end], self.values[base:end],
+                         r1 - r0, self.n_cols, order, n_heavy)
+
+
+def make_schedule(indptr: torch.Tensor, heavy_threshold=None):
+    """Row order (int32) and heavy-row count for a CSR with row pointers `indptr`."""
+    if heavy_threshold is None:
+        heavy_threshold = DEFAULT_HEAVY_THRESHOLD
+    deg = indptr[1:] - indptr[:-1]
+    n = int(deg.numel())
+    if n == 0:
+        return torch.zeros(0, dtype=torch.int32, device=indptr.device), 0
+    order = torch.sort(deg, descending=True, stable=True).indices.to(torch.int32)
+    n_heavy = int((deg > heavy_threshold).sum().item()) if heavy_threshold >= 0 else 0
+    return order.contiguous(), n_heavy

@@ -1,0 +1,90 @@
+"""Device API of the propagation hot path (one hop, K hops) over a `DeviceCSR`.
+
+Every call goes through libsrgnn_hip.so; there is no CPU or torch fallback.  Kernels are enqueued
+on torch's current HIP stream of the operand's device, so torch events / synchronisation see them.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from .csr import DeviceCSR
+
+
+def _stream(device):
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _check_panel(X: torch.Tensor, rows: int, name: str, d=None):
+    if not isinstance(X, torch.Tensor) or not X.is_cuda:
+        raise TypeError(f"{name} must be a CUDA (HIP) tensor")
+    if X.dtype != torch.float32:
+        raise TypeError(f"{name} must be float32, got {X.dtype}")
+    if X.dim() != 2:
+        raise ValueError(f"{name} must be 2-D, got shape {tuple(X.shape)}")
+    if X.shape[0] < rows:
+        raise ValueError(f"{name} has {X.shape[0]} rows, need {rows}")
+    if X.stride(1) != 1:
+        raise ValueError(f"{name} must be row-major with unit column stride")
+    if d is not None and X.shape[1] != d:
+        raise ValueError(f"{name} has {X.shape[1]} columns, expected {d}")
+
+
+def spmm(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor | None = None, accumulate: bool = False,
+         nt_store: bool = False) -> torch.Tensor:
+    """out[r, :] (+)= A[r, :] @ X  for the rows of A (one hop; exact fma chains in CSR order)."""
+    _check_panel(X, A.n_cols, "X")
+    d = X.shape[1]
+    if out is None:
+        if accumulate:
+            raise ValueError("accumulate=True needs an out tensor")
+        out = torch.empty((A.n_rows, d), dtype=torch.float32, device=X.device)
+    _check_panel(out, A.n_rows, "out", d)
+    if out.device != A.device or X.device != A.device:
+        raise ValueError("A, X and out must be on the same device")
+    flags = (_lib.SRG_SPMM_ACCUMULATE if accumulate else 0) | (_lib.SRG_SPMM_NT_STORE if nt_store else 0)
+    rc = _lib.lib().srg_spmm_csr_f32(A.indptr.data_ptr(), A.indices.data_ptr(), A.values.data_ptr(),
+                                     A.n_rows, A.order.data_ptr() if A.n_rows else None, A.n_heavy,
+                                     X.data_ptr(), X.stride(0), out.data_ptr(), out.stride(0), d, flags,
+                                     _stream(X.device))
+    _lib.check(rc, "srg_spmm_csr_f32")
+    return out
+
+
+def propagate(A: DeviceCSR, X: torch.Tensor, K: int, panels: list | None = None,
+              nt_store: bool = False) -> list:
+    """[X, ÂX, …, Â^K X] as device tensors (panels[0] is X itself, like the reference's list).
+
+    Device-resident form of GraphOp.propagate's hop loop (SSRG/operators/base_operator.py:32-35):
+    the K hops run back to back on the GPU with no host round trips."""
+    if A.n_rows != A.n_cols:
+        raise ValueError("propagate needs a square operator")
+    _check_panel(X, A.n_rows, "X")
+    n, d = A.n_rows, X.shape[1]
+    if K < 0:
+        raise ValueError("K must be >= 0")
+    X0 = X
+    if panels is None and X.stride(0) != d:
+        X = X.contiguous()          # kernels need one leading dimension for all panels
+    if panels is None:
+        buf = torch.empty((K, n, d), dtype=torch.float32, device=X.device) if K else None
+        panels = [X] + [buf[k] for k in range(K)]
+    if len(panels) != K + 1:
+        raise ValueError("panels must hold K + 1 tensors")
+    ld = panels[0].stride(0)
+    for k, p in enumerate(panels):
+        _check_panel(p, n, f"panels[{k}]", d)
+        if p.stride(0) != ld:
+            raise ValueError("all panels must share one leading dimension")
+    arr = (ctypes.c_void_p * (K + 1))(*[p.data_ptr() for p in panels])
+    flags = _lib.SRG_SPMM_NT_STORE if nt_store else 0
+    rc = _lib.lib().srg_propagate_khop_f32(A.indptr.data_ptr(), A.indices.data_ptr(),
+                                           A.values.data_ptr(), n,
+                                           A.order.data_ptr() if n else None, A.n_heavy,
+                                           arr, ld, d, K, flags, _stream(X.device))
+    _lib.check(rc, "srg_propagate_khop_f32")
+    if panels[0] is not X0 and X is not X0:
+        panels = [X0] + list(panels[1:])
+    return panels

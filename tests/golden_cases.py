@@ -1,0 +1,80 @@
+"""Loader for the golden fixtures written by tests/golden/make_golden.py (reference outputs)."""
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def manifest():
+    with open(os.path.join(GOLDEN, "manifest.json")) as f:
+        return json.load(f)
+
+
+def names(kind=None):
+    m = manifest()
+    out = [k for k in sorted(m) if not k.startswith("_")]
+    if kind == "norm":
+        out = [k for k in out if m[k]["op"] != "raw_spmm"]
+    elif kind == "raw":
+        out = [k for k in out if m[k]["op"] == "raw_spmm"]
+    return out
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+class Case:
+    def __init__(self, name):
+        self.name = name
+        self.meta = manifest()[name]
+        self.z = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
+
+    def __getitem__(self, k):
+        return self.z[k]
+
+    def has(self, k):
+        return k in self.z.files
+
+    @property
+    def n(self):
+        return int(self.meta["n"])
+
+    @property
+    def k(self):
+        return int(self.meta["k"])
+
+    def adj(self):
+        import scipy.sparse as sp
+        return sp.csr_matrix((self["adj_data"], self["adj_indices"].astype(np.int32),
+                              self["adj_indptr"].astype(np.int32)), shape=(self.n, self.n))
+
+    def x(self):
+        if self.has("x"):
+            return self["x"]
+        sys.path.insert(0, os.path.join(os.path.dirname(GOLDEN), "..", "scalable-roubust-gnn_amd"))
+        from srgnn import synth
+        feats = self.meta["features"]
+        seed = int(feats.split("seed=")[1].rstrip(")"))
+        if feats.startswith("uniform"):
+            x = synth.uniform_features_np(self.n, int(self.meta["d"]), seed=seed)
+        else:
+            x = synth.binary_rownorm_features_np(self.n, int(self.meta["d"]), 18, seed=seed)
+        assert sha(x) == str(self["x_sha256"]), "regenerated features differ from the fixture's"
+        return x
+
+    def ahat(self):
+        return self["ahat_indptr"], self["ahat_indices"], self["ahat_data"]
+
+    def check_hop(self, k, h):
+        """Bit-exact check of hop k against the reference (hash, sampled rows, full if stored)."""
+        h = np.ascontiguousarray(h, dtype=np.float32)
+        rows = self["sample_rows"]
+        np.testing.assert_array_equal(h[rows], self[f"hop{k}_rows"], err_msg=f"{self.name} hop {k} rows")
+        if self.has(f"hop{k}"):
+            np.testing.assert_array_equal(h, self[f"hop{k}"], err_msg=f"{self.name} hop {k}")
+        assert sha(h) == str(self[f"hop{k}_sha256"]), f"{self.name} hop {k}: bytes differ from the reference"

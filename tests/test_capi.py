@@ -1,0 +1,70 @@
+"""The C-ABI library: loads without a GPU, exports every symbol include/srgnn_hip.h declares, and
+rejects bad arguments with a status + message before touching the device."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from srgnn import _lib
+
+HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "srgnn_hip.h")
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(\w+)\s*\(", text, flags=re.M))
+
+
+def test_header_and_python_binding_agree():
+    assert declared_symbols() == set(_lib.EXPORTED_SYMBOLS)
+
+
+def test_library_exports_every_declared_symbol():
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    missing = declared_symbols() - exported
+    assert not missing, f"not exported: {missing}"
+
+
+def test_library_loads_and_reports_version():
+    assert "gfx950" in _lib.version()
+
+
+def test_gfx950_code_object_present():
+    blob = open(_lib.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob, "no gfx950 code object in the fat binary"
+
+
+def test_invalid_arguments_fail_before_launch():
+    L = _lib.lib()
+    rc = L.srg_spmm_csr_f32(None, None, None, -1, None, 0, None, 8, None, 8, 8, 0, None)
+    assert rc == _lib.SRG_ERR_INVALID
+    assert "n_rows" in _lib.last_error()
+    rc = L.srg_spmm_csr_f32(None, None, None, 4, None, 0, None, 2, None, 8, 8, 0, None)
+    assert rc == _lib.SRG_ERR_INVALID and "leading" in _lib.last_error()
+    rc = L.srg_spmm_csr_f32(None, None, None, 4, None, 2, ctypes.c_void_p(16), 8, ctypes.c_void_p(16), 8, 8, 0, None)
+    assert rc == _lib.SRG_ERR_INVALID
+    rc = L.srg_propagate_khop_f32(None, None, None, 4, None, 0, None, 8, 8, -1, 0, None)
+    assert rc == _lib.SRG_ERR_INVALID and "K" in _lib.last_error()
+    rc = L.srg_cheby_step_f64(None, None, None, 4, None, None, None, None, 8, 8, 7, 1.0, 1.0,
+                              None, None, 1, None, 32, None)
+    assert rc == _lib.SRG_ERR_INVALID and "mode" in _lib.last_error()
+    L.srg_clear_error()
+    assert L.srg_last_error_code() == 0
+
+
+def test_empty_problem_is_a_noop_without_device():
+    L = _lib.lib()
+    assert L.srg_spmm_csr_f32(None, None, None, 0, None, 0, None, 8, None, 8, 8, 0, None) == 0
+    # the drop-in entry: zero rows -> returns without touching the device
+    f = ctypes.c_void_p
+    L.FloatCSRMulDenseOMP.argtypes = [f, f, f, f, f, ctypes.c_int, ctypes.c_int]
+    L.FloatCSRMulDenseOMP.restype = None
+    L.FloatCSRMulDenseOMP(None, None, None, None, None, 0, 5)
+    assert L.srg_last_error_code() == 0
+    L.FloatCSRMulDenseOMP(None, None, None, None, None, -3, 5)
+    assert L.srg_last_error_code() == _lib.SRG_ERR_INVALID

@@ -1,0 +1,57 @@
+"""Pin the CPU oracle against the reference's own outputs (tests/golden/, made by running the
+reference's operators) and against the reference's matmul.c compiled from source (oracle/_ref)."""
+import numpy as np
+import pytest
+
+import golden_cases as G
+
+
+@pytest.mark.parametrize("name", G.names("norm"))
+def test_sym_norm_matches_reference(oracle_mod, name):
+    c = G.Case(name)
+    a = c.adj()
+    if c.meta["op"] == "ppr":
+        ip, ix, v = oracle_mod.ppr_norm(a.indptr, a.indices, a.data, c.n, c.meta["r"], c.meta["alpha"])
+    else:
+        ip, ix, v = oracle_mod.sym_norm(a.indptr, a.indices, a.data, c.n, c.meta["r"])
+    np.testing.assert_array_equal(ip, c["ahat_indptr"])
+    np.testing.assert_array_equal(ix, c["ahat_indices"])
+    np.testing.assert_array_equal(v, c["ahat_data64"])          # fp64, bit for bit
+    np.testing.assert_array_equal(v.astype(np.float32), c["ahat_data"])
+
+
+@pytest.mark.parametrize("name", G.names("norm"))
+def test_propagate_matches_reference(oracle_mod, name):
+    c = G.Case(name)
+    hops = oracle_mod.propagate(*c.ahat(), c.x(), c.k)
+    for k in range(1, c.k + 1):
+        c.check_hop(k, hops[k])
+
+
+@pytest.mark.parametrize("name", G.names("raw"))
+def test_raw_spmm_matches_reference(oracle_mod, name):
+    c = G.Case(name)
+    a = c.adj()
+    y = oracle_mod.spmm(a.indptr, a.indices, a.data.astype(np.float32), c.x())
+    c.check_hop(1, y)
+
+
+@pytest.mark.parametrize("name", G.names("raw") + ["rand_d128_r05", "rand_d7_r03", "cora_sym_k3"])
+def test_oracle_equals_reference_build(oracle_mod, name):
+    if oracle_mod.ref_lib() is None:
+        pytest.skip("oracle/_ref/libmatmul_ref.so not built (reference sources absent)")
+    c = G.Case(name)
+    if c.meta["op"] == "raw_spmm":
+        a = c.adj()
+        ip, ix, v = a.indptr, a.indices, a.data.astype(np.float32)
+    else:
+        ip, ix, v = c.ahat()
+    x = c.x()
+    np.testing.assert_array_equal(oracle_mod.spmm(ip, ix, v, x), oracle_mod.ref_spmm(ip, ix, v, x))
+
+
+def test_error_manifest_present():
+    errs = G.manifest()["_errors"]
+    assert errs["coo_adj"] == "TypeError"
+    assert errs["float64_feature"] == "ArgumentError"
+    assert errs["dim_mismatch"] == "ValueError"
