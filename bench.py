@@ -1,0 +1,224 @@
+#!/usr/bin/env python3
+"""Benchmark of the K-hop propagation precompute (BASELINE.json metric) on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config products]
+
+One "step" = one full K-hop propagate ([X, ÂX, …, Â^K X]) of the configuration's synthetic
+power-law graph with inputs already resident in HBM: K = 10 hops of the
+products-shaped graph (N = 2,449,029, 61.9 M undirected edges, d = 128) by default.
+value = propagated edges/s = steps * K * nnz(Â) / time (nnz counts the self-loops), whole job.
+
+N > 1: one process per GPU (torchrun), 1-D row partition balanced by nonzeros, one RCCL
+all-gather of the feature panel per hop (srgnn.dist) -- strong scaling of the same graph.
+
+Extra objects on the JSON line:
+  roofline      the SpMM kernel: algorithmic (no-reuse) bytes per launch / its average duration,
+                timed with HIP events on the launch stream; traffic from rocprofv3 PMC counters
+                (profiles/pmc_<config>.json, written by tools/pmc_traffic.py) or null
+  cpu_baseline  rank 0, N = 1 only: the reference's FloatCSRMulDenseOMP compiled from its own
+                matmul.c (oracle/_ref/libmatmul_ref.so), kernel-only hops on pre-converted buffers
+                of the same graph, bounded to ~--cpu-seconds of work
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "scalable-roubust-gnn_amd"))
+sys.path.insert(0, HERE)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from srgnn import graphs, roofline, synth  # noqa: E402
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="products", choices=sorted(synth.CONFIGS))
+    ap.add_argument("--k", type=int, default=None, help="hops (default: the config's K)")
+    ap.add_argument("--d", type=int, default=None)
+    ap.add_argument("--heavy-threshold", type=int, default=None)
+    ap.add_argument("--roofline-reps", type=int, default=10)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--nt-store", action="store_true")
+    return ap.parse_args()
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(ip, ix, vals, x_host, n, d, budget_s):
+    """The reference's FloatCSRMulDenseOMP (built from SSRG/operators/csrc/matmul.c) on the host."""
+    from oracle import oracle as O
+    L = O.ref_lib()
+    if L is None:
+        return None
+    ip32 = np.ascontiguousarray(ip, dtype=np.int32)
+    ix32 = np.ascontiguousarray(ix, dtype=np.int32)
+    v32 = np.ascontiguousarray(vals, dtype=np.float32)
+    cur = np.ascontiguousarray(x_host)
+    nxt = np.zeros_like(cur)
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
+    hops = 0
+    t0 = time.perf_counter()
+    while True:
+        nxt.fill(0.0)
+        L.FloatCSRMulDenseOMP(O._ptr(nxt), O._ptr(v32), O._ptr(ix32), O._ptr(ip32), O._ptr(cur), n, d)
+        hops += 1
+        cur, nxt = nxt, cur
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    dt = time.perf_counter() - t0
+    nnz = int(ip32[-1])
+    return {"value": hops * nnz / dt, "unit": "propagated edges/s", "cores": threads, "kind": "reference",
+            "sample": f"{hops} hop(s) of the full {n}-node graph (nnz {nnz}, d {d}), kernel-only on "
+                      f"pre-converted int32/fp32 buffers, OMP_NUM_THREADS={threads}, {dt:.1f} s"}
+
+
+def pmc_traffic(config, kernel_hint="k_spmm"):
+    path = os.path.join(HERE, "profiles", f"pmc_{config}.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            rec = json.load(f)
+        return float(rec["hbm_bytes_per_launch"])
+    except Exception:  # noqa: BLE001
+        return None
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        log(f"note: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from srgnn.csr import DeviceCSR
+    from srgnn.spmm import propagate, spmm
+
+    t_build = time.perf_counter()
+    ip, ix, vals, n, d, K = graphs.build(a.config, dev, d=a.d)
+    K = a.k if a.k is not None else K
+    nnz = int(ix.numel())
+    X = synth.uniform_features_t(n, d, seed=synth.FEATURE_SEED, device=dev)
+    torch.cuda.synchronize()
+    log(f"graph {a.config}: n={n} nnz={nnz} d={d} K={K} built in {time.perf_counter() - t_build:.1f}s")
+
+    stream = torch.cuda.current_stream(dev)
+    if world == 1:
+        A = DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, heavy_threshold=a.heavy_threshold, device=dev)
+        log(f"schedule: n_heavy={A.n_heavy}")
+        buf = torch.empty((K, n, d), dtype=torch.float32, device=dev)
+        panels = [X] + [buf[k] for k in range(K)]
+
+        def step():
+            propagate(A, X, K, panels=panels, nt_store=a.nt_store)
+        local_rows, local_nnz = n, nnz
+    else:
+        from srgnn.dist import RowPartitionedOperator
+        op = RowPartitionedOperator(ip, ix, vals, n, heavy_threshold=a.heavy_threshold, device=dev)
+        A = op.A
+        x_loc = op.new_panel(d)
+        x_loc[: op.rows].copy_(X[op.r0:op.r1])
+        panels = [x_loc] + [op.new_panel(d) for _ in range(K)]
+        del X
+
+        def step():
+            op.propagate(x_loc, K, panels=panels)
+        local_rows, local_nnz = op.rows, op.nnz_local
+
+    host_copy = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        host_copy = (ip.cpu().numpy(), ix.cpu().numpy(), vals.cpu().numpy(), X.cpu().numpy())
+    del ip, ix, vals
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    # roofline: average duration of one SpMM launch (this rank's operator), HIP events on its stream
+    src = panels[0] if world == 1 else op._gather(panels[0])
+    dst = panels[1] if world == 1 else panels[1][: op.rows]
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * a.roofline_reps)]
+    for r in range(a.roofline_reps):
+        ev[2 * r].record(stream)
+        spmm(A, src, out=dst, nt_store=a.nt_store)
+        ev[2 * r + 1].record(stream)
+    torch.cuda.synchronize()
+    durs = [ev[2 * r].elapsed_time(ev[2 * r + 1]) * 1e-3 for r in range(a.roofline_reps)]
+    kern_s = float(np.mean(durs))
+    b_alg = roofline.bytes_no_reuse(local_rows, local_nnz, d)
+    achieved = b_alg / kern_s / 1e9
+    peak = roofline.MI355X_HBM_PEAK_GBS
+    traffic = pmc_traffic(a.config) if world == 1 else None
+
+    value = a.steps * K * nnz / dt
+    res = {
+        "metric": "propagated edges/sec (K-hop SpMM precompute)",
+        "value": value,
+        "unit": "propagated edges/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": dt / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (R-MAT power-law graph with the products node/edge counts, U[-1,1) features)",
+        "config": {"workload": f"{a.config}-shaped K-hop propagate", "n_nodes": n, "nnz_ahat": nnz,
+                   "d": d, "K": K, "normalization": "sym r=0.5", "parallelism": f"row-partition x{world}",
+                   "mode": "exact (bit-identical to reference)"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
+                     "frac": achieved / peak, "traffic": traffic,
+                     "kernel": "k_spmm (one hop)", "kernel_ms": kern_s * 1e3,
+                     "algorithmic_bytes_per_launch": b_alg,
+                     "compulsory_bytes_per_launch": roofline.bytes_compulsory(local_rows, local_nnz, d,
+                                                                              n_cols=n)},
+        "cpu_baseline": None,
+    }
+    if host_copy is not None:
+        log("cpu baseline ...")
+        ipn, ixn, vn, xn = host_copy
+        res["cpu_baseline"] = cpu_baseline(ipn, ixn, vn, xn, n, d, a.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -78,7 +78,13 @@ template <> struct Vec<float, 4> { typedef float type __attribute__((ext_vector_
 template <> struct Vec<double, 1> { typedef double type; };
 template <> struct Vec<double, 2> { typedef double type __attribute__((ext_vector_type(2))); };
 
-template <typename V> __device__ __forceinline__ float& el(V& v, int i) { return v[i]; }
+// element i of a scalar-or-vector value
+template <typename T> __device__ __forceinline__ T& elem(T& v, int) { return v; }
+template <typename T> __device__ __forceinline__ const T& elem(const T& v, int) { return v; }
+template <typename T, int N>
+__device__ __forceinline__ T& elem(T __attribute__((ext_vector_type(N)))& v, int i) { return reinterpret_cast<T*>(&v)[i]; }
+template <typename T, int N>
+__device__ __forceinline__ const T& elem(const T __attribute__((ext_vector_type(N)))& v, int i) { return reinterpret_cast<const T*>(&v)[i]; }
 
 template <typename T, int VEC>
 __device__ __forceinline__ typename Vec<T, VEC>::type vload(const T* p)
@@ -102,6 +108,17 @@ __device__ __forceinline__ double link(double a, double x, double acc)
 {
     return __dadd_rn(acc, __dmul_rn(a, x));
 }
+
+// Epilogue arithmetic: fp64 follows numpy/scipy rounding exactly (no contraction into fma);
+// fp32 leaves the compiler free (the fp32 Chebyshev path is tolerance-checked).
+__device__ __forceinline__ double e_mul(double a, double b) { return __dmul_rn(a, b); }
+__device__ __forceinline__ double e_add(double a, double b) { return __dadd_rn(a, b); }
+__device__ __forceinline__ double e_sub(double a, double b) { return __dsub_rn(a, b); }
+__device__ __forceinline__ double e_div(double a, double b) { return __ddiv_rn(a, b); }
+__device__ __forceinline__ float e_mul(float a, float b) { return a * b; }
+__device__ __forceinline__ float e_add(float a, float b) { return a + b; }
+__device__ __forceinline__ float e_sub(float a, float b) { return a - b; }
+__device__ __forceinline__ float e_div(float a, float b) { return a / b; }
 
 template <typename T, int VEC>
 __device__ __forceinline__ void chain(typename Vec<T, VEC>::type& acc, T a,
@@ -346,30 +363,27 @@ k_cheby(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
         if (!act) continue;
         V tn;
         if (mode == SRG_CHEBY_INIT) {
+            // Tn = (L Tc - a2 Tc) / a1 ;  R_s = (c0_s / 2) Tc + c1_s Tn
             const V tc = vload<T, VEC>(Tc + roff + col);
-            if constexpr (VEC == 1) {
-                tn = (acc - a2 * tc) / a1;
-            } else {
 #pragma unroll
-                for (int i = 0; i < VEC; ++i) tn[i] = (acc[i] - a2 * tc[i]) / a1;
-            }
+            for (int i = 0; i < VEC; ++i) elem(tn, i) = e_div(e_sub(elem(acc, i), e_mul(a2, elem(tc, i))), a1);
             for (int s = 0; s < n_scales; ++s) {
                 V r;
-                if constexpr (VEC == 1) {
-                    r = cf.prev[s] * tc + cf.cur[s] * tn;
-                } else {
 #pragma unroll
-                    for (int i = 0; i < VEC; ++i) r[i] = cf.prev[s] * tc[i] + cf.cur[s] * tn[i];
-                }
+                for (int i = 0; i < VEC; ++i)
+                    elem(r, i) = e_add(e_mul(cf.prev[s], elem(tc, i)), e_mul(cf.cur[s], elem(tn, i)));
                 vstore<T, VEC>(R + s * r_stride + roff + col, r, false);
             }
         } else {
+            // Tn = F Tc - To ;  R_s += ck_s Tn
             const V to = vload<T, VEC>(To + roff + col);
-            tn = acc - to;
+#pragma unroll
+            for (int i = 0; i < VEC; ++i) elem(tn, i) = e_sub(elem(acc, i), elem(to, i));
             for (int s = 0; s < n_scales; ++s) {
                 T* rp = R + s * r_stride + roff + col;
                 V r = vload<T, VEC>(rp);
-                r = r + cf.cur[s] * tn;
+#pragma unroll
+                for (int i = 0; i < VEC; ++i) elem(r, i) = e_add(elem(r, i), e_mul(cf.cur[s], elem(tn, i)));
                 vstore<T, VEC>(rp, r, false);
             }
         }

@@ -1,0 +1,24 @@
+"""Benchmark workloads of BASELINE.json / SURVEY.md §8: synthetic power-law graphs with the
+node / edge counts of the OGB graphs, normalised by construct_adj (r = 0.5), plus U[-1,1) features.
+Built on the device (deterministic: the same seed gives the same graph on every rank and on CPU)."""
+from __future__ import annotations
+
+import torch
+
+from . import synth
+from .normalize import sym_norm_binary
+
+
+def build(config: str, device, r: float = 0.5, n=None, n_edges=None, d=None, seed=synth.RMAT_SEED):
+    """Returns (indptr int64, indices int32, values fp32, n, d, K) on `device`."""
+    cfg = dict(synth.CONFIGS[config]) if config in synth.CONFIGS else {}
+    n = n or cfg["n"]
+    n_edges = n_edges or cfg["n_edges"]
+    d = d or cfg["d"]
+    k = cfg.get("k", 3)
+    u, v = synth.rmat_undirected_t(n, n_edges, seed=seed, device=device)
+    ip, ix = synth.symmetric_csr_t(n, u, v)
+    del u, v
+    ip, ix, vals = sym_norm_binary(ip, ix, n, r)
+    torch.cuda.empty_cache() if torch.device(device).type == "cuda" else None
+    return ip, ix, vals, n, d, k

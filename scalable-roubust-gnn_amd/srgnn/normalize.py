@@ -1,0 +1,46 @@
+"""construct_adj on the GPU for binary symmetric adjacencies (the synthetic benchmark graphs).
+
+Restates SSRG/operators/utils.py:81-93 for A binary, symmetric, without self-loops:
+    deg_i = rowsum(A + I) = |row i| + 1                       (exact integers in fp64)
+    Â[i, j] = fp32((1.0 * deg_i^(r-1)) * deg_j^(-r))           for (i, j) in A + I
+The degree powers go through numpy's np.power on the host (N values; the same libm call as the
+reference, hence bit-identical), the products and the fp32 cast run on the device (IEEE multiply
+and round-to-nearest are the same everywhere).  (A+I)^T = A+I here, so the CSR structure is A's
+rows with the diagonal merged in sorted position.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+
+def degree_powers(deg: np.ndarray, r: float):
+    deg = np.asarray(deg, dtype=np.float64)
+    with np.errstate(divide="ignore"):
+        left = np.power(deg, r - 1)
+        right = np.power(deg, -r)
+    left[np.isinf(left)] = 0.0
+    right[np.isinf(right)] = 0.0
+    return left, right
+
+
+def sym_norm_binary(indptr: torch.Tensor, indices: torch.Tensor, n: int, r: float = 0.5):
+    """(indptr int64, indices int32, values fp32) of Â for a binary symmetric A (no self-loops)."""
+    dev = indices.device
+    deg_a = (indptr[1:] - indptr[:-1])
+    rows = torch.repeat_interleave(torch.arange(n, device=dev), deg_a)
+    keys = torch.cat([rows * n + indices.to(torch.int64), torch.arange(n, device=dev) * (n + 1)])
+    keys = torch.sort(keys).values
+    del rows
+    r_i = keys // n
+    c_j = keys % n
+    del keys
+    deg = (deg_a + 1).cpu().numpy()
+    left, right = degree_powers(deg, r)
+    left_t = torch.from_numpy(left).to(dev)
+    right_t = torch.from_numpy(right).to(dev)
+    vals = ((1.0 * left_t[r_i]) * right_t[c_j]).to(torch.float32)
+    counts = torch.bincount(r_i, minlength=n)
+    out_ptr = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    out_ptr[1:] = torch.cumsum(counts, 0)
+    return out_ptr, c_j.to(torch.int32), vals

@@ -1,0 +1,195 @@
+"""Wavelet basis (graph heat-kernel wavelets) of SpectralModel on the GPU.
+
+The reference (SSRG/models/base_scalable/base_model.py:171-265) builds, for tau in [-s, +s]:
+    G = pygsp Graph(nx.adjacency_matrix(nx.Graph(adj)));  L = D - W (combinatorial)
+    c = compute_cheby_coeff(Heat(G, tau), m = order);     lmax = G.estimate_lmax()
+    phi_tau = cheby_op(G, c, identity blocks of 1000 columns), thresholded at `tolerance`
+then L1-normalises each phi row (sklearn normalize).  cheby_op is the Chebyshev recurrence
+    T0 = S,  T1 = (L S - a2 S) / a1,  T_{k+1} = (2/a1)(L - a2 I) T_k - T_{k-1},  a1 = a2 = lmax/2
+    R = c0/2 T0 + sum_k c_k T_k
+Here every Chebyshev order is ONE fused launch of srg_cheby_step_{f64,f32}: the SpMM row-wave
+gather plus an epilogue that forms T_{k+1} and accumulates every scale's output R_s in the same
+pass (all scales share the T_k panels, so two scales cost one recurrence, not two).
+
+pygsp is not available offline: the restatement follows pygsp 0.5.x semantics and is validated
+against a dense eigendecomposition (tests) -- parity with the reference is unpinned.  lmax is an
+explicit input (pygsp's ARPACK estimate uses a random start vector); `estimate_lmax` gives the
+same estimator (eigsh, tol 5e-3, x1.01) with a fixed start vector.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import scipy.sparse as sp
+import torch
+
+from . import _lib
+from .csr import make_schedule
+
+
+def laplacian_from_adj(adj: sp.spmatrix) -> sp.csr_matrix:
+    """L = D - W of nx.Graph(adj): undirected, one weight per node pair (the entry stored last in
+    row-major order wins, as networkx overwrites edge data), self-loops kept.  Every diagonal
+    entry is stored explicitly (also for isolated nodes)."""
+    coo = sp.coo_matrix(adj)
+    n = coo.shape[0]
+    order = np.lexsort((coo.col, coo.row))          # row-major
+    r, c, v = coo.row[order].astype(np.int64), coo.col[order].astype(np.int64), coo.data[order].astype(np.float64)
+    lo, hi = np.minimum(r, c), np.maximum(r, c)
+    key = lo * n + hi
+    rk = key[::-1]
+    _, first_in_rev = np.unique(rk, return_index=True)
+    last = key.size - 1 - first_in_rev               # last occurrence in row-major order
+    lo, hi, v = lo[last], hi[last], v[last]
+    off = lo != hi
+    rows = np.r_[lo, hi[off]]
+    cols = np.r_[hi, lo[off]]
+    vals = np.r_[v, v[off]]
+    W = sp.csr_matrix((vals, (rows, cols)), shape=(n, n))
+    deg = np.asarray(W.sum(axis=1)).ravel()
+    L = (sp.diags(deg) - W).tocsr()
+    # make every diagonal slot explicit
+    L = L + sp.csr_matrix((np.zeros(n), (np.arange(n), np.arange(n))), shape=(n, n))
+    L.sum_duplicates()
+    L.sort_indices()
+    missing = np.diff(L.indptr) == 0
+    if missing.any() or L.nnz < n:
+        Lc = L.tocoo()
+        L = sp.csr_matrix((np.r_[Lc.data, np.zeros(n)],
+                           (np.r_[Lc.row, np.arange(n)], np.r_[Lc.col, np.arange(n)])), shape=(n, n))
+        L.sum_duplicates()
+    return L
+
+
+def _explicit_diagonal(L: sp.csr_matrix) -> sp.csr_matrix:
+    """CSR with one stored entry per diagonal slot (value possibly 0), sorted, no duplicates."""
+    L = sp.csr_matrix(L, dtype=np.float64, copy=True)
+    L.sum_duplicates()
+    n = L.shape[0]
+    rows = np.repeat(np.arange(n), np.diff(L.indptr))
+    have = np.zeros(n, dtype=bool)
+    have[rows[L.indices == rows]] = True
+    if have.all():
+        return L
+    add = np.flatnonzero(~have)
+    r = np.r_[rows, add]
+    c = np.r_[L.indices, add]
+    v = np.r_[L.data, np.zeros(add.size)]
+    order = np.lexsort((c, r))
+    r, c, v = r[order], c[order], v[order]
+    ptr = np.zeros(n + 1, dtype=np.int64)
+    np.add.at(ptr, r + 1, 1)
+    return sp.csr_matrix((v, c.astype(np.int32), np.cumsum(ptr)), shape=(n, n))
+
+
+def estimate_lmax(L: sp.spmatrix) -> float:
+    """pygsp Graph.estimate_lmax: largest eigenvalue by ARPACK (tol 5e-3, ncv <= 10) times 1.01,
+    with a fixed all-ones start vector instead of ARPACK's random one."""
+    n = L.shape[0]
+    if n <= 2:
+        return float(np.linalg.eigvalsh(L.toarray()).max()) * 1.01
+    from scipy.sparse.linalg import eigsh
+    lam = eigsh(L.asfptype() if hasattr(L, "asfptype") else L.astype(np.float64), k=1, tol=5e-3,
+                ncv=min(n, 10), v0=np.ones(n), return_eigenvectors=False)
+    return float(lam[0]) * 1.01
+
+
+def heat_cheby_coeffs(tau: float, lmax: float, order: int) -> np.ndarray:
+    """pygsp compute_cheby_coeff(filters.Heat(G, tau), m=order): g(x) = exp(-tau x / lmax) sampled
+    at the order+1 Chebyshev nodes mapped to [0, lmax]."""
+    N = order + 1
+    a1 = a2 = lmax / 2.0
+    k = np.arange(N)
+    nodes = np.cos(np.pi * (k + 0.5) / N)
+    g = np.exp(-tau * (a1 * nodes + a2) / lmax)
+    return np.array([2.0 / N * np.dot(g, np.cos(np.pi * o * (k + 0.5) / N)) for o in range(order + 1)])
+
+
+class HeatWaveletFilter:
+    """R_s = sum_k c_{s,k} T_k(L~) S for the heat kernels exp(-tau_s x / lmax), every scale at once."""
+
+    def __init__(self, L: sp.spmatrix, taus, order: int = 3, lmax: float | None = None,
+                 dtype=torch.float64, device=None, heavy_threshold=None):
+        if order < 1:
+            raise ValueError("order must be >= 1")
+        if len(taus) < 1 or len(taus) > 8:
+            raise ValueError("1..8 scales")
+        if dtype not in (torch.float64, torch.float32):
+            raise TypeError("dtype must be float64 or float32")
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        L = _explicit_diagonal(sp.csr_matrix(L))
+        self.n = L.shape[0]
+        self.lmax = float(lmax) if lmax is not None else estimate_lmax(L)
+        self.a1 = self.a2 = self.lmax / 2.0
+        self.taus = [float(t) for t in taus]
+        self.coeffs = np.stack([heat_cheby_coeffs(t, self.lmax, order) for t in self.taus])
+        self.dtype = dtype
+        rows = np.repeat(np.arange(self.n), np.diff(L.indptr))
+        lvals = L.data.astype(np.float64)
+        fvals = (2.0 / self.a1) * np.where(L.indices == rows, lvals - self.a2, lvals)   # (2/a1)(L - a2 I)
+        tdt = dtype
+        self.indptr = torch.from_numpy(L.indptr.astype(np.int64)).to(self.device)
+        self.indices = torch.from_numpy(L.indices.astype(np.int32)).to(self.device)
+        self.lvals = torch.from_numpy(lvals).to(self.device, tdt)
+        self.fvals = torch.from_numpy(fvals).to(self.device, tdt)
+        self.order, _ = make_schedule(self.indptr, -1)
+
+    def apply(self, S: torch.Tensor) -> torch.Tensor:
+        """[n_scales, n, d] filter outputs for the panel S [n, d] (device tensor)."""
+        if not S.is_cuda or S.shape[0] != self.n or S.dim() != 2:
+            raise ValueError("S must be a [n, d] device tensor")
+        S = S.to(self.dtype).contiguous()
+        n, d = S.shape
+        ns, nc = self.coeffs.shape
+        R = torch.empty((ns, n, d), dtype=self.dtype, device=S.device)
+        bufs = [torch.empty_like(S) for _ in range(2)]
+        f64 = self.dtype == torch.float64
+        ct = ctypes.c_double if f64 else ctypes.c_float
+        fn = _lib.lib().srg_cheby_step_f64 if f64 else _lib.lib().srg_cheby_step_f32
+        stream = torch.cuda.current_stream(S.device).cuda_stream
+        L = _lib.lib()  # noqa: F841  (keeps the library loaded)
+
+        def launch(vals, Tc, To, Tn, mode, coef_prev, coef):
+            cp = (ct * ns)(*coef_prev) if coef_prev is not None else None
+            cc = (ct * ns)(*coef)
+            rc = fn(self.indptr.data_ptr(), self.indices.data_ptr(), vals.data_ptr(), n,
+                    self.order.data_ptr(), Tc.data_ptr(), To.data_ptr() if To is not None else None,
+                    Tn.data_ptr(), d, d, mode, self.a1, self.a2, cp, cc, ns, R.data_ptr(), n * d, stream)
+            _lib.check(rc, fn.__name__)
+
+        t_old, t_cur = S, bufs[0]
+        launch(self.lvals, S, None, t_cur, _lib.SRG_CHEBY_INIT, self.coeffs[:, 0], self.coeffs[:, 1])
+        spare = bufs[1]
+        for k in range(2, nc):
+            launch(self.fvals, t_cur, t_old, spare, _lib.SRG_CHEBY_STEP, None, self.coeffs[:, k])
+            t_old, t_cur, spare = t_cur, spare, (t_old if t_old is not S else torch.empty_like(S))
+        return R
+
+
+def wavelet_basis(adj: sp.spmatrix, scale: float = 0.5, order: int = 3, tolerance: float = 1e-4,
+                  lmax: float | None = None, batch: int = 1000, device=None):
+    """phi (tau = -scale) and phi^-1 (tau = +scale) as L1-row-normalised fp32 CSR matrices, as
+    SpectralModel.preprocess builds them (base_model.py:186-193, 236-265, 287-290): identity
+    blocks of `batch` columns filtered on the GPU (both scales in one recurrence), entries below
+    `tolerance` zeroed."""
+    L = laplacian_from_adj(adj)
+    filt = HeatWaveletFilter(L, [-scale, scale], order=order, lmax=lmax, device=device)
+    n = L.shape[0]
+    blocks = [[], []]
+    for c0 in range(0, n, batch):
+        w = min(batch, n - c0)
+        S = torch.zeros((n, w), dtype=torch.float64, device=filt.device)
+        S[torch.arange(c0, c0 + w, device=filt.device), torch.arange(w, device=filt.device)] = 1.0
+        R = filt.apply(S).cpu().numpy()
+        for s in range(2):
+            sub = R[s]
+            sub[sub < tolerance] = 0
+            blocks[s].append(sp.csr_matrix(sub.astype(np.float32)))
+    out = []
+    for s in range(2):
+        phi = sp.hstack(blocks[s]).tocsr()
+        rs = np.asarray(abs(phi).sum(axis=1)).ravel()
+        rs[rs == 0] = 1.0
+        out.append(sp.diags((1.0 / rs).astype(np.float32)) @ phi)
+    return out[0].tocsr(), out[1].tocsr(), filt.lmax

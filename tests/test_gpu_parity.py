@@ -1,0 +1,206 @@
+"""HIP kernels vs the reference (golden fixtures) and vs the CPU oracle.  Run on the MI355X box.
+
+Bar: exact mode is BIT-IDENTICAL to the reference's FloatCSRMulDenseOMP (one fp32 fma chain per
+output element in CSR order), so hops are compared by SHA-256 of their bytes.  Each case runs
+through both wave roles of the kernel: row waves only (heavy_threshold=-1 -> n_heavy=0), column-
+slice waves for every row (heavy_threshold=0), and the default split.
+"""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+import torch
+
+import golden_cases as G
+
+pytestmark = pytest.mark.gpu
+
+THRESHOLDS = [-1, 0, None]
+
+
+def _csr(c, thr):
+    from srgnn.csr import DeviceCSR
+    ip, ix, v = c.ahat()
+    return DeviceCSR.from_tensors(ip, ix, v, n_cols=c.n, heavy_threshold=thr, device="cuda")
+
+
+@pytest.mark.parametrize("thr", THRESHOLDS)
+@pytest.mark.parametrize("name", G.names("norm"))
+def test_khop_bit_exact_vs_reference(name, thr):
+    from srgnn.spmm import propagate
+    c = G.Case(name)
+    A = _csr(c, thr)
+    X = torch.from_numpy(c.x()).cuda()
+    hops = propagate(A, X, c.k)
+    torch.cuda.synchronize()
+    assert hops[0] is X
+    for k in range(1, c.k + 1):
+        c.check_hop(k, hops[k].cpu().numpy())
+
+
+@pytest.mark.parametrize("thr", THRESHOLDS)
+@pytest.mark.parametrize("name", G.names("raw"))
+def test_one_hop_raw_bit_exact(name, thr):
+    """Unsorted rows, duplicate entries and F-order inputs: the chain follows STORED order."""
+    from srgnn.csr import DeviceCSR
+    from srgnn.spmm import spmm
+    c = G.Case(name)
+    a = c.adj()
+    A = DeviceCSR.from_tensors(a.indptr, a.indices, a.data.astype(np.float32), n_cols=c.n,
+                               heavy_threshold=thr, device="cuda")
+    y = spmm(A, torch.from_numpy(c.x()).cuda())
+    c.check_hop(1, y.cpu().numpy())
+
+
+@pytest.mark.parametrize("name", G.names("raw") + ["rand_d7_r03", "rand_d130_r1"])
+def test_drop_in_host_entry_bit_exact(name):
+    """operators.utils.csr_sparse_dense_matmul -> libsrgnn_hip FloatCSRMulDenseOMP (host buffers)."""
+    from operators.utils import csr_sparse_dense_matmul
+    c = G.Case(name)
+    if c.meta["op"] == "raw_spmm":
+        adj, x = c.adj(), c.x()
+        c.check_hop(1, csr_sparse_dense_matmul(adj, x))
+    else:
+        ip, ix, v = c.ahat()
+        adj = sp.csr_matrix((v, ix, ip.astype(np.int32)), shape=(c.n, c.n))
+        h = c.x()
+        for k in range(1, c.k + 1):
+            h = csr_sparse_dense_matmul(adj, h)
+            c.check_hop(k, h)
+
+
+def test_cuda_compat_entry_overwrites():
+    from operators.utils import cuda_csr_sparse_dense_matmul
+    c = G.Case("raw_dups_d128")
+    c.check_hop(1, cuda_csr_sparse_dense_matmul(c.adj(), c.x()))
+
+
+@pytest.mark.parametrize("name", ["cora_sym_k3", "cora_asstored_k3", "rand_d36_ppr", "rand_d1_r05"])
+def test_graphop_propagate_end_to_end(name):
+    """The reference API (operators.graph_operator.*) end to end: construct_adj + K hops + list."""
+    from operators.graph_operator.symmetrical_simgraph_laplacian_operator import SymLaplacianGraphOp
+    from operators.graph_operator.symmetrical_simgraph_ppr_operator import PprGraphOp
+    c = G.Case(name)
+    op = (PprGraphOp(c.k, r=c.meta["r"], alpha=c.meta["alpha"]) if c.meta["op"] == "ppr"
+          else SymLaplacianGraphOp(c.k, r=c.meta["r"]))
+    x = c.x()
+    out = op.propagate(c.adj(), x)
+    assert len(out) == c.k + 1 and all(isinstance(t, torch.Tensor) and t.dtype == torch.float32 for t in out)
+    np.testing.assert_array_equal(out[0].numpy(), x)
+    np.testing.assert_array_equal(op.adj.data, c["ahat_data64"])
+    for k in range(1, c.k + 1):
+        c.check_hop(k, out[k].numpy())
+    dev = op.propagate_device(c.adj(), torch.from_numpy(x).cuda())
+    for k in range(1, c.k + 1):
+        c.check_hop(k, dev[k].cpu().numpy())
+
+
+def test_graphop_error_behaviour_matches_reference():
+    import ctypes
+    from operators.graph_operator.symmetrical_simgraph_laplacian_operator import SymLaplacianGraphOp
+    from operators.graph_operator.symmetrical_simgraph_ppr_operator import PprGraphOp
+    errs = G.manifest()["_errors"]
+    c = G.Case("rand_d7_r03")
+    adj, x = c.adj(), c.x()
+
+    def outcome(fn):
+        try:
+            fn()
+            return "ok"
+        except ctypes.ArgumentError:
+            return "ArgumentError"
+        except Exception as e:  # noqa: BLE001
+            return type(e).__name__
+
+    got = {
+        "coo_adj": outcome(lambda: SymLaplacianGraphOp(2).propagate(adj.tocoo(), x)),
+        "float64_feature": outcome(lambda: SymLaplacianGraphOp(2).propagate(adj, x.astype(np.float64))),
+        "dim_mismatch": outcome(lambda: SymLaplacianGraphOp(2).propagate(adj, x[:-1])),
+        "list_feature": outcome(lambda: SymLaplacianGraphOp(2).propagate(adj, x.tolist())),
+        "tensor_feature": outcome(lambda: SymLaplacianGraphOp(2).propagate(adj, torch.from_numpy(x))),
+        "ppr_dense_adj": outcome(lambda: PprGraphOp(2).propagate(adj.toarray(), x)),
+        "k0": outcome(lambda: SymLaplacianGraphOp(0).propagate(adj, x)),
+    }
+    assert got == errs
+
+
+def test_accumulate_and_nt_store_flags(oracle_mod):
+    from srgnn.spmm import spmm
+    c = G.Case("rand_d128_r05")
+    A = _csr(c, None)
+    x = c.x()
+    X = torch.from_numpy(x).cuda()
+    y0 = np.random.default_rng(0).standard_normal((c.n, x.shape[1])).astype(np.float32)
+    Y = torch.from_numpy(y0.copy()).cuda()
+    spmm(A, X, out=Y, accumulate=True)
+    ref = oracle_mod.spmm(*c.ahat(), x, out=y0.copy(), accumulate=True)
+    np.testing.assert_array_equal(Y.cpu().numpy(), ref)
+    Z = spmm(A, X, nt_store=True)
+    np.testing.assert_array_equal(Z.cpu().numpy(), oracle_mod.spmm(*c.ahat(), x))
+
+
+def test_strided_panels_and_row_blocks(oracle_mod):
+    """Leading dimensions > d and a row block with rebased indptr (the multi-GPU layout)."""
+    from srgnn.spmm import spmm
+    c = G.Case("rand_d128_r05")
+    A = _csr(c, None)
+    x = c.x()
+    big = torch.zeros((c.n, 160), device="cuda")
+    big[:, :128] = torch.from_numpy(x).cuda()
+    out = torch.full((c.n, 136), 7.0, device="cuda")
+    spmm(A, big[:, :128], out=out[:, :128])
+    want = oracle_mod.spmm(*c.ahat(), x)
+    np.testing.assert_array_equal(out[:, :128].cpu().numpy(), want)
+    assert bool((out[:, 128:] == 7.0).all())
+    blk = A.rows(50, 140)
+    yb = spmm(blk, torch.from_numpy(x).cuda())
+    np.testing.assert_array_equal(yb.cpu().numpy(), want[50:140])
+
+
+def test_edge_cases_empty_and_special_values(oracle_mod):
+    from srgnn.csr import DeviceCSR
+    from srgnn.spmm import spmm
+    # all-empty matrix
+    A = DeviceCSR.from_tensors(np.zeros(6, np.int64), np.zeros(0, np.int32), np.zeros(0, np.float32),
+                               n_cols=5, device="cuda")
+    y = spmm(A, torch.ones((5, 64), device="cuda"))
+    assert bool((y == 0).all())
+    # -0.0, inf and nan propagate exactly as the fma chain does
+    ip = np.array([0, 2, 3, 5], np.int64)
+    ix = np.array([0, 1, 2, 0, 2], np.int32)
+    v = np.array([1.0, -1.0, 2.0, -0.0, 1.0], np.float32)
+    x = np.zeros((3, 128), np.float32)
+    x[0, 0], x[1, 0], x[2, 1], x[2, 2] = -0.0, 0.0, np.inf, np.nan
+    x[0, 3] = -0.0
+    A = DeviceCSR.from_tensors(ip, ix, v, n_cols=3, device="cuda")
+    got = spmm(A, torch.from_numpy(x).cuda()).cpu().numpy()
+    want = oracle_mod.spmm(ip, ix, v, x)
+    np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+def test_validate_rejects_bad_ids():
+    from srgnn import SrgError
+    from srgnn.csr import DeviceCSR
+    with pytest.raises(SrgError):
+        DeviceCSR.from_tensors(np.array([0, 2], np.int64), np.array([0, 9], np.int32),
+                               np.ones(2, np.float32), n_cols=3, device="cuda")
+    with pytest.raises(SrgError):
+        DeviceCSR.from_tensors(np.array([0, 3, 2], np.int64), np.array([0, 1, 2], np.int32),
+                               np.ones(3, np.float32), n_cols=3, device="cuda")
+
+
+@pytest.mark.parametrize("d", [1, 4, 36, 64, 96, 128, 200, 256, 512])
+def test_rmat_many_widths_bit_exact(oracle_mod, d):
+    """Power-law R-MAT graph (hubs, empty rows) at assorted widths, both wave roles."""
+    from srgnn import synth
+    from srgnn.csr import DeviceCSR
+    from srgnn.spmm import spmm
+    n = 6000
+    u, v = synth.rmat_undirected_t(n, 40000, seed=3)
+    ip, ix = synth.symmetric_csr_t(n, u, v)
+    vals = synth.uniform_features_np(1, int(ix.numel()), seed=99)[0] * 0.5 + 0.5
+    x = synth.uniform_features_np(n, d, seed=4)
+    want = oracle_mod.spmm(ip.numpy(), ix.numpy(), vals, x)
+    for thr in (-1, 0, 16):
+        A = DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, heavy_threshold=thr, device="cuda")
+        got = spmm(A, torch.from_numpy(x).cuda()).cpu().numpy()
+        np.testing.assert_array_equal(got, want, err_msg=f"d={d} thr={thr}")
