@@ -31,7 +31,7 @@ from .csr import make_schedule
 def laplacian_from_adj(adj: sp.spmatrix) -> sp.csr_matrix:
     """L = D - W of nx.Graph(adj): undirected, one weight per node pair (the entry stored last in
     row-major order wins, as networkx overwrites edge data), self-loops kept.  Every diagonal
-    entry is stored explicitly (also for isolated nodes)."""
+    entry is stored explicitly (also for isolated nodes), so L - a2*I keeps L's structure."""
     coo = sp.coo_matrix(adj)
     n = coo.shape[0]
     order = np.lexsort((coo.col, coo.row))          # row-major
@@ -48,18 +48,7 @@ def laplacian_from_adj(adj: sp.spmatrix) -> sp.csr_matrix:
     vals = np.r_[v, v[off]]
     W = sp.csr_matrix((vals, (rows, cols)), shape=(n, n))
     deg = np.asarray(W.sum(axis=1)).ravel()
-    L = (sp.diags(deg) - W).tocsr()
-    # make every diagonal slot explicit
-    L = L + sp.csr_matrix((np.zeros(n), (np.arange(n), np.arange(n))), shape=(n, n))
-    L.sum_duplicates()
-    L.sort_indices()
-    missing = np.diff(L.indptr) == 0
-    if missing.any() or L.nnz < n:
-        Lc = L.tocoo()
-        L = sp.csr_matrix((np.r_[Lc.data, np.zeros(n)],
-                           (np.r_[Lc.row, np.arange(n)], np.r_[Lc.col, np.arange(n)])), shape=(n, n))
-        L.sum_duplicates()
-    return L
+    return _explicit_diagonal((sp.diags(deg) - W).tocsr())
 
 
 def _explicit_diagonal(L: sp.csr_matrix) -> sp.csr_matrix:
@@ -85,13 +74,14 @@ def _explicit_diagonal(L: sp.csr_matrix) -> sp.csr_matrix:
 
 def estimate_lmax(L: sp.spmatrix) -> float:
     """pygsp Graph.estimate_lmax: largest eigenvalue by ARPACK (tol 5e-3, ncv <= 10) times 1.01,
-    with a fixed all-ones start vector instead of ARPACK's random one."""
+    with a fixed start vector (a ramp; the constant vector is L's null space) instead of ARPACK's
+    random one."""
     n = L.shape[0]
     if n <= 2:
         return float(np.linalg.eigvalsh(L.toarray()).max()) * 1.01
     from scipy.sparse.linalg import eigsh
     lam = eigsh(L.asfptype() if hasattr(L, "asfptype") else L.astype(np.float64), k=1, tol=5e-3,
-                ncv=min(n, 10), v0=np.ones(n), return_eigenvectors=False)
+                ncv=min(n, 10), v0=np.linspace(1.0, 2.0, n), return_eigenvectors=False)
     return float(lam[0]) * 1.01
 
 
@@ -128,11 +118,10 @@ class HeatWaveletFilter:
         rows = np.repeat(np.arange(self.n), np.diff(L.indptr))
         lvals = L.data.astype(np.float64)
         fvals = (2.0 / self.a1) * np.where(L.indices == rows, lvals - self.a2, lvals)   # (2/a1)(L - a2 I)
-        tdt = dtype
         self.indptr = torch.from_numpy(L.indptr.astype(np.int64)).to(self.device)
         self.indices = torch.from_numpy(L.indices.astype(np.int32)).to(self.device)
-        self.lvals = torch.from_numpy(lvals).to(self.device, tdt)
-        self.fvals = torch.from_numpy(fvals).to(self.device, tdt)
+        self.lvals = torch.from_numpy(lvals).to(self.device, dtype)
+        self.fvals = torch.from_numpy(fvals).to(self.device, dtype)
         self.order, _ = make_schedule(self.indptr, -1)
 
     def apply(self, S: torch.Tensor) -> torch.Tensor:
@@ -143,12 +132,10 @@ class HeatWaveletFilter:
         n, d = S.shape
         ns, nc = self.coeffs.shape
         R = torch.empty((ns, n, d), dtype=self.dtype, device=S.device)
-        bufs = [torch.empty_like(S) for _ in range(2)]
         f64 = self.dtype == torch.float64
         ct = ctypes.c_double if f64 else ctypes.c_float
         fn = _lib.lib().srg_cheby_step_f64 if f64 else _lib.lib().srg_cheby_step_f32
         stream = torch.cuda.current_stream(S.device).cuda_stream
-        L = _lib.lib()  # noqa: F841  (keeps the library loaded)
 
         def launch(vals, Tc, To, Tn, mode, coef_prev, coef):
             cp = (ct * ns)(*coef_prev) if coef_prev is not None else None
@@ -158,12 +145,16 @@ class HeatWaveletFilter:
                     Tn.data_ptr(), d, d, mode, self.a1, self.a2, cp, cc, ns, R.data_ptr(), n * d, stream)
             _lib.check(rc, fn.__name__)
 
-        t_old, t_cur = S, bufs[0]
+        # T_{k-1}, T_k and the free panel rotate through three buffers (S itself is never written)
+        t_old, t_cur = S, torch.empty_like(S)
+        free = [torch.empty_like(S)] if nc > 2 else []
         launch(self.lvals, S, None, t_cur, _lib.SRG_CHEBY_INIT, self.coeffs[:, 0], self.coeffs[:, 1])
-        spare = bufs[1]
         for k in range(2, nc):
-            launch(self.fvals, t_cur, t_old, spare, _lib.SRG_CHEBY_STEP, None, self.coeffs[:, k])
-            t_old, t_cur, spare = t_cur, spare, (t_old if t_old is not S else torch.empty_like(S))
+            t_new = free.pop() if free else torch.empty_like(S)
+            launch(self.fvals, t_cur, t_old, t_new, _lib.SRG_CHEBY_STEP, None, self.coeffs[:, k])
+            if t_old is not S:
+                free.append(t_old)
+            t_old, t_cur = t_cur, t_new
         return R
 
 
@@ -189,7 +180,16 @@ def wavelet_basis(adj: sp.spmatrix, scale: float = 0.5, order: int = 3, toleranc
     out = []
     for s in range(2):
         phi = sp.hstack(blocks[s]).tocsr()
-        rs = np.asarray(abs(phi).sum(axis=1)).ravel()
-        rs[rs == 0] = 1.0
-        out.append(sp.diags((1.0 / rs).astype(np.float32)) @ phi)
-    return out[0].tocsr(), out[1].tocsr(), filt.lmax
+        out.append(l1_normalize_rows(phi))
+    return out[0], out[1], filt.lmax
+
+
+def l1_normalize_rows(phi: sp.csr_matrix) -> sp.csr_matrix:
+    """sklearn.preprocessing.normalize(phi, norm='l1', axis=1) (base_model.py:287-290): each row
+    divided by the sum of its absolute values; all-zero rows left as they are."""
+    phi = sp.csr_matrix(phi, copy=True)
+    rs = np.add.reduceat(np.abs(phi.data).astype(np.float64), phi.indptr[:-1]) if phi.nnz else np.zeros(0)
+    rs = np.where(np.diff(phi.indptr) > 0, rs if rs.size == phi.shape[0] else 0.0, 1.0)
+    rs[rs == 0] = 1.0
+    phi.data = (phi.data / np.repeat(rs, np.diff(phi.indptr)).astype(phi.dtype)).astype(phi.dtype)
+    return phi

@@ -1,0 +1,75 @@
+"""Wavelet basis restatement (parity UNPINNED: pygsp is absent from the reference tree and this
+image).  The oracle's Chebyshev recurrence is validated against a dense eigendecomposition, and the
+product's host-side helpers (Laplacian, coefficients) against the oracle's independent versions."""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from srgnn import wavelet as W
+
+
+def small_graph(n=40, seed=0, weighted=False):
+    rng = np.random.default_rng(seed)
+    m = rng.random((n, n)) < 0.12
+    m = np.triu(m, 1)
+    w = rng.integers(1, 5, size=(n, n)).astype(float) if weighted else np.ones((n, n))
+    a = np.where(m, w, 0.0)
+    a = a + a.T
+    a[3, :] = a[:, 3] = 0.0                        # an isolated node
+    return sp.csr_matrix(a)
+
+
+def dense_cheby(Ld, coeffs, S, lmax):
+    lam, U = np.linalg.eigh(Ld)
+    a1 = a2 = lmax / 2
+    x = (lam - a2) / a1
+    T = [np.ones_like(x), x]
+    for _ in range(2, coeffs.shape[1]):
+        T.append(2 * x * T[-1] - T[-2])
+    out = []
+    for c in coeffs:
+        p = 0.5 * c[0] * T[0] + sum(c[k] * T[k] for k in range(1, len(c)))
+        out.append(U @ (p[:, None] * (U.T @ S)))
+    return np.stack(out), lam, U
+
+
+@pytest.mark.parametrize("weighted", [False, True])
+def test_oracle_cheby_equals_dense_polynomial(oracle_mod, weighted):
+    a = small_graph(weighted=weighted)
+    n = a.shape[0]
+    L = oracle_mod.laplacian(a.indptr, a.indices, a.data, n)
+    Ld = sp.csr_matrix((L[2], L[1], L[0]), shape=(n, n)).toarray()
+    lmax = float(np.linalg.eigvalsh(Ld).max()) * 1.01
+    coeffs = np.stack([oracle_mod.cheby_coeffs(t, lmax, 3) for t in (-0.5, 0.5)])
+    S = np.random.default_rng(1).standard_normal((n, 5))
+    R = oracle_mod.cheby_op(L, coeffs, S, lmax)
+    want, lam, U = dense_cheby(Ld, coeffs, S, lmax)
+    np.testing.assert_allclose(R, want, rtol=1e-10, atol=1e-10)
+    # and order 3 already approximates the heat kernel itself (loose: approximation error)
+    heat = U @ (np.exp(-0.5 * lam / lmax)[:, None] * (U.T @ S))
+    assert np.abs(R[1] - heat).max() < 5e-2 * np.abs(heat).max()
+
+
+def test_laplacian_and_coefficients_match_oracle(oracle_mod):
+    a = small_graph(weighted=True)
+    # store a conflicting upper/lower pair: nx.Graph keeps the last stored (lower-triangle) weight
+    a = a.tolil()
+    a[5, 9], a[9, 5] = 2.0, 7.0
+    a = a.tocsr()
+    n = a.shape[0]
+    L_prod = W._explicit_diagonal(W.laplacian_from_adj(a))
+    ip, ix, v = oracle_mod.laplacian(a.indptr, a.indices, a.data, n)
+    np.testing.assert_array_equal(L_prod.indptr, ip)
+    np.testing.assert_array_equal(L_prod.indices, ix)
+    np.testing.assert_array_equal(L_prod.data, v)
+    assert L_prod[5, 9] == -7.0 and L_prod[9, 5] == -7.0
+    for tau in (-0.5, 0.5, 2.0):
+        np.testing.assert_array_equal(W.heat_cheby_coeffs(tau, 3.7, 3), oracle_mod.cheby_coeffs(tau, 3.7, 3))
+
+
+def test_estimate_lmax_upper_bounds_spectrum():
+    a = small_graph()
+    L = W.laplacian_from_adj(a)
+    lmax = W.estimate_lmax(L)
+    true = np.linalg.eigvalsh(L.toarray()).max()
+    assert true <= lmax <= true * 1.03

@@ -1,0 +1,82 @@
+"""Wavelet basis on the GPU (fused Chebyshev launches) vs the CPU oracle.
+
+fp64: the kernel follows the oracle's operation order (sequential CSR chains of separate multiply
+and add, uncontracted epilogue), so results are compared BIT FOR BIT.  fp32: normwise relative
+error <= 1e-5 against the fp64 oracle.  (Parity with pygsp itself is unpinned; see
+tests/test_wavelet_cpu.py for the oracle's validation against a dense eigendecomposition.)"""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def graphs():
+    from srgnn import synth
+    rng = np.random.default_rng(0)
+    m = np.triu(rng.random((60, 60)) < 0.1, 1)
+    a = sp.csr_matrix((m + m.T).astype(float))
+    n = 3000
+    u, v = synth.rmat_undirected_t(n, 15000, seed=8)
+    ip, ix = synth.symmetric_csr_t(n, u, v)
+    b = sp.csr_matrix((np.ones(ix.numel()), ix.numpy(), ip.numpy()), shape=(n, n))
+    return {"small": a, "rmat3000": b}
+
+
+@pytest.mark.parametrize("gname", ["small", "rmat3000"])
+@pytest.mark.parametrize("d", [5, 64, 128])
+def test_heat_filter_f64_bit_exact(oracle_mod, gname, d):
+    from srgnn import wavelet as W
+    a = graphs()[gname]
+    L = W.laplacian_from_adj(a)
+    n = a.shape[0]
+    f = W.HeatWaveletFilter(L, [-0.5, 0.5], order=3, lmax=None, device="cuda")
+    S = np.random.default_rng(d).standard_normal((n, d))
+    R = f.apply(torch.from_numpy(S).cuda()).cpu().numpy()
+    want = oracle_mod.cheby_op((L.indptr, L.indices, L.data), f.coeffs, S, f.lmax)
+    np.testing.assert_array_equal(R, want)
+
+
+@pytest.mark.parametrize("order", [1, 2, 5])
+def test_heat_filter_orders(oracle_mod, order):
+    from srgnn import wavelet as W
+    a = graphs()["rmat3000"]
+    L = W.laplacian_from_adj(a)
+    f = W.HeatWaveletFilter(L, [-1.0, 0.3, 2.0], order=order, lmax=7.5, device="cuda")
+    S = np.random.default_rng(1).standard_normal((a.shape[0], 16))
+    R = f.apply(torch.from_numpy(S).cuda()).cpu().numpy()
+    want = oracle_mod.cheby_op((L.indptr, L.indices, L.data), f.coeffs, S, 7.5)
+    np.testing.assert_array_equal(R, want)
+
+
+def test_heat_filter_f32_within_tolerance(oracle_mod):
+    from srgnn import wavelet as W
+    a = graphs()["rmat3000"]
+    L = W.laplacian_from_adj(a)
+    f = W.HeatWaveletFilter(L, [-0.5, 0.5], order=3, lmax=None, dtype=torch.float32, device="cuda")
+    S = np.random.default_rng(3).standard_normal((a.shape[0], 256)).astype(np.float32)
+    R = f.apply(torch.from_numpy(S).cuda()).cpu().numpy().astype(np.float64)
+    want = oracle_mod.cheby_op((L.indptr, L.indices, L.data), f.coeffs, S.astype(np.float64), f.lmax)
+    rel = np.linalg.norm(R - want) / np.linalg.norm(want)
+    assert rel <= 1e-5, rel
+
+
+def test_wavelet_basis_matches_oracle_restatement(oracle_mod):
+    """phi / phi^-1 as SpectralModel.calculate_wavelet + normalize_matrices build them."""
+    from srgnn import wavelet as W
+    a = graphs()["small"]
+    n = a.shape[0]
+    phi, phi_inv, lmax = W.wavelet_basis(a, scale=0.5, order=3, tolerance=1e-4, batch=25, device="cuda")
+    L = W.laplacian_from_adj(a)
+    coeffs = np.stack([oracle_mod.cheby_coeffs(t, lmax, 3) for t in (-0.5, 0.5)])
+    R = oracle_mod.cheby_op((L.indptr, L.indices, L.data), coeffs, np.eye(n), lmax)
+    for s, got in enumerate((phi, phi_inv)):
+        m = R[s].copy()
+        m[m < 1e-4] = 0
+        m = m.astype(np.float32)
+        rs = np.abs(m).sum(axis=1, dtype=np.float64)
+        rs[rs == 0] = 1
+        want = m / rs[:, None]
+        np.testing.assert_allclose(got.toarray(), want, rtol=1e-6, atol=1e-7)
+        assert got.dtype == np.float32

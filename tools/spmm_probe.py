@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""Workload for rocprofv3 counter runs: R single-hop SpMM launches on a benchmark graph.
+
+  --identity   calibration: Â = I on an [N, d] panel larger than the Infinity Cache, so every
+               launch reads exactly N*4d bytes of X (+ index arrays) and writes N*4d bytes of Y
+               with the SAME kernel and access widths as the real hop -> FETCH_SIZE / WRITE_SIZE
+               scale factors for this access pattern (MI355X_MICROARCH.md: FETCH_SIZE under-counts
+               wide reads on gfx950; calibrate on a known byte count).
+Prints one JSON line with the launch geometry and algorithmic bytes.
+"""
+import argparse
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(HERE, "scalable-roubust-gnn_amd"))
+
+import torch  # noqa: E402
+
+from srgnn import graphs, roofline, synth  # noqa: E402
+from srgnn.csr import DeviceCSR  # noqa: E402
+from srgnn.spmm import spmm  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--config", default="products")
+ap.add_argument("--reps", type=int, default=3)
+ap.add_argument("--identity", action="store_true")
+ap.add_argument("--heavy-threshold", type=int, default=None)
+a = ap.parse_args()
+dev = torch.device("cuda", 0)
+if a.identity:
+    n, d = 4 * 1024 * 1024, 128          # 2 GiB panel (> 256 MiB Infinity Cache)
+    ip = torch.arange(n + 1, dtype=torch.int64, device=dev)
+    ix = torch.arange(n, dtype=torch.int32, device=dev)
+    vals = torch.ones(n, dtype=torch.float32, device=dev)
+else:
+    ip, ix, vals, n, d, _ = graphs.build(a.config, dev)
+A = DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, heavy_threshold=a.heavy_threshold, device=dev)
+X = synth.uniform_features_t(n, d, device=dev)
+Y = torch.empty_like(X)
+torch.cuda.synchronize()
+for _ in range(a.reps):
+    spmm(A, X, out=Y)
+torch.cuda.synchronize()
+nnz = A.nnz
+print(json.dumps({"config": "identity" if a.identity else a.config, "n": n, "nnz": nnz, "d": d,
+                  "reps": a.reps, "n_heavy": A.n_heavy,
+                  "algorithmic_bytes": roofline.bytes_no_reuse(n, nnz, d),
+                  "compulsory_bytes": roofline.bytes_compulsory(n, nnz, d),
+                  "x_read_bytes": n * 4 * d, "y_write_bytes": n * 4 * d,
+                  "index_bytes": nnz * 8 + (n + 1) * 8}))

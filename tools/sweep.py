@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""In-process A/B of SpMM schedule variants on one graph (interleaved rounds, cdna guide rule 24).
+Prints per-variant median / min kernel ms and the implied no-reuse roofline fraction."""
+import argparse
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(HERE, "scalable-roubust-gnn_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from srgnn import graphs, roofline, synth  # noqa: E402
+from srgnn.csr import DeviceCSR  # noqa: E402
+from srgnn.spmm import spmm  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--config", default="products")
+ap.add_argument("--thresholds", default="-1,32,64,128,256,512,2048,100000000")
+ap.add_argument("--rounds", type=int, default=5)
+ap.add_argument("--nt", action="store_true")
+a = ap.parse_args()
+dev = torch.device("cuda", 0)
+ip, ix, vals, n, d, _ = graphs.build(a.config, dev)
+X = synth.uniform_features_t(n, d, device=dev)
+Y = torch.empty_like(X)
+variants = {}
+for t in [int(s) for s in a.thresholds.split(",")]:
+    variants[f"thr={t}"] = (DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, heavy_threshold=t, device=dev), False)
+    if a.nt:
+        variants[f"thr={t},nt"] = (variants[f"thr={t}"][0], True)
+ref = None
+times = {k: [] for k in variants}
+for r in range(a.rounds):
+    for k, (A, nt) in variants.items():
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        spmm(A, X, out=Y, nt_store=nt)
+        e.record()
+        torch.cuda.synchronize()
+        times[k].append(s.elapsed_time(e))
+        if r == 0:
+            if ref is None:
+                ref = Y.clone()
+            else:
+                assert torch.equal(ref, Y), f"{k} changed the result"
+b = roofline.bytes_no_reuse(n, ix.numel(), d)
+out = {}
+for k, v in times.items():
+    med = float(np.median(v[1:] if len(v) > 1 else v))
+    out[k] = {"median_ms": med, "min_ms": float(min(v)), "n_heavy": variants[k][0].n_heavy,
+              "frac": b / (med * 1e-3) / 1e9 / roofline.MI355X_HBM_PEAK_GBS}
+print(json.dumps({"config": a.config, "n": n, "nnz": int(ix.numel()), "d": d, "variants": out}, indent=1))
