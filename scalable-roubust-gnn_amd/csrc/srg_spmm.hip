@@ -198,10 +198,11 @@ __device__ __forceinline__ void row_gather(typename Vec<T, VEC>::type& acc,
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 T a;
-                if constexpr (sizeof(T) == 8) {
-                    const long long bits = __builtin_amdgcn_readlane(
-                        (long long)__builtin_bit_cast(long long, a_blk), s0 + u);
-                    a = __builtin_bit_cast(T, bits);
+                if constexpr (sizeof(T) == 8) {   // v_readlane is 32-bit: broadcast both halves
+                    const unsigned long long bits = __builtin_bit_cast(unsigned long long, a_blk);
+                    const unsigned lo = __builtin_amdgcn_readlane((unsigned)bits, s0 + u);
+                    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(bits >> 32), s0 + u);
+                    a = __builtin_bit_cast(T, ((unsigned long long)hi << 32) | lo);
                 } else {
                     a = __builtin_bit_cast(T, __builtin_amdgcn_readlane(__builtin_bit_cast(int, a_blk), s0 + u));
                 }

@@ -23,7 +23,7 @@ import torch
 
 from . import _lib
 
-DEFAULT_HEAVY_THRESHOLD = int(os.environ.get("SRGNN_HEAVY_THRESHOLD", "128"))
+DEFAULT_HEAVY_THRESHOLD = int(os.environ.get("SRGNN_HEAVY_THRESHOLD", "32"))
 
 
 def _dev(device):

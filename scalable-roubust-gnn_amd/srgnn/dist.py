@@ -45,10 +45,13 @@ class RowPartitionedOperator:
     exchange logic with gloo."""
 
     def __init__(self, indptr, indices, values, n: int, group=None, local_spmm=None,
-                 heavy_threshold=None, device=None):
+                 heavy_threshold=None, device=None, rank=None, world=None):
         self.group = group
-        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
-        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        # rank / world may be given explicitly to build one share without a process group
+        # (simulate_propagate: P virtual ranks in one process, e.g. on a single GPU)
+        self.virtual = rank is not None
+        self.rank = rank if rank is not None else (dist.get_rank(group) if dist.is_initialized() else 0)
+        self.world = world if world is not None else (dist.get_world_size(group) if dist.is_initialized() else 1)
         self.n = n
         self.starts = balanced_row_starts(indptr, self.world)
         self.max_rows = max(self.starts[p + 1] - self.starts[p] for p in range(self.world))
@@ -81,6 +84,8 @@ class RowPartitionedOperator:
             self._full = torch.empty((self.world * self.max_rows, d), dtype=block.dtype, device=block.device)
         if self.world == 1:
             self._full.copy_(block)
+        elif self.virtual:
+            raise RuntimeError("virtual shares exchange through simulate_propagate()")
         elif dist.get_backend(self.group) == "nccl":
             dist.all_gather_into_tensor(self._full, block, group=self.group)
         else:
@@ -102,3 +107,24 @@ class RowPartitionedOperator:
             full = self._gather(panels[k - 1])
             self._spmm(self.A, full, panels[k][: self.rows])
         return panels
+
+
+def simulate_propagate(indptr, indices, values, n: int, x: torch.Tensor, K: int, world: int,
+                       heavy_threshold=None, device=None):
+    """P virtual ranks in ONE process: every share computes its rows of each hop from the padded
+    full panel assembled exactly as all_gather_into_tensor would lay it out.  Returns the K+1 full
+    [n, d] panels.  Exercises partition, column remap and padded layout on one device."""
+    shares = [RowPartitionedOperator(indptr, indices, values, n, heavy_threshold=heavy_threshold,
+                                     device=device, rank=p, world=world) for p in range(world)]
+    d = x.shape[1]
+    mr = shares[0].max_rows
+    panels = [[s.new_panel(d) for _ in range(K + 1)] for s in shares]
+    for s, pp in zip(shares, panels):
+        pp[0][: s.rows].copy_(x[s.r0:s.r1])
+    full = torch.empty((world * mr, d), dtype=torch.float32, device=panels[0][0].device)
+    for k in range(1, K + 1):
+        for p in range(world):
+            full[p * mr:(p + 1) * mr].copy_(panels[p][k - 1])
+        for s, pp in zip(shares, panels):
+            s._spmm(s.A, full, pp[k][: s.rows])
+    return [torch.cat([pp[k][: s.rows] for s, pp in zip(shares, panels)]) for k in range(K + 1)]

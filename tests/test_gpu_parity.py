@@ -204,3 +204,58 @@ def test_rmat_many_widths_bit_exact(oracle_mod, d):
         A = DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, heavy_threshold=thr, device="cuda")
         got = spmm(A, torch.from_numpy(x).cuda()).cpu().numpy()
         np.testing.assert_array_equal(got, want, err_msg=f"d={d} thr={thr}")
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_row_partitioned_virtual_ranks_bitwise(world):
+    """The multi-GPU layout (nnz-balanced row blocks, remapped ids, padded gathered panel) on one
+    device: bitwise equal to the single-device propagation."""
+    from srgnn import synth
+    from srgnn.csr import DeviceCSR
+    from srgnn.dist import simulate_propagate
+    from srgnn.normalize import sym_norm_binary
+    from srgnn.spmm import propagate
+    n = 20000
+    u, v = synth.rmat_undirected_t(n, 150000, seed=21, device="cuda")
+    ip, ix = synth.symmetric_csr_t(n, u, v)
+    ip, ix, vals = sym_norm_binary(ip, ix, n, 0.5)
+    x = synth.uniform_features_t(n, 128, device="cuda")
+    want = propagate(DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, device="cuda"), x, 3)
+    got = simulate_propagate(ip, ix, vals, n, x, 3, world, device="cuda")
+    for k in range(1, 4):
+        assert torch.equal(got[k], want[k]), f"hop {k} differs with {world} virtual ranks"
+
+
+def test_products_scale_sampled_rows_bit_exact(oracle_mod):
+    """Full products-shaped graph (126 M nonzeros): each hop checked bit for bit on 3000 sampled
+    rows (plus every heavy row's first slice owner) against the oracle fed with the GPU's previous
+    hop -- a size-independent check of every launch."""
+    from srgnn import graphs, synth
+    from srgnn.csr import DeviceCSR
+    from srgnn.spmm import propagate
+    ip, ix, vals, n, d, _ = graphs.build("products", "cuda")
+    A = DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, device="cuda")
+    x = synth.uniform_features_t(n, d, device="cuda")
+    hops = propagate(A, x, 2)
+    ipn, ixn, vn = ip.cpu().numpy(), ix.cpu().numpy(), vals.cpu().numpy()
+    deg = np.diff(ipn)
+    rng = np.random.default_rng(5)
+    rows = np.unique(np.r_[rng.choice(n, 3000, replace=False), np.argsort(-deg)[:50]])
+    sub_ptr = np.r_[0, np.cumsum(deg[rows])]
+    sub_ix = np.concatenate([ixn[ipn[r]:ipn[r + 1]] for r in rows])
+    sub_v = np.concatenate([vn[ipn[r]:ipn[r + 1]] for r in rows])
+    for k in (1, 2):
+        prev = hops[k - 1].cpu().numpy()
+        want = oracle_mod.spmm(sub_ptr, sub_ix, sub_v, prev)
+        got = hops[k][torch.from_numpy(rows).cuda()].cpu().numpy()
+        np.testing.assert_array_equal(got, want, err_msg=f"hop {k}")
+    # size-independent property: Â is symmetric-normalised with r = 0.5 -> Â 1-vector scaled by
+    # D^(1/2) is an eigenvector with eigenvalue 1: Â (D^(1/2) 1) = D^(1/2) 1 (up to rounding)
+    # every term is positive, so the sequential fp32 chain of row i is within (deg_i + 8) * 2^-24
+    # relative of the exact value (deg_i roundings of the sum, ~3 per term, 1 for the reference)
+    dh = torch.from_numpy(np.sqrt(deg.astype(np.float64)).astype(np.float32)).cuda()
+    y = propagate(A, dh.view(-1, 1).expand(n, 4).contiguous(), 1)[1]
+    rel = ((y[:, 0].double() - dh.double()).abs() / dh.double())
+    bound = (torch.from_numpy(deg).cuda().double() + 8) * 2.0 ** -24
+    assert bool((rel <= bound).all()), float((rel / bound).max())
+    assert bool((y[:, 1:] == y[:, :1]).all())

@@ -1,12 +1,14 @@
 #!/usr/bin/env python3
-"""Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of tools/spmm_probe.py into per-launch
-HBM traffic of the SpMM kernel, calibrated on the identity-operator run.
+"""Per-launch HBM traffic of the SpMM kernel from rocprofv3 --pmc runs of tools/spmm_probe.py.
 
-    python tools/pmc_traffic.py --fetch DIR --write DIR --cal-fetch DIR --cal-write DIR \
-        --probe probe.json --cal-probe cal.json --out profiles/pmc_products.json
+    python tools/pmc_traffic.py --fetch DIR --write DIR [--hits DIR] --probe probe.json --out OUT.json
 
-Calibration: the identity run moves a known byte count (x_read + index reads, y_write) with the
-same kernel; scale = known / counted.  traffic = fetch * scale_r + write * scale_w (bytes/launch).
+traffic = 2 * FETCH_SIZE + WRITE_SIZE  (MI355X_MICROARCH.md, HBM: on gfx950 FETCH_SIZE reports
+exactly half the bytes of wide coalesced reads -- our gathers are whole 512-byte rows read 8 or 16
+bytes per lane; WRITE_SIZE is exact for wide stores).  Cross-check: TCC_MISS_sum * 128 B (L2
+misses, 128-byte lines), recorded beside it when a TCC_HIT/TCC_MISS run is given.  FETCH_SIZE
+counts every L2 miss served by the fabric, so Infinity-Cache hits are included (an upper bound on
+DRAM bytes).
 """
 import argparse
 import csv
@@ -15,7 +17,7 @@ import json
 import os
 
 
-def per_launch(d, counter, kernel_sub="k_spmm"):
+def per_launch(d, counters, kernel_sub="k_spmm"):
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     vals = {}
     for f in files:
@@ -23,45 +25,47 @@ def per_launch(d, counter, kernel_sub="k_spmm"):
             for row in csv.DictReader(fh):
                 if kernel_sub not in row.get("Kernel_Name", ""):
                     continue
-                if row.get("Counter_Name") != counter:
+                name = row.get("Counter_Name")
+                if name not in counters:
                     continue
-                key = (f, row.get("Dispatch_Id"))
+                key = (name, f, row.get("Dispatch_Id"))
                 vals[key] = vals.get(key, 0.0) + float(row["Counter_Value"])
-    if not vals:
-        raise SystemExit(f"no {counter} rows for {kernel_sub} under {d}")
-    v = sorted(vals.values())
-    return v[len(v) // 2] * 1024.0, len(v)        # FETCH_SIZE / WRITE_SIZE are in KiB
+    out = {}
+    for c in counters:
+        v = sorted(x for (n, _, _), x in vals.items() if n == c)
+        if not v:
+            raise SystemExit(f"no {c} rows for {kernel_sub} under {d}")
+        out[c] = (v[len(v) // 2], len(v))
+    return out
 
 
 def main():
     ap = argparse.ArgumentParser()
-    for k in ("fetch", "write", "cal_fetch", "cal_write", "probe", "cal_probe", "out"):
-        ap.add_argument("--" + k.replace("_", "-"), required=True)
+    ap.add_argument("--fetch", required=True)
+    ap.add_argument("--write", required=True)
+    ap.add_argument("--hits")
+    ap.add_argument("--probe", required=True)
+    ap.add_argument("--out", required=True)
     a = ap.parse_args()
     probe = json.load(open(a.probe))
-    cal = json.load(open(a.cal_probe))
-    f_raw, nf = per_launch(a.fetch, "FETCH_SIZE")
-    w_raw, nw = per_launch(a.write, "WRITE_SIZE")
-    cf_raw, _ = per_launch(a.cal_fetch, "FETCH_SIZE")
-    cw_raw, _ = per_launch(a.cal_write, "WRITE_SIZE")
-    known_r = cal["x_read_bytes"] + cal["index_bytes"]
-    known_w = cal["y_write_bytes"]
-    sr, sw = known_r / cf_raw, known_w / cw_raw
-    rec = {
-        "config": probe["config"], "kernel": "k_spmm (one hop)",
-        "fetch_size_raw_bytes": f_raw, "write_size_raw_bytes": w_raw, "launches": [nf, nw],
-        "calibration": {"identity_n": cal["n"], "d": cal["d"], "known_read": known_r, "known_write": known_w,
-                        "fetch_counted": cf_raw, "write_counted": cw_raw,
-                        "read_scale": sr, "write_scale": sw},
-        "hbm_read_bytes_per_launch": f_raw * sr, "hbm_write_bytes_per_launch": w_raw * sw,
-        "hbm_bytes_per_launch": f_raw * sr + w_raw * sw,
-        "algorithmic_bytes_per_launch": probe["algorithmic_bytes"],
-        "compulsory_bytes_per_launch": probe["compulsory_bytes"],
-    }
-    rec["traffic_over_compulsory"] = rec["hbm_bytes_per_launch"] / probe["compulsory_bytes"]
+    f = per_launch(a.fetch, ["FETCH_SIZE"])["FETCH_SIZE"]
+    w = per_launch(a.write, ["WRITE_SIZE"])["WRITE_SIZE"]
+    rec = {"config": probe["config"], "kernel": "k_spmm (one hop)", "n_heavy": probe.get("n_heavy"),
+           "launches": f[1],
+           "fetch_size_kib": f[0], "write_size_kib": w[0],
+           "hbm_read_bytes_per_launch": 2.0 * f[0] * 1024, "hbm_write_bytes_per_launch": w[0] * 1024}
+    rec["hbm_bytes_per_launch"] = rec["hbm_read_bytes_per_launch"] + rec["hbm_write_bytes_per_launch"]
+    if a.hits:
+        h = per_launch(a.hits, ["TCC_HIT_sum", "TCC_MISS_sum"])
+        hit, miss = h["TCC_HIT_sum"][0], h["TCC_MISS_sum"][0]
+        rec["l2_hit_rate"] = hit / (hit + miss)
+        rec["l2_miss_bytes_per_launch"] = miss * 128.0
+    rec["algorithmic_bytes_per_launch"] = probe["algorithmic_bytes"]
+    rec["compulsory_bytes_per_launch"] = probe["compulsory_bytes"]
     rec["traffic_over_algorithmic"] = rec["hbm_bytes_per_launch"] / probe["algorithmic_bytes"]
-    with open(a.out, "w") as f:
-        json.dump(rec, f, indent=1)
+    rec["traffic_over_compulsory"] = rec["hbm_bytes_per_launch"] / probe["compulsory_bytes"]
+    with open(a.out, "w") as fh:
+        json.dump(rec, fh, indent=1)
     print(json.dumps(rec, indent=1))
 
 

@@ -21,9 +21,11 @@ ap.add_argument("--config", default="products")
 ap.add_argument("--thresholds", default="-1,32,64,128,256,512,2048,100000000")
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--nt", action="store_true")
+ap.add_argument("--n", type=int, default=None)
+ap.add_argument("--n-edges", type=int, default=None)
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
-ip, ix, vals, n, d, _ = graphs.build(a.config, dev)
+ip, ix, vals, n, d, _ = graphs.build(a.config, dev, n=a.n, n_edges=a.n_edges)
 X = synth.uniform_features_t(n, d, device=dev)
 Y = torch.empty_like(X)
 variants = {}
