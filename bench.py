@@ -124,7 +124,7 @@ def main():
     stream = torch.cuda.current_stream(dev)
     if world == 1:
         A = DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, heavy_threshold=a.heavy_threshold, device=dev)
-        log(f"schedule: n_heavy={A.n_heavy}")
+        log(f"schedule: n_hub={A.n_hub} n_heavy={A.n_heavy}")
         buf = torch.empty((K, n, d), dtype=torch.float32, device=dev)
         panels = [X] + [buf[k] for k in range(K)]
 

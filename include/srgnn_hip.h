@@ -72,22 +72,26 @@ int FloatCSRMulDense(float answer[], int data_nnz, float data[], int indices[], 
  *   indptr[n_rows+1] int64, indices[nnz] int32 (ids into X's rows), values[nnz] fp32;
  *   row_order: optional (NULL) int32 permutation of [0, n_rows) giving the order in which rows are
  *              scheduled (srgnn plans pass rows by decreasing length so hubs start first);
- *   n_heavy:   the first n_heavy rows of row_order are worked on in 32-column slices, one wave per
- *              slice (long power-law rows); 0 without a row_order.
+ *   n_hub:     the first n_hub rows of row_order are hub rows: one workgroup per 32-column slice
+ *              with producer waves keeping 64 KiB of gathers in flight (launched on a library-owned
+ *              side stream, forked from and joined back into `stream` with events);
+ *   n_heavy:   the next n_heavy rows are worked on in 32-column slices, one wave per slice (long
+ *              power-law rows); both 0 without a row_order.
  *   Neither scheduling argument changes any result: every output element is one fma chain.
  *   X: ldx >= d; Y: ldy >= d.  Device pointers.  Replaces one call of csr_sparse_dense_matmul
  *   (SSRG/operators/utils.py:17-47) inside GraphOp.propagate (SSRG/operators/base_operator.py:33-35). */
 int srg_spmm_csr_f32(const int64_t* indptr, const int32_t* indices, const float* values,
-                     int64_t n_rows, const int32_t* row_order, int64_t n_heavy, const float* X,
-                     int64_t ldx, float* Y, int64_t ldy, int32_t d, uint32_t flags, void* stream);
+                     int64_t n_rows, const int32_t* row_order, int64_t n_hub, int64_t n_heavy,
+                     const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t d, uint32_t flags,
+                     void* stream);
 
 /* K hops: panels[k] = A * panels[k-1] for k = 1..K, panels[0] = X (read only).  `panels` is a
  * HOST array of K+1 device pointers, all with leading dimension ld.  Replaces the hop loop of
  * GraphOp.propagate, SSRG/operators/base_operator.py:32-35 (with the per-hop host round trips of
  * utils.py:38-47 removed).  A square (n_rows == rows of X). */
 int srg_propagate_khop_f32(const int64_t* indptr, const int32_t* indices, const float* values,
-                           int64_t n_rows, const int32_t* row_order, int64_t n_heavy,
-                           float* const* panels,
+                           int64_t n_rows, const int32_t* row_order, int64_t n_hub,
+                           int64_t n_heavy, float* const* panels,
                            int64_t ld, int32_t d, int32_t K, uint32_t flags, void* stream);
 
 /* Chebyshev heat-kernel filter bank (wavelet basis), SSRG/models/base_scalable/base_model.py:

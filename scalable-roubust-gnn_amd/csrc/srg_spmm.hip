@@ -26,6 +26,7 @@
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -336,6 +337,165 @@ k_spmm(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
 }
 
 // ------------------------------------------------------------------------------------------------
+// hub rows: one workgroup per (row, 32-column slice), producer/consumer through LDS
+//
+// A slice wave keeps 8 KiB of gathers in flight, so a row of degree D costs ~D/64 load latencies
+// (~6 ms for the 155,868-entry hub of the products-shaped graph): hidden at 1 GPU, the whole hop
+// at 8.  Here 8 producer waves keep kHubUH = 16 dwordx4 gathers (8 nonzeros' 128-byte slices
+// each) in flight per lane -- 128 KiB per workgroup -- for a window of 1024 nonzeros, with the
+// column ids / values of the NEXT window already in registers (one dependent latency per window,
+// not two).  A window is staged into a transposed LDS tile [32 columns][1024 nonzeros]; one
+// consumer wave then runs the 32 column chains over it in CSR order, reading 4 links per
+// ds_read_b128, while the producers' gathers for the following window are in flight.
+// Still exactly one fma chain per output element, in CSR order.
+// ------------------------------------------------------------------------------------------------
+constexpr int kHubProducers = 8;
+constexpr int kHubUH = 16;
+constexpr int kHubStage = kHubProducers * kHubUH * 8;   // nonzeros per LDS window (1024)
+
+constexpr int kHubThreads = 64 * (kHubProducers + 1);
+// LDS tile [32 columns][kHubLd]: column c holds the window's nonzeros in groups of 4, group index
+// XOR-ed with hub_swz(c).  kHubLd = 1028 (16-byte aligned columns, stride = 4 banks): the
+// consumer's ds_read_b128 of 16 lanes and the producers' ds_write_b32 of 32 lanes are
+// (nearly) conflict-free -- see DESIGN.md §5.1.
+constexpr int kHubLd = kHubStage + 4;
+__device__ __forceinline__ int hub_swz(int c) { return (c >> 2) & 7; }
+
+// ABL (ablation, diagnostic builds only): 0 = the real kernel; 1 = the consumer skips its chains
+// (producer-bound time); 2 = the producers skip their gathers (consumer-bound time).
+template <bool SFULL, typename IP, int ABL = 0>
+__global__ void __launch_bounds__(kHubThreads)
+k_spmm_hub(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
+           const float* __restrict__ vals, const int32_t* __restrict__ hub_rows, int n_slices,
+           const float* __restrict__ X, int64_t ldx, float* __restrict__ Y, int64_t ldy, int d,
+           int accumulate, int nt)
+{
+    typedef typename Vec<float, 4>::type V4;
+    extern __shared__ __attribute__((aligned(16))) float hub_lds[];
+    float* tile = hub_lds;                              // [32 columns][kHubLd], swizzled groups of 4
+    float* aval = hub_lds + kSliceCols * kHubLd;        // [kHubStage]
+    const int item = blockIdx.x;
+    const int row = hub_rows[item / n_slices];
+    const int slice = item % n_slices;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int lane = threadIdx.x & 63;
+    const int64_t beg = indptr[row];
+    const int64_t end = indptr[row + 1];
+    const int n_stages = (int)((end - beg + kHubStage - 1) / kHubStage);
+
+    if (wave == 0) {   // ---------------- consumer: 32 column chains ----------------
+        const int ccol = slice * kSliceCols + lane;
+        const bool cact = lane < kSliceCols && (SFULL || ccol < d);
+        float* __restrict__ yrow = Y + (int64_t)row * ldy;
+        float acc = 0.0f;
+        if (accumulate && cact) acc = yrow[ccol];
+        // lane c reads 4 consecutive nonzeros of column c per ds_read_b128 (one LDS instruction per
+        // 4 chain links: a single wave issues LDS reads at a fraction of the CU rate, so the read
+        // count, not the 4-cycle fma dependency, bounds the chain otherwise).  Reads run 16 links
+        // ahead of the fmas (ping-pong).
+        const int c = lane & 31;
+        const float* tcol = tile + c * kHubLd;
+        const int sw = hub_swz(c);
+        constexpr int G = 4;   // groups of 4 nonzeros per chunk
+        V4 t0[G], a0[G], t1[G], a1[G];
+        auto ld = [&](int grp, V4 (&t)[G], V4 (&a)[G]) {
+#pragma unroll
+            for (int i = 0; i < G; ++i) {
+                t[i] = *reinterpret_cast<const V4*>(tcol + (((grp + i) ^ sw) << 2));
+                a[i] = *reinterpret_cast<const V4*>(aval + ((grp + i) << 2));   // broadcast read
+            }
+        };
+        auto run = [&](const V4 (&t)[G], const V4 (&a)[G]) {
+#pragma unroll
+            for (int i = 0; i < G; ++i) {
+                acc = __builtin_fmaf(a[i][0], t[i][0], acc);
+                acc = __builtin_fmaf(a[i][1], t[i][1], acc);
+                acc = __builtin_fmaf(a[i][2], t[i][2], acc);
+                acc = __builtin_fmaf(a[i][3], t[i][3], acc);
+            }
+        };
+        for (int st = 0; st < n_stages; ++st) {
+            __syncthreads();   // A: producers may overwrite the tile
+            __syncthreads();   // B: window st is in the tile
+            const int64_t sb = beg + (int64_t)st * kHubStage;
+            const int nb = (end - sb) < kHubStage ? (int)(end - sb) : kHubStage;
+            const int nc = ABL == 1 ? 0 : nb / (4 * G);   // full chunks of 16 nonzeros
+            if (nc > 0) ld(0, t0, a0);
+            for (int k = 0; k < nc; k += 2) {
+                if (k + 1 < nc) ld((k + 1) * G, t1, a1);
+                run(t0, a0);
+                if (k + 1 >= nc) break;
+                if (k + 2 < nc) ld((k + 2) * G, t0, a0);
+                run(t1, a1);
+            }
+            if (ABL != 1)
+                for (int q = nc * 4 * G; q < nb; ++q)
+                    acc = __builtin_fmaf(aval[q], tcol[(((q >> 2) ^ sw) << 2) + (q & 3)], acc);
+        }
+        if (cact) {
+            if (nt)
+                __builtin_nontemporal_store(acc, yrow + ccol);
+            else
+                yrow[ccol] = acc;
+        }
+        return;
+    }
+
+    // ---------------- producers ----------------
+    const int p = wave - 1;
+    const int g = lane >> 3;
+    const int qq = lane & 7;
+    const int qcol = slice * kSliceCols + qq * 4;
+    const bool gact = SFULL || qcol < d;
+    V4 x[kHubUH];
+    float av[kHubUH];      // values of the window being gathered
+    int cn[kHubUH];        // column ids of the next window
+    float an[kHubUH];      // values of the next window
+    auto load_ids = [&](int64_t sb) {
+#pragma unroll
+        for (int b = 0; b < kHubUH; ++b) {
+            int64_t jj = sb + (p * kHubUH + b) * 8 + g;
+            jj = jj < end ? jj : end - 1;
+            cn[b] = indices[jj];
+            an[b] = vals[jj];
+        }
+    };
+    auto gather = [&]() {   // gathers of the window whose ids are in cn/an
+#pragma unroll
+        for (int b = 0; b < kHubUH; ++b) {
+            x[b] = (gact && ABL != 2) ? vload<float, 4>(X + (int64_t)cn[b] * ldx + qcol) : vzero<float, 4>();
+            av[b] = an[b];
+        }
+    };
+    if (n_stages > 0) {
+        load_ids(beg);
+        __builtin_amdgcn_sched_barrier(0);
+        gather();
+        if (n_stages > 1) load_ids(beg + kHubStage);
+    }
+    for (int st = 0; st < n_stages; ++st) {
+        __syncthreads();   // A: the consumer is done with the previous window
+#pragma unroll
+        for (int b = 0; b < kHubUH; ++b) {
+            const int nl = (p * kHubUH + b) * 8 + g;     // nonzero within the window
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {               // transposed, swizzled: conflict-free
+                const int cc = qq * 4 + i;
+                tile[cc * kHubLd + ((((nl >> 2) ^ hub_swz(cc)) << 2) | (nl & 3))] = x[b][i];
+            }
+            if (qq == 0) aval[nl] = av[b];
+        }
+        if (st + 1 < n_stages) {
+            gather();                                                   // window st+1 in flight
+            if (st + 2 < n_stages) load_ids(beg + (int64_t)(st + 2) * kHubStage);   // ids of st+2
+        }
+        __syncthreads();   // B: window st published
+    }
+}
+
+constexpr size_t kHubLdsBytes = (size_t)(kSliceCols * kHubLd + kHubStage) * sizeof(float);
+
+// ------------------------------------------------------------------------------------------------
 // Chebyshev step with fused epilogue (wavelet basis)
 // ------------------------------------------------------------------------------------------------
 template <typename T> struct ChebyCoef {
@@ -435,50 +595,118 @@ int pick_vec(int d, int64_t ldx, int64_t ldy, const void* X, const void* Y, size
 
 constexpr int kUnrollHeavy = 8;
 
+// per-device side stream + fork/join events for the hub kernel (created once, never destroyed)
+struct SideStream {
+    hipStream_t stream = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+};
+std::mutex g_side_mu;
+SideStream g_side[64];
+
+int side_stream(SideStream** out)
+{
+    int dev = 0;
+    SRG_HIP_CHECK(hipGetDevice(&dev));
+    if (dev < 0 || dev >= 64) return fail(SRG_ERR_HIP, "device id %d", dev);
+    std::lock_guard<std::mutex> lock(g_side_mu);
+    SideStream& ss = g_side[dev];
+    if (!ss.stream) {
+        SRG_HIP_CHECK(hipStreamCreateWithFlags(&ss.stream, hipStreamNonBlocking));
+        SRG_HIP_CHECK(hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming));
+        SRG_HIP_CHECK(hipEventCreateWithFlags(&ss.join, hipEventDisableTiming));
+        for (const void* fn : {(const void*)k_spmm_hub<true, int>, (const void*)k_spmm_hub<false, int>,
+                               (const void*)k_spmm_hub<true, int64_t>, (const void*)k_spmm_hub<false, int64_t>,
+                               (const void*)k_spmm_hub<true, int, 1>, (const void*)k_spmm_hub<true, int64_t, 1>,
+                               (const void*)k_spmm_hub<true, int, 2>, (const void*)k_spmm_hub<true, int64_t, 2>})
+            SRG_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kHubLdsBytes));
+    }
+    *out = &ss;
+    return SRG_OK;
+}
+
 template <typename IP>
 int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int64_t n_rows,
-                const int32_t* order, int64_t n_heavy, const float* X, int64_t ldx, float* Y,
-                int64_t ldy, int d, uint32_t flags, hipStream_t s)
+                const int32_t* order, int64_t n_hub, int64_t n_heavy, const float* X, int64_t ldx,
+                float* Y, int64_t ldy, int d, uint32_t flags, hipStream_t s)
 {
     if (n_rows <= 0 || d <= 0) return SRG_OK;
-    if (n_heavy < 0 || n_heavy > n_rows || (n_heavy > 0 && !order))
-        return fail(SRG_ERR_INVALID, "n_heavy=%lld needs a row_order and <= n_rows", (long long)n_heavy);
-    // slice waves gather 16-byte chunks: they need d % 4 == 0 and 16-byte aligned rows
+    if (n_hub < 0 || n_heavy < 0 || n_hub + n_heavy > n_rows || ((n_hub + n_heavy) > 0 && !order))
+        return fail(SRG_ERR_INVALID, "n_hub=%lld n_heavy=%lld need a row_order and <= n_rows",
+                    (long long)n_hub, (long long)n_heavy);
+    // slice waves and hub blocks gather 16-byte chunks: they need d % 4 == 0 and aligned rows;
+    // otherwise every row takes the row-wave path (same results)
     const bool slice_ok = d % 4 == 0 && ldx % 4 == 0 && aligned(X, 16);
-    if (!slice_ok) n_heavy = 0;
+    if (!slice_ok) {
+        n_heavy = 0;
+        n_hub = 0;
+    }
     const int n_slices = (d + kSliceCols - 1) / kSliceCols;
-    if (n_heavy * (int64_t)n_slices > INT32_MAX - 64)
+    if ((n_hub + n_heavy) * (int64_t)n_slices > INT32_MAX - 64)
         return fail(SRG_ERR_INVALID, "too many heavy slices");
+    const int acc = (flags & SRG_SPMM_ACCUMULATE) ? 1 : 0;
+    const int nt = (flags & SRG_SPMM_NT_STORE) ? 1 : 0;
+    const bool sfull = d % kSliceCols == 0;
+
+    SideStream* ss = nullptr;
+    if (n_hub > 0) {   // fork: hub blocks run beside the main launch
+        int rc = side_stream(&ss);
+        if (rc) return rc;
+        SRG_HIP_CHECK(hipEventRecord(ss->fork, s));
+        SRG_HIP_CHECK(hipStreamWaitEvent(ss->stream, ss->fork, 0));
+        const dim3 hgrid((unsigned)(n_hub * n_slices));
+        static const int abl = [] { const char* e = getenv("SRGNN_HUB_ABLATION"); return e ? atoi(e) : 0; }();
+        if (sfull && abl == 1)
+            hipLaunchKernelGGL((k_spmm_hub<true, IP, 1>), hgrid, dim3(kHubThreads), kHubLdsBytes,
+                               ss->stream, indptr, indices, vals, order, n_slices, X, ldx, Y, ldy,
+                               d, acc, nt);
+        else if (sfull && abl == 2)
+            hipLaunchKernelGGL((k_spmm_hub<true, IP, 2>), hgrid, dim3(kHubThreads), kHubLdsBytes,
+                               ss->stream, indptr, indices, vals, order, n_slices, X, ldx, Y, ldy,
+                               d, acc, nt);
+        else if (sfull)
+            hipLaunchKernelGGL((k_spmm_hub<true, IP>), hgrid, dim3(kHubThreads), kHubLdsBytes,
+                               ss->stream, indptr, indices, vals, order, n_slices, X, ldx, Y, ldy,
+                               d, acc, nt);
+        else
+            hipLaunchKernelGGL((k_spmm_hub<false, IP>), hgrid, dim3(kHubThreads), kHubLdsBytes,
+                               ss->stream, indptr, indices, vals, order, n_slices, X, ldx, Y, ldy,
+                               d, acc, nt);
+        SRG_HIP_CHECK(hipGetLastError());
+        SRG_HIP_CHECK(hipEventRecord(ss->join, ss->stream));
+    }
+
+    const int32_t* morder = order ? order + n_hub : nullptr;
+    const int64_t m_rows = n_rows - n_hub;
     const int nb_heavy = (int)((n_heavy * n_slices + kWavesPerBlock - 1) / kWavesPerBlock);
-    const int64_t n_light = n_rows - n_heavy;
+    const int64_t n_light = m_rows - n_heavy;
     const int64_t blocks = nb_heavy + (n_light + kWavesPerBlock - 1) / kWavesPerBlock;
     if (blocks > INT32_MAX) return fail(SRG_ERR_INVALID, "grid too large");
     const int vec = pick_vec(d, ldx, ldy, X, Y, sizeof(float));
-    const dim3 grid((unsigned)blocks);
-    const int acc = (flags & SRG_SPMM_ACCUMULATE) ? 1 : 0;
-    const int nt = (flags & SRG_SPMM_NT_STORE) ? 1 : 0;
-    const int nr = (int)n_rows, nh = (int)n_heavy;
+    const int nr = (int)m_rows, nh = (int)n_heavy;
+    if (blocks > 0) {
+        const dim3 grid((unsigned)blocks);
 #define SRG_LAUNCH_SPMM(V, F, SF)                                                               \
     hipLaunchKernelGGL((k_spmm<V, kUnroll, kUnrollHeavy, F, SF, IP>), grid, dim3(kBlock), 0, s,     \
-                       indptr, indices, vals, order, nr, nh, n_slices, nb_heavy, X, ldx, Y, ldy, d, \
-                       acc, nt)
-    const bool full = d % (64 * vec) == 0;        // implies d % 32 == 0
-    const bool sfull = d % kSliceCols == 0;
-    if (vec == 4) {
-        if (full) SRG_LAUNCH_SPMM(4, true, true);
-        else if (sfull) SRG_LAUNCH_SPMM(4, false, true);
-        else SRG_LAUNCH_SPMM(4, false, false);
-    } else if (vec == 2) {
-        if (full) SRG_LAUNCH_SPMM(2, true, true);
-        else if (sfull) SRG_LAUNCH_SPMM(2, false, true);
-        else SRG_LAUNCH_SPMM(2, false, false);
-    } else {
-        if (full) SRG_LAUNCH_SPMM(1, true, true);
-        else if (sfull) SRG_LAUNCH_SPMM(1, false, true);
-        else SRG_LAUNCH_SPMM(1, false, false);
-    }
+                       indptr, indices, vals, morder, nr, nh, n_slices, nb_heavy, X, ldx, Y, ldy, \
+                       d, acc, nt)
+        const bool full = d % (64 * vec) == 0;        // implies d % 32 == 0
+        if (vec == 4) {
+            if (full) SRG_LAUNCH_SPMM(4, true, true);
+            else if (sfull) SRG_LAUNCH_SPMM(4, false, true);
+            else SRG_LAUNCH_SPMM(4, false, false);
+        } else if (vec == 2) {
+            if (full) SRG_LAUNCH_SPMM(2, true, true);
+            else if (sfull) SRG_LAUNCH_SPMM(2, false, true);
+            else SRG_LAUNCH_SPMM(2, false, false);
+        } else {
+            if (full) SRG_LAUNCH_SPMM(1, true, true);
+            else if (sfull) SRG_LAUNCH_SPMM(1, false, true);
+            else SRG_LAUNCH_SPMM(1, false, false);
+        }
 #undef SRG_LAUNCH_SPMM
-    SRG_HIP_CHECK(hipGetLastError());
+        SRG_HIP_CHECK(hipGetLastError());
+    }
+    if (ss) SRG_HIP_CHECK(hipStreamWaitEvent(s, ss->join, 0));   // join
     return SRG_OK;
 }
 
@@ -624,7 +852,7 @@ int host_compat_spmm(float* answer, const float* data, const int* indices, const
         SRG_HIP_CHECK(hipMemcpyAsync(d_y, answer, panel, hipMemcpyHostToDevice, s));
         flags |= SRG_SPMM_ACCUMULATE;
     }
-    rc = launch_spmm<int>(d_ptr, d_idx, d_val, mat_row, nullptr, 0, d_x, mat_col, d_y, mat_col, mat_col, flags, s);
+    rc = launch_spmm<int>(d_ptr, d_idx, d_val, mat_row, nullptr, 0, 0, d_x, mat_col, d_y, mat_col, mat_col, flags, s);
     if (rc) return rc;
     SRG_HIP_CHECK(hipMemcpyAsync(answer, d_y, panel, hipMemcpyDeviceToHost, s));
     SRG_HIP_CHECK(hipStreamSynchronize(s));
@@ -651,19 +879,20 @@ int FloatCSRMulDense(float answer[], int data_nnz, float data[], int indices[], 
 }
 
 int srg_spmm_csr_f32(const int64_t* indptr, const int32_t* indices, const float* values,
-                     int64_t n_rows, const int32_t* row_order, int64_t n_heavy, const float* X,
-                     int64_t ldx, float* Y, int64_t ldy, int32_t d, uint32_t flags, void* stream)
+                     int64_t n_rows, const int32_t* row_order, int64_t n_hub, int64_t n_heavy,
+                     const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t d, uint32_t flags,
+                     void* stream)
 {
     int rc = check_spmm_args(indptr, indices, values, n_rows, X, ldx, Y, ldy, d);
     if (rc) return rc;
-    rc = launch_spmm<int64_t>(indptr, indices, values, n_rows, row_order, n_heavy, X, ldx, Y, ldy, d, flags,
+    rc = launch_spmm<int64_t>(indptr, indices, values, n_rows, row_order, n_hub, n_heavy, X, ldx, Y, ldy, d, flags,
                               static_cast<hipStream_t>(stream));
     return rc ? rc : ok();
 }
 
 int srg_propagate_khop_f32(const int64_t* indptr, const int32_t* indices, const float* values,
-                           int64_t n_rows, const int32_t* row_order, int64_t n_heavy,
-                           float* const* panels,
+                           int64_t n_rows, const int32_t* row_order, int64_t n_hub,
+                           int64_t n_heavy, float* const* panels,
                            int64_t ld, int32_t d, int32_t K, uint32_t flags, void* stream)
 {
     if (K < 0) return fail(SRG_ERR_INVALID, "K=%d < 0", K);
@@ -675,7 +904,7 @@ int srg_propagate_khop_f32(const int64_t* indptr, const int32_t* indices, const 
     if (rc) return rc;
     const uint32_t f = flags & ~SRG_SPMM_ACCUMULATE;
     for (int k = 1; k <= K; ++k) {
-        rc = launch_spmm<int64_t>(indptr, indices, values, n_rows, row_order, n_heavy, panels[k - 1], ld,
+        rc = launch_spmm<int64_t>(indptr, indices, values, n_rows, row_order, n_hub, n_heavy, panels[k - 1], ld,
                                   panels[k], ld, d, f, static_cast<hipStream_t>(stream));
         if (rc) return rc;
     }

@@ -55,9 +55,9 @@ _f64 = ctypes.c_double
 
 
 def _declare(lib):
-    lib.srg_spmm_csr_f32.argtypes = [_p, _p, _p, _i64, _p, _i64, _p, _i64, _p, _i64, _i32, _u32, _p]
+    lib.srg_spmm_csr_f32.argtypes = [_p, _p, _p, _i64, _p, _i64, _i64, _p, _i64, _p, _i64, _i32, _u32, _p]
     lib.srg_spmm_csr_f32.restype = ctypes.c_int
-    lib.srg_propagate_khop_f32.argtypes = [_p, _p, _p, _i64, _p, _i64, _p, _i64, _i32, _i32, _u32, _p]
+    lib.srg_propagate_khop_f32.argtypes = [_p, _p, _p, _i64, _p, _i64, _i64, _p, _i64, _i32, _i32, _u32, _p]
     lib.srg_propagate_khop_f32.restype = ctypes.c_int
     lib.srg_cheby_step_f64.argtypes = [_p, _p, _p, _i64, _p, _p, _p, _p, _i64, _i32, ctypes.c_int,
                                        _f64, _f64, _p, _p, _i32, _p, _i64, _p]

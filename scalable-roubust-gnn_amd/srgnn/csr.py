@@ -6,9 +6,12 @@ A `DeviceCSR` holds the normalised adjacency Â of `GraphOp.construct_adj`
     indptr  int64 [n_rows + 1]     (nnz may exceed 2^31: papers100M / RMAT-26 scale)
     indices int32 [nnz]            column ids, CSR order preserved exactly (the fma chains follow it)
     values  fp32  [nnz]            Â values, already cast to fp32 as utils.py:39 does
-    order   int32 [n_rows]         schedule: rows with more than `heavy_threshold` nonzeros first
-                                   (decreasing length), then the rest (decreasing length)
-    n_heavy int                    those long rows are split into 32-column slices, one wave each
+    order   int32 [n_rows]         schedule, each group by decreasing length:
+                                     n_hub rows with more than `hub_threshold` nonzeros (one
+                                       workgroup per 32-column slice, LDS-staged, side stream),
+                                     n_heavy rows with more than `heavy_threshold` (one wave per
+                                       32-column slice),
+                                     then the rest (one wave per row)
 
 The schedule never changes results -- every output element stays one fma chain in CSR order -- it
 only decides which wave works on what and when (power-law hubs start first).
@@ -24,6 +27,15 @@ import torch
 from . import _lib
 
 DEFAULT_HEAVY_THRESHOLD = int(os.environ.get("SRGNN_HEAVY_THRESHOLD", "32"))
+# "auto": rows whose slice-wave time (~40 ns per nonzero, measured) would exceed about half of the
+# expected hop time (~nnz / 13.5e9 s at the measured hop rate) go to the hub path:
+# threshold = nnz // 1024, at least 8192.  Products on 1 GPU -> only the top hub; 1/8 of it -> ~15 K.
+_HUB_ENV = os.environ.get("SRGNN_HUB_THRESHOLD", "auto")
+DEFAULT_HUB_THRESHOLD = None if _HUB_ENV == "auto" else int(_HUB_ENV)
+
+
+def auto_hub_threshold(nnz: int) -> int:
+    return max(8192, int(nnz) // 1024)
 
 
 def _dev(device):
@@ -44,6 +56,7 @@ class DeviceCSR:
     n_cols: int
     order: torch.Tensor
     n_heavy: int
+    n_hub: int = 0
 
     @property
     def nnz(self) -> int:
@@ -56,7 +69,7 @@ class DeviceCSR:
     # ------------------------------------------------------------------------------------------
     @classmethod
     def from_tensors(cls, indptr, indices, values, n_cols=None, heavy_threshold=None,
-                     validate=True, device=None):
+                     validate=True, device=None, hub_threshold=None):
         """Build from CSR arrays (numpy or torch, any device); copies to `device` if needed."""
         device = _dev(device if device is not None else
                       (indices.device if isinstance(indices, torch.Tensor) and indices.is_cuda else None))
@@ -75,8 +88,8 @@ class DeviceCSR:
             stream = torch.cuda.current_stream(device).cuda_stream
             _lib.check(_lib.lib().srg_csr_validate(ip.data_ptr(), ix.data_ptr(), n_rows, ix.numel(),
                                                    n_cols, stream), "srg_csr_validate")
-        order, n_heavy = make_schedule(ip, heavy_threshold)
-        return cls(ip, ix, vv, n_rows, int(n_cols), order, n_heavy)
+        order, n_heavy, n_hub = make_schedule(ip, heavy_threshold, hub_threshold)
+        return cls(ip, ix, vv, n_rows, int(n_cols), order, n_heavy, n_hub)
 
     @classmethod
     def from_scipy(cls, adj, heavy_threshold=None, device=None):
@@ -86,25 +99,33 @@ class DeviceCSR:
                                 np.asarray(adj.data).astype(np.float32),
                                 n_cols=adj.shape[1], heavy_threshold=heavy_threshold, device=device)
 
-    def rows(self, r0: int, r1: int, heavy_threshold=None) -> "DeviceCSR":
+    def rows(self, r0: int, r1: int, heavy_threshold=None, hub_threshold=None) -> "DeviceCSR":
         """Row block [r0, r1) with rebased row pointers (global column ids kept)."""
         ip = self.indptr[r0:r1 + 1]
         base = int(ip[0].item())
         end = int(ip[-1].item())
         ip = ip - base
-        order, n_heavy = make_schedule(ip, heavy_threshold)
+        order, n_heavy, n_hub = make_schedule(ip, heavy_threshold, hub_threshold)
         return DeviceCSR(ip.contiguous(), self.indices[base:end], self.values[base:end],
-                         r1 - r0, self.n_cols, order, n_heavy)
+                         r1 - r0, self.n_cols, order, n_heavy, n_hub)
 
 
-def make_schedule(indptr: torch.Tensor, heavy_threshold=None):
-    """Row order (int32) and heavy-row count for a CSR with row pointers `indptr`."""
+def make_schedule(indptr: torch.Tensor, heavy_threshold=None, hub_threshold=None):
+    """(order int32, n_heavy, n_hub) for a CSR with row pointers `indptr`: rows sorted by
+    decreasing length; the first n_hub have more than hub_threshold nonzeros, the next n_heavy
+    more than heavy_threshold.  A negative threshold disables that group."""
     if heavy_threshold is None:
         heavy_threshold = DEFAULT_HEAVY_THRESHOLD
+    if hub_threshold is None:
+        hub_threshold = DEFAULT_HUB_THRESHOLD
+    if hub_threshold is None:
+        hub_threshold = auto_hub_threshold(int(indptr[-1]) if indptr.numel() else 0)
     deg = indptr[1:] - indptr[:-1]
     n = int(deg.numel())
     if n == 0:
-        return torch.zeros(0, dtype=torch.int32, device=indptr.device), 0
+        return torch.zeros(0, dtype=torch.int32, device=indptr.device), 0, 0
     order = torch.sort(deg, descending=True, stable=True).indices.to(torch.int32)
-    n_heavy = int((deg > heavy_threshold).sum().item()) if heavy_threshold >= 0 else 0
-    return order.contiguous(), n_heavy
+    n_hub = int((deg > hub_threshold).sum().item()) if hub_threshold >= 0 else 0
+    n_big = int((deg > heavy_threshold).sum().item()) if heavy_threshold >= 0 else 0
+    n_heavy = max(0, n_big - n_hub)
+    return order.contiguous(), n_heavy, n_hub

@@ -46,7 +46,8 @@ def spmm(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor | None = None, accumul
         raise ValueError("A, X and out must be on the same device")
     flags = (_lib.SRG_SPMM_ACCUMULATE if accumulate else 0) | (_lib.SRG_SPMM_NT_STORE if nt_store else 0)
     rc = _lib.lib().srg_spmm_csr_f32(A.indptr.data_ptr(), A.indices.data_ptr(), A.values.data_ptr(),
-                                     A.n_rows, A.order.data_ptr() if A.n_rows else None, A.n_heavy,
+                                     A.n_rows, A.order.data_ptr() if A.n_rows else None, A.n_hub,
+                                     A.n_heavy,
                                      X.data_ptr(), X.stride(0), out.data_ptr(), out.stride(0), d, flags,
                                      _stream(X.device))
     _lib.check(rc, "srg_spmm_csr_f32")
@@ -82,7 +83,7 @@ def propagate(A: DeviceCSR, X: torch.Tensor, K: int, panels: list | None = None,
     flags = _lib.SRG_SPMM_NT_STORE if nt_store else 0
     rc = _lib.lib().srg_propagate_khop_f32(A.indptr.data_ptr(), A.indices.data_ptr(),
                                            A.values.data_ptr(), n,
-                                           A.order.data_ptr() if n else None, A.n_heavy,
+                                           A.order.data_ptr() if n else None, A.n_hub, A.n_heavy,
                                            arr, ld, d, K, flags, _stream(X.device))
     _lib.check(rc, "srg_propagate_khop_f32")
     if panels[0] is not X0 and X is not X0:

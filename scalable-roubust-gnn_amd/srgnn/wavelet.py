@@ -122,7 +122,7 @@ class HeatWaveletFilter:
         self.indices = torch.from_numpy(L.indices.astype(np.int32)).to(self.device)
         self.lvals = torch.from_numpy(lvals).to(self.device, dtype)
         self.fvals = torch.from_numpy(fvals).to(self.device, dtype)
-        self.order, _ = make_schedule(self.indptr, -1)
+        self.order, _, _ = make_schedule(self.indptr, -1, -1)
 
     def apply(self, S: torch.Tensor) -> torch.Tensor:
         """[n_scales, n, d] filter outputs for the panel S [n, d] (device tensor)."""

@@ -41,14 +41,14 @@ def test_gfx950_code_object_present():
 
 def test_invalid_arguments_fail_before_launch():
     L = _lib.lib()
-    rc = L.srg_spmm_csr_f32(None, None, None, -1, None, 0, None, 8, None, 8, 8, 0, None)
+    rc = L.srg_spmm_csr_f32(None, None, None, -1, None, 0, 0, None, 8, None, 8, 8, 0, None)
     assert rc == _lib.SRG_ERR_INVALID
     assert "n_rows" in _lib.last_error()
-    rc = L.srg_spmm_csr_f32(None, None, None, 4, None, 0, None, 2, None, 8, 8, 0, None)
+    rc = L.srg_spmm_csr_f32(None, None, None, 4, None, 0, 0, None, 2, None, 8, 8, 0, None)
     assert rc == _lib.SRG_ERR_INVALID and "leading" in _lib.last_error()
-    rc = L.srg_spmm_csr_f32(None, None, None, 4, None, 2, ctypes.c_void_p(16), 8, ctypes.c_void_p(16), 8, 8, 0, None)
+    rc = L.srg_spmm_csr_f32(None, None, None, 4, None, 0, 2, ctypes.c_void_p(16), 8, ctypes.c_void_p(16), 8, 8, 0, None)
     assert rc == _lib.SRG_ERR_INVALID
-    rc = L.srg_propagate_khop_f32(None, None, None, 4, None, 0, None, 8, 8, -1, 0, None)
+    rc = L.srg_propagate_khop_f32(None, None, None, 4, None, 0, 0, None, 8, 8, -1, 0, None)
     assert rc == _lib.SRG_ERR_INVALID and "K" in _lib.last_error()
     rc = L.srg_cheby_step_f64(None, None, None, 4, None, None, None, None, 8, 8, 7, 1.0, 1.0,
                               None, None, 1, None, 32, None)
@@ -59,7 +59,7 @@ def test_invalid_arguments_fail_before_launch():
 
 def test_empty_problem_is_a_noop_without_device():
     L = _lib.lib()
-    assert L.srg_spmm_csr_f32(None, None, None, 0, None, 0, None, 8, None, 8, 8, 0, None) == 0
+    assert L.srg_spmm_csr_f32(None, None, None, 0, None, 0, 0, None, 8, None, 8, 8, 0, None) == 0
     # the drop-in entry: zero rows -> returns without touching the device
     f = ctypes.c_void_p
     L.FloatCSRMulDenseOMP.argtypes = [f, f, f, f, f, ctypes.c_int, ctypes.c_int]

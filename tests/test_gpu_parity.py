@@ -2,8 +2,8 @@
 
 Bar: exact mode is BIT-IDENTICAL to the reference's FloatCSRMulDenseOMP (one fp32 fma chain per
 output element in CSR order), so hops are compared by SHA-256 of their bytes.  Each case runs
-through both wave roles of the kernel: row waves only (heavy_threshold=-1 -> n_heavy=0), column-
-slice waves for every row (heavy_threshold=0), and the default split.
+through every path of the kernel: row waves only, column-slice waves for every row, hub workgroups
+(LDS producer/consumer) for every row, the default split, and a mixed three-way split.
 """
 import numpy as np
 import pytest
@@ -14,13 +14,16 @@ import golden_cases as G
 
 pytestmark = pytest.mark.gpu
 
-THRESHOLDS = [-1, 0, None]
+# (heavy_threshold, hub_threshold)
+THRESHOLDS = [(-1, -1), (0, -1), (0, 0), (None, None), (4, 64)]
 
 
 def _csr(c, thr):
     from srgnn.csr import DeviceCSR
     ip, ix, v = c.ahat()
-    return DeviceCSR.from_tensors(ip, ix, v, n_cols=c.n, heavy_threshold=thr, device="cuda")
+    heavy, hub = thr if isinstance(thr, tuple) else (thr, None)
+    return DeviceCSR.from_tensors(ip, ix, v, n_cols=c.n, heavy_threshold=heavy, hub_threshold=hub,
+                                  device="cuda")
 
 
 @pytest.mark.parametrize("thr", THRESHOLDS)
@@ -46,7 +49,7 @@ def test_one_hop_raw_bit_exact(name, thr):
     c = G.Case(name)
     a = c.adj()
     A = DeviceCSR.from_tensors(a.indptr, a.indices, a.data.astype(np.float32), n_cols=c.n,
-                               heavy_threshold=thr, device="cuda")
+                               heavy_threshold=thr[0], hub_threshold=thr[1], device="cuda")
     y = spmm(A, torch.from_numpy(c.x()).cuda())
     c.check_hop(1, y.cpu().numpy())
 
@@ -136,6 +139,12 @@ def test_accumulate_and_nt_store_flags(oracle_mod):
     np.testing.assert_array_equal(Y.cpu().numpy(), ref)
     Z = spmm(A, X, nt_store=True)
     np.testing.assert_array_equal(Z.cpu().numpy(), oracle_mod.spmm(*c.ahat(), x))
+    # accumulate through the hub and slice paths too
+    for thr in ((0, 0), (0, -1)):
+        Ah = _csr(c, thr)
+        Y = torch.from_numpy(y0.copy()).cuda()
+        spmm(Ah, X, out=Y, accumulate=True)
+        np.testing.assert_array_equal(Y.cpu().numpy(), ref, err_msg=str(thr))
 
 
 def test_strided_panels_and_row_blocks(oracle_mod):
@@ -154,6 +163,10 @@ def test_strided_panels_and_row_blocks(oracle_mod):
     blk = A.rows(50, 140)
     yb = spmm(blk, torch.from_numpy(x).cuda())
     np.testing.assert_array_equal(yb.cpu().numpy(), want[50:140])
+    hub_blk = A.rows(50, 140, heavy_threshold=2, hub_threshold=5)
+    assert hub_blk.n_hub > 0
+    yh = spmm(hub_blk, torch.from_numpy(x).cuda())
+    np.testing.assert_array_equal(yh.cpu().numpy(), want[50:140])
 
 
 def test_edge_cases_empty_and_special_values(oracle_mod):
@@ -200,8 +213,9 @@ def test_rmat_many_widths_bit_exact(oracle_mod, d):
     vals = synth.uniform_features_np(1, int(ix.numel()), seed=99)[0] * 0.5 + 0.5
     x = synth.uniform_features_np(n, d, seed=4)
     want = oracle_mod.spmm(ip.numpy(), ix.numpy(), vals, x)
-    for thr in (-1, 0, 16):
-        A = DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, heavy_threshold=thr, device="cuda")
+    for thr in ((-1, -1), (0, -1), (16, -1), (0, 0), (16, 300)):
+        A = DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, heavy_threshold=thr[0], hub_threshold=thr[1],
+                                   device="cuda")
         got = spmm(A, torch.from_numpy(x).cuda()).cpu().numpy()
         np.testing.assert_array_equal(got, want, err_msg=f"d={d} thr={thr}")
 
@@ -234,7 +248,8 @@ def test_products_scale_sampled_rows_bit_exact(oracle_mod):
     from srgnn.csr import DeviceCSR
     from srgnn.spmm import propagate
     ip, ix, vals, n, d, _ = graphs.build("products", "cuda")
-    A = DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, device="cuda")
+    A = DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, device="cuda", hub_threshold=4096)
+    assert A.n_hub > 0 and A.n_heavy > 0
     x = synth.uniform_features_t(n, d, device="cuda")
     hops = propagate(A, x, 2)
     ipn, ixn, vn = ip.cpu().numpy(), ix.cpu().numpy(), vals.cpu().numpy()

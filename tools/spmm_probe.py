@@ -45,7 +45,7 @@ for _ in range(a.reps):
 torch.cuda.synchronize()
 nnz = A.nnz
 print(json.dumps({"config": "identity" if a.identity else a.config, "n": n, "nnz": nnz, "d": d,
-                  "reps": a.reps, "n_heavy": A.n_heavy,
+                  "reps": a.reps, "n_heavy": A.n_heavy, "n_hub": A.n_hub,
                   "algorithmic_bytes": roofline.bytes_no_reuse(n, nnz, d),
                   "compulsory_bytes": roofline.bytes_compulsory(n, nnz, d),
                   "x_read_bytes": n * 4 * d, "y_write_bytes": n * 4 * d,

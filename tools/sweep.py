@@ -18,7 +18,8 @@ from srgnn.spmm import spmm  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="products")
-ap.add_argument("--thresholds", default="-1,32,64,128,256,512,2048,100000000")
+ap.add_argument("--thresholds", default="32:-1,32:4096,32:16384,32:65536",
+                help="comma list of heavy:hub thresholds (-1 disables a group)")
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--nt", action="store_true")
 ap.add_argument("--n", type=int, default=None)
@@ -29,10 +30,13 @@ ip, ix, vals, n, d, _ = graphs.build(a.config, dev, n=a.n, n_edges=a.n_edges)
 X = synth.uniform_features_t(n, d, device=dev)
 Y = torch.empty_like(X)
 variants = {}
-for t in [int(s) for s in a.thresholds.split(",")]:
-    variants[f"thr={t}"] = (DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, heavy_threshold=t, device=dev), False)
+for spec in a.thresholds.split(","):
+    h, _, u = spec.partition(":")
+    hub = int(u) if u else -1
+    A = DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, heavy_threshold=int(h), hub_threshold=hub, device=dev)
+    variants[f"thr={spec}"] = (A, False)
     if a.nt:
-        variants[f"thr={t},nt"] = (variants[f"thr={t}"][0], True)
+        variants[f"thr={spec},nt"] = (A, True)
 ref = None
 times = {k: [] for k in variants}
 for r in range(a.rounds):
@@ -53,5 +57,6 @@ out = {}
 for k, v in times.items():
     med = float(np.median(v[1:] if len(v) > 1 else v))
     out[k] = {"median_ms": med, "min_ms": float(min(v)), "n_heavy": variants[k][0].n_heavy,
+              "n_hub": variants[k][0].n_hub,
               "frac": b / (med * 1e-3) / 1e9 / roofline.MI355X_HBM_PEAK_GBS}
 print(json.dumps({"config": a.config, "n": n, "nnz": int(ix.numel()), "d": d, "variants": out}, indent=1))
