@@ -8,8 +8,11 @@ power-law graph with inputs already resident in HBM: K = 10 h
 products-shaped graph (N = 2,449,029, 61.9 M undirected edges, d = 128) by default.
 value = propagated edges/s = steps * K * nnz(Â) / time (nnz counts the self-loops), whole job.
 
-N > 1: one process per GPU (torchrun), 1-D row partition balanced by nonzeros, one RCCL
-all-gather of the feature panel per hop (srgnn.dist) -- strong scaling of the same graph.
+N > 1: one process per GPU (torchrun), 1-D row partition balanced by nonzeros (strong scaling of
+the same graph).  --exchange halo (default): each rank receives only the remote rows its rows
+reference, in nnz-balanced groups exchanged with RCCL all_to_all_single as soon as each group's
+kernel finishes (overlapping the later groups); --exchange allgather: one padded
+all_gather_into_tensor of the whole panel per hop.  Both are bitwise equal to 1 GPU.
 
 Extra objects on the JSON line:
   roofline      the SpMM kernel: algorithmic (no-reuse) bytes per launch / its average duration,
@@ -51,6 +54,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--nt-store", action="store_true")
+    ap.add_argument("--exchange", default="halo", choices=["halo", "allgather"])
+    ap.add_argument("--chunks", type=int, default=4, help="halo exchange groups per hop")
     return ap.parse_args()
 
 
@@ -131,13 +136,27 @@ def main():
         def step():
             propagate(A, X, K, panels=panels, nt_store=a.nt_store)
         local_rows, local_nnz = n, nnz
-    else:
+    elif a.exchange == "allgather":
         from srgnn.dist import RowPartitionedOperator
         op = RowPartitionedOperator(ip, ix, vals, n, heavy_threshold=a.heavy_threshold, device=dev)
         A = op.A
         x_loc = op.new_panel(d)
         x_loc[: op.rows].copy_(X[op.r0:op.r1])
         panels = [x_loc] + [op.new_panel(d) for _ in range(K)]
+        del X
+
+        def step():
+            op.propagate(x_loc, K, panels=panels)
+        local_rows, local_nnz = op.rows, op.nnz_local
+    else:
+        from srgnn.dist import HaloPartitionedOperator
+        op = HaloPartitionedOperator(ip, ix, vals, n, chunks=a.chunks, heavy_threshold=a.heavy_threshold,
+                                     device=dev)
+        log(f"rank {rank}: rows={op.rows} nnz={op.nnz_local} halo={op.halo} "
+            f"hub_rows={op.views[-1][1]} groups={op.n_groups}")
+        panels = [op.new_panel(d) for _ in range(K + 1)]
+        panels[0][: op.rows].copy_(X[op.r0:op.r1])
+        x_loc = panels[0]
         del X
 
         def step():
@@ -168,13 +187,23 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
-    # roofline: average duration of one SpMM launch (this rank's operator), HIP events on its stream
-    src = panels[0] if world == 1 else op._gather(panels[0])
-    dst = panels[1] if world == 1 else panels[1][: op.rows]
+    # roofline: average duration of one hop's SpMM launches on this rank (HIP events on the
+    # launch stream; the hub side stream is joined back into it by the library)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * a.roofline_reps)]
+    if world == 1:
+        def one_hop():
+            spmm(A, panels[0], out=panels[1], nt_store=a.nt_store)
+    elif a.exchange == "allgather":
+        src = op._gather(panels[0])
+
+        def one_hop():
+            spmm(A, src, out=panels[1][: op.rows])
+    else:
+        def one_hop():
+            op.compute(panels[0], panels[1])
     for r in range(a.roofline_reps):
         ev[2 * r].record(stream)
-        spmm(A, src, out=dst, nt_store=a.nt_store)
+        one_hop()
         ev[2 * r + 1].record(stream)
     torch.cuda.synchronize()
     durs = [ev[2 * r].elapsed_time(ev[2 * r + 1]) * 1e-3 for r in range(a.roofline_reps)]
@@ -199,11 +228,13 @@ def main():
         "dtype": "f32",
         "data": "synthetic (R-MAT power-law graph with the products node/edge counts, U[-1,1) features)",
         "config": {"workload": f"{a.config}-shaped K-hop propagate", "n_nodes": n, "nnz_ahat": nnz,
-                   "d": d, "K": K, "normalization": "sym r=0.5", "parallelism": f"row-partition x{world}",
+                   "d": d, "K": K, "normalization": "sym r=0.5",
+                   "parallelism": f"row-partition x{world}" + (f" ({a.exchange} exchange)" if world > 1 else ""),
                    "mode": "exact (bit-identical to reference)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
                      "frac": achieved / peak, "traffic": traffic,
-                     "kernel": "k_spmm (one hop)", "kernel_ms": kern_s * 1e3,
+                     "kernel": "k_spmm (+ k_spmm_hub beside it): one hop" + (" of rank 0's rows" if world > 1 else ""),
+                     "kernel_ms": kern_s * 1e3,
                      "algorithmic_bytes_per_launch": b_alg,
                      "compulsory_bytes_per_launch": roofline.bytes_compulsory(local_rows, local_nnz, d,
                                                                               n_cols=n)},

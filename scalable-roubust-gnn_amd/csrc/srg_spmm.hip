@@ -595,6 +595,18 @@ int pick_vec(int d, int64_t ldx, int64_t ldy, const void* X, const void* Y, size
 
 constexpr int kUnrollHeavy = 8;
 
+// One wave that sleeps ~`us` microseconds (s_memrealtime ticks at 100 MHz).  Enqueued on the main
+// stream right after the hub workgroups are forked onto the side stream, so they are dispatched
+// onto free CUs before the main launch's blocks fill every CU (a hub workgroup needs 9 waves and
+// ~136 KB of LDS on one CU; behind a full-chip launch it could start milliseconds late and become
+// the hop's tail).
+__global__ void k_dispatch_delay(int us)
+{
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long ticks = 100ull * (unsigned long long)us;
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(16);
+}
+
 // per-device side stream + fork/join events for the hub kernel (created once, never destroyed)
 struct SideStream {
     hipStream_t stream = nullptr;
@@ -611,7 +623,11 @@ int side_stream(SideStream** out)
     std::lock_guard<std::mutex> lock(g_side_mu);
     SideStream& ss = g_side[dev];
     if (!ss.stream) {
-        SRG_HIP_CHECK(hipStreamCreateWithFlags(&ss.stream, hipStreamNonBlocking));
+        // highest queue priority: the hub workgroups (9 waves, ~136 KB LDS each) must get CUs
+        // before the main launch's many small blocks occupy them all
+        int least = 0, greatest = 0;
+        SRG_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        SRG_HIP_CHECK(hipStreamCreateWithPriority(&ss.stream, hipStreamNonBlocking, greatest));
         SRG_HIP_CHECK(hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming));
         SRG_HIP_CHECK(hipEventCreateWithFlags(&ss.join, hipEventDisableTiming));
         for (const void* fn : {(const void*)k_spmm_hub<true, int>, (const void*)k_spmm_hub<false, int>,
@@ -673,6 +689,11 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
                                d, acc, nt);
         SRG_HIP_CHECK(hipGetLastError());
         SRG_HIP_CHECK(hipEventRecord(ss->join, ss->stream));
+        static const int delay_us = [] { const char* e = getenv("SRGNN_HUB_DISPATCH_DELAY_US"); return e ? atoi(e) : 20; }();
+        if (delay_us > 0) {
+            hipLaunchKernelGGL(k_dispatch_delay, dim3(1), dim3(64), 0, s, delay_us);
+            SRG_HIP_CHECK(hipGetLastError());
+        }
     }
 
     const int32_t* morder = order ? order + n_hub : nullptr;

@@ -23,12 +23,17 @@ ap.add_argument("--thresholds", default="32:-1,32:4096,32:16384,32:65536",
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--nt", action="store_true")
 ap.add_argument("--n", type=int, default=None)
+ap.add_argument("--bigbuf", type=int, default=0, help="X, Y as slices of one (bigbuf, n, d) buffer")
 ap.add_argument("--n-edges", type=int, default=None)
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 ip, ix, vals, n, d, _ = graphs.build(a.config, dev, n=a.n, n_edges=a.n_edges)
 X = synth.uniform_features_t(n, d, device=dev)
 Y = torch.empty_like(X)
+if a.bigbuf:
+    big = torch.empty((a.bigbuf, n, d), dtype=torch.float32, device=dev)
+    big[0].copy_(X)
+    X, Y = big[0], big[1]
 variants = {}
 for spec in a.thresholds.split(","):
     h, _, u = spec.partition(":")
@@ -56,7 +61,8 @@ b = roofline.bytes_no_reuse(n, ix.numel(), d)
 out = {}
 for k, v in times.items():
     med = float(np.median(v[1:] if len(v) > 1 else v))
-    out[k] = {"median_ms": med, "min_ms": float(min(v)), "n_heavy": variants[k][0].n_heavy,
+    out[k] = {"median_ms": med, "min_ms": float(min(v)), "all_ms": [round(t, 3) for t in v],
+              "n_heavy": variants[k][0].n_heavy,
               "n_hub": variants[k][0].n_hub,
               "frac": b / (med * 1e-3) / 1e9 / roofline.MI355X_HBM_PEAK_GBS}
 print(json.dumps({"config": a.config, "n": n, "nnz": int(ix.numel()), "d": d, "variants": out}, indent=1))
