@@ -92,6 +92,22 @@ __device__ __forceinline__ typename Vec<T, VEC>::type vload(const T* p)
 {
     return *reinterpret_cast<const typename Vec<T, VEC>::type*>(p);
 }
+// Gather of one X row piece.  SRG_GATHER_NT=1 builds issue every gather non-temporally
+// (experiment hook; measured 35 % slower on the products-shaped graph: the gathered rows are
+// re-read from L2 / Infinity Cache).
+#ifndef SRG_GATHER_NT
+#define SRG_GATHER_NT 0
+#endif
+template <typename T, int VEC>
+__device__ __forceinline__ typename Vec<T, VEC>::type gload(const T* p)
+{
+    typedef typename Vec<T, VEC>::type V;
+    if constexpr (SRG_GATHER_NT != 0)
+        return __builtin_nontemporal_load(reinterpret_cast<const V*>(p));
+    else
+        return *reinterpret_cast<const V*>(p);
+}
+
 template <typename T, int VEC>
 __device__ __forceinline__ void vstore(T* p, typename Vec<T, VEC>::type v, bool nt)
 {
@@ -191,7 +207,7 @@ __device__ __forceinline__ void row_gather(typename Vec<T, VEC>::type& acc,
                 const int c = __builtin_amdgcn_readlane(c_blk, s0 + u);
                 const T* p = X + (int64_t)c * ldx + col;
                 if (FULL || act)
-                    x[u] = vload<T, VEC>(p);
+                    x[u] = gload<T, VEC>(p);
                 else
                     x[u] = vzero<T, VEC>();
             }
@@ -271,7 +287,7 @@ __device__ __forceinline__ void slice_wave(const IP* __restrict__ indptr,
         __builtin_amdgcn_sched_barrier(0);   // keep every index load ahead of the first gather
 #pragma unroll
         for (int b = 0; b < UH; ++b)     // ... then UH dependent gathers in flight
-            x[b] = gact ? vload<float, 4>(X + (int64_t)cv[b] * ldx + qcol) : vzero<float, 4>();
+            x[b] = gact ? gload<float, 4>(X + (int64_t)cv[b] * ldx + qcol) : vzero<float, 4>();
 #pragma unroll
         for (int b = 0; b < UH; ++b) {
             const int64_t jb = j + b * 8;
@@ -463,7 +479,7 @@ k_spmm_hub(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
     auto gather = [&]() {   // gathers of the window whose ids are in cn/an
 #pragma unroll
         for (int b = 0; b < kHubUH; ++b) {
-            x[b] = (gact && ABL != 2) ? vload<float, 4>(X + (int64_t)cn[b] * ldx + qcol) : vzero<float, 4>();
+            x[b] = (gact && ABL != 2) ? gload<float, 4>(X + (int64_t)cn[b] * ldx + qcol) : vzero<float, 4>();
             av[b] = an[b];
         }
     };

@@ -36,9 +36,10 @@ if a.bigbuf:
     X, Y = big[0], big[1]
 variants = {}
 for spec in a.thresholds.split(","):
-    h, _, u = spec.partition(":")
-    hub = int(u) if u else -1
-    A = DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, heavy_threshold=int(h), hub_threshold=hub, device=dev)
+    parts = spec.split(":")
+    h = int(parts[0])
+    hub = int(parts[1]) if len(parts) > 1 else -1
+    A = DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, heavy_threshold=h, hub_threshold=hub, device=dev)
     variants[f"thr={spec}"] = (A, False)
     if a.nt:
         variants[f"thr={spec},nt"] = (A, True)
