@@ -115,6 +115,29 @@ int srg_cheby_step_f32(const int64_t* indptr, const int32_t* indices, const floa
                        const float* coef_prev, const float* coef, int32_t n_scales, float* R,
                        int64_t r_stride, void* stream);
 
+/* Hop aggregation without the K+1 panels (fused precompute of SGC / SSGC / GBP).  The reference
+ * combines the hop list on the host (SSRG/operators/message_operator/{sum,mean,simple_weighted}_
+ * message_op.py; operators/utils.py:426-437 one_dim_weighted_add); the host side plans the same
+ * order of element-wise steps (Python sum(): left to right from +0; torch's CPU dim-0 sum: 16-term
+ * blocks folded in levels).  Per element, separate multiply / add / correctly rounded divide:
+ *   SRG_ACC_INIT: agg = 0 + w*y     SRG_ACC_ADD: agg = agg + w*y     SRG_ACC_DIV: agg = agg / w
+ * agg and y are device panels [n_rows, d] with leading dimensions lda / ldy (y unused for DIV). */
+#define SRG_ACC_INIT 0
+#define SRG_ACC_ADD 1
+#define SRG_ACC_DIV 2
+int srg_hop_accumulate_f32(float* agg, int64_t lda, const float* y, int64_t ldy, int64_t n_rows,
+                           int32_t d, float w, int mode, void* stream);
+
+/* The last flat elements (< SRG_TAIL_MAX of them) of a torch dim-0 sum take its scalar row_sum
+ * order (4 interleaved partials).  srg_tail_record_f32 stores w * y[flat_start + e] (flat index of
+ * the row-major [n_rows, d] panel) into hist[e], one call per term with hist advanced by
+ * SRG_TAIL_MAX floats; srg_tail_rowsum_f32 then writes 0 + row_sum(hist[0..n_terms)) into agg. */
+#define SRG_TAIL_MAX 32
+int srg_tail_record_f32(float* hist, const float* y, int64_t ldy, int32_t d, int64_t flat_start,
+                        int32_t len, float w, void* stream);
+int srg_tail_rowsum_f32(float* agg, int64_t lda, int32_t d, int64_t flat_start, int32_t len,
+                        const float* hist, int32_t n_terms, void* stream);
+
 /* Checks a device CSR: indptr[0] == 0, indptr non-decreasing, indptr[n_rows] == nnz, and every
  * column id in [0, n_cols).  Synchronous on `stream`.  Returns SRG_OK or SRG_ERR_INVALID. */
 int srg_csr_validate(const int64_t* indptr, const int32_t* indices, int64_t n_rows,

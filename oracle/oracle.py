@@ -9,6 +9,9 @@ does, and it must not be used as a fallback.
                   GraphOp hop loop                     SSRG/operators/base_operator.py:19-36
   ref_spmm        the reference's own matmul.c, compiled from its source by oracle/Makefile into
                   oracle/_ref/libmatmul_ref.so (the shipped prebuilt libmatmul.so is never loaded)
+  combine         restates MessageOp.combine for last / sum / mean / simple_weighted with the same
+                  torch CPU operations           SSRG/operators/message_operator/*_message_op.py,
+                                                 SSRG/operators/utils.py:426-437
   laplacian, cheby_coeffs, cheby_op
                   restate the wavelet basis' pygsp calls (SSRG/models/base_scalable/
                   base_model.py:180-191, 236-265): PARITY UNPINNED -- pygsp is not in the
@@ -252,3 +255,31 @@ def cheby_op(L, coeffs, S, lmax):
     if rc != 0:
         raise ValueError("cheby_op needs at least 2 coefficients")
     return R
+
+
+def combine(aggr, feat_list, start=None, end=None, alpha=None, weight_list=None):
+    """MessageOp.combine on a list of torch CPU fp32 panels, with the reference's own torch ops:
+    last_message_op.py:9-10, sum_message_op.py:9-10, mean_message_op.py:9-10 and
+    simple_weighted_message_op.py:36-53 -> utils.py:426-437 (vstack of flattened panels, product
+    with the fp32 weight column, dim-0 sum)."""
+    import torch
+    if aggr == "last":
+        return feat_list[-1]
+    if aggr == "sum":
+        return sum(feat_list[start:end])
+    if aggr == "mean":
+        return sum(feat_list[start:end]) / (end - start)
+    if aggr == "simple_weighted":
+        if alpha is not None:
+            w = [alpha]
+            for _ in range(len(feat_list) - 1):
+                w.append((1 - alpha) * w[-1])
+            w = torch.FloatTensor(w[start:end])
+        else:
+            w = torch.FloatTensor(weight_list)
+        sel = feat_list[start:end]
+        assert len(sel) == w.shape[0]
+        shape = sel[0].shape
+        stack = torch.vstack([f.view(1, -1).squeeze(0) for f in sel])
+        return (stack * w.view(-1, 1)).sum(dim=0).view(shape)
+    raise ValueError(aggr)

@@ -569,6 +569,88 @@ k_cheby(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
 }
 
 // ------------------------------------------------------------------------------------------------
+// hop aggregation (fused SGC / SSGC / GBP precompute: MessageOp.combine without the K+1 panels)
+//
+// The reference combines the hop list on the host (SSRG/operators/message_operator/{sum,mean,
+// simple_weighted}_message_op.py, operators/utils.py:426-437).  Python's sum() is a left-to-right
+// accumulation from +0; one_dim_weighted_add is torch's CPU dim-0 sum of rounded products, whose
+// order (ATen cascade_sum) the host plans as a sequence of the element-wise steps below:
+//   INIT: agg = 0 + w*y      ADD: agg = agg + w*y      DIV: agg = agg / w
+// with separate multiply / add / correctly rounded divide (no contraction).  The last < 32 flat
+// elements of a weighted sum take torch's scalar row_sum order instead (k_tail_*).
+// ------------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+k_hop_accumulate(float* __restrict__ agg, int64_t lda, const float* __restrict__ y, int64_t ldy,
+                 int64_t n_rows, int d, float w, int mode)
+{
+    // one wave per row (grid-stride over rows), lanes stride the columns: no index division
+    const int lane = threadIdx.x & 63;
+    const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
+    for (int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); r < n_rows; r += waves) {
+        float* a = agg + r * lda;
+        const float* yr = y + r * ldy;
+        for (int c = lane; c < d; c += 64) {
+            if (mode == SRG_ACC_DIV) {
+                a[c] = __fdiv_rn(a[c], w);
+            } else {
+                const float p = __fmul_rn(w, yr[c]);
+                a[c] = __fadd_rn(mode == SRG_ACC_INIT ? 0.0f : a[c], p);
+            }
+        }
+    }
+}
+
+// torch's multi_row_sum (ATen/native/cpu/SumKernel.cpp) for one element over `count` rows of the
+// tail history, rows start, start + stride, ...: 16-row blocks folded into 4 levels.
+__device__ float torch_multi_row_sum(const float* hist, int start, int stride, int count, int e)
+{
+    int clog2 = 1;
+    if (count > 2) clog2 = 32 - __clz(count - 1);
+    const int lp = clog2 / 4 > 4 ? clog2 / 4 : 4;
+    const int step = 1 << lp, mask = step - 1;
+    float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    int i = 0;
+    while (i + step <= count) {
+        for (int j = 0; j < step; ++j, ++i)
+            acc[0] = __fadd_rn(acc[0], hist[(int64_t)(start + i * stride) * SRG_TAIL_MAX + e]);
+        for (int j = 1; j < 4; ++j) {
+            acc[j] = __fadd_rn(acc[j], acc[j - 1]);
+            acc[j - 1] = 0.0f;
+            if ((i & (mask << (j * lp))) != 0) break;
+        }
+    }
+    for (; i < count; ++i) acc[0] = __fadd_rn(acc[0], hist[(int64_t)(start + i * stride) * SRG_TAIL_MAX + e]);
+    for (int j = 1; j < 4; ++j) acc[0] = __fadd_rn(acc[0], acc[j]);
+    return acc[0];
+}
+
+// hist[term][e] = w * y[flat_start + e] (the rounded products of one hop's tail elements)
+__global__ void k_tail_record(float* __restrict__ hist, const float* __restrict__ y, int64_t ldy, int d,
+                              int64_t flat_start, int len, float w)
+{
+    const int e = threadIdx.x;
+    if (e >= len) return;
+    const int64_t f = flat_start + e;
+    hist[e] = __fmul_rn(w, y[(f / d) * ldy + f % d]);
+}
+
+// torch's row_sum (4 interleaved partial sums, remainder into the first, then folded) over the
+// recorded terms, stored as out = 0 + sum
+__global__ void k_tail_rowsum(float* __restrict__ agg, int64_t lda, int d, int64_t flat_start, int len,
+                              const float* __restrict__ hist, int n_terms)
+{
+    const int e = threadIdx.x;
+    if (e >= len) return;
+    const int n4 = n_terms / 4;
+    float p[4];
+    for (int c = 0; c < 4; ++c) p[c] = torch_multi_row_sum(hist, c, 4, n4, e);
+    for (int i = 4 * n4; i < n_terms; ++i) p[0] = __fadd_rn(p[0], hist[(int64_t)i * SRG_TAIL_MAX + e]);
+    for (int c = 1; c < 4; ++c) p[0] = __fadd_rn(p[0], p[c]);
+    const int64_t f = flat_start + e;
+    agg[(f / d) * lda + f % d] = __fadd_rn(0.0f, p[0]);
+}
+
+// ------------------------------------------------------------------------------------------------
 // validation kernel
 // ------------------------------------------------------------------------------------------------
 __global__ void k_validate(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
@@ -968,6 +1050,51 @@ int srg_cheby_step_f32(const int64_t* indptr, const int32_t* indices, const floa
     return launch_cheby<float>(indptr, indices, values, n_rows, row_order, Tc, To, Tn, ld, d, mode,
                                a1, a2, coef_prev, coef, n_scales, R, r_stride,
                                static_cast<hipStream_t>(stream));
+}
+
+int srg_hop_accumulate_f32(float* agg, int64_t lda, const float* y, int64_t ldy, int64_t n_rows,
+                           int32_t d, float w, int mode, void* stream)
+{
+    if (mode != SRG_ACC_INIT && mode != SRG_ACC_ADD && mode != SRG_ACC_DIV)
+        return fail(SRG_ERR_INVALID, "accumulate mode %d", mode);
+    if (n_rows < 0 || d < 0 || lda < d || (mode != SRG_ACC_DIV && ldy < d))
+        return fail(SRG_ERR_INVALID, "bad shape n_rows=%lld d=%d lda=%lld ldy=%lld", (long long)n_rows, d,
+                    (long long)lda, (long long)ldy);
+    if (n_rows == 0 || d == 0) return ok();
+    if (!agg || (mode != SRG_ACC_DIV && !y)) return fail(SRG_ERR_INVALID, "null pointer");
+    const unsigned blocks = (unsigned)std::min<int64_t>((n_rows + 3) / 4, 256 * 16);
+    hipLaunchKernelGGL(k_hop_accumulate, dim3(blocks), dim3(256), 0, static_cast<hipStream_t>(stream),
+                       agg, lda, y, ldy, n_rows, d, w, mode);
+    SRG_HIP_CHECK(hipGetLastError());
+    return ok();
+}
+
+int srg_tail_record_f32(float* hist, const float* y, int64_t ldy, int32_t d, int64_t flat_start,
+                        int32_t len, float w, void* stream)
+{
+    if (d <= 0 || ldy < d || flat_start < 0 || len < 0 || len > SRG_TAIL_MAX)
+        return fail(SRG_ERR_INVALID, "bad tail d=%d ldy=%lld flat_start=%lld len=%d", d, (long long)ldy,
+                    (long long)flat_start, len);
+    if (len == 0) return ok();
+    if (!hist || !y) return fail(SRG_ERR_INVALID, "null pointer");
+    hipLaunchKernelGGL(k_tail_record, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream),
+                       hist, y, ldy, d, flat_start, len, w);
+    SRG_HIP_CHECK(hipGetLastError());
+    return ok();
+}
+
+int srg_tail_rowsum_f32(float* agg, int64_t lda, int32_t d, int64_t flat_start, int32_t len,
+                        const float* hist, int32_t n_terms, void* stream)
+{
+    if (d <= 0 || lda < d || flat_start < 0 || len < 0 || len > SRG_TAIL_MAX || n_terms < 0)
+        return fail(SRG_ERR_INVALID, "bad tail d=%d lda=%lld flat_start=%lld len=%d n_terms=%d", d,
+                    (long long)lda, (long long)flat_start, len, n_terms);
+    if (len == 0) return ok();
+    if (!agg || (n_terms > 0 && !hist)) return fail(SRG_ERR_INVALID, "null pointer");
+    hipLaunchKernelGGL(k_tail_rowsum, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream),
+                       agg, lda, d, flat_start, len, hist, n_terms);
+    SRG_HIP_CHECK(hipGetLastError());
+    return ok();
 }
 
 int srg_csr_validate(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t nnz,

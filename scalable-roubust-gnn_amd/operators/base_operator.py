@@ -7,6 +7,11 @@ the hop loop is `srgnn.spmm.propagate` (libsrgnn_hip.so, exact fma chains, bit-i
 reference's FloatCSRMulDenseOMP), and the K result panels come back in one batch of copies.
 
 `propagate_device` is the performance entry: same computation, device tensors in and out.
+
+`propagate_aggregate(adj, feature, msg_op)` is `msg_op.aggregate(self.propagate(adj, feature))` --
+the non-learnable branch of BaseSGModel.preprocess (SSRG/models/base_scalable/base_model.py:34-44)
+-- without the hop list: srgnn.aggregate folds each hop into the result as it is produced, in the
+reference's own summation order (bit-identical), so only 4-5 panels are ever resident.
 """
 from __future__ import annotations
 
@@ -81,6 +86,26 @@ class GraphOp:
             A = self._operator(device)
             X = torch.from_numpy(np.ascontiguousarray(feature)).to(A.device)
         return _device_propagate(A, X, self.prop_steps)
+
+    def propagate_aggregate(self, adj, feature, msg_op, device=None, to_host=True):
+        """msg_op.aggregate(self.propagate(adj, feature)) for msg_op in last / sum / mean /
+        simple_weighted, computed on the GPU without materialising the K+1 hops.  Same checks
+        and errors as propagate(); learnable message ops raise ValueError (they need the list)."""
+        from srgnn.aggregate import fused_combine
+        if isinstance(feature, Tensor) and feature.is_cuda:
+            self.adj = self.construct_adj(adj)
+            if not isinstance(adj, sp.csr_matrix):
+                raise TypeError("The adjacency matrix must be a scipy csr sparse matrix!")
+            if self.adj.shape[1] != feature.shape[0]:
+                raise ValueError("Dimension mismatch detected for the adjacency and the feature matrix!")
+            A = self._operator(feature.device)
+            X = feature.to(torch.float32).contiguous()
+        else:
+            feature = self._checked_inputs(adj, feature)
+            A = self._operator(device)
+            X = torch.from_numpy(np.ascontiguousarray(feature)).to(A.device, torch.float32)
+        out = fused_combine(A, X, max(self.prop_steps, 0), msg_op)
+        return out.cpu() if to_host else out
 
 
 # Might include training parameters

@@ -23,6 +23,11 @@ SRG_SPMM_NT_STORE = 0x2
 SRG_CHEBY_INIT = 0
 SRG_CHEBY_STEP = 1
 
+SRG_ACC_INIT = 0
+SRG_ACC_ADD = 1
+SRG_ACC_DIV = 2
+SRG_TAIL_MAX = 32
+
 # every symbol include/srgnn_hip.h declares (checked by tests/test_capi.py)
 EXPORTED_SYMBOLS = (
     "FloatCSRMulDenseOMP",
@@ -31,6 +36,9 @@ EXPORTED_SYMBOLS = (
     "srg_propagate_khop_f32",
     "srg_cheby_step_f64",
     "srg_cheby_step_f32",
+    "srg_hop_accumulate_f32",
+    "srg_tail_record_f32",
+    "srg_tail_rowsum_f32",
     "srg_csr_validate",
     "srg_last_error",
     "srg_last_error_code",
@@ -65,6 +73,12 @@ def _declare(lib):
     lib.srg_cheby_step_f32.argtypes = [_p, _p, _p, _i64, _p, _p, _p, _p, _i64, _i32, ctypes.c_int,
                                        _f32, _f32, _p, _p, _i32, _p, _i64, _p]
     lib.srg_cheby_step_f32.restype = ctypes.c_int
+    lib.srg_hop_accumulate_f32.argtypes = [_p, _i64, _p, _i64, _i64, _i32, _f32, ctypes.c_int, _p]
+    lib.srg_hop_accumulate_f32.restype = ctypes.c_int
+    lib.srg_tail_record_f32.argtypes = [_p, _p, _i64, _i32, _i64, _i32, _f32, _p]
+    lib.srg_tail_record_f32.restype = ctypes.c_int
+    lib.srg_tail_rowsum_f32.argtypes = [_p, _i64, _i32, _i64, _i32, _p, _i32, _p]
+    lib.srg_tail_rowsum_f32.restype = ctypes.c_int
     lib.srg_csr_validate.argtypes = [_p, _p, _i64, _i64, _i64, _p]
     lib.srg_csr_validate.restype = ctypes.c_int
     lib.srg_last_error.argtypes = []

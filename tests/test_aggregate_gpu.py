@@ -1,0 +1,100 @@
+"""Fused hop aggregation on the GPU vs the reference's MessageOp.combine on the full hop list.
+
+Expected values: the hop list from the oracle (bit-exact to the reference, pinned by the golden
+fixtures) combined by oracle.combine (the reference's own torch CPU operations).  Bar: bit-exact.
+"""
+import numpy as np
+import pytest
+import torch
+
+import golden_cases as G
+
+pytestmark = pytest.mark.gpu
+
+
+class _Msg:
+    def __init__(self, aggr, start=None, end=None, combination_type=None, alpha=None, weight_list=None):
+        self.aggr_type, self.start, self.end = aggr, start, end
+        self.combination_type, self.alpha, self.weight_list = combination_type, alpha, weight_list
+
+
+def _ops(K):
+    return [
+        _Msg("last"), _Msg("sum", 0, K + 1), _Msg("mean", 1, K + 1), _Msg("mean", 0, K + 2),
+        _Msg("simple_weighted", 0, K + 1, "alpha", alpha=0.15),
+        _Msg("simple_weighted", 2, K, "alpha", alpha=0.5),
+        _Msg("simple_weighted", 1, 3, "hand_crafted", weight_list=torch.FloatTensor([0.7, -0.3])),
+    ]
+
+
+def _expected(oracle_mod, msg, hops):
+    feats = [torch.from_numpy(h) for h in hops]
+    return oracle_mod.combine(msg.aggr_type, feats, msg.start, msg.end, alpha=msg.alpha,
+                              weight_list=msg.weight_list).numpy()
+
+
+@pytest.mark.parametrize("K", [3, 10, 20])
+@pytest.mark.parametrize("name", ["cora_sym_k3", "pubmed_sym_k3", "rand_d1_r05", "rand_d130_r1",
+                                  "rand_d36_ppr", "rand_d1433_r05"])
+def test_fused_combine_bit_exact(oracle_mod, name, K):
+    from srgnn.aggregate import fused_combine
+    from srgnn.csr import DeviceCSR
+    c = G.Case(name)
+    ip, ix, v = c.ahat()
+    x = c.x()
+    hops = oracle_mod.propagate(ip, ix, v, x, K)
+    for k in range(1, min(K, c.k) + 1):            # the oracle's hops are the reference's
+        c.check_hop(k, hops[k])
+    A = DeviceCSR.from_tensors(ip, ix, v, n_cols=c.n, device="cuda")
+    X = torch.from_numpy(x).cuda()
+    for msg in _ops(K):
+        got = fused_combine(A, X, K, msg).cpu().numpy()
+        want = _expected(oracle_mod, msg, hops)
+        np.testing.assert_array_equal(got, want, err_msg=f"{name} K={K} {msg.aggr_type} {msg.start}:{msg.end}")
+
+
+def test_graphop_propagate_aggregate_matches_aggregate_of_propagate():
+    """operators API: GraphOp.propagate_aggregate(adj, x, msg) == msg.aggregate(GraphOp.propagate(adj, x))."""
+    from operators.graph_operator.symmetrical_simgraph_laplacian_operator import SymLaplacianGraphOp
+    from operators.message_operator.last_message_op import LastMessageOp
+    from operators.message_operator.mean_message_op import MeanMessageOp
+    from operators.message_operator.simple_weighted_message_op import SimpleWeightedMessageOp
+    from operators.message_operator.sum_message_op import SumMessageOp
+    c = G.Case("cora_sym_k3")
+    x = c.x()
+    for K in (2, 12):
+        op = SymLaplacianGraphOp(K, r=0.5)
+        feats = op.propagate(c.adj(), x)
+        for msg in (LastMessageOp(), SumMessageOp(0, K + 1), MeanMessageOp(1, K + 1),
+                    SimpleWeightedMessageOp(0, K + 1, "alpha", 0.1),
+                    SimpleWeightedMessageOp(1, 3, "hand_crafted", [0.25, 0.75])):
+            want = msg.aggregate(feats).numpy()
+            got = op.propagate_aggregate(c.adj(), x, msg)
+            assert isinstance(got, torch.Tensor) and got.dtype == torch.float32 and not got.is_cuda
+            np.testing.assert_array_equal(got.numpy(), want, err_msg=f"K={K} {msg.aggr_type}")
+    op = SymLaplacianGraphOp(3, r=0.5)
+    with pytest.raises(TypeError):
+        op.propagate_aggregate(c.adj().tocoo(), x, SumMessageOp(0, 4))
+    with pytest.raises(ValueError):
+        op.propagate_aggregate(c.adj(), x[:-1], SumMessageOp(0, 4))
+
+
+def test_products_scale_weighted_bit_exact():
+    """Full products-shaped graph, K = 10, GBP-style alpha weights: the fused result equals the
+    reference's one_dim_weighted_add of the hop list (hops from the GPU, bit-exact by the hop tests)."""
+    from srgnn import graphs, synth
+    from srgnn.aggregate import fused_combine
+    from srgnn.csr import DeviceCSR
+    from srgnn.spmm import propagate
+    import oracle.oracle as O
+    ip, ix, vals, n, d, K = graphs.build("products", "cuda")
+    A = DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, device="cuda")
+    del ip, ix, vals
+    x = synth.uniform_features_t(n, d, device="cuda")
+    msg = _Msg("simple_weighted", 0, K + 1, "alpha", alpha=0.15)
+    got = fused_combine(A, x, K, msg).cpu()
+    hops = [h.cpu() for h in propagate(A, x, K)]
+    want = O.combine("simple_weighted", hops, 0, K + 1, alpha=0.15)
+    assert torch.equal(got, want)
+    got = fused_combine(A, x, K, _Msg("mean", 0, K + 1)).cpu()
+    assert torch.equal(got, O.combine("mean", hops, 0, K + 1))
