@@ -189,6 +189,40 @@ class _DeviceSteps:
         return self.slots[0]
 
 
+def step_hop(s):
+    """The hop a step reads (None for folds / div / rowsum)."""
+    if s[0] == "acc":
+        return s[2]
+    if s[0] == "tail":
+        return s[1]
+    return None
+
+
+def schedule(steps):
+    """Groups steps by the hop they wait for: ([steps run when hop k appears] for k = 0..last,
+    [steps run after the last hop]).  Steps that read no hop run with the preceding ones."""
+    groups, trailing, cur = [], [], -1
+    for s in steps:
+        k = step_hop(s)
+        if k is None:
+            (groups[cur] if cur >= 0 else trailing).append(s)
+            continue
+        if k < cur:
+            raise ValueError("steps must visit hops in increasing order")
+        while cur < k:
+            groups.append([])
+            cur += 1
+        groups[k].append(s)
+    if groups:                                   # folds after the last hop's terms go last
+        last = groups[-1]
+        i = len(last)
+        while i > 0 and step_hop(last[i - 1]) is None:
+            i -= 1
+        trailing = last[i:] + trailing
+        del last[i:]
+    return groups, trailing
+
+
 def propagate_aggregate(A: DeviceCSR, X: torch.Tensor, K: int, steps=None, last_only: bool = False):
     """Runs hops 1..K of Â on the device panel X ([n, d], row-major) with two ping-pong panels and
     executes `steps` (combine_steps) as each hop appears; returns the aggregated panel, or Â^K X
@@ -198,27 +232,18 @@ def propagate_aggregate(A: DeviceCSR, X: torch.Tensor, K: int, steps=None, last_
         raise ValueError("propagate_aggregate needs a square operator matching X")
     if X.dim() != 2 or X.dtype != torch.float32 or X.stride(1) != 1 or X.stride(0) < d:
         raise ValueError("X must be a row-major float32 [n, d] device panel")
-    steps = list(steps or [])
-    need = [s[2] for s in steps if s[0] == "acc"]
-    if any(k < 0 or k > K for k in need):
+    groups, trailing = schedule(steps or [])
+    if len(groups) > K + 1:
         raise ValueError("hop index out of range")
-    last = K if last_only else (max(need) if need else 0)
+    last = K if last_only else len(groups) - 1
     ex = None if last_only else _DeviceSteps(n, d, X.device)
-    pos = 0
 
     def consume(k, panel):
-        nonlocal pos
-        while pos < len(steps):
-            s = steps[pos]
-            if s[0] in ("acc", "tail") and s[2] != k:
-                if s[2] < k:
-                    raise ValueError("steps must visit hops in increasing order")
-                return
-            ex.run(s, panel if s[0] in ("acc", "tail") else None)
-            pos += 1
+        if ex is not None and k < len(groups):
+            for s in groups[k]:
+                ex.run(s, panel if step_hop(s) is not None else None)
 
-    if not last_only:
-        consume(0, X)
+    consume(0, X)
     cur = X
     if last >= 1:
         bufs = [torch.empty((n, d), dtype=torch.float32, device=X.device) for _ in range(min(2, last))]
@@ -226,13 +251,11 @@ def propagate_aggregate(A: DeviceCSR, X: torch.Tensor, K: int, steps=None, last_
             nxt = bufs[(k - 1) % len(bufs)]
             spmm(A, cur, out=nxt)
             cur = nxt
-            if not last_only:
-                consume(k, cur)
+            consume(k, cur)
     if last_only:
         return cur.clone() if cur is X else cur
-    while pos < len(steps):                       # folds / div / rowsum after the last hop
-        ex.run(steps[pos])
-        pos += 1
+    for s in trailing:
+        ex.run(s)
     return ex.result()
 
 

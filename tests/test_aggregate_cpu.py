@@ -95,11 +95,19 @@ def _ref(msg, hops):
 
 
 def _fused_np(msg, hops):
+    """Plan -> hop schedule (as propagate_aggregate consumes it) -> numpy execution."""
     mode, terms, div = G.combine_plan(msg, len(hops))
     if mode == "last":
         return hops[-1]
     n, d = hops[0].shape
-    return run_steps_np(G.combine_steps(mode, terms, div), hops, n, d)
+    steps = G.combine_steps(mode, terms, div)
+    groups, trailing = G.schedule(steps)
+    assert len(groups) <= len(hops)
+    flat = [s for g in groups for s in g] + trailing
+    assert sorted(map(id, flat)) == sorted(map(id, steps))
+    for k, g in enumerate(groups):
+        assert all(G.step_hop(s) in (k, None) for s in g)
+    return run_steps_np(flat, hops, n, d)
 
 
 SHAPES = [(7, 1), (3, 3), (5, 7), (40, 33), (101, 13), (256, 128), (37, 500)]
