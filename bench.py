@@ -56,6 +56,10 @@ def parse():
     ap.add_argument("--nt-store", action="store_true")
     ap.add_argument("--exchange", default="halo", choices=["halo", "allgather"])
     ap.add_argument("--chunks", type=int, default=4, help="halo exchange groups per hop")
+    ap.add_argument("--mode", default="auto", choices=["auto", "panels", "last"],
+                    help="panels: all K+1 hop panels kept (GraphOp.propagate); last: two ping-pong "
+                         "panels, only A^K X kept (SGC-style, fused aggregation); auto: panels if "
+                         "they fit in HBM")
     return ap.parse_args()
 
 
@@ -63,32 +67,85 @@ def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
 
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _omp_set_threads(k):
+    """Sets the OpenMP team size of the system libgomp (the one matmul.c / the oracle link)."""
+    import ctypes
+    try:
+        ctypes.CDLL("libgomp.so.1").omp_set_num_threads(int(k))
+        return True
+    except OSError:
+        return False
+
+
 def cpu_baseline(ip, ix, vals, x_host, n, d, budget_s):
-    """The reference's FloatCSRMulDenseOMP (built from SSRG/operators/csrc/matmul.c) on the host."""
+    """The reference's FloatCSRMulDenseOMP (built from SSRG/operators/csrc/matmul.c) on the host:
+    whole hops, all threads, for ~budget_s; plus a 1-thread rate on a row block.  When the graph
+    overflows the reference's int32 offsets (nnz >= 2^31 or N*d >= 2^31, matmul.c:29,33) the
+    oracle's int64 restatement of the same fma chains runs instead, on row blocks ("port")."""
     from oracle import oracle as O
-    L = O.ref_lib()
-    if L is None:
-        return None
-    ip32 = np.ascontiguousarray(ip, dtype=np.int32)
+    nnz = int(ip[-1])
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
+    use_ref = nnz < 2 ** 31 and n * d < 2 ** 31 and O.ref_lib() is not None
+    cur = np.ascontiguousarray(x_host)
     ix32 = np.ascontiguousarray(ix, dtype=np.int32)
     v32 = np.ascontiguousarray(vals, dtype=np.float32)
-    cur = np.ascontiguousarray(x_host)
-    nxt = np.zeros_like(cur)
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
-    hops = 0
-    t0 = time.perf_counter()
+    if use_ref:
+        L = O.ref_lib()
+        ip32 = np.ascontiguousarray(ip, dtype=np.int32)
+
+        def rows(r0, r1, src, dst):      # dst rows [r0, r1) of one hop, zeroed first
+            dst[r0:r1].fill(0.0)
+            L.FloatCSRMulDenseOMP(O._ptr(dst[r0:]), O._ptr(v32), O._ptr(ix32), O._ptr(ip32[r0:]),
+                                  O._ptr(src), r1 - r0, d)
+    else:
+        ip64 = np.ascontiguousarray(ip, dtype=np.int64)
+
+        def rows(r0, r1, src, dst):
+            O.spmm(ip64[r0:r1 + 1], ix32, v32, src, out=dst[r0:r1])
+    nxt = np.empty_like(cur)
+    _omp_set_threads(threads)
+    edges, hops, t0 = 0, 0, time.perf_counter()
+    block = n if use_ref else max(1, int(n * min(1.0, 2e8 / max(nnz, 1))))
+    r0 = 0
     while True:
-        nxt.fill(0.0)
-        L.FloatCSRMulDenseOMP(O._ptr(nxt), O._ptr(v32), O._ptr(ix32), O._ptr(ip32), O._ptr(cur), n, d)
-        hops += 1
-        cur, nxt = nxt, cur
+        r1 = min(n, r0 + block)
+        rows(r0, r1, cur, nxt)
+        edges += int(ip[r1] - ip[r0])
+        r0 = r1
+        if r0 == n:
+            hops += 1
+            r0 = 0
+            cur, nxt = nxt, cur
         if time.perf_counter() - t0 >= budget_s:
             break
     dt = time.perf_counter() - t0
-    nnz = int(ip32[-1])
-    return {"value": hops * nnz / dt, "unit": "propagated edges/s", "cores": threads, "kind": "reference",
-            "sample": f"{hops} hop(s) of the full {n}-node graph (nnz {nnz}, d {d}), kernel-only on "
-                      f"pre-converted int32/fp32 buffers, OMP_NUM_THREADS={threads}, {dt:.1f} s"}
+    # 1 thread, a row block of ~1/8 of the budget
+    one = None
+    if _omp_set_threads(1):
+        r1 = max(1, int(n * min(1.0, (budget_s / 8) * edges / dt / threads / max(nnz, 1))))
+        t1 = time.perf_counter()
+        rows(0, r1, cur, nxt)
+        one = int(ip[r1] - ip[0]) / (time.perf_counter() - t1)
+        _omp_set_threads(threads)
+    what = "the reference's FloatCSRMulDenseOMP (oracle/_ref, built from matmul.c)" if use_ref else \
+        "the oracle's int64 C restatement (the reference's int32 matmul.c cannot address this graph)"
+    return {"value": edges / dt, "unit": "propagated edges/s", "cores": threads,
+            "kind": "reference" if use_ref else "port",
+            "value_1thread": one, "cpu_model": _cpu_model(),
+            "sample": f"{what}: {edges} propagated edges ({hops} full hop(s) + row blocks) of the "
+                      f"{n}-node graph (nnz {nnz}, d {d}), kernel-only on pre-converted int32/fp32 "
+                      f"buffers, OMP_NUM_THREADS={threads}, {dt:.1f} s; value_1thread on a row block"}
 
 
 def pmc_traffic(config, kernel_hint="k_spmm"):
@@ -127,14 +184,27 @@ def main():
     log(f"graph {a.config}: n={n} nnz={nnz} d={d} K={K} built in {time.perf_counter() - t_build:.1f}s")
 
     stream = torch.cuda.current_stream(dev)
+    mode = a.mode
     if world == 1:
         A = DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, heavy_threshold=a.heavy_threshold, device=dev)
         log(f"schedule: n_hub={A.n_hub} n_heavy={A.n_heavy}")
-        buf = torch.empty((K, n, d), dtype=torch.float32, device=dev)
-        panels = [X] + [buf[k] for k in range(K)]
+        if mode == "auto":
+            free, _ = torch.cuda.mem_get_info(dev)
+            mode = "panels" if K * n * d * 4 < 0.9 * free else "last"
+            log(f"mode {mode}: {K} panels need {K * n * d * 4 / 1e9:.1f} GB, {free / 1e9:.1f} GB free")
+        if mode == "panels":
+            buf = torch.empty((K, n, d), dtype=torch.float32, device=dev)
+            panels = [X] + [buf[k] for k in range(K)]
 
-        def step():
-            propagate(A, X, K, panels=panels, nt_store=a.nt_store)
+            def step():
+                propagate(A, X, K, panels=panels, nt_store=a.nt_store)
+        else:
+            from srgnn.aggregate import propagate_aggregate
+            panels = [X, None]
+
+            def step():
+                panels[1] = None
+                panels[1] = propagate_aggregate(A, X, K, last_only=True)
         local_rows, local_nnz = n, nnz
     elif a.exchange == "allgather":
         from srgnn.dist import RowPartitionedOperator
@@ -193,6 +263,8 @@ def main():
     if world == 1:
         def one_hop():
             spmm(A, panels[0], out=panels[1], nt_store=a.nt_store)
+        if panels[1] is None:
+            panels[1] = torch.empty_like(X)
     elif a.exchange == "allgather":
         src = op._gather(panels[0])
 
@@ -230,7 +302,9 @@ def main():
         "config": {"workload": f"{a.config}-shaped K-hop propagate", "n_nodes": n, "nnz_ahat": nnz,
                    "d": d, "K": K, "normalization": "sym r=0.5",
                    "parallelism": f"row-partition x{world}" + (f" ({a.exchange} exchange)" if world > 1 else ""),
-                   "mode": "exact (bit-identical to reference)"},
+                   "mode": "exact (bit-identical to reference)",
+                   "outputs": ("all K+1 hop panels" if mode in ("panels", "auto") else "last hop only (2 ping-pong panels)")
+                   if world == 1 else "all K+1 hop panels (row slices)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
                      "frac": achieved / peak, "traffic": traffic,
                      "kernel": "k_spmm (+ k_spmm_hub beside it): one hop" + (" of rank 0's rows" if world > 1 else ""),

@@ -229,12 +229,17 @@ __device__ __forceinline__ void row_gather(typename Vec<T, VEC>::type& acc,
     }
 }
 
-__device__ __forceinline__ int wave_slot()
+__device__ __forceinline__ int wave_slot(int block_base)
 {
     // wave-uniform by construction; readfirstlane makes that provable to the compiler so that the
     // row's index stream goes through the scalar path.
-    return __builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)));
+    return __builtin_amdgcn_readfirstlane((int)((block_base + (int)blockIdx.x) * kWavesPerBlock + (threadIdx.x >> 6)));
 }
+
+// A dispatch holds < 2^32 work-items per dimension: launches of more rows than that (111 M rows
+// of the papers100M-shaped graph = 7.1e9 lanes) go out in chunks of kMaxLaunchBlocks blocks, the
+// kernel adding the chunk's block_base to blockIdx.x.
+constexpr int64_t kMaxLaunchBlocks = int64_t(1) << 23;
 
 // ------------------------------------------------------------------------------------------------
 // SpMM: Y = A * X  (or Y += A * X)
@@ -324,21 +329,22 @@ __global__ void __launch_bounds__(kBlock)
 k_spmm(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
        const float* __restrict__ vals, const int32_t* __restrict__ order, int n_rows, int n_heavy,
        int n_slices, int nb_heavy, const float* __restrict__ X, int64_t ldx, float* __restrict__ Y,
-       int64_t ldy, int d, int accumulate, int nt)
+       int64_t ldy, int d, int accumulate, int nt, int block_base)
 {
     typedef typename Vec<float, VEC>::type V;
+    const int bid = block_base + (int)blockIdx.x;
     __shared__ __attribute__((aligned(16))) float lds[kWavesPerBlock * 2 * 256];
     const int lane = threadIdx.x & 63;
     const int wib = threadIdx.x >> 6;
-    if ((int)blockIdx.x < nb_heavy) {
-        const int item = __builtin_amdgcn_readfirstlane((int)blockIdx.x * kWavesPerBlock + wib);
+    if (bid < nb_heavy) {
+        const int item = __builtin_amdgcn_readfirstlane(bid * kWavesPerBlock + wib);
         if (item >= n_heavy * n_slices) return;
         const int row = order[item / n_slices];
         slice_wave<UH, SFULL, IP>(indptr, indices, vals, row, item % n_slices, X, ldx, Y, ldy, d,
                            accumulate, nt, lds + wib * 2 * 256);
         return;
     }
-    const int w = __builtin_amdgcn_readfirstlane(((int)blockIdx.x - nb_heavy) * kWavesPerBlock + wib) + n_heavy;
+    const int w = __builtin_amdgcn_readfirstlane((bid - nb_heavy) * kWavesPerBlock + wib) + n_heavy;
     if (w >= n_rows) return;
     const int row = order ? order[w] : w;
     float* __restrict__ yrow = Y + (int64_t)row * ldy;
@@ -524,10 +530,11 @@ __global__ void __launch_bounds__(kBlock)
 k_cheby(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
         const T* __restrict__ vals, const int32_t* __restrict__ order, int n_rows,
         const T* __restrict__ Tc, const T* __restrict__ To, T* __restrict__ Tn, int64_t ld, int d,
-        int mode, T a1, T a2, ChebyCoef<T> cf, int n_scales, T* __restrict__ R, int64_t r_stride)
+        int mode, T a1, T a2, ChebyCoef<T> cf, int n_scales, T* __restrict__ R, int64_t r_stride,
+        int block_base)
 {
     typedef typename Vec<T, VEC>::type V;
-    const int w = wave_slot();
+    const int w = wave_slot(block_base);
     if (w >= n_rows) return;
     const int row = order ? order[w] : w;
     const int lane = threadIdx.x & 63;
@@ -802,12 +809,13 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
     if (blocks > INT32_MAX) return fail(SRG_ERR_INVALID, "grid too large");
     const int vec = pick_vec(d, ldx, ldy, X, Y, sizeof(float));
     const int nr = (int)m_rows, nh = (int)n_heavy;
-    if (blocks > 0) {
-        const dim3 grid((unsigned)blocks);
+    for (int64_t b0 = 0; b0 < blocks; b0 += kMaxLaunchBlocks) {
+        const dim3 grid((unsigned)std::min<int64_t>(kMaxLaunchBlocks, blocks - b0));
+        const int bb = (int)b0;
 #define SRG_LAUNCH_SPMM(V, F, SF)                                                               \
     hipLaunchKernelGGL((k_spmm<V, kUnroll, kUnrollHeavy, F, SF, IP>), grid, dim3(kBlock), 0, s,     \
                        indptr, indices, vals, morder, nr, nh, n_slices, nb_heavy, X, ldx, Y, ldy, \
-                       d, acc, nt)
+                       d, acc, nt, bb)
         const bool full = d % (64 * vec) == 0;        // implies d % 32 == 0
         if (vec == 4) {
             if (full) SRG_LAUNCH_SPMM(4, true, true);
@@ -866,20 +874,24 @@ int launch_cheby(const int64_t* indptr, const int32_t* indices, const T* vals, i
         cf.cur[i] = i < n_scales ? coef[i] : T(0);
     }
     if (n_rows == 0 || d == 0) return ok();
-    const dim3 grid((unsigned)((n_rows + kWavesPerBlock - 1) / kWavesPerBlock));
+    const int64_t blocks = (n_rows + kWavesPerBlock - 1) / kWavesPerBlock;
     const int vec = pick_vec(d, ld, ld, Tc, Tn, sizeof(T)) >= 2 && aligned(R, 2 * sizeof(T)) &&
                             (r_stride % 2 == 0) && (To == nullptr || aligned(To, 2 * sizeof(T)))
                         ? 2
                         : 1;
     const int nr = (int)n_rows;
-    if (vec == 2)
-        hipLaunchKernelGGL((k_cheby<T, 2, kUnroll>), grid, dim3(kBlock), 0, s, indptr, indices,
-                           vals, order, nr, Tc, To, Tn, ld, d, mode, a1, a2, cf, n_scales, R,
-                           r_stride);
-    else
-        hipLaunchKernelGGL((k_cheby<T, 1, kUnroll>), grid, dim3(kBlock), 0, s, indptr, indices,
-                           vals, order, nr, Tc, To, Tn, ld, d, mode, a1, a2, cf, n_scales, R,
-                           r_stride);
+    for (int64_t b0 = 0; b0 < blocks; b0 += kMaxLaunchBlocks) {
+        const dim3 grid((unsigned)std::min<int64_t>(kMaxLaunchBlocks, blocks - b0));
+        if (vec == 2)
+            hipLaunchKernelGGL((k_cheby<T, 2, kUnroll>), grid, dim3(kBlock), 0, s, indptr, indices,
+                               vals, order, nr, Tc, To, Tn, ld, d, mode, a1, a2, cf, n_scales, R,
+                               r_stride, (int)b0);
+        else
+            hipLaunchKernelGGL((k_cheby<T, 1, kUnroll>), grid, dim3(kBlock), 0, s, indptr, indices,
+                               vals, order, nr, Tc, To, Tn, ld, d, mode, a1, a2, cf, n_scales, R,
+                               r_stride, (int)b0);
+        SRG_HIP_CHECK(hipGetLastError());
+    }
     SRG_HIP_CHECK(hipGetLastError());
     return ok();
 }

@@ -44,3 +44,41 @@ def sym_norm_binary(indptr: torch.Tensor, indices: torch.Tensor, n: int, r: floa
     out_ptr = torch.zeros(n + 1, dtype=torch.int64, device=dev)
     out_ptr[1:] = torch.cumsum(counts, 0)
     return out_ptr, c_j.to(torch.int32), vals
+
+
+def sym_norm_edges_blocked(u: torch.Tensor, v: torch.Tensor, n: int, r: float = 0.5, block_nnz: int = 1 << 28):
+    """The same (indptr, indices, values) as symmetric_csr_t + sym_norm_binary, from the undirected
+    edge list (u, v) (unique pairs, no self-loops), built row block by row block so that no sort
+    or temporary exceeds ~block_nnz entries (billion-edge graphs)."""
+    dev = u.device
+    deg_a = torch.bincount(u, minlength=n) + torch.bincount(v, minlength=n)
+    indptr = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    indptr[1:] = torch.cumsum(deg_a + 1, 0)
+    nnz = int(indptr[-1])
+    left, right = degree_powers((deg_a + 1).cpu().numpy(), r)
+    del deg_a
+    left_t = torch.from_numpy(left).to(dev)
+    right_t = torch.from_numpy(right).to(dev)
+    indices = torch.empty(nnz, dtype=torch.int32, device=dev)
+    vals = torch.empty(nnz, dtype=torch.float32, device=dev)
+    n_blocks = max(1, -(-nnz // block_nnz))
+    cuts = torch.searchsorted(indptr, torch.arange(1, n_blocks, device=dev, dtype=torch.int64) * (nnz // n_blocks))
+    bounds = [0] + sorted(set(int(c) for c in cuts.cpu() if 0 < int(c) < n)) + [n]
+    for r0, r1 in zip(bounds[:-1], bounds[1:]):
+        m1 = (u >= r0) & (u < r1)
+        m2 = (v >= r0) & (v < r1)
+        diag = torch.arange(r0, r1, dtype=torch.int64, device=dev)
+        rows = torch.cat([u[m1].to(torch.int64), v[m2].to(torch.int64), diag])
+        cols = torch.cat([v[m1].to(torch.int64), u[m2].to(torch.int64), diag])
+        del m1, m2, diag
+        key = torch.sort((rows - r0) * n + cols).values
+        del rows, cols
+        rr = key // n + r0
+        cc = key % n
+        del key
+        a, b = int(indptr[r0]), int(indptr[r1])
+        assert b - a == cc.numel()
+        vals[a:b] = ((1.0 * left_t[rr]) * right_t[cc]).to(torch.float32)
+        indices[a:b] = cc.to(torch.int32)
+        del rr, cc
+    return indptr, indices, vals

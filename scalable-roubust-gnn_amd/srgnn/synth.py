@@ -191,6 +191,67 @@ def rmat_undirected_t(n: int, n_edges: int, seed: int = RMAT_SEED, device="cpu",
     return perm[lo], perm[hi]
 
 
+def nonzero_chunked(mask, chunk: int = 1 << 30):
+    """torch.nonzero(mask) of a 1-D bool tensor in < 2^31-element pieces (ascending positions)."""
+    parts = [torch.nonzero(mask[i:i + chunk]).squeeze(1) + i for i in range(0, mask.numel(), chunk)]
+    if not parts:
+        return torch.empty(0, dtype=torch.int64, device=mask.device)
+    return parts[0] if len(parts) == 1 else torch.cat(parts)
+
+
+def _first_occurrence(keys, buckets: int):
+    """Bool mask, True where keys[i] is the first occurrence of its value.  Keys are split into
+    hash buckets (equal keys share one) so that no sort exceeds ~numel/buckets elements."""
+    first = torch.zeros(keys.numel(), dtype=torch.bool, device=keys.device)
+    bits = max(1, (buckets - 1).bit_length())
+    shift = 64 - bits
+    for b in range(1 << bits):
+        h = _srl(keys * _to_i64(_GOLDEN), shift)
+        idx = nonzero_chunked(h == b)
+        del h
+        if idx.numel() == 0:
+            continue
+        k = keys[idx]
+        sk, perm = torch.sort(k, stable=True)
+        del k
+        newrun = torch.ones(sk.numel(), dtype=torch.bool, device=keys.device)
+        newrun[1:] = sk[1:] != sk[:-1]
+        first[idx[perm[newrun]]] = True
+    return first
+
+
+def rmat_undirected_blocked_t(n: int, n_edges: int, seed: int = RMAT_SEED, device="cpu", abcd=RMAT_ABCD,
+                              batch: int = 1 << 27, buckets: int = 64):
+    """The same edge list as rmat_undirected_t (first `n_edges` unique undirected edges of the
+    stream, relabelled), built with bounded temporaries for billion-edge graphs: candidates in
+    batches, duplicates found per hash bucket, no sort larger than ~1/buckets of the stream."""
+    scale = max(1, math.ceil(math.log2(max(n, 2))))
+    chunks, produced = [], 0
+    target = max(1024, int(n_edges * 1.35))
+    while True:
+        while produced < target:
+            b = min(batch, target - produced)
+            s, d = rmat_candidates_t(seed, produced, b, scale, abcd, device)
+            ok = (s < n) & (d < n) & (s != d)
+            chunks.append((torch.minimum(s, d) * n + torch.maximum(s, d))[ok])
+            del s, d, ok
+            produced += b
+        keys = chunks[0] if len(chunks) == 1 else torch.cat(chunks)
+        chunks = [keys]
+        first = _first_occurrence(keys, buckets)
+        cnt = int(first.sum())
+        if cnt >= n_edges:
+            break
+        del first
+        target = produced + max(1024, int((n_edges - cnt) * 1.6) + 1024)
+    pos = nonzero_chunked(first)[:n_edges]
+    del first
+    sel = keys[pos]
+    del keys, chunks, pos
+    perm = relabel_permutation_t(n, seed, device)
+    return perm[sel // n], perm[sel % n]
+
+
 def relabel_permutation_t(n: int, seed: int, device="cpu"):
     """new_id[old_id]: rank of hash(seed, 4, old_id) (ties broken by id; stable sort)."""
     h = hash_t(seed, 4, torch.arange(n, dtype=torch.int64, device=device))

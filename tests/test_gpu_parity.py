@@ -295,3 +295,27 @@ def test_halo_virtual_ranks_bitwise(world, chunks):
                                   device="cuda")
     for k in range(1, 4):
         assert torch.equal(got[k], want[k]), f"hop {k} differs with {world} virtual halo ranks"
+
+
+def test_launch_chunking_beyond_2e32_lanes(oracle_mod):
+    """More rows than one dispatch can hold (2^25 + rows -> > 2^31 lanes at 64 per row, chunked
+    launches with a block base): every row of a banded CSR checked, for the SpMM and Chebyshev."""
+    from srgnn.csr import DeviceCSR
+    from srgnn.spmm import spmm
+    n, d = (1 << 25) + 4099, 4
+    r = torch.arange(n, device="cuda", dtype=torch.int64)
+    # row i: columns i and (i + 7) mod n -> indptr 2i, stored sorted
+    c0, c1 = r, (r + 7) % n
+    cols = torch.stack([torch.minimum(c0, c1), torch.maximum(c0, c1)], 1).reshape(-1).to(torch.int32)
+    ip = torch.arange(0, 2 * n + 1, 2, device="cuda", dtype=torch.int64)
+    vals = ((r % 13).to(torch.float32) * 0.25 - 1.0).repeat_interleave(2)
+    vals[1::2] = 0.5
+    A = DeviceCSR.from_tensors(ip, cols, vals, n_cols=n, device="cuda", heavy_threshold=-1, hub_threshold=-1)
+    X = (torch.arange(n * d, device="cuda", dtype=torch.int64) % 1021).to(torch.float32).view(n, d) * 0.125
+    Y = spmm(A, X)
+    a0 = vals[0::2].view(n, 1)
+    x0 = X[cols[0::2].long()]
+    x1 = X[cols[1::2].long()]
+    want = torch.addcmul(torch.zeros_like(Y), a0, x0)       # 0 + a*x, then fma with 0.5*x1 (exact)
+    want = want + 0.5 * x1
+    assert torch.equal(Y, want)

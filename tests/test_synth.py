@@ -42,3 +42,19 @@ def test_rmat_deterministic_and_skewed():
     assert torch.equal(u1, u2) and torch.equal(v1, v2)
     deg = torch.bincount(torch.cat([u1, v1]), minlength=4096)
     assert int(deg.max()) > 20 * float(deg.float().mean())      # power-law hubs present
+
+
+def test_blocked_builders_equal_reference_builders():
+    """The bounded-temporary builders (billion-edge configs) give the same graph and Â."""
+    import torch
+    from srgnn import normalize
+    for n, m, batch, buckets in [(3000, 20000, 5000, 4), (20000, 90000, 1 << 14, 16), (257, 2000, 999, 3)]:
+        u0, v0 = synth.rmat_undirected_t(n, m, seed=5)
+        u1, v1 = synth.rmat_undirected_blocked_t(n, m, seed=5, batch=batch, buckets=buckets)
+        assert torch.equal(u0, u1) and torch.equal(v0, v1)
+        ip, ix = synth.symmetric_csr_t(n, u0, v0)
+        ref = normalize.sym_norm_binary(ip, ix, n, 0.5)
+        for blk in (1 << 12, 1 << 30):
+            got = normalize.sym_norm_edges_blocked(u0.to(torch.int32), v0.to(torch.int32), n, 0.5, block_nnz=blk)
+            for a, b in zip(got, ref):
+                assert torch.equal(a, b)
