@@ -298,7 +298,7 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (R-MAT power-law graph with the products node/edge counts, U[-1,1) features)",
+        "data": f"synthetic (R-MAT power-law graph with the {a.config} node/edge counts, U[-1,1) features)",
         "config": {"workload": f"{a.config}-shaped K-hop propagate", "n_nodes": n, "nnz_ahat": nnz,
                    "d": d, "K": K, "normalization": "sym r=0.5",
                    "parallelism": f"row-partition x{world}" + (f" ({a.exchange} exchange)" if world > 1 else ""),
