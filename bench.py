@@ -56,6 +56,10 @@ def parse():
     ap.add_argument("--nt-store", action="store_true")
     ap.add_argument("--exchange", default="halo", choices=["halo", "allgather"])
     ap.add_argument("--chunks", type=int, default=4, help="halo exchange groups per hop")
+    ap.add_argument("--op", default="khop", choices=["khop", "wavelet"],
+                    help="khop: the K-hop propagate (GraphOp.propagate); wavelet: the heat-wavelet "
+                         "Chebyshev filter bank (order 3, scales -0.5/+0.5) applied to the feature panel")
+    ap.add_argument("--col-block", type=int, default=None, help="wavelet: column block width")
     ap.add_argument("--mode", default="auto", choices=["auto", "panels", "last"],
                     help="panels: all K+1 hop panels kept (GraphOp.propagate); last: two ping-pong "
                          "panels, only A^K X kept (SGC-style, fused aggregation); auto: panels if "
@@ -160,6 +164,81 @@ def pmc_traffic(config, kernel_hint="k_spmm"):
         return None
 
 
+def run_wavelet(a, dev):
+    """SpectralModel's wavelet operator (SSRG/models/base_scalable/base_model.py:180-265) on the
+    config's graph: R_s = sum_k c_{s,k} T_k(L~) X for tau = -0.5, +0.5, Chebyshev order 3, fp32,
+    one process (world size 1).  value = order * nnz(L) * steps / time: every order is one SpMM
+    pass over the whole panel (in column blocks when the panels do not fit)."""
+    from srgnn import wavelet as W
+    from srgnn.csr import DeviceCSR
+    from srgnn.spmm import spmm
+    t_build = time.perf_counter()
+    ip, ix, lv, n, d, lmax = graphs.build_laplacian(a.config, dev, d=a.d)
+    nnz = int(ix.numel())
+    order = 3
+    filt = W.HeatWaveletFilter.from_device(ip, ix, lv, n, [-0.5, 0.5], order=order, lmax=lmax,
+                                           dtype=torch.float32, heavy_threshold=a.heavy_threshold)
+    X = synth.uniform_features_t(n, d, seed=synth.FEATURE_SEED, device=dev)
+    R = torch.empty((2, n, d), dtype=torch.float32, device=dev)
+    torch.cuda.synchronize()
+    free, _ = torch.cuda.mem_get_info(dev)
+    cb = a.col_block or d
+    while not a.col_block and cb > 8 and 3 * n * cb * 4 > 0.9 * free:
+        cb //= 2
+    log(f"wavelet {a.config}: n={n} nnz(L)={nnz} d={d} lmax={lmax} col_block={cb} "
+        f"hub={filt.n_hub} heavy={filt.n_heavy} built in {time.perf_counter() - t_build:.1f}s")
+
+    def step():
+        filt.apply(X, col_block=cb, out=R)
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    # roofline: one order's SpMM launch at the block width (HIP events on the launch stream)
+    stream = torch.cuda.current_stream(dev)
+    Fm = DeviceCSR(filt.indptr, filt.indices, filt.fvals, n, n, filt.order, filt.n_heavy, filt.n_hub)
+    tb = torch.empty((n, cb), dtype=torch.float32, device=dev)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * a.roofline_reps)]
+    for r in range(a.roofline_reps):
+        ev[2 * r].record(stream)
+        spmm(Fm, X[:, :cb], out=tb)
+        ev[2 * r + 1].record(stream)
+    torch.cuda.synchronize()
+    kern_s = float(np.mean([ev[2 * r].elapsed_time(ev[2 * r + 1]) * 1e-3 for r in range(a.roofline_reps)]))
+    del tb
+    b_alg = roofline.bytes_no_reuse(n, nnz, cb)
+    achieved = b_alg / kern_s / 1e9
+    res = {
+        "metric": "propagated edges/sec (wavelet-basis Chebyshev propagation)",
+        "value": a.steps * order * nnz / dt,
+        "unit": "propagated edges/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "f32",
+        "data": f"synthetic (R-MAT power-law graph with the {a.config} node/edge counts, U[-1,1) features)",
+        "config": {"workload": f"{a.config}-shaped heat-wavelet filter bank", "n_nodes": n, "nnz_L": nnz,
+                   "d": d, "chebyshev_order": order, "scales": [-0.5, 0.5], "lmax": lmax,
+                   "col_block": cb, "parallelism": "x1",
+                   "mode": "fp32 (split path bit-identical to the fused Chebyshev kernel)"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": roofline.MI355X_HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / roofline.MI355X_HBM_PEAK_GBS, "traffic": None,
+                     "kernel": f"k_spmm: one Chebyshev order's SpMM over a {cb}-column block",
+                     "kernel_ms": kern_s * 1e3, "algorithmic_bytes_per_launch": b_alg,
+                     "compulsory_bytes_per_launch": roofline.bytes_compulsory(n, nnz, cb, n_cols=n)},
+        "cpu_baseline": None,
+    }
+    if not a.no_cpu_baseline:
+        log("cpu baseline ...")
+        host = (ip.cpu().numpy(), ix.cpu().numpy(), filt.fvals.cpu().numpy(), X.cpu().numpy())
+        cb_res = cpu_baseline(*host, n, d, a.cpu_seconds)
+        cb_res["sample"] = "the SpMM part of each Chebyshev order: " + cb_res["sample"]
+        res["cpu_baseline"] = cb_res
+    print(json.dumps(res), flush=True)
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -169,6 +248,10 @@ def main():
         log(f"note: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if a.op == "wavelet":
+        if world > 1:
+            raise SystemExit("--op wavelet runs on one GPU (world size 1)")
+        return run_wavelet(a, dev)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 

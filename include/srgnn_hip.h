@@ -115,6 +115,16 @@ int srg_cheby_step_f32(const int64_t* indptr, const int32_t* indices, const floa
                        const float* coef_prev, const float* coef, int32_t n_scales, float* R,
                        int64_t r_stride, void* stream);
 
+/* The same Chebyshev order split in two for large graphs: a load-balanced srg_spmm_csr_f32 of
+ * Tc into Tn (slice waves and hub workgroups for the high-degree rows), then this element-wise
+ * epilogue turning Tn = A*Tc into the next T and updating R -- bit-identical to
+ * srg_cheby_step_f32 (same fma chain, same epilogue arithmetic).  Every panel has its own leading
+ * dimension (column blocks of S and R without copies); R_s = R + s*r_stride, rows ldr apart. */
+int srg_cheby_epilogue_f32(float* Tn, int64_t ldn, const float* Tc, int64_t ldc, const float* To,
+                           int64_t ldo, int64_t n_rows, int32_t d, int mode, float a1, float a2,
+                           const float* coef_prev, const float* coef, int32_t n_scales, float* R,
+                           int64_t ldr, int64_t r_stride, void* stream);
+
 /* Hop aggregation without the K+1 panels (fused precompute of SGC / SSGC / GBP).  The reference
  * combines the hop list on the host (SSRG/operators/message_operator/{sum,mean,simple_weighted}_
  * message_op.py; operators/utils.py:426-437 one_dim_weighted_add); the host side plans the same

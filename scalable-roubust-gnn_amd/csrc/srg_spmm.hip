@@ -575,6 +575,38 @@ k_cheby(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
     }
 }
 
+// Chebyshev epilogue after a load-balanced SpMM (fp32, large graphs): Tn holds acc = A*Tc (the
+// same fma chain k_cheby forms, so results are bit-identical to the fused kernel) and becomes
+// Tn; every panel has its own leading dimension, so column blocks of S and R need no copies.
+__global__ void __launch_bounds__(256)
+k_cheby_epilogue(float* __restrict__ Tn, int64_t ldn, const float* __restrict__ Tc, int64_t ldc,
+                 const float* __restrict__ To, int64_t ldo, int64_t n_rows, int d, int mode, float a1,
+                 float a2, ChebyCoef<float> cf, int n_scales, float* __restrict__ R, int64_t ldr,
+                 int64_t r_stride)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
+    for (int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); r < n_rows; r += waves) {
+        float* tn = Tn + r * ldn;
+        float* rr = R + r * ldr;
+        for (int c = lane; c < d; c += 64) {
+            const float acc = tn[c];
+            float t;
+            if (mode == SRG_CHEBY_INIT) {
+                const float tc = Tc[r * ldc + c];
+                t = e_div(e_sub(acc, e_mul(a2, tc)), a1);
+                for (int s = 0; s < n_scales; ++s)
+                    rr[s * r_stride + c] = e_add(e_mul(cf.prev[s], tc), e_mul(cf.cur[s], t));
+            } else {
+                t = e_sub(acc, To[r * ldo + c]);
+                for (int s = 0; s < n_scales; ++s)
+                    rr[s * r_stride + c] = e_add(rr[s * r_stride + c], e_mul(cf.cur[s], t));
+            }
+            tn[c] = t;
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------------------------
 // hop aggregation (fused SGC / SSGC / GBP precompute: MessageOp.combine without the K+1 panels)
 //
@@ -1062,6 +1094,33 @@ int srg_cheby_step_f32(const int64_t* indptr, const int32_t* indices, const floa
     return launch_cheby<float>(indptr, indices, values, n_rows, row_order, Tc, To, Tn, ld, d, mode,
                                a1, a2, coef_prev, coef, n_scales, R, r_stride,
                                static_cast<hipStream_t>(stream));
+}
+
+int srg_cheby_epilogue_f32(float* Tn, int64_t ldn, const float* Tc, int64_t ldc, const float* To,
+                           int64_t ldo, int64_t n_rows, int32_t d, int mode, float a1, float a2,
+                           const float* coef_prev, const float* coef, int32_t n_scales, float* R,
+                           int64_t ldr, int64_t r_stride, void* stream)
+{
+    if (mode != SRG_CHEBY_INIT && mode != SRG_CHEBY_STEP)
+        return fail(SRG_ERR_INVALID, "cheby mode %d", mode);
+    if (n_scales < 1 || n_scales > 8) return fail(SRG_ERR_INVALID, "n_scales=%d not in [1,8]", n_scales);
+    if (!coef || (mode == SRG_CHEBY_INIT && !coef_prev)) return fail(SRG_ERR_INVALID, "null coefficient array");
+    if (n_rows < 0 || d < 0 || ldn < d || ldr < d || (mode == SRG_CHEBY_INIT ? ldc < d : ldo < d))
+        return fail(SRG_ERR_INVALID, "bad shape n_rows=%lld d=%d", (long long)n_rows, d);
+    if (n_scales > 1 && r_stride < n_rows * ldr && r_stride > -n_rows * ldr)
+        return fail(SRG_ERR_INVALID, "r_stride overlaps the scale panels");
+    if (n_rows == 0 || d == 0) return ok();
+    if (!Tn || !R || (mode == SRG_CHEBY_INIT ? !Tc : !To)) return fail(SRG_ERR_INVALID, "null panel");
+    ChebyCoef<float> cf;
+    for (int i = 0; i < 8; ++i) {
+        cf.prev[i] = (mode == SRG_CHEBY_INIT && i < n_scales) ? 0.5f * coef_prev[i] : 0.0f;
+        cf.cur[i] = i < n_scales ? coef[i] : 0.0f;
+    }
+    const unsigned blocks = (unsigned)std::min<int64_t>((n_rows + 3) / 4, 256 * 16);
+    hipLaunchKernelGGL(k_cheby_epilogue, dim3(blocks), dim3(256), 0, static_cast<hipStream_t>(stream),
+                       Tn, ldn, Tc, ldc, To, ldo, n_rows, d, mode, a1, a2, cf, n_scales, R, ldr, r_stride);
+    SRG_HIP_CHECK(hipGetLastError());
+    return ok();
 }
 
 int srg_hop_accumulate_f32(float* agg, int64_t lda, const float* y, int64_t ldy, int64_t n_rows,

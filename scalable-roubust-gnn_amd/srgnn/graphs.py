@@ -36,3 +36,24 @@ def build(config: str, device, r: float = 0.5, n=None, n_edges=None, d=None, see
         ip, ix, vals = sym_norm_binary(ip, ix, n, r)
     torch.cuda.empty_cache() if torch.device(device).type == "cuda" else None
     return ip, ix, vals, n, d, k
+
+
+def build_laplacian(config: str, device, n=None, n_edges=None, d=None, seed=synth.RMAT_SEED):
+    """The wavelet basis' operator for a synthetic config: L = D - A of the same binary symmetric
+    graph as build(), with every diagonal entry stored (wavelet.laplacian_from_adj's layout), fp32
+    values (exact: -1 and integer degrees < 2^24).  Returns (indptr, indices, lvals, n, d, lmax)
+    with lmax = 2 * max degree, the Gershgorin bound of L's spectrum (pygsp's ARPACK estimate is a
+    host computation; the Chebyshev cost does not depend on it)."""
+    cfg = dict(synth.CONFIGS[config]) if config in synth.CONFIGS else {}
+    n = n or cfg["n"]
+    n_edges = n_edges or cfg["n_edges"]
+    d = d or cfg["d"]
+    u, v = synth.rmat_undirected_blocked_t(n, n_edges, seed=seed, device=device)
+    if n < 2 ** 31:
+        u, v = u.to(torch.int32), v.to(torch.int32)
+    torch.cuda.empty_cache() if torch.device(device).type == "cuda" else None
+    ip, ix, lv = sym_norm_edges_blocked(u, v, n, kind="laplacian")
+    del u, v
+    torch.cuda.empty_cache() if torch.device(device).type == "cuda" else None
+    lmax = 2.0 * float((ip[1:] - ip[:-1]).max()) if n else 0.0
+    return ip, ix, lv, n, d, lmax

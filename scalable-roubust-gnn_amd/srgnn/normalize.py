@@ -46,19 +46,28 @@ def sym_norm_binary(indptr: torch.Tensor, indices: torch.Tensor, n: int, r: floa
     return out_ptr, c_j.to(torch.int32), vals
 
 
-def sym_norm_edges_blocked(u: torch.Tensor, v: torch.Tensor, n: int, r: float = 0.5, block_nnz: int = 1 << 28):
+def sym_norm_edges_blocked(u: torch.Tensor, v: torch.Tensor, n: int, r: float = 0.5, block_nnz: int = 1 << 28,
+                           kind: str = "sym"):
     """The same (indptr, indices, values) as symmetric_csr_t + sym_norm_binary, from the undirected
     edge list (u, v) (unique pairs, no self-loops), built row block by row block so that no sort
-    or temporary exceeds ~block_nnz entries (billion-edge graphs)."""
+    or temporary exceeds ~block_nnz entries (billion-edge graphs).
+    kind="laplacian": the same structure (A + I) with the values of L = D - A instead (fp32: -1
+    off the diagonal, the degree on it; exact below 2^24) -- the wavelet basis' operator
+    (wavelet.laplacian_from_adj) for a binary symmetric graph."""
+    if kind not in ("sym", "laplacian"):
+        raise ValueError(kind)
     dev = u.device
     deg_a = torch.bincount(u, minlength=n) + torch.bincount(v, minlength=n)
     indptr = torch.zeros(n + 1, dtype=torch.int64, device=dev)
     indptr[1:] = torch.cumsum(deg_a + 1, 0)
     nnz = int(indptr[-1])
-    left, right = degree_powers((deg_a + 1).cpu().numpy(), r)
+    if kind == "sym":
+        left, right = degree_powers((deg_a + 1).cpu().numpy(), r)
+        left_t = torch.from_numpy(left).to(dev)
+        right_t = torch.from_numpy(right).to(dev)
+    else:
+        deg_f = deg_a.to(torch.float32)
     del deg_a
-    left_t = torch.from_numpy(left).to(dev)
-    right_t = torch.from_numpy(right).to(dev)
     indices = torch.empty(nnz, dtype=torch.int32, device=dev)
     vals = torch.empty(nnz, dtype=torch.float32, device=dev)
     n_blocks = max(1, -(-nnz // block_nnz))
@@ -78,7 +87,10 @@ def sym_norm_edges_blocked(u: torch.Tensor, v: torch.Tensor, n: int, r: float = 
         del key
         a, b = int(indptr[r0]), int(indptr[r1])
         assert b - a == cc.numel()
-        vals[a:b] = ((1.0 * left_t[rr]) * right_t[cc]).to(torch.float32)
+        if kind == "sym":
+            vals[a:b] = ((1.0 * left_t[rr]) * right_t[cc]).to(torch.float32)
+        else:
+            vals[a:b] = torch.where(rr == cc, deg_f[rr], torch.full_like(deg_f[:1], -1.0))
         indices[a:b] = cc.to(torch.int32)
         del rr, cc
     return indptr, indices, vals

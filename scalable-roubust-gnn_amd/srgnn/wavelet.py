@@ -9,7 +9,11 @@ then L1-normalises each phi row (sklearn normalize).  cheby_op is the Chebyshev 
     R = c0/2 T0 + sum_k c_k T_k
 Here every Chebyshev order is ONE fused launch of srg_cheby_step_{f64,f32}: the SpMM row-wave
 gather plus an epilogue that forms T_{k+1} and accumulates every scale's output R_s in the same
-pass (all scales share the T_k panels, so two scales cost one recurrence, not two).
+pass (all scales share the T_k panels, so two scales cost one recurrence, not two).  For fp32 on
+large power-law graphs (`split=True`, the default for fp32) each order is instead the
+load-balanced SpMM (slice waves, hub workgroups) plus srg_cheby_epilogue_f32 -- bit-identical to
+the fused kernel -- and the panel can be filtered in column blocks (`col_block`) so that
+billion-edge graphs with d = 256 fit in HBM (R is written in place, no block copies).
 
 pygsp is not available offline: the restatement follows pygsp 0.5.x semantics and is validated
 against a dense eigendecomposition (tests) -- parity with the reference is unpinned.  lmax is an
@@ -25,7 +29,7 @@ import scipy.sparse as sp
 import torch
 
 from . import _lib
-from .csr import make_schedule
+from .csr import DeviceCSR, make_schedule
 
 
 def laplacian_from_adj(adj: sp.spmatrix) -> sp.csr_matrix:
@@ -100,49 +104,101 @@ class HeatWaveletFilter:
     """R_s = sum_k c_{s,k} T_k(L~) S for the heat kernels exp(-tau_s x / lmax), every scale at once."""
 
     def __init__(self, L: sp.spmatrix, taus, order: int = 3, lmax: float | None = None,
-                 dtype=torch.float64, device=None, heavy_threshold=None):
+                 dtype=torch.float64, device=None, heavy_threshold=None, hub_threshold=None):
+        L = _explicit_diagonal(sp.csr_matrix(L))
+        lmax = float(lmax) if lmax is not None else estimate_lmax(L)
+        dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self._setup(torch.from_numpy(L.indptr.astype(np.int64)).to(dev),
+                    torch.from_numpy(L.indices.astype(np.int32)).to(dev),
+                    torch.from_numpy(L.data.astype(np.float64)).to(dev), L.shape[0], taus, order, lmax,
+                    dtype, heavy_threshold, hub_threshold)
+
+    @classmethod
+    def from_device(cls, indptr: torch.Tensor, indices: torch.Tensor, lvals: torch.Tensor, n: int, taus,
+                    order: int = 3, lmax: float = None, dtype=torch.float32, heavy_threshold=None,
+                    hub_threshold=None):
+        """From a device CSR of L with every diagonal entry stored (e.g. normalize.laplacian_edges_blocked)
+        and an explicit lmax (pygsp's ARPACK estimate is a host computation)."""
+        if lmax is None:
+            raise ValueError("lmax is required for a device-built Laplacian")
+        self = cls.__new__(cls)
+        self._setup(indptr, indices, lvals, n, taus, order, float(lmax), dtype, heavy_threshold, hub_threshold)
+        return self
+
+    def _setup(self, indptr, indices, lvals, n, taus, order, lmax, dtype, heavy_threshold, hub_threshold):
         if order < 1:
             raise ValueError("order must be >= 1")
         if len(taus) < 1 or len(taus) > 8:
             raise ValueError("1..8 scales")
         if dtype not in (torch.float64, torch.float32):
             raise TypeError("dtype must be float64 or float32")
-        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
-        L = _explicit_diagonal(sp.csr_matrix(L))
-        self.n = L.shape[0]
-        self.lmax = float(lmax) if lmax is not None else estimate_lmax(L)
+        self.device = indptr.device
+        self.n = int(n)
+        self.lmax = lmax
         self.a1 = self.a2 = self.lmax / 2.0
         self.taus = [float(t) for t in taus]
         self.coeffs = np.stack([heat_cheby_coeffs(t, self.lmax, order) for t in self.taus])
         self.dtype = dtype
-        rows = np.repeat(np.arange(self.n), np.diff(L.indptr))
-        lvals = L.data.astype(np.float64)
-        fvals = (2.0 / self.a1) * np.where(L.indices == rows, lvals - self.a2, lvals)   # (2/a1)(L - a2 I)
-        self.indptr = torch.from_numpy(L.indptr.astype(np.int64)).to(self.device)
-        self.indices = torch.from_numpy(L.indices.astype(np.int32)).to(self.device)
-        self.lvals = torch.from_numpy(lvals).to(self.device, dtype)
-        self.fvals = torch.from_numpy(fvals).to(self.device, dtype)
-        self.order, _, _ = make_schedule(self.indptr, -1, -1)
+        self.indptr, self.indices = indptr, indices
+        # F = (2/a1)(L - a2 I), formed in fp64 then rounded (the diagonal is stored explicitly)
+        rows = torch.repeat_interleave(torch.arange(self.n, device=self.device),
+                                       indptr[1:] - indptr[:-1]) if self.n else indptr[:0]
+        diag = indices.to(torch.int64) == rows
+        del rows
+        l64 = lvals.to(torch.float64)
+        self.fvals = ((2.0 / self.a1) * torch.where(diag, l64 - self.a2, l64)).to(dtype)
+        del diag, l64
+        self.lvals = lvals.to(dtype)
+        self.order, self.n_heavy, self.n_hub = make_schedule(self.indptr, heavy_threshold, hub_threshold)
 
-    def apply(self, S: torch.Tensor) -> torch.Tensor:
-        """[n_scales, n, d] filter outputs for the panel S [n, d] (device tensor)."""
+    def _coef(self, ct, vals):
+        return (ct * len(vals))(*vals)
+
+    def apply(self, S: torch.Tensor, col_block: int | None = None, split: bool | None = None,
+              out: torch.Tensor | None = None) -> torch.Tensor:
+        """[n_scales, n, d] filter outputs for the panel S [n, d] (device tensor).  fp32 defaults to
+        the split path (load-balanced SpMM + epilogue), in column blocks of `col_block`."""
         if not S.is_cuda or S.shape[0] != self.n or S.dim() != 2:
             raise ValueError("S must be a [n, d] device tensor")
-        S = S.to(self.dtype).contiguous()
+        if split is None:
+            split = self.dtype == torch.float32
+        if split and self.dtype != torch.float32:
+            raise ValueError("the split path is fp32 only")
+        if S.dtype != self.dtype or S.stride(1) != 1:
+            S = S.to(self.dtype).contiguous()
+        n, d = S.shape
+        ns = self.coeffs.shape[0]
+        R = out if out is not None else torch.empty((ns, n, d), dtype=self.dtype, device=S.device)
+        if tuple(R.shape) != (ns, n, d) or R.dtype != self.dtype or R.stride(2) != 1:
+            raise ValueError("out must be a [n_scales, n, d] panel stack of the filter dtype")
+        if not split:
+            if S.stride(0) != d or R.stride(1) != d or R.stride(0) != n * d:
+                S = S.contiguous()
+                if out is not None:
+                    raise ValueError("the fused path needs contiguous S and out")
+            return self._apply_fused(S, R)
+        cb = d if not col_block else min(int(col_block), d)
+        work = [torch.empty((n, cb), dtype=torch.float32, device=S.device) for _ in range(3 if self.coeffs.shape[1] > 2 else 1)]
+        for c0 in range(0, d, cb):
+            w = min(cb, d - c0)
+            self._apply_split(S[:, c0:c0 + w], R[:, :, c0:c0 + w],
+                              [t.view(-1)[: n * w].view(n, w) for t in work])
+        return R
+
+    def _apply_fused(self, S, R):
         n, d = S.shape
         ns, nc = self.coeffs.shape
-        R = torch.empty((ns, n, d), dtype=self.dtype, device=S.device)
         f64 = self.dtype == torch.float64
         ct = ctypes.c_double if f64 else ctypes.c_float
         fn = _lib.lib().srg_cheby_step_f64 if f64 else _lib.lib().srg_cheby_step_f32
         stream = torch.cuda.current_stream(S.device).cuda_stream
 
         def launch(vals, Tc, To, Tn, mode, coef_prev, coef):
-            cp = (ct * ns)(*coef_prev) if coef_prev is not None else None
-            cc = (ct * ns)(*coef)
+            cp = self._coef(ct, coef_prev) if coef_prev is not None else None
             rc = fn(self.indptr.data_ptr(), self.indices.data_ptr(), vals.data_ptr(), n,
                     self.order.data_ptr(), Tc.data_ptr(), To.data_ptr() if To is not None else None,
-                    Tn.data_ptr(), d, d, mode, self.a1, self.a2, cp, cc, ns, R.data_ptr(), n * d, stream)
+                    Tn.data_ptr(), d, d, mode, self.a1, self.a2, cp, self._coef(ct, coef), ns,
+                    R.data_ptr(), n * d, stream)
             _lib.check(rc, fn.__name__)
 
         # T_{k-1}, T_k and the free panel rotate through three buffers (S itself is never written)
@@ -156,6 +212,39 @@ class HeatWaveletFilter:
                 free.append(t_old)
             t_old, t_cur = t_cur, t_new
         return R
+
+    def _csr(self, vals):
+        return DeviceCSR(self.indptr, self.indices, vals, self.n, self.n, self.order, self.n_heavy, self.n_hub)
+
+    def _apply_split(self, Sb, Rb, work):
+        """One column block: Sb [n, w] and Rb [ns, n, w] may be strided views."""
+        from .spmm import spmm
+        n, w = Sb.shape
+        ns, nc = self.coeffs.shape
+        ct = ctypes.c_float
+        fn = _lib.lib().srg_cheby_epilogue_f32
+        stream = torch.cuda.current_stream(Sb.device).cuda_stream
+        Lm, Fm = self._csr(self.lvals), self._csr(self.fvals)
+
+        def epi(Tn, Tc, To, mode, coef_prev, coef):
+            cp = self._coef(ct, coef_prev) if coef_prev is not None else None
+            rc = fn(Tn.data_ptr(), Tn.stride(0), Tc.data_ptr() if Tc is not None else None,
+                    Tc.stride(0) if Tc is not None else w, To.data_ptr() if To is not None else None,
+                    To.stride(0) if To is not None else w, n, w, mode, self.a1, self.a2, cp,
+                    self._coef(ct, coef), ns, Rb.data_ptr(), Rb.stride(1), Rb.stride(0), stream)
+            _lib.check(rc, "srg_cheby_epilogue_f32")
+
+        t_old, t_cur = Sb, work[0]
+        free = list(work[1:])
+        spmm(Lm, Sb, out=t_cur)
+        epi(t_cur, Sb, None, _lib.SRG_CHEBY_INIT, self.coeffs[:, 0], self.coeffs[:, 1])
+        for k in range(2, nc):
+            t_new = free.pop()
+            spmm(Fm, t_cur, out=t_new)
+            epi(t_new, None, t_old, _lib.SRG_CHEBY_STEP, None, self.coeffs[:, k])
+            if t_old is not Sb:
+                free.append(t_old)
+            t_old, t_cur = t_cur, t_new
 
 
 def wavelet_basis(adj: sp.spmatrix, scale: float = 0.5, order: int = 3, tolerance: float = 1e-4,

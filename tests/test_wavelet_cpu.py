@@ -73,3 +73,20 @@ def test_estimate_lmax_upper_bounds_spectrum():
     lmax = W.estimate_lmax(L)
     true = np.linalg.eigvalsh(L.toarray()).max()
     assert true <= lmax <= true * 1.03
+
+
+def test_device_laplacian_builder_matches_host_laplacian():
+    """normalize.sym_norm_edges_blocked(kind="laplacian") == wavelet.laplacian_from_adj on the
+    same binary symmetric graph (structure with the explicit diagonal, and values)."""
+    import scipy.sparse as sp
+    import torch
+    from srgnn import normalize, synth, wavelet
+    n, m = 3000, 15000
+    u, v = synth.rmat_undirected_t(n, m, seed=9)
+    ip, ix, lv = normalize.sym_norm_edges_blocked(u.to(torch.int32), v.to(torch.int32), n, kind="laplacian",
+                                                  block_nnz=1 << 12)
+    adj = sp.csr_matrix((np.ones(2 * m), (np.r_[u.numpy(), v.numpy()], np.r_[v.numpy(), u.numpy()])), shape=(n, n))
+    L = wavelet.laplacian_from_adj(adj)
+    np.testing.assert_array_equal(ip.numpy(), L.indptr)
+    np.testing.assert_array_equal(ix.numpy(), L.indices)
+    np.testing.assert_array_equal(lv.numpy(), L.data.astype(np.float32))

@@ -80,3 +80,41 @@ def test_wavelet_basis_matches_oracle_restatement(oracle_mod):
         want = m / rs[:, None]
         np.testing.assert_allclose(got.toarray(), want, rtol=1e-6, atol=1e-7)
         assert got.dtype == np.float32
+
+
+@pytest.mark.parametrize("thr", [(None, None), (0, -1), (-1, -1), (4, 40)])
+@pytest.mark.parametrize("d,cb", [(128, None), (100, 32), (256, 64), (36, 8)])
+def test_split_path_bit_identical_to_fused(d, cb, thr):
+    """fp32 split path (load-balanced SpMM + srg_cheby_epilogue_f32, column blocks writing into
+    strided views of R) == the fused srg_cheby_step_f32 kernel, bit for bit."""
+    from srgnn import wavelet as W
+    a = graphs()["rmat3000"]
+    L = W.laplacian_from_adj(a)
+    f = W.HeatWaveletFilter(L, [-0.5, 0.5, 1.5], order=4, lmax=None, dtype=torch.float32, device="cuda",
+                            heavy_threshold=thr[0], hub_threshold=thr[1])
+    S = torch.from_numpy(np.random.default_rng(d).standard_normal((a.shape[0], d)).astype(np.float32)).cuda()
+    fused = f.apply(S, split=False)
+    split = f.apply(S, split=True, col_block=cb)
+    assert torch.equal(fused, split)
+    # into a caller-provided stack, and from a strided column window of a wider panel
+    wide = torch.zeros((a.shape[0], d + 12), device="cuda")
+    wide[:, 4:4 + d] = S
+    out = torch.full((3, a.shape[0], d), float("nan"), device="cuda")
+    f.apply(wide[:, 4:4 + d], split=True, col_block=cb, out=out)
+    assert torch.equal(fused, out)
+
+
+def test_device_built_filter_equals_host_built():
+    """HeatWaveletFilter.from_device (device Laplacian from the edge list) == the host-built filter."""
+    from srgnn import normalize, synth, wavelet as W
+    n = 3000
+    u, v = synth.rmat_undirected_t(n, 15000, seed=8)
+    ip, ix, lv = normalize.sym_norm_edges_blocked(u.cuda().to(torch.int32), v.cuda().to(torch.int32), n,
+                                                  kind="laplacian")
+    a = graphs()["rmat3000"]
+    L = W.laplacian_from_adj(a)
+    host = W.HeatWaveletFilter(L, [-0.5, 0.5], order=3, lmax=9.0, dtype=torch.float32, device="cuda")
+    dev = W.HeatWaveletFilter.from_device(ip, ix, lv, n, [-0.5, 0.5], order=3, lmax=9.0, dtype=torch.float32)
+    assert torch.equal(host.fvals, dev.fvals) and torch.equal(host.lvals, dev.lvals)
+    S = torch.from_numpy(np.random.default_rng(2).standard_normal((n, 64)).astype(np.float32)).cuda()
+    assert torch.equal(host.apply(S), dev.apply(S, col_block=16))
