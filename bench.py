@@ -181,6 +181,7 @@ def run_wavelet(a, dev):
     X = synth.uniform_features_t(n, d, seed=synth.FEATURE_SEED, device=dev)
     R = torch.empty((2, n, d), dtype=torch.float32, device=dev)
     torch.cuda.synchronize()
+    torch.cuda.empty_cache()          # the builders' temporaries
     free, _ = torch.cuda.mem_get_info(dev)
     cb = a.col_block or d
     while not a.col_block and cb > 8 and 3 * n * cb * 4 > 0.9 * free:

@@ -148,6 +148,12 @@ int srg_tail_record_f32(float* hist, const float* y, int64_t ldy, int32_t d, int
 int srg_tail_rowsum_f32(float* agg, int64_t lda, int32_t d, int64_t flat_start, int32_t len,
                         const float* hist, int32_t n_terms, void* stream);
 
+/* construct_adj on the device (SSRG/operators/utils.py:81-93, adj_to_symmetric_norm): out[s] =
+ * ((0 + v[p[s]]) + v[p[s]+1]) + ... over vals[seg_ptr[s] .. seg_ptr[s+1]) in fp64, left to right
+ * -- the order in which scipy merges duplicate entries of adj + I and sums the rows for the
+ * degrees.  seg_ptr has n_seg + 1 entries; all pointers are device pointers. */
+int srg_segment_sum_f64(const int64_t* seg_ptr, const double* vals, int64_t n_seg, double* out, void* stream);
+
 /* Checks a device CSR: indptr[0] == 0, indptr non-decreasing, indptr[n_rows] == nnz, and every
  * column id in [0, n_cols).  Synchronous on `stream`.  Returns SRG_OK or SRG_ERR_INVALID. */
 int srg_csr_validate(const int64_t* indptr, const int32_t* indices, int64_t n_rows,

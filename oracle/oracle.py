@@ -92,8 +92,17 @@ def _sum_duplicates_sorted(rows, cols, vals, n):
     order = np.argsort(key, kind="stable")
     key, vals = key[order], vals[order]
     if key.size:
+        # left-to-right sums from +0 (scipy's csr_binop / sum_duplicates order); np.add.reduceat
+        # would add the tail of a run pairwise, a different rounding for 3+ duplicates
         start = np.flatnonzero(np.r_[True, key[1:] != key[:-1]])
-        vals = np.add.reduceat(vals, start)
+        lens = np.diff(np.r_[start, key.size])
+        out = vals[start] + 0.0
+        for i in np.flatnonzero(lens > 1).tolist():
+            acc = 0.0
+            for x in vals[start[i]:start[i] + lens[i]].tolist():
+                acc += x
+            out[i] = acc
+        vals = out
         key = key[start]
     keep = vals != 0
     key, vals = key[keep], vals[keep]

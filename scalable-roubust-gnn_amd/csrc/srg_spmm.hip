@@ -690,6 +690,22 @@ __global__ void k_tail_rowsum(float* __restrict__ agg, int64_t lda, int d, int64
 }
 
 // ------------------------------------------------------------------------------------------------
+// construct_adj on the device: sequential fp64 segment sums (duplicate merging and row degrees in
+// storage order, starting from +0 -- scipy's csr_binop / csr_matvec accumulation order)
+// ------------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+k_segment_sum_f64(const int64_t* __restrict__ seg_ptr, const double* __restrict__ vals, int64_t n_seg,
+                  double* __restrict__ out)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n_seg; s += stride) {
+        double acc = 0.0;
+        for (int64_t j = seg_ptr[s]; j < seg_ptr[s + 1]; ++j) acc = __dadd_rn(acc, vals[j]);
+        out[s] = acc;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // validation kernel
 // ------------------------------------------------------------------------------------------------
 __global__ void k_validate(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
@@ -1164,6 +1180,18 @@ int srg_tail_rowsum_f32(float* agg, int64_t lda, int32_t d, int64_t flat_start, 
     if (!agg || (n_terms > 0 && !hist)) return fail(SRG_ERR_INVALID, "null pointer");
     hipLaunchKernelGGL(k_tail_rowsum, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream),
                        agg, lda, d, flat_start, len, hist, n_terms);
+    SRG_HIP_CHECK(hipGetLastError());
+    return ok();
+}
+
+int srg_segment_sum_f64(const int64_t* seg_ptr, const double* vals, int64_t n_seg, double* out, void* stream)
+{
+    if (n_seg < 0) return fail(SRG_ERR_INVALID, "n_seg=%lld < 0", (long long)n_seg);
+    if (n_seg == 0) return ok();
+    if (!seg_ptr || !out) return fail(SRG_ERR_INVALID, "null pointer");
+    const unsigned blocks = (unsigned)std::min<int64_t>((n_seg + 255) / 256, 1 << 16);
+    hipLaunchKernelGGL(k_segment_sum_f64, dim3(blocks), dim3(256), 0, static_cast<hipStream_t>(stream),
+                       seg_ptr, vals, n_seg, out);
     SRG_HIP_CHECK(hipGetLastError());
     return ok();
 }

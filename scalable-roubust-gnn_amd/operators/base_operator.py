@@ -32,14 +32,46 @@ from srgnn.spmm import propagate as _device_propagate
 class GraphOp:
     def __init__(self, prop_steps):
         self.prop_steps = prop_steps
-        self.adj = None
+        self._adj, self._adj_dev = None, None
+
+    # The reference keeps Â as self.adj (a scipy matrix).  When Â is built on the device
+    # (construct_adj_device) the host copy is made on first access only.
+    @property
+    def adj(self):
+        if self._adj is None and self._adj_dev is not None:
+            from srgnn.construct import to_scipy
+            self._adj = to_scipy(*self._adj_dev)
+        return self._adj
+
+    @adj.setter
+    def adj(self, value):
+        self._adj, self._adj_dev = value, None
 
     def construct_adj(self, adj):
         raise NotImplementedError
 
-    def _checked_inputs(self, adj, feature):
-        """The reference's checks, in its order (base_operator.py:20-30)."""
+    def construct_adj_device(self, adj, device):
+        """(indptr, indices, values fp64) device tensors of construct_adj(adj), bit-identical, or
+        None when the operator has no device form (the host construct_adj is used then)."""
+        return None
+
+    def _build_operator(self, adj, device=None):
+        """construct_adj on the device when the operator has a device form and adj is a square CSR
+        (SURVEY.md §8(f) item 2); otherwise the host construct_adj, with its own errors."""
+        if isinstance(adj, sp.csr_matrix) and adj.shape[0] == adj.shape[1]:
+            dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+            built = self.construct_adj_device(adj, dev)
+            if built is not None:
+                ip, ix, v64 = built
+                self._adj, self._adj_dev = None, (ip, ix, v64, adj.shape[0])
+                return DeviceCSR.from_tensors(ip, ix, v64.to(torch.float32), n_cols=adj.shape[0], device=dev)
         self.adj = self.construct_adj(adj)
+        return None
+
+    def _checked_inputs(self, adj, feature, device=None):
+        """The reference's checks, in its order (base_operator.py:20-30); returns the feature array
+        and the device operator (None when Â was built on the host)."""
+        A = self._build_operator(adj, device)
         if not isinstance(adj, sp.csr_matrix):
             raise TypeError("The adjacency matrix must be a scipy csr sparse matrix!")
         elif not isinstance(feature, np.ndarray):
@@ -47,22 +79,22 @@ class GraphOp:
                 feature = feature.numpy()
             else:
                 raise TypeError("The feature matrix must be a numpy.ndarray!")
-        elif self.adj.shape[1] != feature.shape[0]:
+        elif (adj.shape[0] if A is not None else self.adj.shape[1]) != feature.shape[0]:
             raise ValueError("Dimension mismatch detected for the adjacency and the feature matrix!")
         if self.prop_steps > 0 and feature.dtype != np.float32:
             # the reference's first hop hands the array to an ndpointer(float32) (utils.py:29-34)
             raise ctypes.ArgumentError("argument 5: TypeError: array must have data type float32")
-        return feature
+        return feature, A
 
     def _operator(self, device=None):
         adj = self.adj if isinstance(self.adj, sp.csr_matrix) else sp.csr_matrix(self.adj)
         return DeviceCSR.from_scipy(adj, device=device)
 
     def propagate(self, adj, feature):
-        feature = self._checked_inputs(adj, feature)
+        feature, A = self._checked_inputs(adj, feature)
         if self.prop_steps <= 0:
             return [torch.FloatTensor(feature)]
-        A = self._operator()
+        A = A if A is not None else self._operator()
         X = torch.from_numpy(np.ascontiguousarray(feature)).to(A.device)
         panels = _device_propagate(A, X, self.prop_steps)
         host = [torch.empty(tuple(p.shape), dtype=torch.float32, pin_memory=True) for p in panels[1:]]
@@ -74,16 +106,16 @@ class GraphOp:
     def propagate_device(self, adj, feature, device=None):
         """Same as propagate() but returns device tensors (hop 0 = the feature on the device)."""
         if isinstance(feature, Tensor) and feature.is_cuda:
-            self.adj = self.construct_adj(adj)
+            A = self._build_operator(adj, feature.device)
             if not isinstance(adj, sp.csr_matrix):
                 raise TypeError("The adjacency matrix must be a scipy csr sparse matrix!")
-            if self.adj.shape[1] != feature.shape[0]:
+            if adj.shape[0] != feature.shape[0]:
                 raise ValueError("Dimension mismatch detected for the adjacency and the feature matrix!")
-            A = self._operator(feature.device)
+            A = A if A is not None else self._operator(feature.device)
             X = feature.to(torch.float32)
         else:
-            feature = self._checked_inputs(adj, feature)
-            A = self._operator(device)
+            feature, A = self._checked_inputs(adj, feature, device)
+            A = A if A is not None else self._operator(device)
             X = torch.from_numpy(np.ascontiguousarray(feature)).to(A.device)
         return _device_propagate(A, X, self.prop_steps)
 
@@ -93,16 +125,16 @@ class GraphOp:
         and errors as propagate(); learnable message ops raise ValueError (they need the list)."""
         from srgnn.aggregate import fused_combine
         if isinstance(feature, Tensor) and feature.is_cuda:
-            self.adj = self.construct_adj(adj)
+            A = self._build_operator(adj, feature.device)
             if not isinstance(adj, sp.csr_matrix):
                 raise TypeError("The adjacency matrix must be a scipy csr sparse matrix!")
-            if self.adj.shape[1] != feature.shape[0]:
+            if adj.shape[0] != feature.shape[0]:
                 raise ValueError("Dimension mismatch detected for the adjacency and the feature matrix!")
-            A = self._operator(feature.device)
+            A = A if A is not None else self._operator(feature.device)
             X = feature.to(torch.float32).contiguous()
         else:
-            feature = self._checked_inputs(adj, feature)
-            A = self._operator(device)
+            feature, A = self._checked_inputs(adj, feature, device)
+            A = A if A is not None else self._operator(device)
             X = torch.from_numpy(np.ascontiguousarray(feature)).to(A.device, torch.float32)
         out = fused_combine(A, X, max(self.prop_steps, 0), msg_op)
         return out.cpu() if to_host else out

@@ -13,3 +13,8 @@ class SymLaplacianGraphOp(GraphOp):
 
     def construct_adj(self, adj):
         return adj_to_symmetric_norm(adj.tocoo(), self.r).tocsr()
+
+    def construct_adj_device(self, adj, device):
+        """construct_adj on the GPU (srgnn.construct.sym_norm), bit-identical to the host scipy."""
+        from srgnn.construct import sym_norm
+        return sym_norm(adj.indptr, adj.indices, adj.data, adj.shape[0], self.r, device=device)

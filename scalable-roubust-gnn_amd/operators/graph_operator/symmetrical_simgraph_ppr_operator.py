@@ -19,3 +19,8 @@ class PprGraphOp(GraphOp):
             raise TypeError("The adjacency matrix must be a scipy.sparse.coo_matrix/csr_matrix!")
         norm = adj_to_symmetric_norm(adj, self.r)
         return ((1 - self.alpha) * norm + self.alpha * sp.eye(adj.shape[0])).tocsr()
+
+    def construct_adj_device(self, adj, device):
+        """construct_adj on the GPU (srgnn.construct.ppr_norm), bit-identical to the host scipy."""
+        from srgnn.construct import ppr_norm
+        return ppr_norm(adj.indptr, adj.indices, adj.data, adj.shape[0], self.r, self.alpha, device=device)

@@ -1,0 +1,126 @@
+"""construct_adj on the device: Â of SymLaplacianGraphOp / PprGraphOp
+from any scipy-style adjacency, bit-identical to the reference's scipy arithmetic.
+
+Reference (SSRG/operators/utils.py:81-93, symmetrical_simgraph_ppr_operator.py:13-21):
+    adj = adj + I                                   duplicates merged left to right, zeros dropped
+    deg = adj.sum(1)                                fp64 row sums in column order
+    left = deg^(r-1), right = deg^(-r)              np.power, inf -> 0
+    Â = (adj . diag(left))^T . diag(right)          Â[i, j] = ((A+I)[j, i] * left[i]) * right[j]
+    PPR: (1 - alpha) * Â + alpha * I
+Every step is an elementwise fp64 product, a sort, or a sequential segment sum
+(srg_segment_sum_f64), so the device result equals scipy's bit for bit; np.power stays on the
+host (N values through the same libm call as the reference).  Canonical inputs are pinned by the
+golden fixtures; for non-canonical weighted inputs scipy sums a row in its own merge order, so
+the last fp64 bit may differ there (integer weights are exact in any order).
+"""
+from __future__ import annotations
+
+import numpy as np
+import scipy.sparse as sp
+import torch
+
+from . import _lib
+from .normalize import degree_powers
+
+
+def segment_sum_device(seg_ptr: torch.Tensor, vals: torch.Tensor) -> torch.Tensor:
+    n_seg = seg_ptr.numel() - 1
+    out = torch.empty(n_seg, dtype=torch.float64, device=vals.device)
+    rc = _lib.lib().srg_segment_sum_f64(seg_ptr.data_ptr(), vals.data_ptr() if vals.numel() else None,
+                                        n_seg, out.data_ptr(), torch.cuda.current_stream(vals.device).cuda_stream)
+    _lib.check(rc, "srg_segment_sum_f64")
+    return out
+
+
+def _runs(keys: torch.Tensor):
+    """Start offsets (+ end) of the runs of equal values in a sorted 1-D tensor."""
+    if keys.numel() == 0:
+        return torch.zeros(1, dtype=torch.int64, device=keys.device)
+    new = torch.ones(keys.numel(), dtype=torch.bool, device=keys.device)
+    new[1:] = keys[1:] != keys[:-1]
+    starts = torch.nonzero(new).squeeze(1)
+    return torch.cat([starts, torch.tensor([keys.numel()], dtype=torch.int64, device=keys.device)])
+
+
+def canonical_sum(rows, cols, vals, n_cols, segsum):
+    """Sorted (row, col) triplets with duplicates summed in input order and zeros dropped."""
+    key = rows * n_cols + cols
+    key, perm = torch.sort(key, stable=True)
+    ptr = _runs(key)
+    summed = segsum(ptr, vals[perm])
+    key = key[ptr[:-1]]
+    keep = summed != 0
+    key, summed = key[keep], summed[keep]
+    return key // n_cols, key % n_cols, summed
+
+
+def _indptr(rows, n):
+    ptr = torch.zeros(n + 1, dtype=torch.int64, device=rows.device)
+    ptr[1:] = torch.cumsum(torch.bincount(rows, minlength=n), 0)
+    return ptr
+
+
+def sym_norm(indptr, indices, data, n: int, r: float, device=None, segsum=None):
+    """Â = D^(r-1) (A+I)^T D^(-r) of the CSR (indptr, indices, data) (host arrays or tensors).
+    Returns device tensors (indptr int64, indices int32, values fp64), canonical CSR."""
+    segsum = segsum or segment_sum_device
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    ip = torch.as_tensor(np.asarray(indptr, dtype=np.int64) if not torch.is_tensor(indptr) else indptr).to(dev, torch.int64)
+    ix = torch.as_tensor(np.asarray(indices) if not torch.is_tensor(indices) else indices).to(dev, torch.int64)
+    v = torch.as_tensor(np.asarray(data, dtype=np.float64) if not torch.is_tensor(data) else data).to(dev, torch.float64)
+    rows = torch.repeat_interleave(torch.arange(n, device=dev), ip[1:] - ip[:-1])
+    diag = torch.arange(n, device=dev)
+    # adj + I: the identity's entry is added after the row's own (duplicate) entries
+    rows, cols, vals = canonical_sum(torch.cat([rows, diag]), torch.cat([ix, diag]),
+                                     torch.cat([v, torch.ones(n, dtype=torch.float64, device=dev)]), n, segsum)
+    deg = segsum(_indptr(rows, n), vals)
+    left, right = degree_powers(deg.cpu().numpy(), r)
+    left_t = torch.from_numpy(left).to(dev)
+    right_t = torch.from_numpy(right).to(dev)
+    # stored (rows, cols) of A+I lands at (cols, rows) of Â
+    step1 = vals * left_t[cols]
+    keep = step1 != 0
+    rows, cols, step1 = rows[keep], cols[keep], step1[keep]
+    step2 = step1 * right_t[rows]
+    keep = step2 != 0
+    t_rows, t_cols, step2 = cols[keep], rows[keep], step2[keep]
+    key, perm = torch.sort(t_rows * n + t_cols)
+    return _indptr(key // n, n), (key % n).to(torch.int32), step2[perm]
+
+
+def ppr_norm(indptr, indices, data, n: int, r: float, alpha: float, device=None, segsum=None):
+    """(1 - alpha) Â + alpha I (symmetrical_simgraph_ppr_operator.py:19-21) on the device."""
+    segsum = segsum or segment_sum_device
+    ip, ix, v = sym_norm(indptr, indices, data, n, r, device, segsum)
+    dev = ip.device
+    rows = torch.repeat_interleave(torch.arange(n, device=dev), ip[1:] - ip[:-1])
+    v = (1 - alpha) * v
+    diag = torch.arange(n, device=dev)
+    rows, cols, vals = canonical_sum(torch.cat([rows, diag]), torch.cat([ix.to(torch.int64), diag]),
+                                     torch.cat([v, torch.full((n,), alpha, dtype=torch.float64, device=dev)]),
+                                     n, segsum)
+    return _indptr(rows, n), cols.to(torch.int32), vals
+
+
+def to_scipy(indptr, indices, values, n: int) -> sp.csr_matrix:
+    """Host scipy copy (the reference keeps Â as GraphOp.adj)."""
+    return sp.csr_matrix((values.cpu().numpy(), indices.cpu().numpy(), indptr.cpu().numpy()), shape=(n, n))
+
+
+def edge_index_to_adj(edge_index, n: int, symmetric: bool = False, device=None, segsum=None):
+    """csr_matrix((ones, (row, col)), shape=(n, n)) of an int64 [2, E] edge list on the device
+    (duplicates summed), optionally symmetrised first by appending the reversed edges -- the
+    dataset adjacency the reference's loaders build from edge_index.pt.
+    Returns device tensors (indptr int64, indices int32, values fp64)."""
+    segsum = segsum or segment_sum_device
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    e = torch.as_tensor(edge_index).to(dev, torch.int64)
+    if e.dim() != 2 or e.shape[0] != 2:
+        raise ValueError("edge_index must be [2, E]")
+    row, col = e[0], e[1]
+    if e.numel() and (int(e.min()) < 0 or int(e.max()) >= n):
+        raise ValueError("edge_index holds node ids outside [0, n)")
+    if symmetric:
+        row, col = torch.cat([row, col]), torch.cat([col, row])
+    rows, cols, vals = canonical_sum(row, col, torch.ones(row.numel(), dtype=torch.float64, device=dev), n, segsum)
+    return _indptr(rows, n), cols.to(torch.int32), vals

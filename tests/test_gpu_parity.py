@@ -319,3 +319,40 @@ def test_launch_chunking_beyond_2e32_lanes(oracle_mod):
     want = torch.addcmul(torch.zeros_like(Y), a0, x0)       # 0 + a*x, then fma with 0.5*x1 (exact)
     want = want + 0.5 * x1
     assert torch.equal(Y, want)
+
+
+@pytest.mark.parametrize("name", G.names("norm"))
+def test_device_construct_adj_bit_exact(name):
+    """construct_adj on the GPU (srgnn.construct: sorts, sequential fp64 segment sums, host
+    np.power) == the reference's scipy Â stored in the fixture, bit for bit (fp64 values)."""
+    from srgnn import construct as C
+    c = G.Case(name)
+    a = c.adj()
+    if c.meta["op"] == "ppr":
+        ip, ix, v = C.ppr_norm(a.indptr, a.indices, a.data, c.n, c.meta["r"], c.meta["alpha"], device="cuda")
+    else:
+        ip, ix, v = C.sym_norm(a.indptr, a.indices, a.data, c.n, c.meta["r"], device="cuda")
+    np.testing.assert_array_equal(ip.cpu().numpy(), c["ahat_indptr"])
+    np.testing.assert_array_equal(ix.cpu().numpy(), c["ahat_indices"])
+    np.testing.assert_array_equal(v.cpu().numpy(), c["ahat_data64"])
+
+
+def test_device_construct_weighted_duplicates_equal_oracle(oracle_mod):
+    from srgnn import construct as C
+    rng = np.random.default_rng(4)
+    n, m = 5000, 60000
+    r, c = rng.integers(0, n, m), rng.integers(0, n, m)
+    v = rng.random(m) * 3
+    order = np.lexsort((rng.random(m), r))
+    r, c, v = r[order], c[order], v[order]
+    ptr = np.r_[0, np.cumsum(np.bincount(r, minlength=n))]
+    ip, ix, vals = C.sym_norm(ptr, c.astype(np.int32), v, n, 0.4, device="cuda")
+    want = oracle_mod.sym_norm(ptr, c, v, n, 0.4)
+    for got, w in zip((ip, ix, vals), want):
+        np.testing.assert_array_equal(got.cpu().numpy(), w)
+    e = np.stack([r, c]).astype(np.int64)
+    ip, ix, vals = C.edge_index_to_adj(torch.from_numpy(e), n, symmetric=True, device="cuda")
+    want = sp.csr_matrix((np.ones(2 * m), (np.r_[r, c], np.r_[c, r])), shape=(n, n))
+    np.testing.assert_array_equal(ip.cpu().numpy(), want.indptr)
+    np.testing.assert_array_equal(ix.cpu().numpy(), want.indices)
+    np.testing.assert_array_equal(vals.cpu().numpy(), want.data)
