@@ -363,28 +363,36 @@ k_spmm(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
 //
 // A slice wave keeps 8 KiB of gathers in flight, so a row of degree D costs ~D/64 load latencies
 // (~6 ms for the 155,868-entry hub of the products-shaped graph): hidden at 1 GPU, the whole hop
-// at 8.  Here 8 producer waves keep kHubUH = 16 dwordx4 gathers (8 nonzeros' 128-byte slices
-// each) in flight per lane -- 128 KiB per workgroup -- for a window of 1024 nonzeros, with the
-// column ids / values of the NEXT window already in registers (one dependent latency per window,
-// not two).  A window is staged into a transposed LDS tile [32 columns][1024 nonzeros]; one
-// consumer wave then runs the 32 column chains over it in CSR order, reading 4 links per
-// ds_read_b128, while the producers' gathers for the following window are in flight.
+// at 8.  Here the row's chain is fed from LDS by 8 producer waves:
+//   * windows of kHubW = 512 nonzeros, double-buffered tiles: while the consumer runs window h
+//     from one tile, the producers write window h+1 into the other (one barrier per window);
+//   * each producer lane gathers kHubUW = 8 dwordx4 (8 nonzeros' 128-byte slices per wave
+//     instruction) per window into one of two register sets, so a window's gathers are issued
+//     two windows before they are written (~2 us of latency cover); the column ids / values of
+//     the next window are loaded one window ahead;
+//   * the tile is transposed, [32 columns][kHubLd] with the 4-nonzero group index XOR-swizzled
+//     per column group (conflict-free ds_write_b32 and ds_read_b128, see kHubLd);
+//   * the consumer wave (lanes 0..31, one column each) runs the 32 chains, 4 links per
+//     ds_read_b128, with a ring of three 16-link register sets so every LDS read is issued two
+//     sets (~32 links) before its fmas.
 // Still exactly one fma chain per output element, in CSR order.
 // ------------------------------------------------------------------------------------------------
 constexpr int kHubProducers = 8;
-constexpr int kHubUH = 16;
-constexpr int kHubStage = kHubProducers * kHubUH * 8;   // nonzeros per LDS window (1024)
-
+constexpr int kHubW = 512;                                   // nonzeros per window
+constexpr int kHubUW = kHubW / (kHubProducers * 8);          // gathers per producer lane per window (8)
 constexpr int kHubThreads = 64 * (kHubProducers + 1);
-// LDS tile [32 columns][kHubLd]: column c holds the window's nonzeros in groups of 4, group index
-// XOR-ed with hub_swz(c).  kHubLd = 1028 (16-byte aligned columns, stride = 4 banks): the
-// consumer's ds_read_b128 of 16 lanes and the producers' ds_write_b32 of 32 lanes are
-// (nearly) conflict-free -- see DESIGN.md §5.1.
-constexpr int kHubLd = kHubStage + 4;
+// floats per tile column: 528 == 16 (mod 64).  With the 4-link group index XOR-ed by (c >> 2) & 7,
+// both the producers' transposed ds_write_b32 (lanes: 4 nonzeros x 8 column chunks) and the
+// consumer's ds_read_b128 (lanes: 32 columns, 16-lane groups) are bank-conflict-free (exhaustive
+// check over all window offsets; the 4 (mod 64) stride of the first version made the reads 2-way)
+constexpr int kHubLd = kHubW + 16;
+constexpr int kHubTile = kSliceCols * kHubLd;                // floats per tile
 __device__ __forceinline__ int hub_swz(int c) { return (c >> 2) & 7; }
 
-// ABL (ablation, diagnostic builds only): 0 = the real kernel; 1 = the consumer skips its chains
-// (producer-bound time); 2 = the producers skip their gathers (consumer-bound time).
+// ABL (diagnostic ablations, SRGNN_HUB_ABLATION): 0 = the kernel; 1 = the consumer skips its
+// chains; 2 = the producers skip gathers and LDS writes; 3 = the consumer's fmas read registers
+// only (no LDS reads); 4 = producers gather but skip the LDS writes; 5 / 6 = the consumer reads
+// only the tile / only the values from LDS.
 template <bool SFULL, typename IP, int ABL = 0>
 __global__ void __launch_bounds__(kHubThreads)
 k_spmm_hub(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
@@ -394,8 +402,8 @@ k_spmm_hub(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
 {
     typedef typename Vec<float, 4>::type V4;
     extern __shared__ __attribute__((aligned(16))) float hub_lds[];
-    float* tile = hub_lds;                              // [32 columns][kHubLd], swizzled groups of 4
-    float* aval = hub_lds + kSliceCols * kHubLd;        // [kHubStage]
+    // [2 tiles][32 columns][kHubLd] then [2][kHubW] values
+    float* aval_base = hub_lds + 2 * kHubTile;
     const int item = blockIdx.x;
     const int row = hub_rows[item / n_slices];
     const int slice = item % n_slices;
@@ -403,56 +411,89 @@ k_spmm_hub(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
     const int lane = threadIdx.x & 63;
     const int64_t beg = indptr[row];
     const int64_t end = indptr[row + 1];
-    const int n_stages = (int)((end - beg + kHubStage - 1) / kHubStage);
+    const int n_win = (int)((end - beg + kHubW - 1) / kHubW);
 
     if (wave == 0) {   // ---------------- consumer: 32 column chains ----------------
-        const int ccol = slice * kSliceCols + lane;
+        const int c = lane & 31;
+        const int ccol = slice * kSliceCols + c;
         const bool cact = lane < kSliceCols && (SFULL || ccol < d);
         float* __restrict__ yrow = Y + (int64_t)row * ldy;
         float acc = 0.0f;
         if (accumulate && cact) acc = yrow[ccol];
-        // lane c reads 4 consecutive nonzeros of column c per ds_read_b128 (one LDS instruction per
-        // 4 chain links: a single wave issues LDS reads at a fraction of the CU rate, so the read
-        // count, not the 4-cycle fma dependency, bounds the chain otherwise).  Reads run 16 links
-        // ahead of the fmas (ping-pong).
-        const int c = lane & 31;
-        const float* tcol = tile + c * kHubLd;
         const int sw = hub_swz(c);
-        constexpr int G = 4;   // groups of 4 nonzeros per chunk
-        V4 t0[G], a0[G], t1[G], a1[G];
-        auto ld = [&](int grp, V4 (&t)[G], V4 (&a)[G]) {
+        constexpr int G = 2;                      // groups of 4 links per register set (8 links)
+        V4 tA[G], aA[G], tB[G], aB[G], tC[G], aC[G], tD[G], aD[G];
+        for (int h = 0; h < n_win; ++h) {
+            __syncthreads();                      // window h is in tile h & 1
+            if (lane < kSliceCols) {
+                const float* tcol = hub_lds + (h & 1) * kHubTile + c * kHubLd;
+                const float* av = aval_base + (h & 1) * kHubW;
+                const int64_t sb = beg + (int64_t)h * kHubW;
+                const int nb = (end - sb) < kHubW ? (int)(end - sb) : kHubW;
+                const int nc = nb / (4 * G);      // full 8-link sets
+                auto ld = [&](int set, V4 (&t)[G], V4 (&a)[G]) {
 #pragma unroll
-            for (int i = 0; i < G; ++i) {
-                t[i] = *reinterpret_cast<const V4*>(tcol + (((grp + i) ^ sw) << 2));
-                a[i] = *reinterpret_cast<const V4*>(aval + ((grp + i) << 2));   // broadcast read
-            }
-        };
-        auto run = [&](const V4 (&t)[G], const V4 (&a)[G]) {
+                    for (int i = 0; i < G; ++i) {
+                        const int grp = set * G + i;
+                        if (ABL != 6) t[i] = *reinterpret_cast<const V4*>(tcol + ((grp ^ sw) << 2));
+                        if (ABL != 5) a[i] = *reinterpret_cast<const V4*>(av + (grp << 2));   // broadcast
+                    }
+                };
+                auto run = [&](const V4 (&t)[G], const V4 (&a)[G]) {
 #pragma unroll
-            for (int i = 0; i < G; ++i) {
-                acc = __builtin_fmaf(a[i][0], t[i][0], acc);
-                acc = __builtin_fmaf(a[i][1], t[i][1], acc);
-                acc = __builtin_fmaf(a[i][2], t[i][2], acc);
-                acc = __builtin_fmaf(a[i][3], t[i][3], acc);
-            }
-        };
-        for (int st = 0; st < n_stages; ++st) {
-            __syncthreads();   // A: producers may overwrite the tile
-            __syncthreads();   // B: window st is in the tile
-            const int64_t sb = beg + (int64_t)st * kHubStage;
-            const int nb = (end - sb) < kHubStage ? (int)(end - sb) : kHubStage;
-            const int nc = ABL == 1 ? 0 : nb / (4 * G);   // full chunks of 16 nonzeros
-            if (nc > 0) ld(0, t0, a0);
-            for (int k = 0; k < nc; k += 2) {
-                if (k + 1 < nc) ld((k + 1) * G, t1, a1);
-                run(t0, a0);
-                if (k + 1 >= nc) break;
-                if (k + 2 < nc) ld((k + 2) * G, t0, a0);
-                run(t1, a1);
-            }
-            if (ABL != 1)
+                    for (int i = 0; i < G; ++i) {
+                        acc = __builtin_fmaf(a[i][0], t[i][0], acc);
+                        acc = __builtin_fmaf(a[i][1], t[i][1], acc);
+                        acc = __builtin_fmaf(a[i][2], t[i][2], acc);
+                        acc = __builtin_fmaf(a[i][3], t[i][3], acc);
+                    }
+                };
+                if (ABL == 1) continue;
+                if (ABL == 5 || ABL == 6)
+                    for (int i = 0; i < G; ++i)
+                        tA[i] = tB[i] = tC[i] = tD[i] = aA[i] = aB[i] = aC[i] = aD[i] = vzero<float, 4>();
+                // unconditional: sets past nc read stale tile / value words, never used (and the
+                // waitcnt pass then sees one issue order on every path into the loop)
+                ld(0, tA, aA);
+                __builtin_amdgcn_sched_barrier(0);
+                ld(1, tB, aB);
+                __builtin_amdgcn_sched_barrier(0);
+                ld(2, tC, aC);
+                __builtin_amdgcn_sched_barrier(0);
+                if (ABL == 3) ld(3, tD, aD);
+                int k = 0;
+                // ring of four 8-link sets: every read is issued three sets (24 links) before its
+                // fmas, with at most 12 LDS reads outstanding (lgkmcnt counts 15).  The loop's
+                // loads are unconditional (k + 6 < nc) and the scheduling barriers keep the ring's
+                // order; the last <= 6 sets run after it.
+                for (; k + 7 <= nc; k += 4) {
+                    if (ABL != 3) ld(k + 3, tD, aD);
+                    __builtin_amdgcn_sched_barrier(0);
+                    run(tA, aA);
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (ABL != 3) ld(k + 4, tA, aA);
+                    __builtin_amdgcn_sched_barrier(0);
+                    run(tB, aB);
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (ABL != 3) ld(k + 5, tB, aB);
+                    __builtin_amdgcn_sched_barrier(0);
+                    run(tC, aC);
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (ABL != 3) ld(k + 6, tC, aC);
+                    __builtin_amdgcn_sched_barrier(0);
+                    run(tD, aD);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                if (k < nc) run(tA, aA);
+                if (k + 1 < nc) run(tB, aB);
+                if (k + 2 < nc) run(tC, aC);
+                for (int j = k + 3; j < nc; ++j) {
+                    if (ABL != 3) ld(j, tD, aD);
+                    run(tD, aD);
+                }
                 for (int q = nc * 4 * G; q < nb; ++q)
-                    acc = __builtin_fmaf(aval[q], tcol[(((q >> 2) ^ sw) << 2) + (q & 3)], acc);
+                    acc = __builtin_fmaf(av[q], tcol[(((q >> 2) ^ sw) << 2) + (q & 3)], acc);
+            }
         }
         if (cact) {
             if (nt)
@@ -465,57 +506,72 @@ k_spmm_hub(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
 
     // ---------------- producers ----------------
     const int p = wave - 1;
-    const int g = lane >> 3;
-    const int qq = lane & 7;
+    const int g = lane >> 3;          // nonzero within a gather's group of 8
+    const int qq = lane & 7;          // 16-byte chunk = columns qq*4 .. qq*4+3 of the slice
     const int qcol = slice * kSliceCols + qq * 4;
     const bool gact = SFULL || qcol < d;
-    V4 x[kHubUH];
-    float av[kHubUH];      // values of the window being gathered
-    int cn[kHubUH];        // column ids of the next window
-    float an[kHubUH];      // values of the next window
-    auto load_ids = [&](int64_t sb) {
+    V4 x0[kHubUW], x1[kHubUW];        // gathered windows, two register sets (even / odd windows)
+    float a0[kHubUW], a1[kHubUW];
+    int cn[kHubUW];                   // column ids / values of the next window to gather
+    float an[kHubUW];
+    auto load_ids = [&](int w) {
+        const int64_t sb = beg + (int64_t)w * kHubW;
 #pragma unroll
-        for (int b = 0; b < kHubUH; ++b) {
-            int64_t jj = sb + (p * kHubUH + b) * 8 + g;
+        for (int b = 0; b < kHubUW; ++b) {
+            int64_t jj = sb + (p * kHubUW + b) * 8 + g;
             jj = jj < end ? jj : end - 1;
             cn[b] = indices[jj];
             an[b] = vals[jj];
         }
     };
-    auto gather = [&]() {   // gathers of the window whose ids are in cn/an
+    auto gather = [&](V4 (&x)[kHubUW], float (&a)[kHubUW]) {
 #pragma unroll
-        for (int b = 0; b < kHubUH; ++b) {
+        for (int b = 0; b < kHubUW; ++b) {
             x[b] = (gact && ABL != 2) ? gload<float, 4>(X + (int64_t)cn[b] * ldx + qcol) : vzero<float, 4>();
-            av[b] = an[b];
+            a[b] = an[b];
         }
     };
-    if (n_stages > 0) {
-        load_ids(beg);
-        __builtin_amdgcn_sched_barrier(0);
-        gather();
-        if (n_stages > 1) load_ids(beg + kHubStage);
-    }
-    for (int st = 0; st < n_stages; ++st) {
-        __syncthreads();   // A: the consumer is done with the previous window
+    auto put = [&](int w, const V4 (&x)[kHubUW], const float (&a)[kHubUW]) {
+        if (ABL == 2 || ABL == 4) return;
+        float* tile = hub_lds + (w & 1) * kHubTile;
+        float* av = aval_base + (w & 1) * kHubW;
 #pragma unroll
-        for (int b = 0; b < kHubUH; ++b) {
-            const int nl = (p * kHubUH + b) * 8 + g;     // nonzero within the window
+        for (int b = 0; b < kHubUW; ++b) {
+            const int nl = (p * kHubUW + b) * 8 + g;   // nonzero within the window
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {               // transposed, swizzled: conflict-free
+            for (int i = 0; i < 4; ++i) {             // transposed, swizzled: conflict-free
                 const int cc = qq * 4 + i;
                 tile[cc * kHubLd + ((((nl >> 2) ^ hub_swz(cc)) << 2) | (nl & 3))] = x[b][i];
             }
-            if (qq == 0) aval[nl] = av[b];
+            if (qq == 0) av[nl] = a[b];
         }
-        if (st + 1 < n_stages) {
-            gather();                                                   // window st+1 in flight
-            if (st + 2 < n_stages) load_ids(beg + (int64_t)(st + 2) * kHubStage);   // ids of st+2
-        }
-        __syncthreads();   // B: window st published
+    };
+    // prologue: windows 0 and 1 in flight, window 0 published, window 2 in flight
+    if (n_win > 0) {
+        load_ids(0);
+        __builtin_amdgcn_sched_barrier(0);
+        gather(x0, a0);
+        if (n_win > 1) { load_ids(1); gather(x1, a1); }
+        if (n_win > 2) load_ids(2);
+        put(0, x0, a0);
+        if (n_win > 2) { gather(x0, a0); if (n_win > 3) load_ids(3); }
     }
+    __syncthreads();                              // window 0 published
+    for (int h = 0; h + 1 < n_win; h += 2) {
+        // window h+1 (odd, set 1) -> tile 1 while the consumer runs window h; then gather h+3
+        put(h + 1, x1, a1);
+        if (h + 3 < n_win) { gather(x1, a1); if (h + 4 < n_win) load_ids(h + 4); }
+        __syncthreads();
+        if (h + 2 >= n_win) break;
+        // window h+2 (even, set 0) -> tile 0 while the consumer runs window h+1; then gather h+4
+        put(h + 2, x0, a0);
+        if (h + 4 < n_win) { gather(x0, a0); if (h + 5 < n_win) load_ids(h + 5); }
+        __syncthreads();
+    }
+    // barrier count: 1 (prologue) + (n_win - 1) in the loop == the consumer's n_win
 }
 
-constexpr size_t kHubLdsBytes = (size_t)(kSliceCols * kHubLd + kHubStage) * sizeof(float);
+constexpr size_t kHubLdsBytes = (size_t)(2 * kHubTile + 2 * kHubW) * sizeof(float);
 
 // ------------------------------------------------------------------------------------------------
 // Chebyshev step with fused epilogue (wavelet basis)
@@ -784,9 +840,7 @@ int side_stream(SideStream** out)
         SRG_HIP_CHECK(hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming));
         SRG_HIP_CHECK(hipEventCreateWithFlags(&ss.join, hipEventDisableTiming));
         for (const void* fn : {(const void*)k_spmm_hub<true, int>, (const void*)k_spmm_hub<false, int>,
-                               (const void*)k_spmm_hub<true, int64_t>, (const void*)k_spmm_hub<false, int64_t>,
-                               (const void*)k_spmm_hub<true, int, 1>, (const void*)k_spmm_hub<true, int64_t, 1>,
-                               (const void*)k_spmm_hub<true, int, 2>, (const void*)k_spmm_hub<true, int64_t, 2>})
+                               (const void*)k_spmm_hub<true, int64_t>, (const void*)k_spmm_hub<false, int64_t>})
             SRG_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kHubLdsBytes));
     }
     *out = &ss;
@@ -824,15 +878,21 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
         SRG_HIP_CHECK(hipStreamWaitEvent(ss->stream, ss->fork, 0));
         const dim3 hgrid((unsigned)(n_hub * n_slices));
         static const int abl = [] { const char* e = getenv("SRGNN_HUB_ABLATION"); return e ? atoi(e) : 0; }();
-        if (sfull && abl == 1)
-            hipLaunchKernelGGL((k_spmm_hub<true, IP, 1>), hgrid, dim3(kHubThreads), kHubLdsBytes,
-                               ss->stream, indptr, indices, vals, order, n_slices, X, ldx, Y, ldy,
-                               d, acc, nt);
-        else if (sfull && abl == 2)
-            hipLaunchKernelGGL((k_spmm_hub<true, IP, 2>), hgrid, dim3(kHubThreads), kHubLdsBytes,
-                               ss->stream, indptr, indices, vals, order, n_slices, X, ldx, Y, ldy,
-                               d, acc, nt);
-        else if (sfull)
+        if (sfull && abl >= 1 && abl <= 6) {
+            auto k = abl == 1 ? k_spmm_hub<true, IP, 1> : abl == 2 ? k_spmm_hub<true, IP, 2>
+                   : abl == 3 ? k_spmm_hub<true, IP, 3> : abl == 4 ? k_spmm_hub<true, IP, 4>
+                   : abl == 5 ? k_spmm_hub<true, IP, 5> : k_spmm_hub<true, IP, 6>;
+            static bool attr = false;
+            if (!attr) {
+                for (auto f : {k_spmm_hub<true, IP, 1>, k_spmm_hub<true, IP, 2>, k_spmm_hub<true, IP, 3>,
+                               k_spmm_hub<true, IP, 4>, k_spmm_hub<true, IP, 5>, k_spmm_hub<true, IP, 6>})
+                    SRG_HIP_CHECK(hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                      (int)kHubLdsBytes));
+                attr = true;
+            }
+            hipLaunchKernelGGL(k, hgrid, dim3(kHubThreads), kHubLdsBytes, ss->stream, indptr, indices, vals,
+                               order, n_slices, X, ldx, Y, ldy, d, acc, nt);
+        } else if (sfull)
             hipLaunchKernelGGL((k_spmm_hub<true, IP>), hgrid, dim3(kHubThreads), kHubLdsBytes,
                                ss->stream, indptr, indices, vals, order, n_slices, X, ldx, Y, ldy,
                                d, acc, nt);

@@ -34,8 +34,16 @@ _HUB_ENV = os.environ.get("SRGNN_HUB_THRESHOLD", "auto")
 DEFAULT_HUB_THRESHOLD = None if _HUB_ENV == "auto" else int(_HUB_ENV)
 
 
-def auto_hub_threshold(nnz: int) -> int:
-    return max(8192, int(nnz) // 1024)
+def auto_hub_threshold(nnz: int, launches: int = 1) -> int:
+    """Row length above which a row goes to the hub workgroups (side stream, beside the main
+    launch).  A slice wave needs ~38 ns per nonzero (one dependent gather per 8-nonzero group
+    of its row), so a row should be a hub once that latency nears the duration of the launch it
+    belongs to: ~nnz * 520 B / 6.5 TB/s at d = 128, split over `launches` back-to-back launches
+    (the halo exchange's row groups).  Calibrated on the products-shaped graph: one launch ->
+    nnz / 1024 (floor 8192); C launches -> nnz / (1024 C) (floor 2048)."""
+    if launches <= 1:
+        return max(8192, int(nnz) // 1024)
+    return max(2048, int(nnz) // (1024 * int(launches)))
 
 
 def _dev(device):

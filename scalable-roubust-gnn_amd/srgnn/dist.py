@@ -183,7 +183,7 @@ class HaloPartitionedOperator:
         thr = torch.empty(P, dtype=torch.int64, device=dev)
         for q in range(P):
             nnz_q = int(gip[self.starts[q + 1]] - gip[self.starts[q]])
-            thr[q] = auto_hub_threshold(nnz_q) if hub_threshold is None else (
+            thr[q] = auto_hub_threshold(nnz_q, launches=max(1, int(chunks))) if hub_threshold is None else (
                 hub_threshold if hub_threshold >= 0 else (1 << 62))
         is_hub = deg > thr[owner]
         # chunk of every row (contiguous nnz-balanced ranges inside each owner's block)

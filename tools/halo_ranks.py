@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""Per-rank compute of the halo-exchange partition, measured on ONE GPU with virtual ranks.
+
+For P in --worlds, builds every rank's HaloPartitionedOperator share of the products-shaped graph
+and times, with HIP events, one hop of its local kernels (each group's launch, the hub group
+separately) on halo-filled panels.  The max over ranks is the compute floor of one hop at P GPUs;
+together with each rank's inbound halo bytes it bounds what the driver's N-GPU run can reach.
+
+    python tools/halo_ranks.py [--config products] [--worlds 2,4,8] [--reps 5]   -> JSON
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", "scalable-roubust-gnn_amd"))
+
+import torch  # noqa: E402
+
+from srgnn import graphs, synth  # noqa: E402
+from srgnn.dist import HaloPartitionedOperator  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="products")
+    ap.add_argument("--worlds", default="2,4,8")
+    ap.add_argument("--chunks", type=int, default=4)
+    ap.add_argument("--reps", type=int, default=5)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    ip, ix, vals, n, d, K = graphs.build(a.config, dev)
+    x = synth.uniform_features_t(n, d, device=dev)
+    out = {"config": a.config, "n": n, "nnz": int(ix.numel()), "d": d, "worlds": {}}
+    for P in [int(w) for w in a.worlds.split(",")]:
+        ranks = []
+        for q in range(P):
+            op = HaloPartitionedOperator(ip, ix, vals, n, chunks=a.chunks, device=dev, rank=q, world=P)
+            src = op.new_panel(d)
+            src[: op.rows].copy_(x[op.r0:op.r1])
+            src[op.rows:].uniform_(-1, 1)
+            dst = op.new_panel(d)
+            times = {}
+            for name, groups in (("all", range(op.n_groups)), ("hub", [op.C]), ("chunks", range(op.C))):
+                ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * a.reps)]
+                for r in range(a.reps):
+                    ev[2 * r].record()
+                    for g in groups:
+                        if op.views[g][1]:
+                            op._spmm(op._A[g], src, dst[: op.rows])
+                    ev[2 * r + 1].record()
+                torch.cuda.synchronize()
+                ms = sorted(ev[2 * r].elapsed_time(ev[2 * r + 1]) for r in range(a.reps))
+                times[name] = ms[len(ms) // 2]
+            ranks.append({"rank": q, "rows": op.rows, "nnz": op.nnz_local, "halo_rows": op.halo,
+                          "halo_bytes": op.halo * d * 4, "hub_rows": op.views[op.C][1],
+                          "ms_all_serial": times["all"], "ms_hub": times["hub"], "ms_chunks": times["chunks"]})
+            del op, src, dst
+            torch.cuda.empty_cache()
+        worst = max(ranks, key=lambda r: max(r["ms_hub"], r["ms_chunks"]))
+        out["worlds"][P] = {"ranks": ranks,
+                            "max_compute_ms": max(max(r["ms_hub"], r["ms_chunks"]) for r in ranks),
+                            "mean_chunks_ms": sum(r["ms_chunks"] for r in ranks) / P,
+                            "worst_rank": worst["rank"],
+                            "max_halo_GB": max(r["halo_bytes"] for r in ranks) / 1e9}
+        print(f"P={P}: max compute {out['worlds'][P]['max_compute_ms']:.3f} ms "
+              f"(rank {worst['rank']}: chunks {worst['ms_chunks']:.3f}, hub {worst['ms_hub']:.3f}), "
+              f"mean chunks {out['worlds'][P]['mean_chunks_ms']:.3f} ms, max halo "
+              f"{out['worlds'][P]['max_halo_GB']:.2f} GB", file=sys.stderr, flush=True)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
