@@ -269,16 +269,45 @@ def wavelet_basis(adj: sp.spmatrix, scale: float = 0.5, order: int = 3, toleranc
     out = []
     for s in range(2):
         phi = sp.hstack(blocks[s]).tocsr()
-        out.append(l1_normalize_rows(phi))
+        out.append(l1_normalize_rows(phi, device=filt.device))
     return out[0], out[1], filt.lmax
 
 
-def l1_normalize_rows(phi: sp.csr_matrix) -> sp.csr_matrix:
-    """sklearn.preprocessing.normalize(phi, norm='l1', axis=1) (base_model.py:287-290): each row
-    divided by the sum of its absolute values; all-zero rows left as they are."""
+def l1_normalize_rows(phi: sp.csr_matrix, device=None) -> sp.csr_matrix:
+    """sklearn.preprocessing.normalize(phi, norm='l1', axis=1) (base_model.py:287-290) on the GPU:
+    per row, the fp64 sum of |x| left to right (srg_segment_sum_f64), then x / sum in fp64
+    rounded to the matrix dtype; all-zero rows left as they are -- sklearn's
+    _inplace_csr_row_normalize_l1 arithmetic exactly."""
+    from .construct import segment_sum_device
     phi = sp.csr_matrix(phi, copy=True)
-    rs = np.add.reduceat(np.abs(phi.data).astype(np.float64), phi.indptr[:-1]) if phi.nnz else np.zeros(0)
-    rs = np.where(np.diff(phi.indptr) > 0, rs if rs.size == phi.shape[0] else 0.0, 1.0)
-    rs[rs == 0] = 1.0
-    phi.data = (phi.data / np.repeat(rs, np.diff(phi.indptr)).astype(phi.dtype)).astype(phi.dtype)
+    if phi.nnz == 0:
+        return phi
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    ip = torch.from_numpy(phi.indptr.astype(np.int64)).to(dev)
+    x = torch.from_numpy(phi.data).to(dev)
+    sums = segment_sum_device(ip, x.to(torch.float64).abs())
+    rows = torch.repeat_interleave(torch.arange(phi.shape[0], device=dev), ip[1:] - ip[:-1])
+    den = sums[rows]
+    out = torch.where(den == 0, x.to(torch.float64), x.to(torch.float64) / den).to(x.dtype)
+    phi.data = out.cpu().numpy()
     return phi
+
+
+def spectral_features(adj: sp.spmatrix, feature, scale: float = 0.5, order: int = 3, tolerance: float = 1e-4,
+                      lmax: float | None = None, batch: int = 1000, device=None):
+    """SpectralModel.preprocess's processed_feature (base_model.py:180-219):
+    [X | relu(phi phi^-1 X)] as a CPU float32 tensor, with phi / phi^-1 from wavelet_basis.
+
+    The reference forms the product matrix phi phi^-1 with torch_sparse.spspmm and then multiplies
+    X; here phi (phi^-1 X) is two exact-chain SpMMs on the GPU (no SpGEMM, no N x N product).
+    Same value up to floating-point association -- parity unpinned (torch_sparse is absent), the
+    tests compare against a dense fp64 evaluation."""
+    from .csr import DeviceCSR
+    from .spmm import spmm
+    phi, phi_inv, lmax = wavelet_basis(adj, scale, order, tolerance, lmax, batch, device)
+    X = torch.as_tensor(np.asarray(feature, dtype=np.float32))
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    A_inv = DeviceCSR.from_scipy(phi_inv, device=dev)
+    A_phi = DeviceCSR.from_scipy(phi, device=dev)
+    loc = torch.relu(spmm(A_phi, spmm(A_inv, X.to(dev).contiguous())))
+    return torch.cat((X, loc.cpu()), dim=1), phi, phi_inv, lmax

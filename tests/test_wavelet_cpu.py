@@ -90,3 +90,24 @@ def test_device_laplacian_builder_matches_host_laplacian():
     np.testing.assert_array_equal(ip.numpy(), L.indptr)
     np.testing.assert_array_equal(ix.numpy(), L.indices)
     np.testing.assert_array_equal(lv.numpy(), L.data.astype(np.float32))
+
+
+def test_l1_normalization_restatement_matches_sklearn():
+    """The arithmetic srgnn.wavelet.l1_normalize_rows runs on the GPU (sequential fp64 sum of |x|,
+    fp64 divide, round to fp32; empty rows kept), restated in numpy, equals sklearn's normalize."""
+    import scipy.sparse as sp
+    from sklearn.preprocessing import normalize
+    rng = np.random.default_rng(3)
+    M = sp.random(400, 300, density=0.2, format="csr", dtype=np.float32, random_state=4)
+    M.data = (rng.random(M.nnz).astype(np.float32) * 3 - 1).astype(np.float32)
+    M = sp.csr_matrix(M)
+    got = M.copy()
+    for i in range(M.shape[0]):
+        lo, hi = M.indptr[i], M.indptr[i + 1]
+        acc = 0.0
+        for x in M.data[lo:hi].tolist():
+            acc += abs(x)
+        if acc != 0.0:
+            got.data[lo:hi] = (M.data[lo:hi].astype(np.float64) / acc).astype(np.float32)
+    want = normalize(M, norm="l1", axis=1)
+    np.testing.assert_array_equal(got.data, want.data)

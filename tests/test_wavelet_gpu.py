@@ -71,15 +71,30 @@ def test_wavelet_basis_matches_oracle_restatement(oracle_mod):
     L = W.laplacian_from_adj(a)
     coeffs = np.stack([oracle_mod.cheby_coeffs(t, lmax, 3) for t in (-0.5, 0.5)])
     R = oracle_mod.cheby_op((L.indptr, L.indices, L.data), coeffs, np.eye(n), lmax)
+    from sklearn.preprocessing import normalize   # what the reference calls (base_model.py:290)
     for s, got in enumerate((phi, phi_inv)):
         m = R[s].copy()
         m[m < 1e-4] = 0
-        m = m.astype(np.float32)
-        rs = np.abs(m).sum(axis=1, dtype=np.float64)
-        rs[rs == 0] = 1
-        want = m / rs[:, None]
-        np.testing.assert_allclose(got.toarray(), want, rtol=1e-6, atol=1e-7)
+        want = normalize(sp.csr_matrix(m.astype(np.float32)), norm="l1", axis=1)
         assert got.dtype == np.float32
+        np.testing.assert_array_equal(got.indptr, want.indptr)
+        np.testing.assert_array_equal(got.indices, want.indices)
+        np.testing.assert_array_equal(got.data, want.data)      # bit-exact (sklearn's arithmetic)
+
+
+def test_spectral_features_vs_dense_fp64(oracle_mod):
+    """SpectralModel.preprocess's processed_feature [X | relu(phi phi^-1 X)] vs a dense fp64
+    evaluation on the same phi / phi^-1 (the product association differs: tolerance 1e-5)."""
+    from srgnn import wavelet as W
+    a = graphs()["rmat3000"]
+    n = a.shape[0]
+    X = np.random.default_rng(5).random((n, 24)).astype(np.float32)
+    out, phi, phi_inv, lmax = W.spectral_features(a, X, scale=0.5, order=3, tolerance=1e-4, batch=700, device="cuda")
+    assert out.shape == (n, 48) and out.dtype == torch.float32
+    np.testing.assert_array_equal(out[:, :24].numpy(), X)
+    want = np.maximum((phi.toarray().astype(np.float64) @ phi_inv.toarray().astype(np.float64)) @ X.astype(np.float64), 0)
+    got = out[:, 24:].numpy().astype(np.float64)
+    assert np.linalg.norm(got - want) / np.linalg.norm(want) <= 1e-5
 
 
 @pytest.mark.parametrize("thr", [(None, None), (0, -1), (-1, -1), (4, 40)])
