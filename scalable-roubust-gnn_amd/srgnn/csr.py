@@ -39,11 +39,10 @@ def auto_hub_threshold(nnz: int, launches: int = 1) -> int:
     launch).  A slice wave needs ~38 ns per nonzero (one dependent gather per 8-nonzero group
     of its row), so a row should be a hub once that latency nears the duration of the launch it
     belongs to: ~nnz * 520 B / 6.5 TB/s at d = 128, split over `launches` back-to-back launches
-    (the halo exchange's row groups).  Calibrated on the products-shaped graph: one launch ->
-    nnz / 1024 (floor 8192); C launches -> nnz / (1024 C) (floor 2048)."""
-    if launches <= 1:
-        return max(8192, int(nnz) // 1024)
-    return max(2048, int(nnz) // (1024 * int(launches)))
+    (the halo exchange's row groups): nnz / (1024 * launches), floor 2048.  Sweeps
+    (profiles/r01_sweep_hub_threshold_*.json): products 123,209 (only the top row) is best;
+    arxiv 2,048-4,096 run a hop in 0.208 ms vs 0.236 ms at the former floor of 8,192."""
+    return max(2048, int(nnz) // (1024 * max(1, int(launches))))
 
 
 def _dev(device):
