@@ -60,6 +60,9 @@ def parse():
                     help="khop: the K-hop propagate (GraphOp.propagate); wavelet: the heat-wavelet "
                          "Chebyshev filter bank (order 3, scales -0.5/+0.5) applied to the feature panel")
     ap.add_argument("--col-block", type=int, default=None, help="wavelet: column block width")
+    ap.add_argument("--aggregate", default=None, choices=["sum", "mean", "weighted"],
+                    help="one GPU: fused hop aggregation (SGC/SSGC/GBP precompute) instead of the K+1 "
+                         "panels: sum / mean over hops 0..K, or GBP weights alpha(1-alpha)^k, alpha 0.15")
     ap.add_argument("--mode", default="auto", choices=["auto", "panels", "last"],
                     help="panels: all K+1 hop panels kept (GraphOp.propagate); last: two ping-pong "
                          "panels, only A^K X kept (SGC-style, fused aggregation); auto: panels if "
@@ -276,7 +279,21 @@ def main():
             free, _ = torch.cuda.mem_get_info(dev)
             mode = "panels" if K * n * d * 4 < 0.9 * free else "last"
             log(f"mode {mode}: {K} panels need {K * n * d * 4 / 1e9:.1f} GB, {free / 1e9:.1f} GB free")
-        if mode == "panels":
+        if a.aggregate:
+            from srgnn.aggregate import combine_plan, combine_steps, propagate_aggregate
+
+            class _Msg:
+                aggr_type = {"weighted": "simple_weighted"}.get(a.aggregate, a.aggregate)
+                start, end, combination_type, alpha, weight_list = 0, K + 1, "alpha", 0.15, None
+            plan_mode, terms, div = combine_plan(_Msg(), K + 1)
+            steps_plan = combine_steps(plan_mode, terms, div)
+            mode = f"aggregate-{a.aggregate}"
+            panels = [X, None]
+
+            def step():
+                panels[1] = None
+                panels[1] = propagate_aggregate(A, X, K, steps_plan)
+        elif mode == "panels":
             buf = torch.empty((K, n, d), dtype=torch.float32, device=dev)
             panels = [X] + [buf[k] for k in range(K)]
 
@@ -387,7 +404,9 @@ def main():
                    "d": d, "K": K, "normalization": "sym r=0.5",
                    "parallelism": f"row-partition x{world}" + (f" ({a.exchange} exchange)" if world > 1 else ""),
                    "mode": "exact (bit-identical to reference)",
-                   "outputs": ("all K+1 hop panels" if mode in ("panels", "auto") else "last hop only (2 ping-pong panels)")
+                   "outputs": ("all K+1 hop panels" if mode in ("panels", "auto") else
+                               f"fused {a.aggregate} of hops 0..K (srgnn.aggregate, bit-exact vs the reference combine)"
+                               if a.aggregate else "last hop only (2 ping-pong panels)")
                    if world == 1 else "all K+1 hop panels (row slices)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
                      "frac": achieved / peak, "traffic": traffic,

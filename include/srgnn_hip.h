@@ -138,6 +138,15 @@ int srg_cheby_epilogue_f32(float* Tn, int64_t ldn, const float* Tc, int64_t ldc,
 int srg_hop_accumulate_f32(float* agg, int64_t lda, const float* y, int64_t ldy, int64_t n_rows,
                            int32_t d, float w, int mode, void* stream);
 
+/* srg_spmm_csr_f32 with the aggregation step fused into its epilogue: Y = A*X as above and, for
+ * every element y stored, agg = (agg_init ? 0 : agg) + w*y (separate multiply / add) -- the same
+ * result as srg_spmm_csr_f32 followed by srg_hop_accumulate_f32(INIT or ADD), one panel pass less.
+ * agg: device panel [n_rows, d], leading dimension lda, must not alias Y. */
+int srg_spmm_agg_f32(const int64_t* indptr, const int32_t* indices, const float* values,
+                     int64_t n_rows, const int32_t* row_order, int64_t n_hub, int64_t n_heavy,
+                     const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t d, uint32_t flags,
+                     float* agg, int64_t lda, float w, int agg_init, void* stream);
+
 /* The last flat elements (< SRG_TAIL_MAX of them) of a torch dim-0 sum take its scalar row_sum
  * order (4 interleaved partials).  srg_tail_record_f32 stores w * y[flat_start + e] (flat index of
  * the row-major [n_rows, d] panel) into hist[e], one call per term with hist advanced by

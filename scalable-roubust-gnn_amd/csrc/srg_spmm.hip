@@ -258,13 +258,25 @@ constexpr int64_t kMaxLaunchBlocks = int64_t(1) << 23;
 // ------------------------------------------------------------------------------------------------
 constexpr int kSliceCols = 32;
 
+// Fused hop aggregation epilogue (srgnn.aggregate): with agg != nullptr every output element y a
+// kernel stores is also folded into the accumulator panel, agg = (init ? 0 : agg) + w*y, with
+// separate multiply and add -- the same arithmetic as a following srg_hop_accumulate_f32 step,
+// without re-reading Y.
+struct AggEpi {
+    float* agg;
+    int64_t lda;
+    float w;
+    int init;
+};
+
+
 template <int UH, bool SFULL, typename IP>
 __device__ __forceinline__ void slice_wave(const IP* __restrict__ indptr,
                                            const int32_t* __restrict__ indices,
                                            const float* __restrict__ vals, int row, int slice,
                                            const float* __restrict__ X, int64_t ldx,
                                            float* __restrict__ Y, int64_t ldy, int d, int accumulate,
-                                           int nt, float* __restrict__ lds)
+                                           int nt, float* __restrict__ lds, const AggEpi& epi)
 {
     typedef typename Vec<float, 4>::type V4;
     const int lane = threadIdx.x & 63;
@@ -276,6 +288,7 @@ __device__ __forceinline__ void slice_wave(const IP* __restrict__ indptr,
     float* __restrict__ yrow = Y + (int64_t)row * ldy;
     float acc = 0.0f;
     if (accumulate && cact) acc = yrow[ccol];
+    const float aprev = (epi.agg && !epi.init && cact) ? epi.agg[(int64_t)row * epi.lda + ccol] : 0.0f;
     const int64_t beg = indptr[row];
     const int64_t end = indptr[row + 1];
     for (int64_t j = beg; j < end; j += 8 * UH) {
@@ -321,6 +334,7 @@ __device__ __forceinline__ void slice_wave(const IP* __restrict__ indptr,
             __builtin_nontemporal_store(acc, yrow + ccol);
         else
             yrow[ccol] = acc;
+        if (epi.agg) epi.agg[(int64_t)row * epi.lda + ccol] = __fadd_rn(aprev, __fmul_rn(epi.w, acc));
     }
 }
 
@@ -329,7 +343,7 @@ __global__ void __launch_bounds__(kBlock)
 k_spmm(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
        const float* __restrict__ vals, const int32_t* __restrict__ order, int n_rows, int n_heavy,
        int n_slices, int nb_heavy, const float* __restrict__ X, int64_t ldx, float* __restrict__ Y,
-       int64_t ldy, int d, int accumulate, int nt, int block_base)
+       int64_t ldy, int d, int accumulate, int nt, int block_base, AggEpi epi)
 {
     typedef typename Vec<float, VEC>::type V;
     const int bid = block_base + (int)blockIdx.x;
@@ -341,7 +355,7 @@ k_spmm(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
         if (item >= n_heavy * n_slices) return;
         const int row = order[item / n_slices];
         slice_wave<UH, SFULL, IP>(indptr, indices, vals, row, item % n_slices, X, ldx, Y, ldy, d,
-                           accumulate, nt, lds + wib * 2 * 256);
+                           accumulate, nt, lds + wib * 2 * 256, epi);
         return;
     }
     const int w = __builtin_amdgcn_readfirstlane((bid - nb_heavy) * kWavesPerBlock + wib) + n_heavy;
@@ -353,8 +367,19 @@ k_spmm(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
         const bool act = col < d;
         V acc = vzero<float, VEC>();
         if (accumulate && (FULL || act)) acc = vload<float, VEC>(yrow + col);
+        // the accumulator row is loaded before the chain, so its latency hides under the gathers
+        V aprev = vzero<float, VEC>();
+        float* arow = epi.agg ? epi.agg + (int64_t)row * epi.lda : nullptr;
+        if (arow && !epi.init && (FULL || act)) aprev = vload<float, VEC>(arow + col);
         row_gather<float, VEC, U, FULL, IP>(acc, indptr, indices, vals, row, X, ldx, col, act);
-        if (FULL || act) vstore<float, VEC>(yrow + col, acc, nt != 0);
+        if (FULL || act) {
+            vstore<float, VEC>(yrow + col, acc, nt != 0);
+            if (arow) {
+#pragma unroll
+                for (int i = 0; i < VEC; ++i) elem(aprev, i) = __fadd_rn(elem(aprev, i), __fmul_rn(epi.w, elem(acc, i)));
+                vstore<float, VEC>(arow + col, aprev, false);
+            }
+        }
     }
 }
 
@@ -398,7 +423,7 @@ __global__ void __launch_bounds__(kHubThreads)
 k_spmm_hub(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
            const float* __restrict__ vals, const int32_t* __restrict__ hub_rows, int n_slices,
            const float* __restrict__ X, int64_t ldx, float* __restrict__ Y, int64_t ldy, int d,
-           int accumulate, int nt)
+           int accumulate, int nt, AggEpi epi)
 {
     typedef typename Vec<float, 4>::type V4;
     extern __shared__ __attribute__((aligned(16))) float hub_lds[];
@@ -420,6 +445,7 @@ k_spmm_hub(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
         float* __restrict__ yrow = Y + (int64_t)row * ldy;
         float acc = 0.0f;
         if (accumulate && cact) acc = yrow[ccol];
+        const float aprev = (epi.agg && !epi.init && cact) ? epi.agg[(int64_t)row * epi.lda + ccol] : 0.0f;
         const int sw = hub_swz(c);
         constexpr int G = 2;                      // groups of 4 links per register set (8 links)
         V4 tA[G], aA[G], tB[G], aB[G], tC[G], aC[G], tD[G], aD[G];
@@ -500,6 +526,7 @@ k_spmm_hub(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
                 __builtin_nontemporal_store(acc, yrow + ccol);
             else
                 yrow[ccol] = acc;
+            if (epi.agg) epi.agg[(int64_t)row * epi.lda + ccol] = __fadd_rn(aprev, __fmul_rn(epi.w, acc));
         }
         return;
     }
@@ -850,7 +877,8 @@ int side_stream(SideStream** out)
 template <typename IP>
 int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int64_t n_rows,
                 const int32_t* order, int64_t n_hub, int64_t n_heavy, const float* X, int64_t ldx,
-                float* Y, int64_t ldy, int d, uint32_t flags, hipStream_t s)
+                float* Y, int64_t ldy, int d, uint32_t flags, hipStream_t s,
+                AggEpi epi = AggEpi{nullptr, 0, 0.0f, 0})
 {
     if (n_rows <= 0 || d <= 0) return SRG_OK;
     if (n_hub < 0 || n_heavy < 0 || n_hub + n_heavy > n_rows || ((n_hub + n_heavy) > 0 && !order))
@@ -891,15 +919,15 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
                 attr = true;
             }
             hipLaunchKernelGGL(k, hgrid, dim3(kHubThreads), kHubLdsBytes, ss->stream, indptr, indices, vals,
-                               order, n_slices, X, ldx, Y, ldy, d, acc, nt);
+                               order, n_slices, X, ldx, Y, ldy, d, acc, nt, epi);
         } else if (sfull)
             hipLaunchKernelGGL((k_spmm_hub<true, IP>), hgrid, dim3(kHubThreads), kHubLdsBytes,
                                ss->stream, indptr, indices, vals, order, n_slices, X, ldx, Y, ldy,
-                               d, acc, nt);
+                               d, acc, nt, epi);
         else
             hipLaunchKernelGGL((k_spmm_hub<false, IP>), hgrid, dim3(kHubThreads), kHubLdsBytes,
                                ss->stream, indptr, indices, vals, order, n_slices, X, ldx, Y, ldy,
-                               d, acc, nt);
+                               d, acc, nt, epi);
         SRG_HIP_CHECK(hipGetLastError());
         SRG_HIP_CHECK(hipEventRecord(ss->join, ss->stream));
         static const int delay_us = [] { const char* e = getenv("SRGNN_HUB_DISPATCH_DELAY_US"); return e ? atoi(e) : 20; }();
@@ -923,7 +951,7 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
 #define SRG_LAUNCH_SPMM(V, F, SF)                                                               \
     hipLaunchKernelGGL((k_spmm<V, kUnroll, kUnrollHeavy, F, SF, IP>), grid, dim3(kBlock), 0, s,     \
                        indptr, indices, vals, morder, nr, nh, n_slices, nb_heavy, X, ldx, Y, ldy, \
-                       d, acc, nt, bb)
+                       d, acc, nt, bb, epi)
         const bool full = d % (64 * vec) == 0;        // implies d % 32 == 0
         if (vec == 4) {
             if (full) SRG_LAUNCH_SPMM(4, true, true);
@@ -1126,6 +1154,21 @@ int srg_spmm_csr_f32(const int64_t* indptr, const int32_t* indices, const float*
     if (rc) return rc;
     rc = launch_spmm<int64_t>(indptr, indices, values, n_rows, row_order, n_hub, n_heavy, X, ldx, Y, ldy, d, flags,
                               static_cast<hipStream_t>(stream));
+    return rc ? rc : ok();
+}
+
+int srg_spmm_agg_f32(const int64_t* indptr, const int32_t* indices, const float* values,
+                     int64_t n_rows, const int32_t* row_order, int64_t n_hub, int64_t n_heavy,
+                     const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t d, uint32_t flags,
+                     float* agg, int64_t lda, float w, int agg_init, void* stream)
+{
+    int rc = check_spmm_args(indptr, indices, values, n_rows, X, ldx, Y, ldy, d);
+    if (rc) return rc;
+    if (n_rows > 0 && d > 0 && (!agg || lda < d))
+        return fail(SRG_ERR_INVALID, "aggregation panel: agg=%p lda=%lld < d=%d", (void*)agg, (long long)lda, d);
+    if (agg && agg == Y) return fail(SRG_ERR_INVALID, "agg must not alias Y");
+    rc = launch_spmm<int64_t>(indptr, indices, values, n_rows, row_order, n_hub, n_heavy, X, ldx, Y, ldy, d, flags,
+                              static_cast<hipStream_t>(stream), AggEpi{agg, lda, w, agg_init ? 1 : 0});
     return rc ? rc : ok();
 }
 

@@ -27,7 +27,7 @@ import torch
 
 from . import _lib
 from .csr import DeviceCSR
-from .spmm import spmm
+from .spmm import spmm, spmm_agg
 
 
 def _slice_indices(n: int, start, end):
@@ -182,6 +182,13 @@ class _DeviceSteps:
         else:
             raise ValueError(f"unknown step {s!r}")
 
+    def fused_target(self, s):
+        """(panel, init) that an ("acc", 0, k, w) step folds into when fused into hop k's SpMM."""
+        if 0 not in self.slots:
+            self.slots[0] = self._buf()
+            return self.slots[0], True
+        return self.slots[0], False
+
     def result(self):
         if 0 not in self.slots:
             self.slots[0] = self._buf()
@@ -223,10 +230,13 @@ def schedule(steps):
     return groups, trailing
 
 
-def propagate_aggregate(A: DeviceCSR, X: torch.Tensor, K: int, steps=None, last_only: bool = False):
+def propagate_aggregate(A: DeviceCSR, X: torch.Tensor, K: int, steps=None, last_only: bool = False,
+                        fuse: bool = True):
     """Runs hops 1..K of Â on the device panel X ([n, d], row-major) with two ping-pong panels and
     executes `steps` (combine_steps) as each hop appears; returns the aggregated panel, or Â^K X
-    when last_only.  Hops beyond the last one a step needs are not computed."""
+    when last_only.  Hops beyond the last one a step needs are not computed.  With `fuse`, a hop's
+    first accumulation step runs in the SpMM's epilogue (srg_spmm_agg_f32: same arithmetic, one
+    panel pass less)."""
     n, d = X.shape
     if A.n_rows != n or A.n_cols != n:
         raise ValueError("propagate_aggregate needs a square operator matching X")
@@ -249,9 +259,17 @@ def propagate_aggregate(A: DeviceCSR, X: torch.Tensor, K: int, steps=None, last_
         bufs = [torch.empty((n, d), dtype=torch.float32, device=X.device) for _ in range(min(2, last))]
         for k in range(1, last + 1):
             nxt = bufs[(k - 1) % len(bufs)]
-            spmm(A, cur, out=nxt)
-            cur = nxt
-            consume(k, cur)
+            g = groups[k] if ex is not None and k < len(groups) else []
+            if fuse and g and g[0][0] == "acc" and g[0][1] == 0:
+                agg, init = ex.fused_target(g[0])
+                spmm_agg(A, cur, nxt, agg, g[0][3], init)
+                cur = nxt
+                for s_ in g[1:]:
+                    ex.run(s_, cur if step_hop(s_) is not None else None)
+            else:
+                spmm(A, cur, out=nxt)
+                cur = nxt
+                consume(k, cur)
     if last_only:
         return cur.clone() if cur is X else cur
     for s in trailing:

@@ -54,6 +54,26 @@ def spmm(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor | None = None, accumul
     return out
 
 
+def spmm_agg(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, agg: torch.Tensor, w: float, init: bool,
+             nt_store: bool = False) -> torch.Tensor:
+    """out = A @ X and, fused into the same kernels' epilogue, agg = (0 if init else agg) + w * out
+    (srg_spmm_agg_f32; the arithmetic of spmm followed by one srg_hop_accumulate_f32 step)."""
+    _check_panel(X, A.n_cols, "X")
+    d = X.shape[1]
+    _check_panel(out, A.n_rows, "out", d)
+    _check_panel(agg, A.n_rows, "agg", d)
+    if not (out.device == X.device == agg.device == A.device):
+        raise ValueError("A, X, out and agg must be on the same device")
+    flags = _lib.SRG_SPMM_NT_STORE if nt_store else 0
+    rc = _lib.lib().srg_spmm_agg_f32(A.indptr.data_ptr(), A.indices.data_ptr(), A.values.data_ptr(),
+                                     A.n_rows, A.order.data_ptr() if A.n_rows else None, A.n_hub, A.n_heavy,
+                                     X.data_ptr(), X.stride(0), out.data_ptr(), out.stride(0), d, flags,
+                                     agg.data_ptr(), agg.stride(0), float(w), 1 if init else 0,
+                                     _stream(X.device))
+    _lib.check(rc, "srg_spmm_agg_f32")
+    return out
+
+
 def propagate(A: DeviceCSR, X: torch.Tensor, K: int, panels: list | None = None,
               nt_store: bool = False) -> list:
     """[X, ÂX, …, Â^K X] as device tensors (panels[0] is X itself, like the reference's list).

@@ -98,3 +98,32 @@ def test_products_scale_weighted_bit_exact():
     assert torch.equal(got, want)
     got = fused_combine(A, x, K, _Msg("mean", 0, K + 1)).cpu()
     assert torch.equal(got, O.combine("mean", hops, 0, K + 1))
+
+
+@pytest.mark.parametrize("thr", [(-1, -1), (0, -1), (0, 0), (None, None), (4, 64)])
+@pytest.mark.parametrize("d", [1, 7, 64, 128, 130])
+def test_spmm_agg_epilogue_equals_separate_steps(thr, d):
+    """srg_spmm_agg_f32 (aggregation fused into the row-wave, slice-wave and hub epilogues) ==
+    srg_spmm_csr_f32 followed by srg_hop_accumulate_f32, bit for bit, INIT and ADD."""
+    from srgnn import _lib, synth
+    from srgnn.aggregate import _DeviceSteps
+    from srgnn.csr import DeviceCSR
+    from srgnn.spmm import spmm, spmm_agg
+    n = 3000
+    u, v = synth.rmat_undirected_t(n, 30000, seed=3)
+    ip, ix = synth.symmetric_csr_t(n, u, v)
+    vals = torch.from_numpy(np.random.default_rng(d).random(ix.numel()).astype(np.float32))
+    A = DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, heavy_threshold=thr[0], hub_threshold=thr[1], device="cuda")
+    X = torch.from_numpy(np.random.default_rng(1).standard_normal((n, d)).astype(np.float32)).cuda()
+    prev = torch.from_numpy(np.random.default_rng(2).standard_normal((n, d)).astype(np.float32)).cuda()
+    ex = _DeviceSteps(n, d, X.device)
+    for init in (True, False):
+        y_ref = spmm(A, X)
+        agg_ref = prev.clone()
+        ex._acc(agg_ref, y_ref, 0.37, _lib.SRG_ACC_INIT if init else _lib.SRG_ACC_ADD)
+        y = torch.empty_like(y_ref)
+        agg = prev.clone()
+        spmm_agg(A, X, y, agg, 0.37, init)
+        assert torch.equal(y, y_ref) and torch.equal(agg, agg_ref)
+    with pytest.raises(Exception):
+        spmm_agg(A, X, y, y, 0.5, True)            # agg aliasing Y is refused
