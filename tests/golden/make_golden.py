@@ -212,6 +212,44 @@ def main():
         manifest[name] = store_case(name, adj, np.ascontiguousarray(X), [X, y], None,
                                     {"op": "raw_spmm", "f_order_input": forder})
 
+    # 7b. hop aggregation: the reference's own message operators on reference hop lists
+    from operators.message_operator.last_message_op import LastMessageOp
+    from operators.message_operator.mean_message_op import MeanMessageOp
+    from operators.message_operator.simple_weighted_message_op import SimpleWeightedMessageOp
+    from operators.message_operator.sum_message_op import SumMessageOp
+
+    def agg_ops(K):
+        return {"last": LastMessageOp(), "sum_all": SumMessageOp(0, K + 1), "mean_1_end": MeanMessageOp(1, K + 1),
+                "gbp_alpha015": SimpleWeightedMessageOp(0, K + 1, "alpha", 0.15),
+                "gbp_alpha03_2_k": SimpleWeightedMessageOp(2, K, "alpha", 0.3),
+                "hand_1_3": SimpleWeightedMessageOp(1, 3, "hand_crafted", [0.7, -0.3])}
+
+    def store_agg(name, adj, X, K, r, meta):
+        op = SymLap(K, r=r)
+        feats = op.propagate(adj, X)
+        arrs = {"adj_indptr": adj.indptr.astype(np.int64), "adj_indices": adj.indices.astype(np.int32),
+                "adj_data": adj.data.astype(np.float64), "x_sha256": np.array(sha(X))}
+        if X.size <= FULL_LIMIT:
+            arrs["x"] = X
+        rows = sample_rows(adj.shape[0])
+        arrs["sample_rows"] = rows
+        ops = agg_ops(K)
+        for key, mop in ops.items():
+            out = np.ascontiguousarray(mop.aggregate(feats).numpy(), dtype=np.float32)
+            arrs[f"{key}_sha256"] = np.array(sha(out))
+            arrs[f"{key}_rows"] = out[rows]
+        np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **arrs)
+        rec = {"n": adj.shape[0], "d": X.shape[1], "k": K, "op": "aggregate", "r": r, "msg_ops": sorted(ops),
+               "torch": torch.__version__}
+        rec.update(meta)
+        return rec
+
+    adj, _ = planetoid_adj("cora_0_0", True)
+    manifest["agg_cora_k3"] = store_agg("agg_cora_k3", adj, Xc, 3, 0.5, {"features": "binary_rownorm(18, seed=7)"})
+    adj = random_adj(200, 0.05, seed=400)
+    X = synth.uniform_features_np(200, 37, seed=60)
+    manifest["agg_rand_k20"] = store_agg("agg_rand_k20", adj, X, 20, 0.5, {"features": "uniform(seed=60)"})
+
     # 7. error behaviour of GraphOp.propagate (base_operator.py:20-30, utils.py:23-45)
     errs = {}
     adj = random_adj(30, 0.1, seed=7)

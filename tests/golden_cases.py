@@ -18,9 +18,11 @@ def names(kind=None):
     m = manifest()
     out = [k for k in sorted(m) if not k.startswith("_")]
     if kind == "norm":
-        out = [k for k in out if m[k]["op"] != "raw_spmm"]
+        out = [k for k in out if m[k]["op"] in ("sym_laplacian", "ppr")]
     elif kind == "raw":
         out = [k for k in out if m[k]["op"] == "raw_spmm"]
+    elif kind == "aggregate":
+        out = [k for k in out if m[k]["op"] == "aggregate"]
     return out
 
 
@@ -70,6 +72,12 @@ class Case:
     def ahat(self):
         return self["ahat_indptr"], self["ahat_indices"], self["ahat_data"]
 
+    def check_output(self, key, h):
+        """Bit-exact check of a named output (aggregation cases) against the reference."""
+        h = np.ascontiguousarray(h, dtype=np.float32)
+        np.testing.assert_array_equal(h[self["sample_rows"]], self[f"{key}_rows"], err_msg=f"{self.name} {key} rows")
+        assert sha(h) == str(self[f"{key}_sha256"]), f"{self.name} {key}: bytes differ from the reference"
+
     def check_hop(self, k, h):
         """Bit-exact check of hop k against the reference (hash, sampled rows, full if stored)."""
         h = np.ascontiguousarray(h, dtype=np.float32)
@@ -78,3 +86,23 @@ class Case:
         if self.has(f"hop{k}"):
             np.testing.assert_array_equal(h, self[f"hop{k}"], err_msg=f"{self.name} hop {k}")
         assert sha(h) == str(self[f"hop{k}_sha256"]), f"{self.name} hop {k}: bytes differ from the reference"
+
+
+def agg_specs(K):
+    """The message operators of the aggregation fixtures (make_golden.py agg_ops), as
+    (aggr_type, start, end, combination_type, alpha, weight_list)."""
+    return {"last": ("last", None, None, None, None, None),
+            "sum_all": ("sum", 0, K + 1, None, None, None),
+            "mean_1_end": ("mean", 1, K + 1, None, None, None),
+            "gbp_alpha015": ("simple_weighted", 0, K + 1, "alpha", 0.15, None),
+            "gbp_alpha03_2_k": ("simple_weighted", 2, K, "alpha", 0.3, None),
+            "hand_1_3": ("simple_weighted", 1, 3, "hand_crafted", None, [0.7, -0.3])}
+
+
+class Msg:
+    """Duck-typed message operator (the attributes srgnn.aggregate.combine_plan reads)."""
+
+    def __init__(self, aggr, start, end, combination_type, alpha, weight_list):
+        self.aggr_type, self.start, self.end = aggr, start, end
+        self.combination_type, self.alpha = combination_type, alpha
+        self.weight_list = None if weight_list is None else __import__("torch").FloatTensor(weight_list)

@@ -127,3 +127,19 @@ def test_spmm_agg_epilogue_equals_separate_steps(thr, d):
         assert torch.equal(y, y_ref) and torch.equal(agg, agg_ref)
     with pytest.raises(Exception):
         spmm_agg(A, X, y, y, 0.5, True)            # agg aliasing Y is refused
+
+
+@pytest.mark.parametrize("name", G.names("aggregate"))
+def test_fused_combine_equals_reference_message_ops(name):
+    """Device construct_adj + fused hops/aggregation == the reference's own message operators
+    (fixtures from make_golden.py), for every message operator of the fixture."""
+    from srgnn import construct as C
+    from srgnn.aggregate import fused_combine
+    from srgnn.csr import DeviceCSR
+    c = G.Case(name)
+    a = c.adj()
+    ip, ix, v64 = C.sym_norm(a.indptr, a.indices, a.data, c.n, c.meta["r"], device="cuda")
+    A = DeviceCSR.from_tensors(ip, ix, v64.to(torch.float32), n_cols=c.n, device="cuda")
+    X = torch.from_numpy(c.x()).cuda()
+    for key, spec in G.agg_specs(c.k).items():
+        c.check_output(key, fused_combine(A, X, c.k, G.Msg(*spec)).cpu().numpy())

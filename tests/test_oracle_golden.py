@@ -55,3 +55,35 @@ def test_error_manifest_present():
     assert errs["coo_adj"] == "TypeError"
     assert errs["float64_feature"] == "ArgumentError"
     assert errs["dim_mismatch"] == "ValueError"
+
+
+@pytest.mark.parametrize("name", G.names("aggregate"))
+def test_oracle_combine_equals_reference_message_ops(oracle_mod, name):
+    """oracle.combine on the oracle's hops == the reference's own message operators (fixtures)."""
+    import torch
+    c = G.Case(name)
+    a = c.adj()
+    ip, ix, v64 = oracle_mod.sym_norm(a.indptr, a.indices, a.data, c.n, c.meta["r"])
+    hops = oracle_mod.propagate(ip, ix, v64.astype(np.float32), c.x(), c.k)
+    feats = [torch.from_numpy(h) for h in hops]
+    for key, (aggr, s, e, ct, alpha, wl) in G.agg_specs(c.k).items():
+        out = oracle_mod.combine(aggr, feats, s, e, alpha=alpha, weight_list=wl)
+        c.check_output(key, out.numpy())
+
+
+@pytest.mark.parametrize("name", G.names("aggregate"))
+def test_aggregation_plan_equals_reference_message_ops(oracle_mod, name):
+    """srgnn.aggregate's planned step order, executed in numpy fp32, == the reference's combine."""
+    from srgnn import aggregate as AG
+    from test_aggregate_cpu import run_steps_np
+    c = G.Case(name)
+    a = c.adj()
+    ip, ix, v64 = oracle_mod.sym_norm(a.indptr, a.indices, a.data, c.n, c.meta["r"])
+    hops = oracle_mod.propagate(ip, ix, v64.astype(np.float32), c.x(), c.k)
+    for key, spec in G.agg_specs(c.k).items():
+        mode, terms, div = AG.combine_plan(G.Msg(*spec), c.k + 1)
+        if mode == "last":
+            out = hops[-1]
+        else:
+            out = run_steps_np(AG.combine_steps(mode, terms, div), hops, c.n, hops[0].shape[1])
+        c.check_output(key, out)
