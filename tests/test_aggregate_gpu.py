@@ -143,3 +143,37 @@ def test_fused_combine_equals_reference_message_ops(name):
     X = torch.from_numpy(c.x()).cuda()
     for key, spec in G.agg_specs(c.k).items():
         c.check_output(key, fused_combine(A, X, c.k, G.Msg(*spec)).cpu().numpy())
+
+
+def test_degenerate_inputs():
+    """K = 0, empty graphs, rows without entries, zero-width panels: same results as the reference
+    combine on the (trivial) hop lists, no launches on empty shapes."""
+    import scipy.sparse as sp
+    from srgnn import construct as C
+    from srgnn.aggregate import fused_combine
+    from srgnn.csr import DeviceCSR
+    import oracle.oracle as O
+    # K = 0: the hop list is [X]
+    n, d = 50, 9
+    adj = sp.random(n, n, density=0.1, format="csr", random_state=0)
+    ip, ix, v = C.sym_norm(adj.indptr, adj.indices, adj.data, n, 0.5, device="cuda")
+    A = DeviceCSR.from_tensors(ip, ix, v.to(torch.float32), n_cols=n, device="cuda")
+    X = torch.from_numpy(np.random.default_rng(0).standard_normal((n, d)).astype(np.float32))
+    for spec in G.agg_specs(0).values():
+        m = G.Msg(*spec)
+        if m.aggr_type == "simple_weighted" and m.combination_type == "hand_crafted":
+            continue                                  # needs 2 hops in its slice
+        if m.aggr_type in ("sum", "mean") and not range(1)[slice(m.start, m.end)]:
+            continue
+        want = O.combine(m.aggr_type, [X], m.start, m.end, alpha=m.alpha, weight_list=m.weight_list)
+        assert torch.equal(fused_combine(A, X.cuda(), 0, m).cpu(), want)
+    # empty graph (n = 0) and an edgeless graph
+    ip, ix, v = C.sym_norm(np.zeros(1, np.int64), np.zeros(0, np.int32), np.zeros(0), 0, 0.5, device="cuda")
+    assert ip.tolist() == [0] and ix.numel() == 0
+    A0 = DeviceCSR.from_tensors(ip, ix, v.to(torch.float32), n_cols=0, device="cuda")
+    out = fused_combine(A0, torch.zeros((0, 4), device="cuda"), 3, G.Msg("sum", 0, 4, None, None, None))
+    assert out.shape == (0, 4)
+    e = C.edge_index_to_adj(torch.zeros((2, 0), dtype=torch.int64), 5, device="cuda")
+    assert e[0].tolist() == [0] * 6 and e[1].numel() == 0
+    ip, ix, v = C.sym_norm(*(t.cpu().numpy() for t in e), 5, 0.5, device="cuda")
+    assert ip.tolist() == list(range(6)) and torch.equal(v.cpu(), torch.ones(5, dtype=torch.float64))
