@@ -167,11 +167,14 @@ def pmc_traffic(config, kernel_hint="k_spmm"):
         return None
 
 
-def run_wavelet(a, dev):
+def run_wavelet(a, dev, world=1, rank=0):
     """SpectralModel's wavelet operator (SSRG/models/base_scalable/base_model.py:180-265) on the
-    config's graph: R_s = sum_k c_{s,k} T_k(L~) X for tau = -0.5, +0.5, Chebyshev order 3, fp32,
-    one process (world size 1).  value = order * nnz(L) * steps / time: every order is one SpMM
-    pass over the whole panel (in column blocks when the panels do not fit)."""
+    config's graph: R_s = sum_k c_{s,k} T_k(L~) X for tau = -0.5, +0.5, Chebyshev order 3, fp32.
+    value = order * nnz(L) * steps / time: every order is one SpMM pass over the whole panel (in
+    column blocks when the panels do not fit one GPU).  N > 1: srgnn.dist.HaloWaveletFilter (row
+    partition, one halo exchange per order, bitwise equal to one GPU)."""
+    if world > 1:
+        return run_wavelet_dist(a, dev, world, rank)
     from srgnn import wavelet as W
     from srgnn.csr import DeviceCSR
     from srgnn.spmm import spmm
@@ -243,6 +246,48 @@ def run_wavelet(a, dev):
     print(json.dumps(res), flush=True)
 
 
+def run_wavelet_dist(a, dev, world, rank):
+    from srgnn.dist import HaloWaveletFilter
+    t_build = time.perf_counter()
+    ip, ix, lv, n, d, lmax = graphs.build_laplacian(a.config, dev, d=a.d)
+    nnz = int(ix.numel())
+    order = 3
+    f = HaloWaveletFilter(ip, ix, lv, n, [-0.5, 0.5], order=order, lmax=lmax, chunks=a.chunks,
+                          heavy_threshold=a.heavy_threshold, device=dev)
+    X = synth.uniform_features_t(n, d, seed=synth.FEATURE_SEED, device=dev)
+    S_local = X[f.r0:f.r1].contiguous()
+    del X, ip, ix, lv
+    torch.cuda.empty_cache()
+    log(f"rank {rank}: wavelet rows={f.rows} halo={f.opL.halo} built in {time.perf_counter() - t_build:.1f}s")
+    for _ in range(a.warmup):
+        f.apply(S_local)
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        f.apply(S_local)
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    res = {"metric": "propagated edges/sec (wavelet-basis Chebyshev propagation)",
+           "value": a.steps * order * nnz / dt, "unit": "propagated edges/s", "n_gpus": world,
+           "steps": a.steps, "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True,
+           "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+           "data": f"synthetic (R-MAT power-law graph with the {a.config} node/edge counts, U[-1,1) features)",
+           "config": {"workload": f"{a.config}-shaped heat-wavelet filter bank", "n_nodes": n, "nnz_L": nnz, "d": d,
+                      "chebyshev_order": order, "scales": [-0.5, 0.5], "lmax": lmax,
+                      "parallelism": f"row-partition x{world} (halo exchange per order)"},
+           "roofline": None, "cpu_baseline": None}
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -254,8 +299,8 @@ def main():
     dev = torch.device("cuda", local)
     if a.op == "wavelet":
         if world > 1:
-            raise SystemExit("--op wavelet runs on one GPU (world size 1)")
-        return run_wavelet(a, dev)
+            dist.init_process_group("nccl", device_id=dev)
+        return run_wavelet(a, dev, world, rank)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 

@@ -13,6 +13,7 @@ multi-GPU result is bitwise equal to the single-GPU one.
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -203,6 +204,7 @@ class HaloPartitionedOperator:
         r0, r1 = self.starts[p], self.starts[p + 1]
         self.r0, self.r1, self.rows = r0, r1, r1 - r0
         b0, b1 = int(gip[r0]), int(gip[r1])
+        self._b0, self._b1 = b0, b1
         my_cols = gix[b0:b1].to(torch.int64)
         self.nnz_local = b1 - b0
 
@@ -290,6 +292,22 @@ class HaloPartitionedOperator:
         """[own rows | halo] panel for this rank."""
         return torch.zeros((self.rows + self.halo, d), dtype=torch.float32, device=self.device)
 
+    def with_values(self, values: torch.Tensor) -> "HaloPartitionedOperator":
+        """The same partition, halo plan and schedules for an operator with the same structure and
+        other values (e.g. the Chebyshev F = (2/a1)(L - a2 I) next to L); `values` is global."""
+        import copy
+        other = copy.copy(self)
+        lvv = values[self._b0:self._b1].to(self.device).contiguous()
+        other._lvv = lvv
+        if isinstance(self._A[0], tuple):
+            other._A = [(a[0], a[1], lvv, a[3]) for a in self._A]
+        else:
+            from .csr import DeviceCSR
+            other._A = [DeviceCSR(a.indptr, a.indices, lvv, a.n_rows, a.n_cols, a.order, a.n_heavy, a.n_hub)
+                        for a in self._A]
+        other._streams = None
+        return other
+
     def _exchange_group(self, panel: torch.Tensor, g: int):
         P, p = self.world, self.rank
         off = self.rows + self.group_offsets[g]
@@ -356,6 +374,19 @@ class HaloPartitionedOperator:
         return panels
 
 
+def _virtual_exchange(shares, panels):
+    """all_to_all of P virtual shares emulated by copies: panels[q] is share q's [rows + halo, d]."""
+    for g in range(shares[0].n_groups):
+        for q, sq in enumerate(shares):             # receiver
+            off = sq.rows + sq.group_offsets[g]
+            for s, ss in enumerate(shares):         # source, in receive order
+                cnt = sq.recv_counts[g][s]
+                if cnt:
+                    idx = ss.send_idx[g][q]
+                    panels[q][off:off + cnt].copy_(panels[s][: ss.rows].index_select(0, idx))
+                off += cnt
+
+
 def simulate_halo_propagate(indptr, indices, values, n: int, x: torch.Tensor, K: int, world: int,
                             chunks: int = 3, heavy_threshold=None, hub_threshold=None, device=None):
     """P virtual halo-exchange ranks in ONE process (all_to_all emulated by copies); returns the
@@ -365,23 +396,121 @@ def simulate_halo_propagate(indptr, indices, values, n: int, x: torch.Tensor, K:
               for q in range(world)]
     d = x.shape[1]
     panels = [[s.new_panel(d) for _ in range(K + 1)] for s in shares]
-
-    def exchange(k):
-        for g in range(shares[0].n_groups):
-            for q, sq in enumerate(shares):             # receiver
-                off = sq.rows + sq.group_offsets[g]
-                for s, ss in enumerate(shares):         # source, in receive order
-                    cnt = sq.recv_counts[g][s]
-                    if cnt:
-                        idx = ss.send_idx[g][q]
-                        panels[q][k][off:off + cnt].copy_(panels[s][k][: ss.rows].index_select(0, idx))
-                    off += cnt
-
     for s, pp in zip(shares, panels):
         pp[0][: s.rows].copy_(x[s.r0:s.r1])
-    exchange(0)
+    _virtual_exchange(shares, [pp[0] for pp in panels])
     for k in range(1, K + 1):
         for s, pp in zip(shares, panels):
             s.compute(pp[k - 1], pp[k])
-        exchange(k)
+        _virtual_exchange(shares, [pp[k] for pp in panels])
     return [torch.cat([pp[k][: s.rows] for s, pp in zip(shares, panels)]) for k in range(K + 1)]
+
+
+# ----------------------------------------------------------------------------------------------
+# the wavelet basis' Chebyshev filter bank over the halo partition
+# ----------------------------------------------------------------------------------------------
+def _epilogue_device(Tn, Tc, To, mode, a1, a2, coef_prev, coef, R):
+    import ctypes
+    from . import _lib
+    ns = R.shape[0]
+    n, w = Tn.shape
+    ct = ctypes.c_float
+    cp = (ct * ns)(*coef_prev) if coef_prev is not None else None
+    rc = _lib.lib().srg_cheby_epilogue_f32(Tn.data_ptr(), Tn.stride(0), Tc.data_ptr() if Tc is not None else None,
+                                           Tc.stride(0) if Tc is not None else w,
+                                           To.data_ptr() if To is not None else None,
+                                           To.stride(0) if To is not None else w, n, w, mode, a1, a2, cp,
+                                           (ct * ns)(*coef), ns, R.data_ptr(), R.stride(1), R.stride(0),
+                                           torch.cuda.current_stream(Tn.device).cuda_stream)
+    _lib.check(rc, "srg_cheby_epilogue_f32")
+
+
+class HaloWaveletFilter:
+    """HeatWaveletFilter's fp32 split path (wavelet.py) over the halo-exchange partition: every
+    Chebyshev order is the local SpMM of this rank's rows (L for order 1, F = (2/a1)(L - a2 I)
+    after), the element-wise epilogue on the own rows, and one halo exchange of the new T_k --
+    the same arithmetic per element as one GPU, so the result is bitwise equal to it.
+    SpectralModel's operator at the RMAT-26 configuration (BASELINE.json) on P GPUs."""
+
+    def __init__(self, indptr, indices, lvals, n: int, taus, order: int = 3, lmax: float = None,
+                 group=None, chunks: int = 4, heavy_threshold=None, hub_threshold=None, device=None,
+                 rank=None, world=None, local_spmm=None, epilogue=None):
+        from .wavelet import heat_cheby_coeffs
+        if lmax is None:
+            raise ValueError("lmax is required")
+        dev = torch.device(device) if device is not None else indices.device
+        ip = indptr.to(dev, torch.int64)
+        lv64 = lvals.to(dev, torch.float64)
+        rows = torch.repeat_interleave(torch.arange(n, device=dev), ip[1:] - ip[:-1])
+        diag = indices.to(dev).to(torch.int64) == rows
+        del rows
+        self.lmax = float(lmax)
+        self.a1 = self.a2 = self.lmax / 2.0
+        fvals = ((2.0 / self.a1) * torch.where(diag, lv64 - self.a2, lv64)).to(torch.float32)
+        del diag
+        self.opL = HaloPartitionedOperator(ip, indices, lvals.to(dev, torch.float32), n, group=group, chunks=chunks,
+                                           heavy_threshold=heavy_threshold, hub_threshold=hub_threshold,
+                                           device=dev, rank=rank, world=world, local_spmm=local_spmm)
+        self.opF = self.opL.with_values(fvals)
+        self.taus = [float(t) for t in taus]
+        self.coeffs = np.stack([heat_cheby_coeffs(t, self.lmax, order) for t in self.taus])
+        self.rows, self.r0, self.r1 = self.opL.rows, self.opL.r0, self.opL.r1
+        self._epi = epilogue or _epilogue_device
+
+    def new_panel(self, d):
+        return self.opL.new_panel(d)
+
+    def steps(self, S_panel, work, R):
+        """Generator over the orders: yields after each order's local compute + epilogue with the
+        panel whose halo must be exchanged next (the caller exchanges it).  S_panel's halo must
+        already be filled; work = three [rows + halo, d] panels; R = [ns, rows, d]."""
+        ns, nc = self.coeffs.shape
+        r = self.rows
+        t_old, t_cur = S_panel, work[0]
+        free = list(work[1:])
+        self.opL.compute(S_panel, t_cur)
+        self._epi(t_cur[:r], S_panel[:r], None, 0, self.a1, self.a2, self.coeffs[:, 0], self.coeffs[:, 1], R)
+        yield t_cur
+        for k in range(2, nc):
+            t_new = free.pop()
+            self.opF.compute(t_cur, t_new)
+            self._epi(t_new[:r], None, t_old[:r], 1, self.a1, self.a2, None, self.coeffs[:, k], R)
+            if t_old is not S_panel:
+                free.append(t_old)
+            t_old, t_cur = t_cur, t_new
+            if k + 1 < nc:
+                yield t_cur
+
+    def apply(self, S_local: torch.Tensor) -> torch.Tensor:
+        """[n_scales, rows, d] filter outputs for this rank's rows of the panel S (real ranks)."""
+        d = S_local.shape[1]
+        S_panel = self.new_panel(d)
+        S_panel[: self.rows].copy_(S_local[: self.rows])
+        self.opL.exchange(S_panel)
+        R = torch.empty((self.coeffs.shape[0], self.rows, d), dtype=torch.float32, device=S_panel.device)
+        work = [self.new_panel(d) for _ in range(3)]
+        for panel in self.steps(S_panel, work, R):
+            self.opL.exchange(panel)
+        return R
+
+
+def simulate_halo_wavelet(indptr, indices, lvals, n: int, S: torch.Tensor, taus, order: int, lmax: float,
+                          world: int, chunks: int = 3, heavy_threshold=None, hub_threshold=None, device=None):
+    """P virtual HaloWaveletFilter ranks in one process; returns the full [n_scales, n, d] output."""
+    shares = [HaloWaveletFilter(indptr, indices, lvals, n, taus, order, lmax, chunks=chunks,
+                                heavy_threshold=heavy_threshold, hub_threshold=hub_threshold, device=device,
+                                rank=q, world=world) for q in range(world)]
+    d = S.shape[1]
+    ops = [f.opL for f in shares]
+    S_p = [f.new_panel(d) for f in shares]
+    for f, sp_ in zip(shares, S_p):
+        sp_[: f.rows].copy_(S[f.r0:f.r1])
+    _virtual_exchange(ops, S_p)
+    Rs = [torch.empty((len(taus), f.rows, d), dtype=torch.float32, device=S_p[0].device) for f in shares]
+    gens = [f.steps(sp_, [f.new_panel(d) for _ in range(3)], R) for f, sp_, R in zip(shares, S_p, Rs)]
+    while True:
+        outs = [next(g, None) for g in gens]
+        if outs[0] is None:
+            break
+        _virtual_exchange(ops, outs)
+    return torch.cat(Rs, dim=1)

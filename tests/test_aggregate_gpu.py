@@ -163,8 +163,8 @@ def test_degenerate_inputs():
         m = G.Msg(*spec)
         if m.aggr_type == "simple_weighted" and m.combination_type == "hand_crafted":
             continue                                  # needs 2 hops in its slice
-        if m.aggr_type in ("sum", "mean") and not range(1)[slice(m.start, m.end)]:
-            continue
+        if m.aggr_type != "last" and not range(1)[slice(m.start, m.end)]:
+            continue                                  # the reference fails on an empty slice too
         want = O.combine(m.aggr_type, [X], m.start, m.end, alpha=m.alpha, weight_list=m.weight_list)
         assert torch.equal(fused_combine(A, X.cuda(), 0, m).cpu(), want)
     # empty graph (n = 0) and an edgeless graph

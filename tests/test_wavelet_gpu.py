@@ -133,3 +133,20 @@ def test_device_built_filter_equals_host_built():
     assert torch.equal(host.fvals, dev.fvals) and torch.equal(host.lvals, dev.lvals)
     S = torch.from_numpy(np.random.default_rng(2).standard_normal((n, 64)).astype(np.float32)).cuda()
     assert torch.equal(host.apply(S), dev.apply(S, col_block=16))
+
+
+@pytest.mark.parametrize("world,chunks", [(2, 3), (8, 4)])
+def test_halo_wavelet_virtual_ranks_bitwise(world, chunks):
+    """The wavelet filter bank over the halo partition (P virtual ranks on one GPU, one exchange per
+    Chebyshev order) == HeatWaveletFilter's split path on one GPU, bit for bit."""
+    from srgnn import normalize, synth, wavelet as W
+    from srgnn.dist import simulate_halo_wavelet
+    n = 4000
+    u, v = synth.rmat_undirected_t(n, 40000, seed=17, device="cuda")
+    ip, ix, lv = normalize.sym_norm_edges_blocked(u.to(torch.int32), v.to(torch.int32), n, kind="laplacian")
+    S = synth.uniform_features_t(n, 64, seed=5, device="cuda")
+    lmax = 2.0 * float((ip[1:] - ip[:-1]).max())
+    one = W.HeatWaveletFilter.from_device(ip, ix, lv, n, [-0.5, 0.5], order=3, lmax=lmax, dtype=torch.float32)
+    want = one.apply(S, split=True)
+    got = simulate_halo_wavelet(ip, ix, lv, n, S, [-0.5, 0.5], 3, lmax, world, chunks=chunks, device="cuda")
+    assert torch.equal(got, want)
