@@ -43,6 +43,9 @@ extern "C" {
  * (SSRG/operators/csrc/matmul.c:23-40) given a zeroed answer (SSRG/operators/utils.py:38). */
 #define SRG_SPMM_ACCUMULATE 0x1u   /* chains start from Y's current content (matmul.c contract) */
 #define SRG_SPMM_NT_STORE 0x2u     /* non-temporal stores of Y */
+/* Diagnostic: keep one row per wave also for d <= 32 (the default runs 64 / S rows per wave,
+ * S = the power of two >= d lanes per row).  Results are identical either way. */
+#define SRG_SPMM_WIDE_ROWS 0x4
 
 /* =============================================================================================
  * (A) drop-in entry points

@@ -338,7 +338,66 @@ __device__ __forceinline__ void slice_wave(const IP* __restrict__ indptr,
     }
 }
 
-template <int VEC, int U, int UH, bool FULL, bool SFULL, typename IP>
+// Narrow panels (d <= 32): a row wave would leave 64 - d lanes idle, so here one wave runs
+// R = 64 / S rows at once, S = the power of two >= d lanes per row (lane = sub-row g, column c).
+// Each lane loads its own row's (column id, value) stream -- the S lanes of a row read the same
+// address, one instruction for the whole wave -- then U gathers in flight, then U fma links.
+// Rows come from the degree-sorted schedule, so the R rows of a wave have similar lengths.
+// Still one sequential fma chain per output element, in CSR order.
+template <int S, int U, typename IP>
+__device__ __forceinline__ void narrow_rows(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
+                                            const float* __restrict__ vals, const int32_t* __restrict__ order,
+                                            int n_rows, int first, const float* __restrict__ X, int64_t ldx,
+                                            float* __restrict__ Y, int64_t ldy, int d, int accumulate, int nt,
+                                            const AggEpi& epi)
+{
+    const int lane = threadIdx.x & 63;
+    const int g = lane / S, c = lane % S;
+    const int slot = first + g;
+    const bool rv = slot < n_rows;
+    const int row = rv ? (order ? order[slot] : slot) : 0;
+    const bool act = rv && c < d;
+    const int64_t beg = rv ? (int64_t)indptr[row] : 0;
+    const int len = rv ? (int)((int64_t)indptr[row + 1] - beg) : 0;
+    int maxlen = len;
+#pragma unroll
+    for (int off = S; off < 64; off <<= 1) {
+        const int o = __shfl_xor(maxlen, off);
+        maxlen = o > maxlen ? o : maxlen;
+    }
+    maxlen = __builtin_amdgcn_readfirstlane(maxlen);
+    float* __restrict__ yrow = Y + (int64_t)row * ldy;
+    float acc = (accumulate && act) ? yrow[c] : 0.0f;
+    const float aprev = (epi.agg && !epi.init && act) ? epi.agg[(int64_t)row * epi.lda + c] : 0.0f;
+    for (int j = 0; j < maxlen; j += U) {
+        int cv[U];
+        float av[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool ok = j + u < len;
+            const int64_t p = beg + (ok ? j + u : 0);
+            cv[u] = ok ? indices[p] : 0;
+            av[u] = ok ? vals[p] : 0.0f;
+        }
+        __builtin_amdgcn_sched_barrier(0);   // every id load ahead of the first gather
+        float x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            x[u] = (act && j + u < len) ? X[(int64_t)cv[u] * ldx + c] : 0.0f;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (act && j + u < len) acc = __builtin_fmaf(av[u], x[u], acc);
+    }
+    if (act) {
+        if (nt)
+            __builtin_nontemporal_store(acc, yrow + c);
+        else
+            yrow[c] = acc;
+        if (epi.agg) epi.agg[(int64_t)row * epi.lda + c] = __fadd_rn(aprev, __fmul_rn(epi.w, acc));
+    }
+}
+
+template <int VEC, int U, int UH, bool FULL, bool SFULL, typename IP, int NS = 0>
 __global__ void __launch_bounds__(kBlock)
 k_spmm(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
        const float* __restrict__ vals, const int32_t* __restrict__ order, int n_rows, int n_heavy,
@@ -356,6 +415,12 @@ k_spmm(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
         const int row = order[item / n_slices];
         slice_wave<UH, SFULL, IP>(indptr, indices, vals, row, item % n_slices, X, ldx, Y, ldy, d,
                            accumulate, nt, lds + wib * 2 * 256, epi);
+        return;
+    }
+    if constexpr (NS > 0) {   // narrow panel: 64 / NS light rows per wave
+        const int first = __builtin_amdgcn_readfirstlane((bid - nb_heavy) * kWavesPerBlock + wib) * (64 / NS) + n_heavy;
+        if (first >= n_rows) return;
+        narrow_rows<NS, U, IP>(indptr, indices, vals, order, n_rows, first, X, ldx, Y, ldy, d, accumulate, nt, epi);
         return;
     }
     const int w = __builtin_amdgcn_readfirstlane((bid - nb_heavy) * kWavesPerBlock + wib) + n_heavy;
@@ -941,7 +1006,10 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
     const int64_t m_rows = n_rows - n_hub;
     const int nb_heavy = (int)((n_heavy * n_slices + kWavesPerBlock - 1) / kWavesPerBlock);
     const int64_t n_light = m_rows - n_heavy;
-    const int64_t blocks = nb_heavy + (n_light + kWavesPerBlock - 1) / kWavesPerBlock;
+    // narrow panels: S lanes per row (power of two >= d), 64 / S rows per wave
+    const int ns = (d <= 32 && !(flags & SRG_SPMM_WIDE_ROWS)) ? (d <= 1 ? 1 : d <= 2 ? 2 : d <= 4 ? 4 : d <= 8 ? 8 : d <= 16 ? 16 : 32) : 0;
+    const int64_t rows_per_block = (int64_t)kWavesPerBlock * (ns ? 64 / ns : 1);
+    const int64_t blocks = nb_heavy + (n_light + rows_per_block - 1) / rows_per_block;
     if (blocks > INT32_MAX) return fail(SRG_ERR_INVALID, "grid too large");
     const int vec = pick_vec(d, ldx, ldy, X, Y, sizeof(float));
     const int nr = (int)m_rows, nh = (int)n_heavy;
@@ -953,7 +1021,24 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
                        indptr, indices, vals, morder, nr, nh, n_slices, nb_heavy, X, ldx, Y, ldy, \
                        d, acc, nt, bb, epi)
         const bool full = d % (64 * vec) == 0;        // implies d % 32 == 0
-        if (vec == 4) {
+#define SRG_LAUNCH_NARROW(NSV, SF)                                                                 \
+    hipLaunchKernelGGL((k_spmm<1, kUnroll, kUnrollHeavy, false, SF, IP, NSV>), grid, dim3(kBlock), 0, s, \
+                       indptr, indices, vals, morder, nr, nh, n_slices, nb_heavy, X, ldx, Y, ldy,     \
+                       d, acc, nt, bb, epi)
+        if (ns == 32) {
+            if (sfull) SRG_LAUNCH_NARROW(32, true);
+            else SRG_LAUNCH_NARROW(32, false);
+        } else if (ns == 16) {
+            SRG_LAUNCH_NARROW(16, false);
+        } else if (ns == 8) {
+            SRG_LAUNCH_NARROW(8, false);
+        } else if (ns == 4) {
+            SRG_LAUNCH_NARROW(4, false);
+        } else if (ns == 2) {
+            SRG_LAUNCH_NARROW(2, false);
+        } else if (ns == 1) {
+            SRG_LAUNCH_NARROW(1, false);
+        } else if (vec == 4) {
             if (full) SRG_LAUNCH_SPMM(4, true, true);
             else if (sfull) SRG_LAUNCH_SPMM(4, false, true);
             else SRG_LAUNCH_SPMM(4, false, false);
@@ -967,6 +1052,7 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
             else SRG_LAUNCH_SPMM(1, false, false);
         }
 #undef SRG_LAUNCH_SPMM
+#undef SRG_LAUNCH_NARROW
         SRG_HIP_CHECK(hipGetLastError());
     }
     if (ss) SRG_HIP_CHECK(hipStreamWaitEvent(s, ss->join, 0));   // join

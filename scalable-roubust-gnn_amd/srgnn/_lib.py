@@ -19,6 +19,7 @@ SRG_ERR_ALLOC = -3
 
 SRG_SPMM_ACCUMULATE = 0x1
 SRG_SPMM_NT_STORE = 0x2
+SRG_SPMM_WIDE_ROWS = 0x4
 
 SRG_CHEBY_INIT = 0
 SRG_CHEBY_STEP = 1

@@ -356,3 +356,33 @@ def test_device_construct_weighted_duplicates_equal_oracle(oracle_mod):
     np.testing.assert_array_equal(ip.cpu().numpy(), want.indptr)
     np.testing.assert_array_equal(ix.cpu().numpy(), want.indices)
     np.testing.assert_array_equal(vals.cpu().numpy(), want.data)
+
+
+@pytest.mark.parametrize("thr", [(-1, -1), (None, None), (4, 64)])
+@pytest.mark.parametrize("d", [1, 2, 3, 4, 5, 8, 13, 16, 17, 31, 32])
+def test_narrow_rows_per_wave_bit_exact(oracle_mod, thr, d):
+    """d <= 32: 64/S rows per wave (narrow path) == one row per wave == the oracle, bit for bit,
+    including ACCUMULATE, the fused aggregation epilogue and strided panels."""
+    from srgnn import synth
+    from srgnn.csr import DeviceCSR
+    from srgnn.spmm import spmm, spmm_agg
+    n = 2500
+    u, v = synth.rmat_undirected_t(n, 20000, seed=30 + d)
+    ip, ix = synth.symmetric_csr_t(n, u, v)
+    vals = torch.from_numpy(np.random.default_rng(d).random(ix.numel()).astype(np.float32))
+    A = DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, heavy_threshold=thr[0], hub_threshold=thr[1], device="cuda")
+    wide = torch.from_numpy(np.random.default_rng(2).standard_normal((n, d + 5)).astype(np.float32)).cuda()
+    X = wide[:, 2:2 + d]                                   # strided panel (ld = d + 5)
+    y = spmm(A, X)
+    np.testing.assert_array_equal(y.cpu().numpy(),
+                                  oracle_mod.spmm(ip.numpy(), ix.numpy(), vals.numpy(), X.cpu().numpy()))
+    assert torch.equal(spmm(A, X, wide_rows=True), y)
+    y2 = y.clone()
+    spmm(A, X, out=y2, accumulate=True)
+    y3 = y.clone()
+    spmm(A, X, out=y3, accumulate=True, wide_rows=True)
+    assert torch.equal(y2, y3)
+    agg = torch.ones_like(y)
+    out = torch.empty_like(y)
+    spmm_agg(A, X, out, agg, 0.25, False)
+    assert torch.equal(out, y) and torch.equal(agg, 1.0 + 0.25 * y)
