@@ -457,6 +457,9 @@ def main():
                      "frac": achieved / peak, "traffic": traffic,
                      "kernel": "k_spmm (+ k_spmm_hub beside it): one hop" + (" of rank 0's rows" if world > 1 else ""),
                      "kernel_ms": kern_s * 1e3,
+                     # measured HBM bytes (PMC) per launch / the same launch duration: the share of
+                     # the 8 TB/s peak the kernel actually moves (the no-reuse frac counts cache hits)
+                     "traffic_frac": (traffic / kern_s / 1e9 / peak) if traffic else None,
                      "algorithmic_bytes_per_launch": b_alg,
                      "compulsory_bytes_per_launch": roofline.bytes_compulsory(local_rows, local_nnz, d,
                                                                               n_cols=n)},
