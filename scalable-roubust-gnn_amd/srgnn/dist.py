@@ -1,15 +1,19 @@
-"""Multi-GPU propagation: 1-D row partition of Â, one process per GPU, one all-gather per hop.
+"""Multi-GPU propagation: 1-D row partition of Â, one process per GPU (torch.distributed; the
+"nccl" backend is RCCL over xGMI; gloo on CPU for tests).  SURVEY.md §8(e).
 
-SURVEY.md §8(e).  Rank p owns the contiguous row block [starts[p], starts[p+1]) of Â (blocks
-balanced by nonzeros) and the same rows of every hop panel.  Before each hop the ranks all-gather
-their current panel blocks into a full panel (RCCL over xGMI with the "nccl" backend; gloo on CPU
-for tests), then each rank computes its rows of the next hop with the local kernel.
+Rank p owns the contiguous row block [starts[p], starts[p+1]) of Â (blocks balanced by nonzeros)
+and the same rows of every hop panel.  Two exchanges:
 
-Layout: blocks are gathered into a PADDED full panel [P * max_rows, d] (one fixed-size collective,
-no re-packing), so the local operator's column ids are remapped once, at partition time, from
-global id c (in block q) to q * max_rows + (c - starts[q]).  The remap is monotone, so every row's
-nonzeros keep their CSR order and each output element is the same fma chain as on one GPU: the
-multi-GPU result is bitwise equal to the single-GPU one.
+* HaloPartitionedOperator (default): each rank receives only the remote rows its own rows
+  reference, group by group (nnz-balanced row chunks + the hub rows), with one all_to_all_single
+  per group on a communication stream as soon as that group's kernel is done -- overlapping the
+  later groups' kernels.  HaloWaveletFilter runs the wavelet basis' Chebyshev recurrence on the
+  same plan (one exchange per order).
+* RowPartitionedOperator: one padded all_gather_into_tensor of the whole panel per hop.
+
+In both, the local operator's column ids are remapped into the local panel layout with every
+row's entries kept in their CSR order, so each output element is the same fma chain as on one
+GPU: the multi-GPU results are bitwise equal to the single-GPU ones.
 """
 from __future__ import annotations
 

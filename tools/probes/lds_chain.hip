@@ -6,7 +6,7 @@
 typedef float V4 __attribute__((ext_vector_type(4)));
 constexpr int LD = 528, W = 512;
 
-template <int MODE>   // 0: tile + value reads, 1: tile only, 2: value only, 3: none (registers)
+template <int MODE>   // 0: tile + value reads, 1: tile only, 2: value only, 3: none (registers), 4: tile + DPP-broadcast values
 __global__ void __launch_bounds__(576) k(const float* in, float* out, long long* cyc, int reps, int busy, int prio, int active)
 {
     __shared__ __attribute__((aligned(16))) float lds[32 * LD + W];
@@ -43,6 +43,39 @@ __global__ void __launch_bounds__(576) k(const float* in, float* out, long long*
                 for (int i = 0; i < 2; ++i)
                     for (int e = 0; e < 4; ++e) acc = __builtin_fmaf(aa[i][e], tt[i][e], acc);
             };
+            if constexpr (MODE == 4) {
+                // sets of 16 links: 4 tile ds_read_b128 + ONE ds_read_b32 of values (lane l holds value
+                // l & 15), broadcast per 16-lane row by DPP row_newbcast inside the fma; ring of 3 sets
+                struct Set { V4 t[4]; float v; };
+                auto ld4 = [&](int set, Set& st) {
+                    for (int i = 0; i < 4; ++i)
+                        st.t[i] = *reinterpret_cast<const V4*>(tcol + ((((set * 4 + i) & 127) ^ sw) << 2));
+                    st.v = av[((set * 16) + (lane & 15)) & 511];
+                };
+#define F(n, xv) asm volatile("v_fmac_f32_dpp %0, %1, %2 row_newbcast:" #n " row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(st.v), "v"(xv))
+                auto run4 = [&](const Set& st) {
+                    F(0, st.t[0][0]); F(1, st.t[0][1]); F(2, st.t[0][2]); F(3, st.t[0][3]);
+                    F(4, st.t[1][0]); F(5, st.t[1][1]); F(6, st.t[1][2]); F(7, st.t[1][3]);
+                    F(8, st.t[2][0]); F(9, st.t[2][1]); F(10, st.t[2][2]); F(11, st.t[2][3]);
+                    F(12, st.t[3][0]); F(13, st.t[3][1]); F(14, st.t[3][2]); F(15, st.t[3][3]);
+                };
+#undef F
+                Set A, B, C;
+                ld4(0, A); __builtin_amdgcn_sched_barrier(0);
+                ld4(1, B); __builtin_amdgcn_sched_barrier(0);
+                for (int kk = 0; kk + 5 <= 30; kk += 3) {   // 30 sets of 16 = 480 links per rep
+                    ld4(kk + 2, C); __builtin_amdgcn_sched_barrier(0);
+                    asm volatile("s_waitcnt lgkmcnt(10)" ::: "memory");
+                    run4(A); __builtin_amdgcn_sched_barrier(0);
+                    ld4(kk + 3, A); __builtin_amdgcn_sched_barrier(0);
+                    asm volatile("s_waitcnt lgkmcnt(10)" ::: "memory");
+                    run4(B); __builtin_amdgcn_sched_barrier(0);
+                    ld4(kk + 4, B); __builtin_amdgcn_sched_barrier(0);
+                    asm volatile("s_waitcnt lgkmcnt(10)" ::: "memory");
+                    run4(C); __builtin_amdgcn_sched_barrier(0);
+                }
+                continue;
+            }
             ld(0, t[0], a[0]); __builtin_amdgcn_sched_barrier(0);
             ld(1, t[1], a[1]); __builtin_amdgcn_sched_barrier(0);
             ld(2, t[2], a[2]); __builtin_amdgcn_sched_barrier(0);
@@ -70,15 +103,16 @@ int main()
     (void)hipMemset(in, 0, (32 * LD + W) * 4);
     const int reps = 200;
     const long long links = (long long)reps * 15 * 4 * 8;   // 15 iterations x 4 sets x 8 links
-    const char* names[] = {"tile+value", "tile only", "value only", "registers"};
-    for (int active : {4, 8, 16, 32, 64})
-        for (int mode = 0; mode < 4; ++mode) {
-            auto fn = mode == 0 ? k<0> : mode == 1 ? k<1> : mode == 2 ? k<2> : k<3>;
+    const char* names[] = {"tile+value", "tile only", "value only", "registers", "tile+dpp"};
+    for (int active : {32, 64})
+        for (int mode = 0; mode < 5; ++mode) {
+            auto fn = mode == 0 ? k<0> : mode == 1 ? k<1> : mode == 2 ? k<2> : mode == 3 ? k<3> : k<4>;
             hipLaunchKernelGGL(fn, dim3(1), dim3(576), 0, 0, in, out, cyc, reps, 0, 0, active);
             (void)hipDeviceSynchronize();
             long long c;
             (void)hipMemcpy(&c, cyc, 8, hipMemcpyDeviceToHost);
-            printf("active=%2d %-11s %.2f cycles/link\n", active, names[mode], (double)c / links);
+            const long long l = mode == 4 ? (long long)reps * 9 * 3 * 16 : links;
+            printf("active=%2d %-11s %.2f cycles/link\n", active, names[mode], (double)c / l);
         }
     return 0;
 }
