@@ -386,3 +386,32 @@ def test_narrow_rows_per_wave_bit_exact(oracle_mod, thr, d):
     out = torch.empty_like(y)
     spmm_agg(A, X, out, agg, 0.25, False)
     assert torch.equal(out, y) and torch.equal(agg, 1.0 + 0.25 * y)
+
+
+def test_papers100M_scale_sampled_rows_bit_exact(oracle_mod):
+    """The papers100M-shaped graph on one GPU (111 M rows, 3.34e9 nonzeros: indptr beyond 2^31,
+    launches chunked beyond 2^32 lanes): one hop checked bit for bit on 2000 sampled rows plus the
+    longest rows, against the oracle on the compacted sub-problem (the rows' own column lists and
+    the X rows they gather)."""
+    from srgnn import graphs, synth
+    from srgnn.csr import DeviceCSR
+    from srgnn.spmm import spmm
+    free, _ = torch.cuda.mem_get_info()
+    if free < 200e9:
+        pytest.skip("needs a full MI355X (200 GB free)")
+    ip, ix, vals, n, d, _ = graphs.build("papers100M", "cuda")
+    assert int(ip[-1]) > 2 ** 31
+    A = DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, device="cuda")
+    x = synth.uniform_features_t(n, d, device="cuda")
+    y = spmm(A, x)
+    deg = ip[1:] - ip[:-1]
+    g = torch.Generator(device="cpu").manual_seed(9)
+    rows = torch.unique(torch.cat([torch.randint(0, n, (2000,), generator=g).cuda(),
+                                   torch.sort(deg, descending=True).indices[:20]]))
+    beg, cnt = ip[rows], deg[rows]
+    pos = torch.repeat_interleave(beg - torch.cumsum(cnt, 0) + cnt, cnt) + torch.arange(int(cnt.sum()), device="cuda")
+    cols, vv = ix[pos].long(), vals[pos]
+    ucols, inv = torch.unique(cols, return_inverse=True)
+    sub_ip = np.r_[0, np.cumsum(cnt.cpu().numpy())]
+    want = oracle_mod.spmm(sub_ip, inv.to(torch.int32).cpu().numpy(), vv.cpu().numpy(), x[ucols].cpu().numpy())
+    np.testing.assert_array_equal(y[rows].cpu().numpy(), want)
