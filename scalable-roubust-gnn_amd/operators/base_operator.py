@@ -29,6 +29,38 @@ from srgnn.csr import DeviceCSR
 from srgnn.spmm import propagate as _device_propagate
 
 
+def _hops_to_host(A, X, K, ring=3):
+    """Hops 1..K of A on the device panel X, each copied to pinned host memory on a copy stream
+    while the next hop runs (the D2H of the reference-shaped list overlaps the kernels); device
+    memory holds a ring of `ring` hop panels.  Returns the K host tensors."""
+    from srgnn.spmm import spmm
+    dev = A.device
+    main = torch.cuda.current_stream(dev)
+    copy_s = torch.cuda.Stream(dev)
+    R = max(1, min(K, ring))
+    bufs = [torch.empty_like(X) for _ in range(R)]
+    host = [torch.empty(tuple(X.shape), dtype=torch.float32, pin_memory=True) for _ in range(K)]
+    copied = []
+    prev = X
+    for k in range(1, K + 1):
+        buf = bufs[(k - 1) % R]
+        if k > R:
+            main.wait_event(copied[k - 1 - R])      # the ring slot's previous hop is on the host
+        spmm(A, prev, out=buf)
+        done = torch.cuda.Event()
+        done.record(main)
+        copy_s.wait_event(done)
+        with torch.cuda.stream(copy_s):
+            host[k - 1].copy_(buf, non_blocking=True)
+        c = torch.cuda.Event()
+        c.record(copy_s)
+        copied.append(c)
+        prev = buf
+    copy_s.synchronize()
+    main.synchronize()
+    return host
+
+
 class GraphOp:
     def __init__(self, prop_steps):
         self.prop_steps = prop_steps
@@ -96,12 +128,7 @@ class GraphOp:
             return [torch.FloatTensor(feature)]
         A = A if A is not None else self._operator()
         X = torch.from_numpy(np.ascontiguousarray(feature)).to(A.device)
-        panels = _device_propagate(A, X, self.prop_steps)
-        host = [torch.empty(tuple(p.shape), dtype=torch.float32, pin_memory=True) for p in panels[1:]]
-        for h, p in zip(host, panels[1:]):
-            h.copy_(p, non_blocking=True)
-        torch.cuda.current_stream(A.device).synchronize()
-        return [torch.FloatTensor(feature)] + host
+        return [torch.FloatTensor(feature)] + _hops_to_host(A, X, self.prop_steps)
 
     def propagate_device(self, adj, feature, device=None):
         """Same as propagate() but returns device tensors (hop 0 = the feature on the device)."""

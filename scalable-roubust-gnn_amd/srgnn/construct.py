@@ -65,9 +65,11 @@ def sym_norm(indptr, indices, data, n: int, r: float, device=None, segsum=None):
     Returns device tensors (indptr int64, indices int32, values fp64), canonical CSR."""
     segsum = segsum or segment_sum_device
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
-    ip = torch.as_tensor(np.asarray(indptr, dtype=np.int64) if not torch.is_tensor(indptr) else indptr).to(dev, torch.int64)
-    ix = torch.as_tensor(np.asarray(indices) if not torch.is_tensor(indices) else indices).to(dev, torch.int64)
-    v = torch.as_tensor(np.asarray(data, dtype=np.float64) if not torch.is_tensor(data) else data).to(dev, torch.float64)
+    # copy in the stored dtypes and widen on the device (a host-side int32 -> int64 conversion of
+    # the column ids cost 0.24 s at products size)
+    ip = torch.as_tensor(np.asarray(indptr) if not torch.is_tensor(indptr) else indptr).to(dev).to(torch.int64)
+    ix = torch.as_tensor(np.asarray(indices) if not torch.is_tensor(indices) else indices).to(dev).to(torch.int64)
+    v = torch.as_tensor(np.asarray(data) if not torch.is_tensor(data) else data).to(dev).to(torch.float64)
     rows = torch.repeat_interleave(torch.arange(n, device=dev), ip[1:] - ip[:-1])
     diag = torch.arange(n, device=dev)
     # adj + I: the identity's entry is added after the row's own (duplicate) entries

@@ -80,9 +80,11 @@ class DeviceCSR:
         """Build from CSR arrays (numpy or torch, any device); copies to `device` if needed."""
         device = _dev(device if device is not None else
                       (indices.device if isinstance(indices, torch.Tensor) and indices.is_cuda else None))
-        ip = torch.as_tensor(indptr).to(device=device, dtype=torch.int64)
-        ix = torch.as_tensor(indices).to(device=device, dtype=torch.int32)
-        vv = torch.as_tensor(values).to(device=device, dtype=torch.float32)
+        # copy in the stored dtypes, convert on the device (host-side conversions of 1e8-entry
+        # arrays are single-threaded and slower than the copy)
+        ip = torch.as_tensor(indptr).to(device=device).to(torch.int64)
+        ix = torch.as_tensor(indices).to(device=device).to(torch.int32)
+        vv = torch.as_tensor(values).to(device=device).to(torch.float32)
         n_rows = int(ip.numel()) - 1
         if n_rows < 0:
             raise ValueError("indptr must have n_rows + 1 entries")
@@ -101,9 +103,9 @@ class DeviceCSR:
     @classmethod
     def from_scipy(cls, adj, heavy_threshold=None, device=None):
         """From a scipy.sparse.csr_matrix (values cast to fp32 like SSRG/operators/utils.py:39)."""
-        return cls.from_tensors(np.asarray(adj.indptr, dtype=np.int64),
+        return cls.from_tensors(np.asarray(adj.indptr),
                                 np.asarray(adj.indices, dtype=np.int32),
-                                np.asarray(adj.data).astype(np.float32),
+                                np.asarray(adj.data),   # cast to fp32 on the device (round to nearest, as astype)
                                 n_cols=adj.shape[1], heavy_threshold=heavy_threshold, device=device)
 
     def rows(self, r0: int, r1: int, heavy_threshold=None, hub_threshold=None) -> "DeviceCSR":
