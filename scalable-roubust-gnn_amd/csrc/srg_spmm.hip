@@ -995,7 +995,7 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
                                d, acc, nt, epi);
         SRG_HIP_CHECK(hipGetLastError());
         SRG_HIP_CHECK(hipEventRecord(ss->join, ss->stream));
-        static const int delay_us = [] { const char* e = getenv("SRGNN_HUB_DISPATCH_DELAY_US"); return e ? atoi(e) : 20; }();
+        static const int delay_us = [] { const char* e = getenv("SRGNN_HUB_DISPATCH_DELAY_US"); return e ? atoi(e) : 10; }();
         if (delay_us > 0) {
             hipLaunchKernelGGL(k_dispatch_delay, dim3(1), dim3(64), 0, s, delay_us);
             SRG_HIP_CHECK(hipGetLastError());
