@@ -16,7 +16,6 @@ reference's own summation order (bit-identical), so only 4-5 panels are ever res
 from __future__ import annotations
 
 import ctypes
-import platform
 
 import numpy as np
 import scipy.sparse as sp
@@ -190,7 +189,7 @@ class MessageOp(nn.Module):
 
 
 def ada_platform_one_step_propagation(adj, x):
-    """One hop with host arrays (base_operator.py:309-314): the GPU SpMM on Linux, scipy elsewhere."""
-    if platform.system() == "Linux":
-        return csr_sparse_dense_matmul(adj, x)
-    return adj.dot(x)
+    """One hop with host arrays (base_operator.py:309-314).  The reference takes its C kernel on
+    Linux and scipy's adj.dot elsewhere; this build is gfx950/Linux only, so it is always the GPU
+    SpMM (csr_sparse_dense_matmul -> libsrgnn_hip), with no CPU path to fall back to."""
+    return csr_sparse_dense_matmul(adj, x)
