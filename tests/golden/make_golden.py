@@ -56,6 +56,14 @@ def _load_synth():
     return mod
 
 
+def _load_golden_cases():
+    path = os.path.join(REPO, "tests", "golden_cases.py")
+    spec = importlib.util.spec_from_file_location("_golden_cases", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
 def import_reference():
     if not os.path.exists(REF_LIB):
         raise SystemExit(f"{REF_LIB} missing: run `make -C oracle` first")
@@ -155,6 +163,31 @@ def store_case(name, adj, X, hops, ahat=None, meta=None, x_stored=True):
     return rec
 
 
+def family_ops(TwoOrder, Com, TwoDir, norm):
+    synth = _load_synth()
+    gc = _load_golden_cases()
+    family_adj, family_construct = gc.family_adj, gc.family_construct
+    adj = family_adj()
+    n = adj.shape[0]
+    X = synth.uniform_features_np(n, 24, seed=70)
+    K = 3
+    out = {}
+    for name, base in (("two_order", TwoOrder), ("complex", Com), ("two_dir", TwoDir)):
+        cons = family_construct(name, norm)
+        cls = type(f"Golden_{name}", (base,), {"construct_adj": lambda self, a, c=cons: c(a)})
+        lists = cls(K).propagate(adj, X)
+        arrs = {"adj_indptr": adj.indptr.astype(np.int64), "adj_indices": adj.indices.astype(np.int32),
+                "adj_data": adj.data.astype(np.float64), "x": X}
+        for li, lst in enumerate(lists):
+            for k, t in enumerate(lst):
+                h = np.ascontiguousarray(t.numpy(), dtype=np.float32)
+                arrs[f"list{li}_hop{k}_sha256"] = np.array(sha(h))
+                arrs[f"list{li}_hop{k}"] = h
+        np.savez_compressed(os.path.join(OUT, f"fam_{name}.npz"), **arrs)
+        out[f"fam_{name}"] = {"n": n, "d": 24, "k": K, "op": "family", "family": name, "lists": len(lists)}
+    return out
+
+
 def main():
     SymLap, Ppr, csr_mm, _ = import_reference()
     synth = _load_synth()
@@ -249,6 +282,13 @@ def main():
     adj = random_adj(200, 0.05, seed=400)
     X = synth.uniform_features_np(200, 37, seed=60)
     manifest["agg_rand_k20"] = store_agg("agg_rand_k20", adj, X, 20, 0.5, {"features": "uniform(seed=60)"})
+
+    # 7c. the other operator families (base_operator.py:60-307) with scipy-only construct_adj
+    #     subclasses defined here (the reference's own subclasses need torch_scatter / PyG)
+    from operators.base_operator import ComGraphOp, TwoDirGraphOp, TwoOrderPprApproxGraphOp
+    from operators.utils import adj_to_symmetric_norm
+    for k, v in family_ops(TwoOrderPprApproxGraphOp, ComGraphOp, TwoDirGraphOp, adj_to_symmetric_norm).items():
+        manifest[k] = v
 
     # 7. error behaviour of GraphOp.propagate (base_operator.py:20-30, utils.py:23-45)
     errs = {}

@@ -23,6 +23,8 @@ def names(kind=None):
         out = [k for k in out if m[k]["op"] == "raw_spmm"]
     elif kind == "aggregate":
         out = [k for k in out if m[k]["op"] == "aggregate"]
+    elif kind == "family":
+        out = [k for k in out if m[k]["op"] == "family"]
     return out
 
 
@@ -106,3 +108,27 @@ class Msg:
         self.aggr_type, self.start, self.end = aggr, start, end
         self.combination_type, self.alpha = combination_type, alpha
         self.weight_list = None if weight_list is None else __import__("torch").FloatTensor(weight_list)
+
+
+def family_adj(seed=500, n=150):
+    """The directed weighted graph (asymmetric) of the operator-family fixtures."""
+    import scipy.sparse as sp
+    rng = np.random.default_rng(seed)
+    mask = rng.random((n, n)) < 0.04
+    np.fill_diagonal(mask, False)
+    w = rng.integers(1, 9, size=(n, n)) / 4.0
+    return sp.csr_matrix(np.where(mask, w, 0.0))
+
+
+def family_construct(name, norm):
+    """construct_adj of the fixtures' test subclasses; `norm` = adj_to_symmetric_norm (the
+    reference's, or this build's host mirror of it -- bit-identical)."""
+    import scipy.sparse as sp
+    if name == "two_order":
+        return lambda adj: (norm(adj, 0.5).tocsr(), norm(adj, 0.3).tocsr())
+    if name == "complex":
+        return lambda adj: (norm(adj, 0.5).tocsr(), (norm(adj, 0.5) - norm(adj.T.tocsr(), 0.5)).tocsr() * 0.5)
+    if name == "two_dir":
+        return lambda adj: (norm((adj + adj.T).tocsr(), 0.5).tocsr(), norm(sp.tril(adj).tocsr(), 0.5).tocsr(),
+                            norm(sp.triu(adj).tocsr(), 0.5).tocsr())
+    raise ValueError(name)
