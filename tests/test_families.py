@@ -72,3 +72,15 @@ def test_family_gpu_equals_reference(name):
         cls(c.k).propagate(c.adj().tocoo(), c["x"])
     with pytest.raises(ValueError):
         cls(c.k).propagate(c.adj(), c["x"][:-1])
+
+
+def test_family_message_ops():
+    import torch
+    from operators.message_operator.twodir_message_operator.twodir_last_message_op import TwoDirLastMessageOp
+    from operators.message_operator.twoorder_message_operator.twoorder_last_message_op import TwoOrderLastMessageOp
+    a = [torch.zeros(2), torch.ones(2)]
+    b = [torch.ones(2), torch.full((2,), 2.0)]
+    assert TwoOrderLastMessageOp().aggregate(a, b)[1].tolist() == [2.0, 2.0]
+    assert TwoDirLastMessageOp().aggregate(a, b, a)[2].tolist() == [1.0, 1.0]
+    with pytest.raises(TypeError):
+        TwoOrderLastMessageOp().aggregate([np.zeros(2)], b)
