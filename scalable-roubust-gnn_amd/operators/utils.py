@@ -116,3 +116,13 @@ def two_dim_weighted_add(feat_list, weight_list):
         raise ValueError("The weight list should be a 2d tensor!")
     stacked = torch.stack(feat_list, dim=2)
     return torch.bmm(stacked, weight_list.unsqueeze(dim=2)).squeeze(dim=2)
+
+
+def squeeze_first_dimension(feat_list):
+    """Mirror of utils.py:452-460: drop a leading batch dimension of 3-d feature tensors
+    (in place for a list, like the reference)."""
+    if isinstance(feat_list, Tensor):
+        return feat_list[0] if feat_list.dim() == 3 else feat_list
+    if isinstance(feat_list, list) and feat_list[0].dim() == 3:
+        feat_list[:] = [f.squeeze(dim=0) for f in feat_list]
+    return feat_list

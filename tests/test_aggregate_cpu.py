@@ -161,3 +161,30 @@ def test_plan_shape():
     assert ("fold", 1, 0) in steps
     assert G.tail_range(2708, 1433) == (2708 * 1433 // 32 * 32, 2708 * 1433 % 32)
     assert G.tail_range(1, 7) == (4, 3) and G.tail_range(2449029, 128)[1] == 0
+
+
+def test_operators_utils_helpers():
+    """operators.utils weighted adds / squeeze (host helpers the reference's message operators call,
+    utils.py:426-460): same values and error classes as the reference's definitions."""
+    from operators.utils import one_dim_weighted_add, squeeze_first_dimension, two_dim_weighted_add
+    g = torch.Generator().manual_seed(0)
+    feats = [torch.randn(5, 3, generator=g) for _ in range(4)]
+    w = torch.tensor([0.5, -1.0, 0.25, 2.0])
+    want = sum(wi * f for wi, f in zip(w, feats))
+    torch.testing.assert_close(one_dim_weighted_add(feats, w), want)
+    w2 = torch.randn(5, 4, generator=g)
+    want2 = sum(w2[:, i:i + 1] * f for i, f in enumerate(feats))
+    torch.testing.assert_close(two_dim_weighted_add(feats, w2), want2)
+    with pytest.raises(TypeError):
+        one_dim_weighted_add(feats, w.tolist())
+    with pytest.raises(ValueError):
+        one_dim_weighted_add(feats, w[:3])
+    with pytest.raises(IndexError):                # the reference indexes shape[1] before its 2-d check
+        two_dim_weighted_add(feats, w)
+    with pytest.raises(ValueError):
+        two_dim_weighted_add(feats, w2[:, :3])
+    batched = [f.unsqueeze(0) for f in feats]
+    out = squeeze_first_dimension(batched)
+    assert out is batched and all(torch.equal(a, b) for a, b in zip(out, feats))
+    assert torch.equal(squeeze_first_dimension(feats[0].unsqueeze(0)), feats[0])
+    assert squeeze_first_dimension(feats[0]) is feats[0]
