@@ -386,275 +386,6 @@ class HaloPartitionedOperator:
         main.wait_stream(comm_s)
 
     def propagate(self, x_local: torch.Tensor, K: int, panels=None):
-        """[X, ÂX, …, Â^K X] restricted to this rank's rows (each [max_rows, d], first `rows` valid).
-        x_local: this rank's rows of X ([rows, d] or a padded [max_rows, d] panel)."""
-        d = x_local.shape[1]
-        if panels is None:
-            panels = [self.new_panel(d) for _ in range(K + 1)]
-        if x_local.shape[0] != self.max_rows or x_local.data_ptr() != panels[0].data_ptr():
-            panels[0][: self.rows].copy_(x_local[: self.rows])
-        for k in range(1, K + 1):
-            full = self._gather(panels[k - 1])
-            self._spmm(self.A, full, panels[k][: self.rows])
-        return panels
-
-
-def simulate_propagate(indptr, indices, values, n: int, x: torch.Tensor, K: int, world: int,
-                       heavy_threshold=None, device=None):
-    """P virtual ranks in ONE process: every share computes its rows of each hop from the padded
-    full panel assembled exactly as all_gather_into_tensor would lay it out.  Returns the K+1 full
-    [n, d] panels.  Exercises partition, column remap and padded layout on one device."""
-    shares = [RowPartitionedOperator(indptr, indices, values, n, heavy_threshold=heavy_threshold,
-                                     device=device, rank=p, world=world) for p in range(world)]
-    d = x.shape[1]
-    mr = shares[0].max_rows
-    panels = [[s.new_panel(d) for _ in range(K + 1)] for s in shares]
-    for s, pp in zip(shares, panels):
-        pp[0][: s.rows].copy_(x[s.r0:s.r1])
-    full = torch.empty((world * mr, d), dtype=torch.float32, device=panels[0][0].device)
-    for k in range(1, K + 1):
-        for p in range(world):
-            full[p * mr:(p + 1) * mr].copy_(panels[p][k - 1])
-        for s, pp in zip(shares, panels):
-            s._spmm(s.A, full, pp[k][: s.rows])
-    return [torch.cat([pp[k][: s.rows] for s, pp in zip(shares, panels)]) for k in range(K + 1)]
-
-
-# ================================================================================================
-# Halo exchange: each rank receives only the remote X rows its rows reference, group by group,
-# overlapped with the computation of the later groups.
-# ================================================================================================
-
-def _chunk_bounds(indptr_local: torch.Tensor, chunks: int):
-    """Contiguous local row ranges with about equal nonzeros (like balanced_row_starts)."""
-    return balanced_row_starts(indptr_local, chunks)
-
-
-class HaloPartitionedOperator:
-    """Rank p's share of Â for the halo-exchange multi-GPU propagation.
-
-    Setup (deterministic from the GLOBAL operator, identical on every rank, no messages):
-      * rows: the nnz-balanced block [starts[p], starts[p+1]);
-      * groups: the block's rows are split into `chunks` contiguous ranges balanced by nonzeros
-        (hub rows excluded), plus one group of hub rows (more than the owner's hub threshold);
-        exchange order = chunk 0 .. chunk C-1, then hubs (the hub kernel finishes last);
-      * every rank q's needs from every source s: the distinct columns of q's rows owned by s,
-        by (group on s, source, id) -- so sends and receives are known without negotiation;
-      * local panel layout: [own rows | halo rows ordered by (group, source, id)], and the local
-        operator's column ids remapped into it (each row's entries keep their CSR order, so
-        every output element is the same fma chain as on one GPU).
-    Per hop k: the groups' kernels write the own part of panel k+1 (hub group on its own stream),
-    and as each group completes its rows that peers need are packed and exchanged with one
-    all_to_all_single (RCCL) on a communication stream, overlapping the next groups' kernels.
-    """
-
-    def __init__(self, indptr, indices, values, n: int, group=None, chunks: int = 4,
-                 heavy_threshold=None, hub_threshold=None, device=None, rank=None, world=None,
-                 local_spmm=None):
-        from .csr import DEFAULT_HEAVY_THRESHOLD, DEFAULT_HUB_THRESHOLD, auto_hub_threshold
-        self.group = group
-        self.virtual = rank is not None
-        self.rank = rank if rank is not None else (dist.get_rank(group) if dist.is_initialized() else 0)
-        self.world = world if world is not None else (dist.get_world_size(group) if dist.is_initialized() else 1)
-        P, p = self.world, self.rank
-        dev = torch.device(device) if device is not None else indices.device
-        self.device = dev
-        self.n = n
-        gip = indptr.to(dev, torch.int64)
-        gix = indices.to(dev)
-        self.starts = balanced_row_starts(gip, P)
-        st = torch.tensor(self.starts, dtype=torch.int64, device=dev)
-        self.nnz_total = int(gip[-1])
-        deg = gip[1:] - gip[:-1]
-        owner = torch.bucketize(torch.arange(n, device=dev), st[1:], right=True)   # owner rank of each row
-        # hub flags: each owner's threshold (auto from its own nonzero count unless given)
-        if hub_threshold is None:
-            hub_threshold = DEFAULT_HUB_THRESHOLD
-        thr = torch.empty(P, dtype=torch.int64, device=dev)
-        for q in range(P):
-            nnz_q = int(gip[self.starts[q + 1]] - gip[self.starts[q]])
-            thr[q] = auto_hub_threshold(nnz_q, launches=max(1, int(chunks))) if hub_threshold is None else (
-                hub_threshold if hub_threshold >= 0 else (1 << 62))
-        is_hub = deg > thr[owner]
-        # chunk of every row (contiguous nnz-balanced ranges inside each owner's block)
-        C = max(1, int(chunks))
-        self.C = C
-        grp = torch.empty(n, dtype=torch.int64, device=dev)
-        for q in range(P):
-            s0, s1 = self.starts[q], self.starts[q + 1]
-            lip = gip[s0:s1 + 1] - gip[s0]
-            cb = _chunk_bounds(lip, C)
-            for c in range(C):
-                grp[s0 + cb[c]:s0 + cb[c + 1]] = c
-        grp[is_hub] = C
-        self.n_groups = C + 1
-        G = self.n_groups
-        # --- my needs: distinct remote columns of my rows, ordered by (group, source, id)
-        r0, r1 = self.starts[p], self.starts[p + 1]
-        self.r0, self.r1, self.rows = r0, r1, r1 - r0
-        b0, b1 = int(gip[r0]), int(gip[r1])
-        self._b0, self._b1 = b0, b1
-        my_cols = gix[b0:b1].to(torch.int64)
-        self.nnz_local = b1 - b0
-
-        def needs_of(q):
-            q0, q1 = int(gip[self.starts[q]]), int(gip[self.starts[q + 1]])
-            cols = torch.unique(gix[q0:q1].to(torch.int64))
-            cols = cols[(cols < self.starts[q]) | (cols >= self.starts[q + 1])]
-            key = (grp[cols] * P + owner[cols]) * n + cols          # sort by (group, source, id)
-            return cols[torch.argsort(key)]
-
-        need = needs_of(p)
-        ng, ns = grp[need], owner[need]
-        counts = torch.zeros((G, P), dtype=torch.int64, device=dev)
-        counts.index_put_((ng, ns), torch.ones_like(need), accumulate=True)
-        self.recv_counts = counts.cpu().tolist()                 # [group][source]
-        self.halo = int(need.numel())
-        self.group_offsets = []                                  # start of each group's halo region
-        off = 0
-        for g in range(G):
-            self.group_offsets.append(off)
-            off += sum(self.recv_counts[g])
-        # --- my sends: for every peer q, my rows q needs, per group, in q's receive order
-        self.send_idx = [[None] * P for _ in range(G)]
-        self.send_counts = [[0] * P for _ in range(G)]
-        for q in range(P):
-            if q == p:
-                continue
-            nq = needs_of(q)
-            mine = nq[owner[nq] == p]                             # already sorted by (group, id)
-            gm = grp[mine]
-            for g in range(G):
-                sel = mine[gm == g] - r0
-                self.send_idx[g][q] = sel
-                self.send_counts[g][q] = int(sel.numel())
-        self.send_cat = []
-        for g in range(G):
-            parts = [self.send_idx[g][q] for q in range(P) if q != p and self.send_counts[g][q] > 0]
-            self.send_cat.append(torch.cat(parts) if parts else torch.zeros(0, dtype=torch.int64, device=dev))
-        # --- local operator with columns remapped into [own rows | halo]
-        g2l = torch.full((n,), -1, dtype=torch.int64, device=dev)
-        g2l[r0:r1] = torch.arange(self.rows, device=dev)
-        g2l[need] = self.rows + torch.arange(self.halo, device=dev)
-        lix = g2l[my_cols]
-        if bool((lix < 0).any()):
-            raise RuntimeError("halo layout misses a referenced column")
-        lip = (gip[r0:r1 + 1] - b0).contiguous()
-        lix = lix.to(torch.int32).contiguous()
-        lvv = values[b0:b1].to(dev).contiguous()
-        self.ncols_local = self.rows + self.halo
-        # --- per-group row schedules (local row ids; long rows first)
-        lgrp = grp[r0:r1]
-        ldeg = deg[r0:r1]
-        heavy_t = DEFAULT_HEAVY_THRESHOLD if heavy_threshold is None else heavy_threshold
-        self.views = []
-        for g in range(G):
-            rows_g = torch.nonzero(lgrp == g).flatten()
-            rows_g = rows_g[torch.sort(ldeg[rows_g], descending=True, stable=True).indices]
-            n_g = int(rows_g.numel())
-            if g == C:
-                n_hub, n_heavy = n_g, 0
-            else:
-                n_hub = 0
-                n_heavy = int((ldeg[rows_g] > heavy_t).sum()) if heavy_t >= 0 else 0
-            self.views.append((rows_g.to(torch.int32).contiguous(), n_g, n_heavy, n_hub))
-        self._lip, self._lix, self._lvv = lip, lix, lvv
-        if local_spmm is None:
-            from .csr import DeviceCSR
-            from .spmm import spmm
-            if dev.type == "cuda":
-                from . import _lib
-                _lib.check(_lib.lib().srg_csr_validate(lip.data_ptr(), lix.data_ptr(), self.rows,
-                                                       lix.numel(), self.ncols_local,
-                                                       torch.cuda.current_stream(dev).cuda_stream),
-                           "srg_csr_validate")
-            self._A = [DeviceCSR(lip, lix, lvv, n_g, self.ncols_local, order, n_heavy, n_hub)
-                       for (order, n_g, n_heavy, n_hub) in self.views]
-            self._spmm = lambda A, X, out: spmm(A, X, out=out)
-        else:
-            self._A = [(lip, lix, lvv, order) for (order, _, _, _) in self.views]
-            self._spmm = local_spmm
-        self._streams = None
-
-    # ------------------------------------------------------------------------------------------
-    def new_panel(self, d: int) -> torch.Tensor:
-        """[own rows | halo] panel for this rank."""
-        return torch.zeros((self.rows + self.halo, d), dtype=torch.float32, device=self.device)
-
-    def with_values(self, values: torch.Tensor) -> "HaloPartitionedOperator":
-        """The same partition, halo plan and schedules for an operator with the same structure and
-        other values (e.g. the Chebyshev F = (2/a1)(L - a2 I) next to L); `values` is global."""
-        import copy
-        other = copy.copy(self)
-        lvv = values[self._b0:self._b1].to(self.device).contiguous()
-        other._lvv = lvv
-        if isinstance(self._A[0], tuple):
-            other._A = [(a[0], a[1], lvv, a[3]) for a in self._A]
-        else:
-            from .csr import DeviceCSR
-            other._A = [DeviceCSR(a.indptr, a.indices, lvv, a.n_rows, a.n_cols, a.order, a.n_heavy, a.n_hub)
-                        for a in self._A]
-        other._streams = None
-        return other
-
-    def _exchange_group(self, panel: torch.Tensor, g: int):
-        P, p = self.world, self.rank
-        off = self.rows + self.group_offsets[g]
-        out_splits = [self.recv_counts[g][q] for q in range(P)]
-        in_splits = [self.send_counts[g][q] for q in range(P)]
-        total_in = sum(out_splits)
-        if P == 1 or (total_in == 0 and sum(in_splits) == 0 and not dist.is_initialized()):
-            return
-        recv = panel[off:off + total_in]
-        send = panel[: self.rows].index_select(0, self.send_cat[g]) if self.send_cat[g].numel() else \
-            panel.new_zeros((0, panel.shape[1]))
-        if self.virtual:
-            raise RuntimeError("virtual shares exchange through simulate_halo_propagate()")
-        dist.all_to_all_single(recv, send, out_splits, in_splits, group=self.group)
-
-    def exchange(self, panel: torch.Tensor):
-        for g in range(self.n_groups):
-            self._exchange_group(panel, g)
-
-    def compute(self, src: torch.Tensor, dst: torch.Tensor):
-        """dst[:rows] = local Â rows @ src (all groups, no exchange)."""
-        for g in range(self.n_groups):
-            if self.views[g][1]:
-                self._spmm(self._A[g], src, dst[: self.rows])
-
-    def hop(self, src: torch.Tensor, dst: torch.Tensor, exchange: bool = True):
-        """One hop: dst own rows from src, then (unless exchange=False, e.g. the last hop, whose halo
-        no later hop reads) dst's halo, group by group, overlapped with the later groups' kernels."""
-        if self.device.type != "cuda" or self.world == 1:
-            self.compute(src, dst)
-            if exchange:
-                self.exchange(dst)
-            return
-        if self._streams is None:
-            self._streams = (torch.cuda.Stream(self.device), torch.cuda.Stream(self.device))
-        hub_s, comm_s = self._streams
-        main = torch.cuda.current_stream(self.device)
-        C = self.C
-        done = [torch.cuda.Event() for _ in range(self.n_groups)]
-        hub_s.wait_stream(main)
-        if self.views[C][1]:
-            with torch.cuda.stream(hub_s):
-                self._spmm(self._A[C], src, dst[: self.rows])
-        done[C].record(hub_s)
-        for c in range(C):
-            if self.views[c][1]:
-                self._spmm(self._A[c], src, dst[: self.rows])
-            done[c].record(main)
-        if not exchange:
-            main.wait_event(done[C])
-            return
-        with torch.cuda.stream(comm_s):
-            for g in list(range(C)) + [C]:
-                comm_s.wait_event(done[g])
-                self._exchange_group(dst, g)
-        main.wait_stream(comm_s)
-
-    def propagate(self, x_local: torch.Tensor, K: int, panels=None):
         """[X, ÂX, …, Â^K X] on this rank's rows: K+1 panels [rows + halo, d] (first `rows` are
         this rank's rows in natural order)."""
         d = x_local.shape[1]
