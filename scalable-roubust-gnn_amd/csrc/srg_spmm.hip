@@ -478,6 +478,7 @@ constexpr int kHubThreads = 64 * (kHubProducers + 1);
 constexpr int kHubLd = kHubW + 16;
 constexpr int kHubTile = kSliceCols * kHubLd;                // floats per tile
 __device__ __forceinline__ int hub_swz(int c) { return (c >> 2) & 7; }
+constexpr int kHubL = 7;   // consumer: (tile, value) LDS read pairs in flight in a full window
 
 // ABL (diagnostic ablations, SRGNN_HUB_ABLATION): 0 = the kernel; 1 = the consumer skips its
 // chains; 2 = the producers skip gathers and LDS writes; 3 = the consumer's fmas read registers
@@ -540,6 +541,44 @@ k_spmm_hub(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
                     }
                 };
                 if (ABL == 1) continue;
+                if ((ABL == 0 || ABL == 2 || ABL == 4) && nb == kHubW) {
+                    // full window, fully unrolled: every LDS read is a per-lane base (the XOR swizzle
+                    // of group k & 7 folded in, hoisted per window) or the value base, plus an
+                    // immediate offset -- no address arithmetic between the fmas.  A ring of kHubL
+                    // (tile, value) read pairs in flight (2 * kHubL <= 15 = lgkmcnt's range).
+                    // Same links, same order: the chain is unchanged.
+                    constexpr int NG = kHubW / 4;
+                    const float* tb[8];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) tb[k] = hub_lds + (h & 1) * kHubTile + c * kHubLd + ((k ^ sw) << 2);
+                    auto rt = [&](int grp) { return *reinterpret_cast<const V4*>(tb[grp & 7] + (grp >> 3) * 32); };
+                    auto ra = [&](int grp) { return *reinterpret_cast<const V4*>(av + (grp << 2)); };
+                    V4 t[kHubL], a[kHubL];
+#pragma unroll
+                    for (int i = 0; i < kHubL; ++i) {
+                        t[i] = rt(i);
+                        a[i] = ra(i);
+                    }
+#pragma unroll
+                    for (int g0 = 0; g0 < NG; g0 += kHubL) {
+#pragma unroll
+                        for (int i = 0; i < kHubL; ++i) {
+                            const int grp = g0 + i;
+                            if (grp < NG) {
+                                acc = __builtin_fmaf(a[i][0], t[i][0], acc);
+                                acc = __builtin_fmaf(a[i][1], t[i][1], acc);
+                                acc = __builtin_fmaf(a[i][2], t[i][2], acc);
+                                acc = __builtin_fmaf(a[i][3], t[i][3], acc);
+                                if (grp + kHubL < NG) {
+                                    t[i] = rt(grp + kHubL);
+                                    a[i] = ra(grp + kHubL);
+                                }
+                                __builtin_amdgcn_sched_barrier(0);
+                            }
+                        }
+                    }
+                    continue;
+                }
                 if (ABL == 5 || ABL == 6)
                     for (int i = 0; i < G; ++i)
                         tA[i] = tB[i] = tC[i] = tD[i] = aA[i] = aB[i] = aC[i] = aD[i] = vzero<float, 4>();
