@@ -150,6 +150,18 @@ int srg_spmm_agg_f32(const int64_t* indptr, const int32_t* indices, const float*
                      const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t d, uint32_t flags,
                      float* agg, int64_t lda, float w, int agg_init, void* stream);
 
+/* srg_spmm_csr_f32 with the halo pack of the multi-GPU exchange fused into its epilogue
+ * (srgnn/dist.py HaloPartitionedOperator; no reference counterpart -- the reference is single
+ * process): every row r it computes is also stored, unchanged, into the send-buffer rows
+ * send_slot[send_ptr[r] .. send_ptr[r+1]) (leading dimension lds), one per peer that needs it.
+ * Y is bitwise the same as srg_spmm_csr_f32's; send rows equal the gathered rows of Y.
+ * send_ptr: int64 [n_rows + 1] over the local rows; send_slot: int32 row ids in `send`. */
+int srg_spmm_send_f32(const int64_t* indptr, const int32_t* indices, const float* values,
+                      int64_t n_rows, const int32_t* row_order, int64_t n_hub, int64_t n_heavy,
+                      const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t d, uint32_t flags,
+                      float* send, int64_t lds, const int64_t* send_ptr, const int32_t* send_slot,
+                      void* stream);
+
 /* The last flat elements (< SRG_TAIL_MAX of them) of a torch dim-0 sum take its scalar row_sum
  * order (4 interleaved partials).  srg_tail_record_f32 stores w * y[flat_start + e] (flat index of
  * the row-major [n_rows, d] panel) into hist[e], one call per term with hist advanced by

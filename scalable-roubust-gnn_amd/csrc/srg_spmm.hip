@@ -258,25 +258,43 @@ constexpr int64_t kMaxLaunchBlocks = int64_t(1) << 23;
 // ------------------------------------------------------------------------------------------------
 constexpr int kSliceCols = 32;
 
-// Fused hop aggregation epilogue (srgnn.aggregate): with agg != nullptr every output element y a
-// kernel stores is also folded into the accumulator panel, agg = (init ? 0 : agg) + w*y, with
-// separate multiply and add -- the same arithmetic as a following srg_hop_accumulate_f32 step,
-// without re-reading Y.
-struct AggEpi {
+// Epilogues of the SpMM kernels (every output element y a kernel stores may also go to):
+//  * fused hop aggregation (srgnn.aggregate): with agg != nullptr it is folded into the accumulator
+//    panel, agg = (init ? 0 : agg) + w*y, with separate multiply and add -- the same arithmetic as a
+//    following srg_hop_accumulate_f32 step, without re-reading Y;
+//  * fused halo pack (srgnn.dist): with send != nullptr row r is also stored into the send-buffer
+//    rows send_slot[send_ptr[r] .. send_ptr[r+1]) (one per peer that needs it), so the exchange
+//    reads a ready buffer instead of gathering the rows again.
+struct Epi {
     float* agg;
     int64_t lda;
     float w;
     int init;
+    float* send;
+    int64_t lds;
+    const int64_t* send_ptr;
+    const int32_t* send_slot;
 };
 
+// SEND is a template parameter and every call site sits under `if constexpr (SEND)`: a runtime
+// branch cost the plain kernels ~20 %, and even an empty inlined call (the reference-bound acc)
+// changed the gather loop's schedule (+10 % per hop on products); guarded, the SEND=false kernels
+// are instruction-for-instruction the plain ones.
+template <int VEC>
+__device__ __forceinline__ void send_row(const Epi& e, int row, int col, const typename Vec<float, VEC>::type& v)
+{
+    const int64_t s0 = e.send_ptr[row], s1 = e.send_ptr[row + 1];
+    for (int64_t s = s0; s < s1; ++s)
+        vstore<float, VEC>(e.send + (int64_t)e.send_slot[s] * e.lds + col, v, false);
+}
 
-template <int UH, bool SFULL, typename IP>
+template <int UH, bool SFULL, typename IP, bool SEND>
 __device__ __forceinline__ void slice_wave(const IP* __restrict__ indptr,
                                            const int32_t* __restrict__ indices,
                                            const float* __restrict__ vals, int row, int slice,
                                            const float* __restrict__ X, int64_t ldx,
                                            float* __restrict__ Y, int64_t ldy, int d, int accumulate,
-                                           int nt, float* __restrict__ lds, const AggEpi& epi)
+                                           int nt, float* __restrict__ lds, const Epi& epi)
 {
     typedef typename Vec<float, 4>::type V4;
     const int lane = threadIdx.x & 63;
@@ -335,6 +353,7 @@ __device__ __forceinline__ void slice_wave(const IP* __restrict__ indptr,
         else
             yrow[ccol] = acc;
         if (epi.agg) epi.agg[(int64_t)row * epi.lda + ccol] = __fadd_rn(aprev, __fmul_rn(epi.w, acc));
+        if constexpr (SEND) send_row<1>(epi, row, ccol, acc);
     }
 }
 
@@ -344,12 +363,12 @@ __device__ __forceinline__ void slice_wave(const IP* __restrict__ indptr,
 // address, one instruction for the whole wave -- then U gathers in flight, then U fma links.
 // Rows come from the degree-sorted schedule, so the R rows of a wave have similar lengths.
 // Still one sequential fma chain per output element, in CSR order.
-template <int S, int U, typename IP>
+template <int S, int U, typename IP, bool SEND>
 __device__ __forceinline__ void narrow_rows(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
                                             const float* __restrict__ vals, const int32_t* __restrict__ order,
                                             int n_rows, int first, const float* __restrict__ X, int64_t ldx,
                                             float* __restrict__ Y, int64_t ldy, int d, int accumulate, int nt,
-                                            const AggEpi& epi)
+                                            const Epi& epi)
 {
     const int lane = threadIdx.x & 63;
     const int g = lane / S, c = lane % S;
@@ -394,15 +413,16 @@ __device__ __forceinline__ void narrow_rows(const IP* __restrict__ indptr, const
         else
             yrow[c] = acc;
         if (epi.agg) epi.agg[(int64_t)row * epi.lda + c] = __fadd_rn(aprev, __fmul_rn(epi.w, acc));
+        if constexpr (SEND) send_row<1>(epi, row, c, acc);
     }
 }
 
-template <int VEC, int U, int UH, bool FULL, bool SFULL, typename IP, int NS = 0>
+template <int VEC, int U, int UH, bool FULL, bool SFULL, typename IP, int NS = 0, bool SEND = false>
 __global__ void __launch_bounds__(kBlock)
 k_spmm(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
        const float* __restrict__ vals, const int32_t* __restrict__ order, int n_rows, int n_heavy,
        int n_slices, int nb_heavy, const float* __restrict__ X, int64_t ldx, float* __restrict__ Y,
-       int64_t ldy, int d, int accumulate, int nt, int block_base, AggEpi epi)
+       int64_t ldy, int d, int accumulate, int nt, int block_base, Epi epi)
 {
     typedef typename Vec<float, VEC>::type V;
     const int bid = block_base + (int)blockIdx.x;
@@ -413,14 +433,14 @@ k_spmm(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
         const int item = __builtin_amdgcn_readfirstlane(bid * kWavesPerBlock + wib);
         if (item >= n_heavy * n_slices) return;
         const int row = order[item / n_slices];
-        slice_wave<UH, SFULL, IP>(indptr, indices, vals, row, item % n_slices, X, ldx, Y, ldy, d,
+        slice_wave<UH, SFULL, IP, SEND>(indptr, indices, vals, row, item % n_slices, X, ldx, Y, ldy, d,
                            accumulate, nt, lds + wib * 2 * 256, epi);
         return;
     }
     if constexpr (NS > 0) {   // narrow panel: 64 / NS light rows per wave
         const int first = __builtin_amdgcn_readfirstlane((bid - nb_heavy) * kWavesPerBlock + wib) * (64 / NS) + n_heavy;
         if (first >= n_rows) return;
-        narrow_rows<NS, U, IP>(indptr, indices, vals, order, n_rows, first, X, ldx, Y, ldy, d, accumulate, nt, epi);
+        narrow_rows<NS, U, IP, SEND>(indptr, indices, vals, order, n_rows, first, X, ldx, Y, ldy, d, accumulate, nt, epi);
         return;
     }
     const int w = __builtin_amdgcn_readfirstlane((bid - nb_heavy) * kWavesPerBlock + wib) + n_heavy;
@@ -444,6 +464,7 @@ k_spmm(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
                 for (int i = 0; i < VEC; ++i) elem(aprev, i) = __fadd_rn(elem(aprev, i), __fmul_rn(epi.w, elem(acc, i)));
                 vstore<float, VEC>(arow + col, aprev, false);
             }
+            if constexpr (SEND) send_row<VEC>(epi, row, col, acc);
         }
     }
 }
@@ -484,12 +505,12 @@ constexpr int kHubL = 7;   // consumer: (tile, value) LDS read pairs in flight i
 // chains; 2 = the producers skip gathers and LDS writes; 3 = the consumer's fmas read registers
 // only (no LDS reads); 4 = producers gather but skip the LDS writes; 5 / 6 = the consumer reads
 // only the tile / only the values from LDS.
-template <bool SFULL, typename IP, int ABL = 0>
+template <bool SFULL, typename IP, int ABL = 0, bool SEND = false>
 __global__ void __launch_bounds__(kHubThreads)
 k_spmm_hub(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
            const float* __restrict__ vals, const int32_t* __restrict__ hub_rows, int n_slices,
            const float* __restrict__ X, int64_t ldx, float* __restrict__ Y, int64_t ldy, int d,
-           int accumulate, int nt, AggEpi epi)
+           int accumulate, int nt, Epi epi)
 {
     typedef typename Vec<float, 4>::type V4;
     extern __shared__ __attribute__((aligned(16))) float hub_lds[];
@@ -631,6 +652,7 @@ k_spmm_hub(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
             else
                 yrow[ccol] = acc;
             if (epi.agg) epi.agg[(int64_t)row * epi.lda + ccol] = __fadd_rn(aprev, __fmul_rn(epi.w, acc));
+            if constexpr (SEND) send_row<1>(epi, row, ccol, acc);
         }
         return;
     }
@@ -978,11 +1000,11 @@ int side_stream(SideStream** out)
     return SRG_OK;
 }
 
-template <typename IP>
+template <typename IP, bool SEND = false>
 int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int64_t n_rows,
                 const int32_t* order, int64_t n_hub, int64_t n_heavy, const float* X, int64_t ldx,
                 float* Y, int64_t ldy, int d, uint32_t flags, hipStream_t s,
-                AggEpi epi = AggEpi{nullptr, 0, 0.0f, 0})
+                Epi epi = Epi{})
 {
     if (n_rows <= 0 || d <= 0) return SRG_OK;
     if (n_hub < 0 || n_heavy < 0 || n_hub + n_heavy > n_rows || ((n_hub + n_heavy) > 0 && !order))
@@ -1010,7 +1032,7 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
         SRG_HIP_CHECK(hipStreamWaitEvent(ss->stream, ss->fork, 0));
         const dim3 hgrid((unsigned)(n_hub * n_slices));
         static const int abl = [] { const char* e = getenv("SRGNN_HUB_ABLATION"); return e ? atoi(e) : 0; }();
-        if (sfull && abl >= 1 && abl <= 6) {
+        if (!SEND && sfull && abl >= 1 && abl <= 6) {
             auto k = abl == 1 ? k_spmm_hub<true, IP, 1> : abl == 2 ? k_spmm_hub<true, IP, 2>
                    : abl == 3 ? k_spmm_hub<true, IP, 3> : abl == 4 ? k_spmm_hub<true, IP, 4>
                    : abl == 5 ? k_spmm_hub<true, IP, 5> : k_spmm_hub<true, IP, 6>;
@@ -1025,11 +1047,11 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
             hipLaunchKernelGGL(k, hgrid, dim3(kHubThreads), kHubLdsBytes, ss->stream, indptr, indices, vals,
                                order, n_slices, X, ldx, Y, ldy, d, acc, nt, epi);
         } else if (sfull)
-            hipLaunchKernelGGL((k_spmm_hub<true, IP>), hgrid, dim3(kHubThreads), kHubLdsBytes,
+            hipLaunchKernelGGL((k_spmm_hub<true, IP, 0, SEND>), hgrid, dim3(kHubThreads), kHubLdsBytes,
                                ss->stream, indptr, indices, vals, order, n_slices, X, ldx, Y, ldy,
                                d, acc, nt, epi);
         else
-            hipLaunchKernelGGL((k_spmm_hub<false, IP>), hgrid, dim3(kHubThreads), kHubLdsBytes,
+            hipLaunchKernelGGL((k_spmm_hub<false, IP, 0, SEND>), hgrid, dim3(kHubThreads), kHubLdsBytes,
                                ss->stream, indptr, indices, vals, order, n_slices, X, ldx, Y, ldy,
                                d, acc, nt, epi);
         SRG_HIP_CHECK(hipGetLastError());
@@ -1050,18 +1072,20 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
     const int64_t rows_per_block = (int64_t)kWavesPerBlock * (ns ? 64 / ns : 1);
     const int64_t blocks = nb_heavy + (n_light + rows_per_block - 1) / rows_per_block;
     if (blocks > INT32_MAX) return fail(SRG_ERR_INVALID, "grid too large");
-    const int vec = pick_vec(d, ldx, ldy, X, Y, sizeof(float));
+    int vec = pick_vec(d, ldx, ldy, X, Y, sizeof(float));
+    if (epi.send) vec = std::min(vec, pick_vec(d, epi.lds, epi.lds, epi.send, epi.send, sizeof(float)));
+    if (epi.agg) vec = std::min(vec, pick_vec(d, epi.lda, epi.lda, epi.agg, epi.agg, sizeof(float)));
     const int nr = (int)m_rows, nh = (int)n_heavy;
     for (int64_t b0 = 0; b0 < blocks; b0 += kMaxLaunchBlocks) {
         const dim3 grid((unsigned)std::min<int64_t>(kMaxLaunchBlocks, blocks - b0));
         const int bb = (int)b0;
 #define SRG_LAUNCH_SPMM(V, F, SF)                                                               \
-    hipLaunchKernelGGL((k_spmm<V, kUnroll, kUnrollHeavy, F, SF, IP>), grid, dim3(kBlock), 0, s,     \
+    hipLaunchKernelGGL((k_spmm<V, kUnroll, kUnrollHeavy, F, SF, IP, 0, SEND>), grid, dim3(kBlock), 0, s,     \
                        indptr, indices, vals, morder, nr, nh, n_slices, nb_heavy, X, ldx, Y, ldy, \
                        d, acc, nt, bb, epi)
         const bool full = d % (64 * vec) == 0;        // implies d % 32 == 0
 #define SRG_LAUNCH_NARROW(NSV, SF)                                                                 \
-    hipLaunchKernelGGL((k_spmm<1, kUnroll, kUnrollHeavy, false, SF, IP, NSV>), grid, dim3(kBlock), 0, s, \
+    hipLaunchKernelGGL((k_spmm<1, kUnroll, kUnrollHeavy, false, SF, IP, NSV, SEND>), grid, dim3(kBlock), 0, s, \
                        indptr, indices, vals, morder, nr, nh, n_slices, nb_heavy, X, ldx, Y, ldy,     \
                        d, acc, nt, bb, epi)
         if (ns == 32) {
@@ -1293,7 +1317,25 @@ int srg_spmm_agg_f32(const int64_t* indptr, const int32_t* indices, const float*
         return fail(SRG_ERR_INVALID, "aggregation panel: agg=%p lda=%lld < d=%d", (void*)agg, (long long)lda, d);
     if (agg && agg == Y) return fail(SRG_ERR_INVALID, "agg must not alias Y");
     rc = launch_spmm<int64_t>(indptr, indices, values, n_rows, row_order, n_hub, n_heavy, X, ldx, Y, ldy, d, flags,
-                              static_cast<hipStream_t>(stream), AggEpi{agg, lda, w, agg_init ? 1 : 0});
+                              static_cast<hipStream_t>(stream), Epi{agg, lda, w, agg_init ? 1 : 0, nullptr, 0, nullptr, nullptr});
+    return rc ? rc : ok();
+}
+
+int srg_spmm_send_f32(const int64_t* indptr, const int32_t* indices, const float* values,
+                      int64_t n_rows, const int32_t* row_order, int64_t n_hub, int64_t n_heavy,
+                      const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t d, uint32_t flags,
+                      float* send, int64_t lds, const int64_t* send_ptr, const int32_t* send_slot,
+                      void* stream)
+{
+    int rc = check_spmm_args(indptr, indices, values, n_rows, X, ldx, Y, ldy, d);
+    if (rc) return rc;
+    if (n_rows > 0 && d > 0 && send && (lds < d || !send_ptr || !send_slot))
+        return fail(SRG_ERR_INVALID, "send buffer: lds=%lld < d=%d or null slot map", (long long)lds, d);
+    rc = send ? launch_spmm<int64_t, true>(indptr, indices, values, n_rows, row_order, n_hub, n_heavy, X, ldx, Y, ldy,
+                                           d, flags, static_cast<hipStream_t>(stream),
+                                           Epi{nullptr, 0, 0.0f, 0, send, lds, send_ptr, send_slot})
+              : launch_spmm<int64_t>(indptr, indices, values, n_rows, row_order, n_hub, n_heavy, X, ldx, Y, ldy, d,
+                                     flags, static_cast<hipStream_t>(stream));
     return rc ? rc : ok();
 }
 

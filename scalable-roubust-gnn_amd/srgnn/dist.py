@@ -247,6 +247,21 @@ class HaloPartitionedOperator:
         for g in range(G):
             parts = [self.send_idx[g][q] for q in range(P) if q != p and self.send_counts[g][q] > 0]
             self.send_cat.append(torch.cat(parts) if parts else torch.zeros(0, dtype=torch.int64, device=dev))
+        # fused pack: all groups' send rows in one buffer [group 0 | group 1 | ...]; every local row
+        # lists the buffer rows it goes to (srg_spmm_send_f32 stores them as it computes the row)
+        self.send_offsets = [0]
+        for g in range(G):
+            self.send_offsets.append(self.send_offsets[-1] + int(self.send_cat[g].numel()))
+        rows_all = torch.cat(self.send_cat) if self.send_offsets[-1] else torch.zeros(0, dtype=torch.int64, device=dev)
+        self._send_slot = torch.argsort(rows_all, stable=True).to(torch.int32).contiguous()
+        self._send_ptr = torch.zeros(self.rows + 1, dtype=torch.int64, device=dev)
+        if rows_all.numel():
+            self._send_ptr[1:] = torch.cumsum(torch.bincount(rows_all, minlength=self.rows), 0)
+        self._send_buf = None
+        # opt-in: measured slower on products (P = 8 chunks 0.84 -> 1.61 ms with the pack fused, vs
+        # 1.08 ms for the chunks plus the separate index_select pack; the per-row slot lookups sit
+        # at the end of every row's chain), profiles/r01_halo_ranks_products_fused_pack_probe.json
+        self.fused_pack = False
         # --- local operator with columns remapped into [own rows | halo]
         g2l = torch.full((n,), -1, dtype=torch.int64, device=dev)
         g2l[r0:r1] = torch.arange(self.rows, device=dev)
@@ -289,6 +304,7 @@ class HaloPartitionedOperator:
         else:
             self._A = [(lip, lix, lvv, order) for (order, _, _, _) in self.views]
             self._spmm = local_spmm
+        self._hip = local_spmm is None and dev.type == "cuda"      # the HIP kernels (fused pack possible)
         self._streams = None
 
     # ------------------------------------------------------------------------------------------
@@ -312,7 +328,15 @@ class HaloPartitionedOperator:
         other._streams = None
         return other
 
-    def _exchange_group(self, panel: torch.Tensor, g: int):
+    def send_buffer(self, d: int) -> torch.Tensor:
+        """The fused-pack send rows of all groups, [sum of send counts, d] (allocated once per d)."""
+        if self._send_buf is None or self._send_buf.shape[1] != d:
+            self._send_buf = torch.empty((self.send_offsets[-1], d), dtype=torch.float32, device=self.device)
+        return self._send_buf
+
+    def _exchange_group(self, panel: torch.Tensor, g: int, packed: torch.Tensor | None = None):
+        """all_to_all of group g's rows: from `packed` (the fused-pack buffer, already filled by
+        this group's kernels) or gathered from the panel's own rows here."""
         P, p = self.world, self.rank
         off = self.rows + self.group_offsets[g]
         out_splits = [self.recv_counts[g][q] for q in range(P)]
@@ -321,8 +345,12 @@ class HaloPartitionedOperator:
         if P == 1 or (total_in == 0 and sum(in_splits) == 0 and not dist.is_initialized()):
             return
         recv = panel[off:off + total_in]
-        send = panel[: self.rows].index_select(0, self.send_cat[g]) if self.send_cat[g].numel() else \
-            panel.new_zeros((0, panel.shape[1]))
+        if packed is not None:
+            send = packed[self.send_offsets[g]:self.send_offsets[g + 1]]
+        elif self.send_cat[g].numel():
+            send = panel[: self.rows].index_select(0, self.send_cat[g])
+        else:
+            send = panel.new_zeros((0, panel.shape[1]))
         if self.virtual:
             raise RuntimeError("virtual shares exchange through simulate_halo_propagate()")
         dist.all_to_all_single(recv, send, out_splits, in_splits, group=self.group)
@@ -331,10 +359,11 @@ class HaloPartitionedOperator:
         for g in range(self.n_groups):
             self._exchange_group(panel, g)
 
-    def _launch_groups(self, src: torch.Tensor, dst: torch.Tensor):
+    def _launch_groups(self, src: torch.Tensor, dst: torch.Tensor, packed: torch.Tensor | None = None):
         """dst[:rows] = local Â rows @ src: the hub group on its own stream (its kernel is a
         latency-bound chain that runs beside the others), the row chunks in order on the current
-        stream.  Returns the per-group completion events (CUDA) or None (CPU ranks)."""
+        stream; with `packed`, the kernels also store every row peers need into it (fused pack).
+        Returns the per-group completion events (CUDA) or None (CPU ranks)."""
         if self.device.type != "cuda":
             for g in range(self.n_groups):
                 if self.views[g][1]:
@@ -345,17 +374,35 @@ class HaloPartitionedOperator:
         hub_s = self._streams[0]
         main = torch.cuda.current_stream(self.device)
         C = self.C
+
+        def run(g):
+            if packed is None:
+                self._spmm(self._A[g], src, dst[: self.rows])
+            else:
+                from .spmm import spmm_send
+                spmm_send(self._A[g], src, dst[: self.rows], packed, self._send_ptr, self._send_slot)
+
         done = [torch.cuda.Event() for _ in range(self.n_groups)]
         hub_s.wait_stream(main)
         if self.views[C][1]:
             with torch.cuda.stream(hub_s):
-                self._spmm(self._A[C], src, dst[: self.rows])
+                run(C)
         done[C].record(hub_s)
         for c in range(C):
             if self.views[c][1]:
-                self._spmm(self._A[c], src, dst[: self.rows])
+                run(c)
             done[c].record(main)
         return done
+
+    def compute_packed(self, src: torch.Tensor, dst: torch.Tensor) -> torch.Tensor:
+        """compute() with the fused pack: returns the send buffer (all groups' rows peers need, in
+        exchange order), ordered on the current stream.  GPU ranks only."""
+        if not self._hip:
+            raise RuntimeError("the fused pack needs the HIP kernels (a CUDA operator without local_spmm)")
+        packed = self.send_buffer(src.shape[1])
+        done = self._launch_groups(src, dst, packed)
+        torch.cuda.current_stream(self.device).wait_event(done[self.C])
+        return packed
 
     def compute(self, src: torch.Tensor, dst: torch.Tensor):
         """dst[:rows] = local Â rows @ src (all groups, no exchange); ordered on the current stream."""
@@ -367,7 +414,10 @@ class HaloPartitionedOperator:
         """One hop: dst own rows from src, then (unless exchange=False, e.g. the last hop, whose halo
         no later hop reads) dst's halo, group by group, each group's all_to_all_single issued on the
         communication stream as soon as its kernel is done (overlapping the later groups)."""
-        done = self._launch_groups(src, dst)
+        packed = None
+        if exchange and self.fused_pack and self.world > 1 and not self.virtual and self._hip:
+            packed = self.send_buffer(src.shape[1])
+        done = self._launch_groups(src, dst, packed)
         if not exchange:
             if done is not None:
                 torch.cuda.current_stream(self.device).wait_event(done[self.C])
@@ -382,8 +432,8 @@ class HaloPartitionedOperator:
         with torch.cuda.stream(comm_s):
             for g in list(range(self.C)) + [self.C]:
                 comm_s.wait_event(done[g])
-                self._exchange_group(dst, g)
-        main.wait_stream(comm_s)
+                self._exchange_group(dst, g, packed)
+        main.wait_stream(comm_s)     # also orders the next hop's writes into `packed` after these sends
 
     def propagate(self, x_local: torch.Tensor, K: int, panels=None):
         """[X, ÂX, …, Â^K X] on this rank's rows: K+1 panels [rows + halo, d] (first `rows` are

@@ -76,6 +76,32 @@ def spmm_agg(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, agg: torch.Tensor
     return out
 
 
+def spmm_send(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, send: torch.Tensor, send_ptr: torch.Tensor,
+              send_slot: torch.Tensor) -> torch.Tensor:
+    """out = A @ X and, fused into the same kernels' epilogue, send[send_slot[send_ptr[r]:send_ptr[r+1]]]
+    = out[r] for every row r of A (srg_spmm_send_f32: the halo pack of srgnn.dist, bitwise the rows
+    of out).  send_ptr is indexed by the row ids A's schedule names (A may be a row-group view)."""
+    _check_panel(X, A.n_cols, "X")
+    d = X.shape[1]
+    _check_panel(out, A.n_rows, "out", d)
+    if not isinstance(send, torch.Tensor) or send.dtype != torch.float32 or send.dim() != 2 or \
+            send.shape[1] != d or send.stride(1) != 1 or send.device != A.device:
+        raise ValueError("send must be a float32 [m, d] row-major tensor on A's device")
+    if send_ptr.dtype != torch.int64 or send_ptr.dim() != 1 or send_ptr.numel() < 1 or send_slot.dtype != torch.int32 \
+            or send_ptr.device != A.device or send_slot.device != A.device:
+        raise ValueError("send_ptr must be int64 [rows + 1] (indexed by A's row ids) and send_slot int32, on A's device")
+    if send_slot.numel() and send.shape[0] == 0:
+        raise ValueError("send slots into an empty send buffer")
+    rc = _lib.lib().srg_spmm_send_f32(A.indptr.data_ptr(), A.indices.data_ptr(), A.values.data_ptr(),
+                                      A.n_rows, A.order.data_ptr() if A.n_rows else None, A.n_hub, A.n_heavy,
+                                      X.data_ptr(), X.stride(0), out.data_ptr(), out.stride(0), d, 0,
+                                      send.data_ptr() if send.numel() else None, max(send.stride(0), d),
+                                      send_ptr.data_ptr(), send_slot.data_ptr() if send_slot.numel() else None,
+                                      _stream(X.device))
+    _lib.check(rc, "srg_spmm_send_f32")
+    return out
+
+
 def propagate(A: DeviceCSR, X: torch.Tensor, K: int, panels: list | None = None,
               nt_store: bool = False) -> list:
     """[X, ÂX, …, Â^K X] as device tensors (panels[0] is X itself, like the reference's list).

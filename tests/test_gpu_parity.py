@@ -297,6 +297,35 @@ def test_halo_virtual_ranks_bitwise(world, chunks):
         assert torch.equal(got[k], want[k]), f"hop {k} differs with {world} virtual halo ranks"
 
 
+@pytest.mark.parametrize("world,chunks,d", [(3, 2, 128), (8, 4, 128), (4, 3, 36), (2, 2, 7), (4, 2, 256)])
+def test_halo_fused_pack_equals_gathered_rows(world, chunks, d):
+    """srg_spmm_send_f32 (the halo pack fused into the SpMM epilogue, every path: row waves incl.
+    narrow panels, slice waves, hub workgroups): the panel is bitwise the plain kernels' and the
+    send buffer is exactly the rows peers need, gathered from it, for every virtual rank."""
+    from srgnn import synth
+    from srgnn.dist import HaloPartitionedOperator
+    from srgnn.normalize import sym_norm_binary
+    n = 20000
+    u, v = synth.rmat_undirected_t(n, 150000, seed=23, device="cuda")
+    ip, ix = synth.symmetric_csr_t(n, u, v)
+    ip, ix, vals = sym_norm_binary(ip, ix, n, 0.5)
+    for q in range(world):
+        op = HaloPartitionedOperator(ip, ix, vals, n, chunks=chunks, hub_threshold=300, device="cuda",
+                                     rank=q, world=world)
+        assert op.views[op.C][1] > 0 or world > 4     # the hub group is exercised
+        src = op.new_panel(d)
+        src.uniform_(-1, 1)
+        want = op.new_panel(d)
+        op.compute(src, want)
+        got = op.new_panel(d)
+        got.fill_(float("nan"))
+        packed = op.compute_packed(src, got)
+        torch.cuda.synchronize()
+        assert torch.equal(got[: op.rows], want[: op.rows])
+        ref = torch.cat([want[: op.rows].index_select(0, op.send_cat[g]) for g in range(op.n_groups)])
+        assert packed.shape == ref.shape and torch.equal(packed, ref), f"rank {q}/{world}"
+
+
 def test_launch_chunking_beyond_2e32_lanes(oracle_mod):
     """More rows than one dispatch can hold (2^25 + rows -> > 2^31 lanes at 64 per row, chunked
     launches with a block base): every row of a banded CSR checked, for the SpMM and Chebyshev."""

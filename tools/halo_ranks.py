@@ -55,7 +55,52 @@ def main():
                 torch.cuda.synchronize()
                 ms = sorted(ev[2 * r].elapsed_time(ev[2 * r + 1]) for r in range(a.reps))
                 times[name] = ms[len(ms) // 2]
-            ranks.append({"rank": q, "rows": op.rows, "nnz": op.nnz_local, "halo_rows": op.halo,
+            # the send-side pack (index_select of the rows peers need, per group) alone, and the
+            # chunks with each group's pack on a second stream as the real hop issues it
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * a.reps)]
+            for r in range(a.reps):
+                ev[2 * r].record()
+                for g in range(op.n_groups):
+                    if op.send_cat[g].numel():
+                        src[: op.rows].index_select(0, op.send_cat[g])
+                ev[2 * r + 1].record()
+            torch.cuda.synchronize()
+            ms = sorted(ev[2 * r].elapsed_time(ev[2 * r + 1]) for r in range(a.reps))
+            times["pack"] = ms[len(ms) // 2]
+            side = torch.cuda.Stream(dev)
+            main = torch.cuda.current_stream(dev)
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * a.reps)]
+            for r in range(a.reps):
+                ev[2 * r].record()
+                for g in range(op.C):
+                    if op.views[g][1]:
+                        op._spmm(op._A[g], src, dst[: op.rows])
+                    e = torch.cuda.Event()
+                    e.record(main)
+                    side.wait_event(e)
+                    if op.send_cat[g].numel():
+                        with torch.cuda.stream(side):
+                            dst[: op.rows].index_select(0, op.send_cat[g])
+                main.wait_stream(side)
+                ev[2 * r + 1].record()
+            torch.cuda.synchronize()
+            ms = sorted(ev[2 * r].elapsed_time(ev[2 * r + 1]) for r in range(a.reps))
+            times["chunks_pack"] = ms[len(ms) // 2]
+            # the fused pack (srg_spmm_send_f32): the chunks' kernels store the send rows themselves
+            from srgnn.spmm import spmm_send
+            packed = op.send_buffer(d)
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * a.reps)]
+            for r in range(a.reps):
+                ev[2 * r].record()
+                for g in range(op.C):
+                    if op.views[g][1]:
+                        spmm_send(op._A[g], src, dst[: op.rows], packed, op._send_ptr, op._send_slot)
+                ev[2 * r + 1].record()
+            torch.cuda.synchronize()
+            ms = sorted(ev[2 * r].elapsed_time(ev[2 * r + 1]) for r in range(a.reps))
+            times["chunks_fused"] = ms[len(ms) // 2]
+            ranks.append({"rank": q, "ms_pack": times["pack"], "ms_chunks_with_pack": times["chunks_pack"],
+                          "ms_chunks_fused_pack": times["chunks_fused"], "rows": op.rows, "nnz": op.nnz_local, "halo_rows": op.halo,
                           "halo_bytes": op.halo * d * 4, "hub_rows": op.views[op.C][1],
                           "ms_all_serial": times["all"], "ms_hub": times["hub"], "ms_chunks": times["chunks"]})
             del op, src, dst
@@ -69,7 +114,8 @@ def main():
         print(f"P={P}: max compute {out['worlds'][P]['max_compute_ms']:.3f} ms "
               f"(rank {worst['rank']}: chunks {worst['ms_chunks']:.3f}, hub {worst['ms_hub']:.3f}), "
               f"mean chunks {out['worlds'][P]['mean_chunks_ms']:.3f} ms, max halo "
-              f"{out['worlds'][P]['max_halo_GB']:.2f} GB", file=sys.stderr, flush=True)
+              f"{out['worlds'][P]['max_halo_GB']:.2f} GB; pack {worst['ms_pack']:.3f} ms alone, chunks+pack "
+              f"{worst['ms_chunks_with_pack']:.3f} ms", file=sys.stderr, flush=True)
     print(json.dumps(out), flush=True)
 
 
