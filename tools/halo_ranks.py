@@ -30,10 +30,13 @@ def main():
     ap.add_argument("--worlds", default="2,4,8")
     ap.add_argument("--chunks", type=int, default=4)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--d", type=int, default=None, help="feature width (default: the config's)")
+    ap.add_argument("--fused", action="store_true", help="also time the opt-in fused pack (srg_spmm_send_f32)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
-    ip, ix, vals, n, d, K = graphs.build(a.config, dev)
+    ip, ix, vals, n, d, K = graphs.build(a.config, dev, d=a.d)
     x = synth.uniform_features_t(n, d, device=dev)
+    print(f"{a.config}: n={n} nnz={int(ix.numel())} d={d} built", file=sys.stderr, flush=True)
     out = {"config": a.config, "n": n, "nnz": int(ix.numel()), "d": d, "worlds": {}}
     for P in [int(w) for w in a.worlds.split(",")]:
         ranks = []
@@ -86,23 +89,28 @@ def main():
             torch.cuda.synchronize()
             ms = sorted(ev[2 * r].elapsed_time(ev[2 * r + 1]) for r in range(a.reps))
             times["chunks_pack"] = ms[len(ms) // 2]
-            # the fused pack (srg_spmm_send_f32): the chunks' kernels store the send rows themselves
-            from srgnn.spmm import spmm_send
-            packed = op.send_buffer(d)
-            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * a.reps)]
-            for r in range(a.reps):
-                ev[2 * r].record()
-                for g in range(op.C):
-                    if op.views[g][1]:
-                        spmm_send(op._A[g], src, dst[: op.rows], packed, op._send_ptr, op._send_slot)
-                ev[2 * r + 1].record()
-            torch.cuda.synchronize()
-            ms = sorted(ev[2 * r].elapsed_time(ev[2 * r + 1]) for r in range(a.reps))
-            times["chunks_fused"] = ms[len(ms) // 2]
-            ranks.append({"rank": q, "ms_pack": times["pack"], "ms_chunks_with_pack": times["chunks_pack"],
-                          "ms_chunks_fused_pack": times["chunks_fused"], "rows": op.rows, "nnz": op.nnz_local, "halo_rows": op.halo,
-                          "halo_bytes": op.halo * d * 4, "hub_rows": op.views[op.C][1],
-                          "ms_all_serial": times["all"], "ms_hub": times["hub"], "ms_chunks": times["chunks"]})
+            rec = {"rank": q, "ms_pack": times["pack"], "ms_chunks_with_pack": times["chunks_pack"],
+                   "rows": op.rows, "nnz": op.nnz_local, "halo_rows": op.halo,
+                   "halo_bytes": op.halo * d * 4, "send_rows": int(sum(t.numel() for t in op.send_cat)),
+                   "hub_rows": op.views[op.C][1],
+                   "ms_all_serial": times["all"], "ms_hub": times["hub"], "ms_chunks": times["chunks"]}
+            if a.fused:
+                # the fused pack (srg_spmm_send_f32): the chunks' kernels store the send rows themselves
+                from srgnn.spmm import spmm_send
+                packed = op.send_buffer(d)
+                ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * a.reps)]
+                for r in range(a.reps):
+                    ev[2 * r].record()
+                    for g in range(op.C):
+                        if op.views[g][1]:
+                            spmm_send(op._A[g], src, dst[: op.rows], packed, op._send_ptr, op._send_slot)
+                    ev[2 * r + 1].record()
+                torch.cuda.synchronize()
+                ms = sorted(ev[2 * r].elapsed_time(ev[2 * r + 1]) for r in range(a.reps))
+                rec["ms_chunks_fused_pack"] = ms[len(ms) // 2]
+            ranks.append(rec)
+            print(f"  P={P} rank {q}: rows={op.rows} halo={op.halo} chunks {times['chunks']:.3f} ms, "
+                  f"hub {times['hub']:.3f} ms", file=sys.stderr, flush=True)
             del op, src, dst
             torch.cuda.empty_cache()
         worst = max(ranks, key=lambda r: max(r["ms_hub"], r["ms_chunks"]))
