@@ -178,6 +178,14 @@ int srg_tail_rowsum_f32(float* agg, int64_t lda, int32_t d, int64_t flat_start, 
  * degrees.  seg_ptr has n_seg + 1 entries; all pointers are device pointers. */
 int srg_segment_sum_f64(const int64_t* seg_ptr, const double* vals, int64_t n_seg, double* out, void* stream);
 
+/* Row gather, the send-side pack of the multi-GPU halo exchange (srgnn/dist.py; no reference
+ * counterpart -- the reference is single process): dst[i, :] = src[idx[i], :] for i < n_idx, a C
+ * host's pack step before its RCCL sends.  src [n_src, d] / dst [n_idx, d] are device panels with
+ * leading dimensions lds / ldd; idx is int64 on the device.  An index outside [0, n_src) leaves its
+ * dst row unwritten (no fault).  Asynchronous on `stream`. */
+int srg_gather_rows_f32(const float* src, int64_t lds, int64_t n_src, const int64_t* idx, int64_t n_idx,
+                        float* dst, int64_t ldd, int32_t d, void* stream);
+
 /* Checks a device CSR: indptr[0] == 0, indptr non-decreasing, indptr[n_rows] == nnz, and every
  * column id in [0, n_cols).  Synchronous on `stream`.  Returns SRG_OK or SRG_ERR_INVALID. */
 int srg_csr_validate(const int64_t* indptr, const int32_t* indices, int64_t n_rows,

@@ -848,6 +848,41 @@ k_hop_accumulate(float* __restrict__ agg, int64_t lda, const float* __restrict__
     }
 }
 
+// Row gather (the send-side pack of the halo exchange, srgnn.dist): dst[i, :] = src[idx[i], :].
+// S lanes per row (the power of two >= the row's VEC-chunks, at most 64), 64 / S rows per wave
+// step and U = 4 steps in flight: 16-byte loads at d = 128 are 2 rows per wave-instruction, 8 rows
+// per wave in flight.  Indices outside [0, n_src) leave their dst row unwritten (never a fault).
+template <int VEC, int S>
+__global__ void __launch_bounds__(256)
+k_gather_rows(const float* __restrict__ src, int64_t lds, int64_t n_src, const int64_t* __restrict__ idx,
+              int64_t n_idx, float* __restrict__ dst, int64_t ldd, int cpr)
+{
+    typedef typename Vec<float, VEC>::type V;
+    constexpr int R = 64 / S, U = 4;
+    const int lane = threadIdx.x & 63;
+    const int g = lane / S, c0 = lane % S;
+    const int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
+    for (int64_t base = wave * (R * U); base < n_idx; base += waves * (R * U)) {
+        int64_t sr[U], dr[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            dr[u] = base + u * R + g;
+            sr[u] = dr[u] < n_idx ? idx[dr[u]] : -1;
+            if (sr[u] >= n_src) sr[u] = -1;
+        }
+        for (int c = c0; c < cpr; c += S) {
+            V v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (sr[u] >= 0) v[u] = vload<float, VEC>(src + sr[u] * lds + (int64_t)c * VEC);
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (sr[u] >= 0) vstore<float, VEC>(dst + dr[u] * ldd + (int64_t)c * VEC, v[u], false);
+        }
+    }
+}
+
 // torch's multi_row_sum (ATen/native/cpu/SumKernel.cpp) for one element over `count` rows of the
 // tail history, rows start, start + stride, ...: 16-row blocks folded into 4 levels.
 __device__ float torch_multi_row_sum(const float* hist, int start, int stride, int count, int e)
@@ -1450,6 +1485,41 @@ int srg_tail_rowsum_f32(float* agg, int64_t lda, int32_t d, int64_t flat_start, 
     if (!agg || (n_terms > 0 && !hist)) return fail(SRG_ERR_INVALID, "null pointer");
     hipLaunchKernelGGL(k_tail_rowsum, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream),
                        agg, lda, d, flat_start, len, hist, n_terms);
+    SRG_HIP_CHECK(hipGetLastError());
+    return ok();
+}
+
+int srg_gather_rows_f32(const float* src, int64_t lds, int64_t n_src, const int64_t* idx, int64_t n_idx,
+                        float* dst, int64_t ldd, int32_t d, void* stream)
+{
+    if (n_idx < 0 || n_src < 0 || d < 0 || (d > 0 && (lds < d || ldd < d)))
+        return fail(SRG_ERR_INVALID, "bad gather shape n_idx=%lld n_src=%lld d=%d lds=%lld ldd=%lld",
+                    (long long)n_idx, (long long)n_src, d, (long long)lds, (long long)ldd);
+    if (n_idx == 0 || d == 0) return ok();
+    if (!src || !idx || !dst) return fail(SRG_ERR_INVALID, "null pointer");
+    const int vec = pick_vec(d, lds, ldd, src, dst, sizeof(float));
+    const int cpr = d / vec;
+    const int S = cpr >= 64 ? 64 : cpr > 16 ? 32 : cpr > 8 ? 16 : cpr > 4 ? 8 : 4;
+    const int64_t rows_per_block = (int64_t)(256 / 64) * (64 / S) * 4;
+    const unsigned blocks = (unsigned)std::min<int64_t>((n_idx + rows_per_block - 1) / rows_per_block, 256 * 64);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+#define SRG_GATHER(V, SS) hipLaunchKernelGGL((k_gather_rows<V, SS>), dim3(blocks), dim3(256), 0, st, src, lds, n_src, \
+                                             idx, n_idx, dst, ldd, cpr)
+#define SRG_GATHER_S(V)                          \
+    if (S == 64) SRG_GATHER(V, 64);              \
+    else if (S == 32) SRG_GATHER(V, 32);         \
+    else if (S == 16) SRG_GATHER(V, 16);         \
+    else if (S == 8) SRG_GATHER(V, 8);           \
+    else SRG_GATHER(V, 4);
+    if (vec == 4) {
+        SRG_GATHER_S(4)
+    } else if (vec == 2) {
+        SRG_GATHER_S(2)
+    } else {
+        SRG_GATHER_S(1)
+    }
+#undef SRG_GATHER_S
+#undef SRG_GATHER
     SRG_HIP_CHECK(hipGetLastError());
     return ok();
 }

@@ -44,6 +44,7 @@ EXPORTED_SYMBOLS = (
     "srg_tail_record_f32",
     "srg_tail_rowsum_f32",
     "srg_segment_sum_f64",
+    "srg_gather_rows_f32",
     "srg_csr_validate",
     "srg_last_error",
     "srg_last_error_code",
@@ -95,6 +96,8 @@ def _declare(lib):
     lib.srg_tail_rowsum_f32.restype = ctypes.c_int
     lib.srg_segment_sum_f64.argtypes = [_p, _p, _i64, _p, _p]
     lib.srg_segment_sum_f64.restype = ctypes.c_int
+    lib.srg_gather_rows_f32.argtypes = [_p, _i64, _i64, _p, _i64, _p, _i64, _i32, _p]
+    lib.srg_gather_rows_f32.restype = ctypes.c_int
     lib.srg_csr_validate.argtypes = [_p, _p, _i64, _i64, _i64, _p]
     lib.srg_csr_validate.restype = ctypes.c_int
     lib.srg_last_error.argtypes = []

@@ -102,6 +102,25 @@ def spmm_send(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, send: torch.Tens
     return out
 
 
+def gather_rows(src: torch.Tensor, idx: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """out[i] = src[idx[i]] (srg_gather_rows_f32; the halo exchange's send-side pack), the same rows
+    as src.index_select(0, idx).  idx: int64 on src's device, every entry in [0, src.shape[0])."""
+    _check_panel(src, 0, "src")
+    d = src.shape[1]
+    if not isinstance(idx, torch.Tensor) or idx.dtype != torch.int64 or idx.dim() != 1 or idx.device != src.device:
+        raise ValueError("idx must be a 1-D int64 tensor on src's device")
+    if not idx.is_contiguous():
+        idx = idx.contiguous()
+    if out is None:
+        out = torch.empty((idx.numel(), d), dtype=torch.float32, device=src.device)
+    _check_panel(out, idx.numel(), "out", d)
+    rc = _lib.lib().srg_gather_rows_f32(src.data_ptr(), max(src.stride(0), d), src.shape[0],
+                                        idx.data_ptr() if idx.numel() else None, idx.numel(),
+                                        out.data_ptr(), max(out.stride(0), d), d, _stream(src.device))
+    _lib.check(rc, "srg_gather_rows_f32")
+    return out
+
+
 def propagate(A: DeviceCSR, X: torch.Tensor, K: int, panels: list | None = None,
               nt_store: bool = False) -> list:
     """[X, ÂX, …, Â^K X] as device tensors (panels[0] is X itself, like the reference's list).

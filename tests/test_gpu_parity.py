@@ -444,3 +444,23 @@ def test_papers100M_scale_sampled_rows_bit_exact(oracle_mod):
     sub_ip = np.r_[0, np.cumsum(cnt.cpu().numpy())]
     want = oracle_mod.spmm(sub_ip, inv.to(torch.int32).cpu().numpy(), vv.cpu().numpy(), x[ucols].cpu().numpy())
     np.testing.assert_array_equal(y[rows].cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("d", [1, 3, 7, 36, 128, 256, 1433])
+def test_gather_rows_equals_index_select(d):
+    """srg_gather_rows_f32 (the halo exchange's send-side pack): the rows of index_select, for every
+    vector width / lanes-per-row variant, strided panels, duplicate indices and an empty list."""
+    from srgnn.spmm import gather_rows
+    g = torch.Generator(device="cuda").manual_seed(d)
+    n = 5003
+    big = torch.rand((n, d + 5), generator=g, device="cuda")
+    for src in (big[:, :d].contiguous(), big[:, :d]):
+        for m in (0, 1, 17, 4099):
+            idx = torch.randint(0, n, (m,), generator=g, device="cuda")
+            got = gather_rows(src, idx)
+            torch.cuda.synchronize()
+            assert torch.equal(got, src.index_select(0, idx)), f"d={d} m={m} ld={src.stride(0)}"
+    out = torch.full((3, d + 2), 7.0, device="cuda")[:, :d]
+    gather_rows(big[:, :d], torch.tensor([2, 0, 2], device="cuda"), out=out)
+    torch.cuda.synchronize()
+    assert torch.equal(out, big[[2, 0, 2], :d])

@@ -22,6 +22,7 @@ import torch  # noqa: E402
 
 from srgnn import graphs, synth  # noqa: E402
 from srgnn.dist import HaloPartitionedOperator  # noqa: E402
+from srgnn.spmm import gather_rows  # noqa: E402
 
 
 def main():
@@ -60,16 +61,17 @@ def main():
                 times[name] = ms[len(ms) // 2]
             # the send-side pack (index_select of the rows peers need, per group) alone, and the
             # chunks with each group's pack on a second stream as the real hop issues it
-            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * a.reps)]
-            for r in range(a.reps):
-                ev[2 * r].record()
-                for g in range(op.n_groups):
-                    if op.send_cat[g].numel():
-                        src[: op.rows].index_select(0, op.send_cat[g])
-                ev[2 * r + 1].record()
-            torch.cuda.synchronize()
-            ms = sorted(ev[2 * r].elapsed_time(ev[2 * r + 1]) for r in range(a.reps))
-            times["pack"] = ms[len(ms) // 2]
+            for name, fn in (("pack_index_select", lambda t, i: t.index_select(0, i)), ("pack", gather_rows)):
+                ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * a.reps)]
+                for r in range(a.reps):
+                    ev[2 * r].record()
+                    for g in range(op.n_groups):
+                        if op.send_cat[g].numel():
+                            fn(src[: op.rows], op.send_cat[g])
+                    ev[2 * r + 1].record()
+                torch.cuda.synchronize()
+                ms = sorted(ev[2 * r].elapsed_time(ev[2 * r + 1]) for r in range(a.reps))
+                times[name] = ms[len(ms) // 2]
             side = torch.cuda.Stream(dev)
             main = torch.cuda.current_stream(dev)
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * a.reps)]
@@ -83,13 +85,13 @@ def main():
                     side.wait_event(e)
                     if op.send_cat[g].numel():
                         with torch.cuda.stream(side):
-                            dst[: op.rows].index_select(0, op.send_cat[g])
+                            gather_rows(dst[: op.rows], op.send_cat[g])
                 main.wait_stream(side)
                 ev[2 * r + 1].record()
             torch.cuda.synchronize()
             ms = sorted(ev[2 * r].elapsed_time(ev[2 * r + 1]) for r in range(a.reps))
             times["chunks_pack"] = ms[len(ms) // 2]
-            rec = {"rank": q, "ms_pack": times["pack"], "ms_chunks_with_pack": times["chunks_pack"],
+            rec = {"rank": q, "ms_pack": times["pack"], "ms_pack_index_select": times["pack_index_select"], "ms_chunks_with_pack": times["chunks_pack"],
                    "rows": op.rows, "nnz": op.nnz_local, "halo_rows": op.halo,
                    "halo_bytes": op.halo * d * 4, "send_rows": int(sum(t.numel() for t in op.send_cat)),
                    "hub_rows": op.views[op.C][1],
@@ -122,7 +124,7 @@ def main():
         print(f"P={P}: max compute {out['worlds'][P]['max_compute_ms']:.3f} ms "
               f"(rank {worst['rank']}: chunks {worst['ms_chunks']:.3f}, hub {worst['ms_hub']:.3f}), "
               f"mean chunks {out['worlds'][P]['mean_chunks_ms']:.3f} ms, max halo "
-              f"{out['worlds'][P]['max_halo_GB']:.2f} GB; pack {worst['ms_pack']:.3f} ms alone, chunks+pack "
+              f"{out['worlds'][P]['max_halo_GB']:.2f} GB; pack {worst['ms_pack']:.3f} ms alone (index_select {worst['ms_pack_index_select']:.3f}), chunks+pack "
               f"{worst['ms_chunks_with_pack']:.3f} ms", file=sys.stderr, flush=True)
     print(json.dumps(out), flush=True)
 
