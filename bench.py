@@ -56,6 +56,9 @@ def parse():
     ap.add_argument("--nt-store", action="store_true")
     ap.add_argument("--exchange", default="halo", choices=["halo", "allgather"])
     ap.add_argument("--chunks", type=int, default=4, help="halo exchange groups per hop")
+    ap.add_argument("--ghost-max-degree", type=int, default=None,
+                    help="halo exchange: compute halo rows of at most this degree locally instead of "
+                         "receiving them (default: the operator's cost model; 0 = off)")
     ap.add_argument("--op", default="khop", choices=["khop", "wavelet"],
                     help="khop: the K-hop propagate (GraphOp.propagate); wavelet: the heat-wavelet "
                          "Chebyshev filter bank (order 3, scales -0.5/+0.5) applied to the feature panel")
@@ -367,8 +370,9 @@ def main():
     else:
         from srgnn.dist import HaloPartitionedOperator
         op = HaloPartitionedOperator(ip, ix, vals, n, chunks=a.chunks, heavy_threshold=a.heavy_threshold,
-                                     device=dev)
-        log(f"rank {rank}: rows={op.rows} nnz={op.nnz_local} halo={op.halo} "
+                                     device=dev, ghost_max_degree=a.ghost_max_degree)
+        log(f"rank {rank}: rows={op.rows} nnz={op.nnz_local} halo={op.halo} (received {op.n_recv}, "
+            f"ghosts {op.n_ghost} <= degree {op.ghost_max_degree}, {op._ghost_pos.numel()} ghost nnz) "
             f"hub_rows={op.views[-1][1]} groups={op.n_groups}")
         panels = [op.new_panel(d) for _ in range(K + 1)]
         panels[0][: op.rows].copy_(X[op.r0:op.r1])
@@ -377,7 +381,8 @@ def main():
 
         def step():
             op.propagate(x_loc, K, panels=panels)
-        local_rows, local_nnz = op.rows, op.nnz_local
+        # one hop's kernels also compute the ghost rows (the roofline counts that work)
+        local_rows, local_nnz = op.rows + op.n_ghost, op.nnz_local + int(op._ghost_pos.numel())
 
     host_copy = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -447,7 +452,8 @@ def main():
         "data": f"synthetic (R-MAT power-law graph with the {a.config} node/edge counts, U[-1,1) features)",
         "config": {"workload": f"{a.config}-shaped K-hop propagate", "n_nodes": n, "nnz_ahat": nnz,
                    "d": d, "K": K, "normalization": "sym r=0.5",
-                   "parallelism": f"row-partition x{world}" + (f" ({a.exchange} exchange)" if world > 1 else ""),
+                   "parallelism": f"row-partition x{world}" + (f" ({a.exchange} exchange)" if world > 1 else "")
+                   + (f", ghost rows <= degree {op.ghost_max_degree}" if world > 1 and a.exchange == "halo" else ""),
                    "mode": "exact (bit-identical to reference)",
                    "outputs": ("all K+1 hop panels" if mode in ("panels", "auto") else
                                f"fused {a.aggregate} of hops 0..K (srgnn.aggregate, bit-exact vs the reference combine)"

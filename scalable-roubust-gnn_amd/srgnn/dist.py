@@ -145,6 +145,71 @@ def _chunk_bounds(indptr_local: torch.Tensor, chunks: int):
     return balanced_row_starts(indptr_local, chunks)
 
 
+# ghost rows: candidates are scanned up to this degree; the automatic cap is chosen among these
+GHOST_SCAN_MAX = 64
+GHOST_CAPS = (0, 1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64)
+# cost model of ghost_plan(): gathered X-row bytes per second of one GPU's SpMM (products, P = 2:
+# 63.1 M nonzeros x 512 B in 3.85 ms) and one peer link's rate per direction (half of the
+# ~153 GB/s xGMI link figure, minus RCCL overhead); a row is 4d bytes on both sides, so d cancels
+GHOST_GATHER_BPS = 8.4e12
+GHOST_LINK_BPS = 64e9
+
+
+def _row_positions(gip: torch.Tensor, rows: torch.Tensor, lens: torch.Tensor) -> torch.Tensor:
+    """Global nonzero ids of `rows` (their CSR ranges, concatenated in the given row order)."""
+    total = int(lens.sum()) if lens.numel() else 0
+    if total == 0:
+        return torch.zeros(0, dtype=torch.int64, device=gip.device)
+    starts = torch.repeat_interleave(gip[rows], lens)
+    first = torch.repeat_interleave(torch.cumsum(lens, 0) - lens, lens)
+    return starts + (torch.arange(total, device=gip.device) - first)
+
+
+def _ghost_candidates(gip, gix, deg, halo, s0: int, s1: int, n: int, max_degree: int) -> torch.Tensor:
+    """Mask over `halo` (rank q's full halo; q owns rows [s0, s1)): rows with at most `max_degree`
+    nonzeros whose every column is one of q's own rows or halo rows -- q can compute them from its
+    own panel, so it need not receive them."""
+    ok = torch.zeros(halo.numel(), dtype=torch.bool, device=halo.device)
+    if max_degree <= 0 or halo.numel() == 0:
+        return ok
+    cand = torch.nonzero(deg[halo] <= max_degree).flatten()
+    if cand.numel() == 0:
+        return ok
+    rows = halo[cand]
+    lens = deg[rows]
+    mark = torch.zeros(n, dtype=torch.bool, device=halo.device)
+    mark[s0:s1] = True
+    mark[halo] = True
+    pos = _row_positions(gip, rows, lens)
+    seg = torch.repeat_interleave(torch.arange(rows.numel(), device=halo.device), lens)
+    bad = torch.zeros(rows.numel(), dtype=torch.int64, device=halo.device)
+    bad.index_add_(0, seg, (~mark[gix[pos].to(torch.int64)]).to(torch.int64))
+    ok[cand[bad == 0]] = True
+    return ok
+
+
+def ghost_plan(halos, elig, deg, owner, gip, starts, caps=GHOST_CAPS):
+    """The ghost degree cap minimising the modelled hop time max over ranks q of
+    max(q's SpMM incl. ghosts, q's busiest peer link), with the rates GHOST_GATHER_BPS /
+    GHOST_LINK_BPS.  Returns (cap, {cap: modelled seconds per byte of row}).  Deterministic
+    from the global plan, so every rank picks the same cap."""
+    P = len(halos)
+    model = {}
+    for c in caps:
+        worst = 0.0
+        for q in range(P):
+            h, e = halos[q], elig[q]
+            dh = deg[h]
+            gmask = e & (dh <= c)
+            nnz_q = int(gip[starts[q + 1]] - gip[starts[q]]) + int(dh[gmask].sum())
+            recv = torch.bincount(owner[h[~gmask]], minlength=P)
+            link = int(recv.max()) if recv.numel() else 0
+            worst = max(worst, nnz_q / GHOST_GATHER_BPS, link / GHOST_LINK_BPS)
+        model[c] = worst
+    best = min(caps, key=lambda c: (model[c], c))
+    return best, model
+
+
 class HaloPartitionedOperator:
     """Rank p's share of Â for the halo-exchange multi-GPU propagation.
 
@@ -155,17 +220,23 @@ class HaloPartitionedOperator:
         exchange order = chunk 0 .. chunk C-1, then hubs (the hub kernel finishes last);
       * every rank q's needs from every source s: the distinct columns of q's rows owned by s,
         by (group on s, source, id) -- so sends and receives are known without negotiation;
-      * local panel layout: [own rows | halo rows ordered by (group, source, id)], and the local
-        operator's column ids remapped into it (each row's entries keep their CSR order, so
-        every output element is the same fma chain as on one GPU).
+      * ghost rows: a halo row whose own neighbours all lie in this rank's rows or halo, with at
+        most `ghost_max_degree` nonzeros, is computed here every hop (the same CSR row, the same
+        fma chain, so the same bits) instead of received -- on a power-law graph most of the halo
+        is such low-degree rows, and a pair of GPUs shares one xGMI link (see ghost_plan());
+      * local panel layout: [own rows | received halo rows by (group, source, id) | ghost rows by
+        (source, id)], and the local operator (own rows and ghost rows) with its column ids
+        remapped into it (each row's entries keep their CSR order, so every output element is the
+        same fma chain as on one GPU).
     Per hop k: the groups' kernels write the own part of panel k+1 (hub group on its own stream),
     and as each group completes its rows that peers need are packed and exchanged with one
-    all_to_all_single (RCCL) on a communication stream, overlapping the next groups' kernels.
+    all_to_all_single (RCCL) on a communication stream, overlapping the next groups' kernels and
+    the ghost rows' kernel.  Only X's first exchange also carries the ghost rows.
     """
 
     def __init__(self, indptr, indices, values, n: int, group=None, chunks: int = 4,
                  heavy_threshold=None, hub_threshold=None, device=None, rank=None, world=None,
-                 local_spmm=None):
+                 local_spmm=None, ghost_max_degree=None):
         from .csr import DEFAULT_HEAVY_THRESHOLD, DEFAULT_HUB_THRESHOLD, auto_hub_threshold
         self.group = group
         self.virtual = rank is not None
@@ -204,49 +275,74 @@ class HaloPartitionedOperator:
         grp[is_hub] = C
         self.n_groups = C + 1
         G = self.n_groups
-        # --- my needs: distinct remote columns of my rows, ordered by (group, source, id)
         r0, r1 = self.starts[p], self.starts[p + 1]
         self.r0, self.r1, self.rows = r0, r1, r1 - r0
         b0, b1 = int(gip[r0]), int(gip[r1])
         self._b0, self._b1 = b0, b1
-        my_cols = gix[b0:b1].to(torch.int64)
         self.nnz_local = b1 - b0
 
         def needs_of(q):
+            """q's full halo (distinct remote columns of its rows), sorted by (group, source, id)."""
             q0, q1 = int(gip[self.starts[q]]), int(gip[self.starts[q + 1]])
             cols = torch.unique(gix[q0:q1].to(torch.int64))
             cols = cols[(cols < self.starts[q]) | (cols >= self.starts[q + 1])]
             key = (grp[cols] * P + owner[cols]) * n + cols          # sort by (group, source, id)
             return cols[torch.argsort(key)]
 
-        need = needs_of(p)
+        # --- every rank's halo and its ghost candidates (identical on all ranks: sends follow)
+        halos, elig = [], []
+        for q in range(P):
+            hq = needs_of(q)
+            halos.append(hq)
+            elig.append(_ghost_candidates(gip, gix, deg, hq, self.starts[q], self.starts[q + 1], n,
+                                          GHOST_SCAN_MAX if ghost_max_degree is None else ghost_max_degree))
+        if ghost_max_degree is None:
+            ghost_max_degree = ghost_plan(halos, elig, deg, owner, gip, self.starts)[0]
+        self.ghost_max_degree = int(ghost_max_degree)
+        ghosts = [e & (deg[h] <= self.ghost_max_degree) for h, e in zip(halos, elig)]
+        need = halos[p][~ghosts[p]]                                  # received: (group, source, id)
+        gh = halos[p][ghosts[p]]
+        gh = gh[torch.argsort(owner[gh] * n + gh)]                   # ghosts: (source, id)
         ng, ns = grp[need], owner[need]
         counts = torch.zeros((G, P), dtype=torch.int64, device=dev)
         counts.index_put_((ng, ns), torch.ones_like(need), accumulate=True)
         self.recv_counts = counts.cpu().tolist()                 # [group][source]
-        self.halo = int(need.numel())
+        self.ghost_recv_counts = torch.bincount(owner[gh], minlength=P).cpu().tolist()
+        self.n_recv = int(need.numel())
+        self.n_ghost = int(gh.numel())
+        self.halo = self.n_recv + self.n_ghost
         self.group_offsets = []                                  # start of each group's halo region
         off = 0
         for g in range(G):
             self.group_offsets.append(off)
             off += sum(self.recv_counts[g])
-        # --- my sends: for every peer q, my rows q needs, per group, in q's receive order
+        # --- my sends: for every peer q, my rows q receives, per group, in q's receive order, and
+        # (first exchange only) my rows q computes as ghosts, by id
         self.send_idx = [[None] * P for _ in range(G)]
         self.send_counts = [[0] * P for _ in range(G)]
+        self.ghost_send_idx = [None] * P
+        self.ghost_send_counts = [0] * P
         for q in range(P):
             if q == p:
                 continue
-            nq = needs_of(q)
-            mine = nq[owner[nq] == p]                             # already sorted by (group, id)
+            hq = halos[q]
+            from_me = owner[hq] == p
+            mine = hq[from_me & ~ghosts[q]]                      # already sorted by (group, id)
             gm = grp[mine]
             for g in range(G):
                 sel = mine[gm == g] - r0
                 self.send_idx[g][q] = sel
                 self.send_counts[g][q] = int(sel.numel())
+            gq = torch.sort(hq[from_me & ghosts[q]]).values - r0
+            self.ghost_send_idx[q] = gq
+            self.ghost_send_counts[q] = int(gq.numel())
+        del halos, elig, ghosts
         self.send_cat = []
         for g in range(G):
             parts = [self.send_idx[g][q] for q in range(P) if q != p and self.send_counts[g][q] > 0]
             self.send_cat.append(torch.cat(parts) if parts else torch.zeros(0, dtype=torch.int64, device=dev))
+        parts = [self.ghost_send_idx[q] for q in range(P) if q != p and self.ghost_send_counts[q] > 0]
+        self.ghost_send_cat = torch.cat(parts) if parts else torch.zeros(0, dtype=torch.int64, device=dev)
         # fused pack: all groups' send rows in one buffer [group 0 | group 1 | ...]; every local row
         # lists the buffer rows it goes to (srg_spmm_send_f32 stores them as it computes the row)
         self.send_offsets = [0]
@@ -262,16 +358,22 @@ class HaloPartitionedOperator:
         # 1.08 ms for the chunks plus the separate index_select pack; the per-row slot lookups sit
         # at the end of every row's chain), profiles/r01_halo_ranks_products_fused_pack_probe.json
         self.fused_pack = False
-        # --- local operator with columns remapped into [own rows | halo]
+        # --- local operator over the panel rows [own | received (empty rows) | ghosts], columns
+        # remapped into the same layout
         g2l = torch.full((n,), -1, dtype=torch.int64, device=dev)
         g2l[r0:r1] = torch.arange(self.rows, device=dev)
-        g2l[need] = self.rows + torch.arange(self.halo, device=dev)
-        lix = g2l[my_cols]
+        g2l[need] = self.rows + torch.arange(self.n_recv, device=dev)
+        g2l[gh] = self.rows + self.n_recv + torch.arange(self.n_ghost, device=dev)
+        gdeg = deg[gh]
+        self._ghost_pos = _row_positions(gip, gh, gdeg)              # global nnz ids of the ghost rows
+        lix = g2l[torch.cat([gix[b0:b1].to(torch.int64), gix[self._ghost_pos].to(torch.int64)])]
         if bool((lix < 0).any()):
             raise RuntimeError("halo layout misses a referenced column")
-        lip = (gip[r0:r1 + 1] - b0).contiguous()
+        lens = torch.cat([deg[r0:r1], torch.zeros(self.n_recv, dtype=torch.int64, device=dev), gdeg])
+        lip = torch.zeros(self.rows + self.halo + 1, dtype=torch.int64, device=dev)
+        torch.cumsum(lens, 0, out=lip[1:])
         lix = lix.to(torch.int32).contiguous()
-        lvv = values[b0:b1].to(dev).contiguous()
+        lvv = self._local_values(values)
         self.ncols_local = self.rows + self.halo
         # --- per-group row schedules (local row ids; long rows first)
         lgrp = grp[r0:r1]
@@ -288,21 +390,26 @@ class HaloPartitionedOperator:
                 n_hub = 0
                 n_heavy = int((ldeg[rows_g] > heavy_t).sum()) if heavy_t >= 0 else 0
             self.views.append((rows_g.to(torch.int32).contiguous(), n_g, n_heavy, n_hub))
+        # the ghost rows: one more launch (no exchange), panel rows rows + n_recv + i
+        gsort = torch.sort(gdeg, descending=True, stable=True)
+        g_rows = (self.rows + self.n_recv + gsort.indices).to(torch.int32).contiguous()
+        g_heavy = int((gsort.values > heavy_t).sum()) if heavy_t >= 0 else 0
+        self.ghost_view = (g_rows, self.n_ghost, g_heavy, 0)
         self._lip, self._lix, self._lvv = lip, lix, lvv
         if local_spmm is None:
             from .csr import DeviceCSR
             from .spmm import spmm
             if dev.type == "cuda":
                 from . import _lib
-                _lib.check(_lib.lib().srg_csr_validate(lip.data_ptr(), lix.data_ptr(), self.rows,
+                _lib.check(_lib.lib().srg_csr_validate(lip.data_ptr(), lix.data_ptr(), self.rows + self.halo,
                                                        lix.numel(), self.ncols_local,
                                                        torch.cuda.current_stream(dev).cuda_stream),
                            "srg_csr_validate")
             self._A = [DeviceCSR(lip, lix, lvv, n_g, self.ncols_local, order, n_heavy, n_hub)
-                       for (order, n_g, n_heavy, n_hub) in self.views]
+                       for (order, n_g, n_heavy, n_hub) in self.views + [self.ghost_view]]
             self._spmm = lambda A, X, out: spmm(A, X, out=out)
         else:
-            self._A = [(lip, lix, lvv, order) for (order, _, _, _) in self.views]
+            self._A = [(lip, lix, lvv, order) for (order, _, _, _) in self.views + [self.ghost_view]]
             self._spmm = local_spmm
         self._hip = local_spmm is None and dev.type == "cuda"      # the HIP kernels (fused pack possible)
         self._streams = None
@@ -317,7 +424,7 @@ class HaloPartitionedOperator:
         other values (e.g. the Chebyshev F = (2/a1)(L - a2 I) next to L); `values` is global."""
         import copy
         other = copy.copy(self)
-        lvv = values[self._b0:self._b1].to(self.device).contiguous()
+        lvv = self._local_values(values)
         other._lvv = lvv
         if isinstance(self._A[0], tuple):
             other._A = [(a[0], a[1], lvv, a[3]) for a in self._A]
@@ -327,6 +434,13 @@ class HaloPartitionedOperator:
                         for a in self._A]
         other._streams = None
         return other
+
+    def _local_values(self, values: torch.Tensor) -> torch.Tensor:
+        """The local operator's values: the own rows' slice, then the ghost rows' entries."""
+        own = values[self._b0:self._b1].to(self.device)
+        if self.n_ghost:
+            own = torch.cat([own, values[self._ghost_pos.to(values.device)].to(self.device)])
+        return own.contiguous()
 
     def send_buffer(self, d: int) -> torch.Tensor:
         """The fused-pack send rows of all groups, [sum of send counts, d] (allocated once per d)."""
@@ -359,19 +473,48 @@ class HaloPartitionedOperator:
             raise RuntimeError("virtual shares exchange through simulate_halo_propagate()")
         dist.all_to_all_single(recv, send, out_splits, in_splits, group=self.group)
 
-    def exchange(self, panel: torch.Tensor):
+    def _exchange_ghosts(self, panel: torch.Tensor):
+        """all_to_all of the ghost rows (X's first exchange only: later hops compute them)."""
+        P = self.world
+        if P == 1 or self.ghost_max_degree == 0:       # the cap is global: every rank skips alike
+            return
+        off = self.rows + self.n_recv
+        recv = panel[off:off + self.n_ghost]
+        if self.ghost_send_cat.numel():
+            if self._hip:
+                from .spmm import gather_rows
+                send = gather_rows(panel[: self.rows], self.ghost_send_cat)
+            else:
+                send = panel[: self.rows].index_select(0, self.ghost_send_cat)
+        else:
+            send = panel.new_zeros((0, panel.shape[1]))
+        if self.virtual:
+            raise RuntimeError("virtual shares exchange through simulate_halo_propagate()")
+        dist.all_to_all_single(recv, send, list(self.ghost_recv_counts), list(self.ghost_send_counts),
+                               group=self.group)
+
+    def exchange(self, panel: torch.Tensor, ghosts: bool = False):
+        """The whole halo of `panel` from its owners: the received rows, group by group, and with
+        ghosts=True (the first panel, X) the ghost rows too."""
         for g in range(self.n_groups):
             self._exchange_group(panel, g)
+        if ghosts:
+            self._exchange_ghosts(panel)
 
-    def _launch_groups(self, src: torch.Tensor, dst: torch.Tensor, packed: torch.Tensor | None = None):
+    def _launch_groups(self, src: torch.Tensor, dst: torch.Tensor, packed: torch.Tensor | None = None,
+                       ghosts: bool = True):
         """dst[:rows] = local Â rows @ src: the hub group on its own stream (its kernel is a
         latency-bound chain that runs beside the others), the row chunks in order on the current
-        stream; with `packed`, the kernels also store every row peers need into it (fused pack).
+        stream, then (ghosts=True) the ghost rows into their halo slots of dst; with `packed`, the
+        kernels also store every row peers need into it (fused pack).
         Returns the per-group completion events (CUDA) or None (CPU ranks)."""
+        gA = self._A[self.n_groups]
         if self.device.type != "cuda":
             for g in range(self.n_groups):
                 if self.views[g][1]:
                     self._spmm(self._A[g], src, dst[: self.rows])
+            if ghosts and self.n_ghost:
+                self._spmm(gA, src, dst)
             return None
         if self._streams is None:
             self._streams = (torch.cuda.Stream(self.device), torch.cuda.Stream(self.device))
@@ -396,6 +539,8 @@ class HaloPartitionedOperator:
             if self.views[c][1]:
                 run(c)
             done[c].record(main)
+        if ghosts and self.n_ghost:      # after the chunks: their exchanges start first
+            self._spmm(gA, src, dst)
         return done
 
     def compute_packed(self, src: torch.Tensor, dst: torch.Tensor) -> torch.Tensor:
@@ -408,9 +553,10 @@ class HaloPartitionedOperator:
         torch.cuda.current_stream(self.device).wait_event(done[self.C])
         return packed
 
-    def compute(self, src: torch.Tensor, dst: torch.Tensor):
-        """dst[:rows] = local Â rows @ src (all groups, no exchange); ordered on the current stream."""
-        done = self._launch_groups(src, dst)
+    def compute(self, src: torch.Tensor, dst: torch.Tensor, ghosts: bool = True):
+        """dst[:rows] = local Â rows @ src (all groups, no exchange) and, with ghosts, the ghost
+        rows of dst's halo; ordered on the current stream."""
+        done = self._launch_groups(src, dst, ghosts=ghosts)
         if done is not None:
             torch.cuda.current_stream(self.device).wait_event(done[self.C])
 
@@ -421,7 +567,7 @@ class HaloPartitionedOperator:
         packed = None
         if exchange and self.fused_pack and self.world > 1 and not self.virtual and self._hip:
             packed = self.send_buffer(src.shape[1])
-        done = self._launch_groups(src, dst, packed)
+        done = self._launch_groups(src, dst, packed, ghosts=exchange)   # no later hop reads the last ghosts
         if not exchange:
             if done is not None:
                 torch.cuda.current_stream(self.device).wait_event(done[self.C])
@@ -448,13 +594,13 @@ class HaloPartitionedOperator:
         if x_local.data_ptr() != panels[0].data_ptr():
             panels[0][: self.rows].copy_(x_local[: self.rows])
         if K > 0:
-            self.exchange(panels[0])
+            self.exchange(panels[0], ghosts=True)
         for k in range(1, K + 1):
             self.hop(panels[k - 1], panels[k], exchange=k < K)    # the last hop's halo is never read
         return panels
 
 
-def _virtual_exchange(shares, panels):
+def _virtual_exchange(shares, panels, ghosts: bool = False):
     """all_to_all of P virtual shares emulated by copies: panels[q] is share q's [rows + halo, d]."""
     for g in range(shares[0].n_groups):
         for q, sq in enumerate(shares):             # receiver
@@ -465,20 +611,32 @@ def _virtual_exchange(shares, panels):
                     idx = ss.send_idx[g][q]
                     panels[q][off:off + cnt].copy_(panels[s][: ss.rows].index_select(0, idx))
                 off += cnt
+    if ghosts:
+        for q, sq in enumerate(shares):
+            off = sq.rows + sq.n_recv
+            for s, ss in enumerate(shares):
+                cnt = sq.ghost_recv_counts[s]
+                if cnt:
+                    panels[q][off:off + cnt].copy_(panels[s][: ss.rows].index_select(0, ss.ghost_send_idx[q]))
+                off += cnt
 
 
 def simulate_halo_propagate(indptr, indices, values, n: int, x: torch.Tensor, K: int, world: int,
-                            chunks: int = 3, heavy_threshold=None, hub_threshold=None, device=None):
+                            chunks: int = 3, heavy_threshold=None, hub_threshold=None, device=None,
+                            ghost_max_degree=None, shares=None):
     """P virtual halo-exchange ranks in ONE process (all_to_all emulated by copies); returns the
-    K+1 full [n, d] panels.  Exercises the group split, halo layout and column remap on a device."""
-    shares = [HaloPartitionedOperator(indptr, indices, values, n, chunks=chunks, heavy_threshold=heavy_threshold,
-                                      hub_threshold=hub_threshold, device=device, rank=q, world=world)
-              for q in range(world)]
+    K+1 full [n, d] panels.  Exercises the group split, ghost rows, halo layout and column remap
+    on a device."""
+    if shares is None:
+        shares = [HaloPartitionedOperator(indptr, indices, values, n, chunks=chunks, heavy_threshold=heavy_threshold,
+                                          hub_threshold=hub_threshold, device=device, rank=q, world=world,
+                                          ghost_max_degree=ghost_max_degree)
+                  for q in range(world)]
     d = x.shape[1]
     panels = [[s.new_panel(d) for _ in range(K + 1)] for s in shares]
     for s, pp in zip(shares, panels):
         pp[0][: s.rows].copy_(x[s.r0:s.r1])
-    _virtual_exchange(shares, [pp[0] for pp in panels])
+    _virtual_exchange(shares, [pp[0] for pp in panels], ghosts=True)
     for k in range(1, K + 1):
         for s, pp in zip(shares, panels):
             s.compute(pp[k - 1], pp[k])
@@ -530,7 +688,8 @@ class HaloWaveletFilter:
         del diag
         self.opL = HaloPartitionedOperator(ip, indices, lvals.to(dev, torch.float32), n, group=group, chunks=chunks,
                                            heavy_threshold=heavy_threshold, hub_threshold=hub_threshold,
-                                           device=dev, rank=rank, world=world, local_spmm=local_spmm)
+                                           device=dev, rank=rank, world=world, local_spmm=local_spmm,
+                                           ghost_max_degree=0)   # the epilogue runs on own rows only
         self.opF = self.opL.with_values(fvals)
         self.taus = [float(t) for t in taus]
         self.coeffs = np.stack([heat_cheby_coeffs(t, self.lmax, order) for t in self.taus])

@@ -82,7 +82,7 @@ def test_balanced_row_starts_and_remap():
     assert bool((m[1:] > m[:-1]).all())          # monotone: CSR order (and fma chains) preserved
 
 
-def _halo_worker(rank, world, port, out_path, chunks):
+def _halo_worker(rank, world, port, out_path, chunks, ghost=None):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     repo = os.path.dirname(here)
@@ -100,8 +100,9 @@ def _halo_worker(rank, world, port, out_path, chunks):
 
     ip, ix, vals, x, n = _graph()
     op = HaloPartitionedOperator(ip, ix, vals, n, chunks=chunks, hub_threshold=60, local_spmm=local_spmm,
-                                 device="cpu")
+                                 device="cpu", ghost_max_degree=ghost)
     assert op.views[-1][1] > 0 or world > 2          # some hub rows exist at this threshold
+    assert ghost is None or (op.n_ghost > 0) == (ghost > 0)
     panels = op.propagate(x[op.r0:op.r1], 3)
     rows = torch.tensor([op.rows])
     all_rows = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
@@ -118,11 +119,12 @@ def _halo_worker(rank, world, port, out_path, chunks):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,chunks", [(2, 3), (3, 2)])
-def test_halo_exchange_bitwise_equals_single(tmp_path, oracle_mod, world, chunks):
-    """Halo exchange (only referenced remote rows, grouped all_to_all_single) over gloo ranks."""
+@pytest.mark.parametrize("world,chunks,ghost", [(2, 3, None), (3, 2, None), (2, 2, 0), (3, 3, 16)])
+def test_halo_exchange_bitwise_equals_single(tmp_path, oracle_mod, world, chunks, ghost):
+    """Halo exchange (only referenced remote rows, grouped all_to_all_single; ghost rows computed
+    locally, exchanged once with X) over gloo ranks."""
     out = str(tmp_path / "halo.npy")
-    mp.spawn(_halo_worker, args=(world, _free_port(), out, chunks), nprocs=world, join=True)
+    mp.spawn(_halo_worker, args=(world, _free_port(), out, chunks, ghost), nprocs=world, join=True)
     ip, ix, vals, x, n = _graph()
     want = oracle_mod.propagate(ip.numpy(), ix.numpy(), vals.numpy(), x.numpy(), 3)[3]
     np.testing.assert_array_equal(np.load(out), want)
@@ -144,13 +146,65 @@ def test_halo_layout_virtual_ranks(oracle_mod):
                                           local_spmm=local_spmm) for q in range(world)]
         for s in shares:
             assert s.halo <= n - s.rows
-            assert sum(map(sum, s.recv_counts)) == s.halo
+            assert sum(map(sum, s.recv_counts)) == s.n_recv
+            assert sum(s.ghost_recv_counts) == s.n_ghost and s.n_recv + s.n_ghost == s.halo
         # every send list matches the receiver's count
         for g in range(shares[0].n_groups):
             for q, sq in enumerate(shares):
                 for src, ss in enumerate(shares):
                     if src != q:
                         assert ss.send_counts[g][q] == sq.recv_counts[g][src]
+        for q, sq in enumerate(shares):
+            for src, ss in enumerate(shares):
+                if src != q:
+                    assert ss.ghost_send_counts[q] == sq.ghost_recv_counts[src]
+
+
+@pytest.mark.parametrize("world,cap", [(2, 0), (2, 8), (3, 64), (4, 3)])
+def test_halo_ghost_rows_virtual_ranks_bitwise(oracle_mod, world, cap):
+    """Ghost rows (low-degree halo rows computed locally instead of received) with the oracle as
+    the local product: K hops over P virtual ranks are bitwise the single-rank propagation, and
+    the ghosts really replace received rows."""
+    from srgnn.dist import HaloPartitionedOperator, simulate_halo_propagate
+    ip, ix, vals, x, n = _graph()
+
+    def local_spmm(A, X, out):
+        lip, lix, lvv, order = A
+        full = torch.from_numpy(oracle_mod.spmm(lip.numpy(), lix.numpy(), lvv.numpy(), X.numpy()))
+        o = order.long()
+        out[o] = full[o]
+
+    shares = [HaloPartitionedOperator(ip, ix, vals, n, chunks=2, hub_threshold=60, device="cpu", rank=q,
+                                      world=world, local_spmm=local_spmm, ghost_max_degree=cap)
+              for q in range(world)]
+    full_halo = [HaloPartitionedOperator(ip, ix, vals, n, chunks=2, device="cpu", rank=q, world=world,
+                                         local_spmm=local_spmm, ghost_max_degree=0).halo for q in range(world)]
+    for s, h in zip(shares, full_halo):
+        assert s.halo == h and s.ghost_max_degree == cap
+        assert (s.n_ghost > 0) == (cap > 0)
+    got = simulate_halo_propagate(ip, ix, vals, n, x, 4, world, shares=shares)
+    want = oracle_mod.propagate(ip.numpy(), ix.numpy(), vals.numpy(), x.numpy(), 4)
+    for k in range(5):
+        np.testing.assert_array_equal(got[k].numpy(), want[k])
+
+
+def test_ghost_plan_cost_model():
+    """The automatic cap: no ghosts when the links are (modelled as) free, ghosts when they are
+    slow; every cap is one of the candidates, and all ranks agree."""
+    import srgnn.dist as D
+    ip, ix, vals, x, n = _graph()
+    saved = D.GHOST_LINK_BPS
+    try:
+        D.GHOST_LINK_BPS = 1e30
+        caps = {D.HaloPartitionedOperator(ip, ix, vals, n, chunks=2, device="cpu", rank=q, world=2,
+                                          local_spmm=lambda *a: None).ghost_max_degree for q in range(2)}
+        assert caps == {0}
+        D.GHOST_LINK_BPS = 1e3
+        caps = {D.HaloPartitionedOperator(ip, ix, vals, n, chunks=2, device="cpu", rank=q, world=2,
+                                          local_spmm=lambda *a: None).ghost_max_degree for q in range(2)}
+        assert len(caps) == 1 and caps.pop() in D.GHOST_CAPS[1:]
+    finally:
+        D.GHOST_LINK_BPS = saved
 
 
 def _cpu_epilogue(Tn, Tc, To, mode, a1, a2, coef_prev, coef, R):

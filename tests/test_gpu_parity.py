@@ -276,10 +276,11 @@ def test_products_scale_sampled_rows_bit_exact(oracle_mod):
     assert bool((y[:, 1:] == y[:, :1]).all())
 
 
-@pytest.mark.parametrize("world,chunks", [(2, 3), (8, 4)])
-def test_halo_virtual_ranks_bitwise(world, chunks):
-    """The halo-exchange multi-GPU layout (groups, remapped columns, hub group) on one device with
-    the real kernels: bitwise equal to the single-device propagation."""
+@pytest.mark.parametrize("world,chunks,ghost", [(2, 3, None), (8, 4, None), (2, 3, 0), (4, 2, 64), (8, 3, 8)])
+def test_halo_virtual_ranks_bitwise(world, chunks, ghost):
+    """The halo-exchange multi-GPU layout (groups, remapped columns, hub group, ghost rows
+    computed into the halo) on one device with the real kernels: bitwise equal to the
+    single-device propagation."""
     from srgnn import synth
     from srgnn.csr import DeviceCSR
     from srgnn.dist import simulate_halo_propagate
@@ -292,7 +293,7 @@ def test_halo_virtual_ranks_bitwise(world, chunks):
     x = synth.uniform_features_t(n, 128, device="cuda")
     want = propagate(DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, device="cuda"), x, 3)
     got = simulate_halo_propagate(ip, ix, vals, n, x, 3, world, chunks=chunks, hub_threshold=300,
-                                  device="cuda")
+                                  device="cuda", ghost_max_degree=ghost)
     for k in range(1, 4):
         assert torch.equal(got[k], want[k]), f"hop {k} differs with {world} virtual halo ranks"
 

@@ -33,27 +33,36 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--d", type=int, default=None, help="feature width (default: the config's)")
     ap.add_argument("--fused", action="store_true", help="also time the opt-in fused pack (srg_spmm_send_f32)")
+    ap.add_argument("--ghost", default="auto",
+                    help="ghost row degree cap(s): 'auto' (the operator's cost model) or a comma list")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     ip, ix, vals, n, d, K = graphs.build(a.config, dev, d=a.d)
     x = synth.uniform_features_t(n, d, device=dev)
     print(f"{a.config}: n={n} nnz={int(ix.numel())} d={d} built", file=sys.stderr, flush=True)
     out = {"config": a.config, "n": n, "nnz": int(ix.numel()), "d": d, "worlds": {}}
-    for P in [int(w) for w in a.worlds.split(",")]:
+    ghosts = [None] if a.ghost == "auto" else [int(c) for c in a.ghost.split(",")]
+    for P, ghost in [(int(w), gc) for w in a.worlds.split(",") for gc in ghosts]:
         ranks = []
         for q in range(P):
-            op = HaloPartitionedOperator(ip, ix, vals, n, chunks=a.chunks, device=dev, rank=q, world=P)
+            op = HaloPartitionedOperator(ip, ix, vals, n, chunks=a.chunks, device=dev, rank=q, world=P,
+                                         ghost_max_degree=ghost)
             src = op.new_panel(d)
             src[: op.rows].copy_(x[op.r0:op.r1])
             src[op.rows:].uniform_(-1, 1)
             dst = op.new_panel(d)
             times = {}
-            for name, groups in (("all", range(op.n_groups)), ("hub", [op.C]), ("chunks", range(op.C))):
+            G = op.n_groups            # op._A[G] is the ghost rows' launch (into dst's halo)
+            for name, groups in (("all", range(G + 1)), ("hub", [op.C]), ("chunks", list(range(op.C)) + [G]),
+                                 ("ghosts", [G])):
                 ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * a.reps)]
                 for r in range(a.reps):
                     ev[2 * r].record()
                     for g in groups:
-                        if op.views[g][1]:
+                        if g == G:
+                            if op.n_ghost:
+                                op._spmm(op._A[G], src, dst)
+                        elif op.views[g][1]:
                             op._spmm(op._A[g], src, dst[: op.rows])
                     ev[2 * r + 1].record()
                 torch.cuda.synchronize()
@@ -80,6 +89,8 @@ def main():
                 for g in range(op.C):
                     if op.views[g][1]:
                         op._spmm(op._A[g], src, dst[: op.rows])
+                    if g == op.C - 1 and op.n_ghost:
+                        op._spmm(op._A[G], src, dst)
                     e = torch.cuda.Event()
                     e.record(main)
                     side.wait_event(e)
@@ -92,8 +103,11 @@ def main():
             ms = sorted(ev[2 * r].elapsed_time(ev[2 * r + 1]) for r in range(a.reps))
             times["chunks_pack"] = ms[len(ms) // 2]
             rec = {"rank": q, "ms_pack": times["pack"], "ms_pack_index_select": times["pack_index_select"], "ms_chunks_with_pack": times["chunks_pack"],
-                   "rows": op.rows, "nnz": op.nnz_local, "halo_rows": op.halo,
-                   "halo_bytes": op.halo * d * 4, "send_rows": int(sum(t.numel() for t in op.send_cat)),
+                   "rows": op.rows, "nnz": op.nnz_local, "halo_rows": op.halo, "recv_rows": op.n_recv,
+                   "ghost_rows": op.n_ghost, "ghost_nnz": int(op._ghost_pos.numel()),
+                   "ghost_max_degree": op.ghost_max_degree, "ms_ghosts": times["ghosts"],
+                   "max_link_rows": max(sum(op.recv_counts[g][s] for g in range(G)) for s in range(P)),
+                   "halo_bytes": op.n_recv * d * 4, "send_rows": int(sum(t.numel() for t in op.send_cat)),
                    "hub_rows": op.views[op.C][1],
                    "ms_all_serial": times["all"], "ms_hub": times["hub"], "ms_chunks": times["chunks"]}
             if a.fused:
@@ -111,20 +125,22 @@ def main():
                 ms = sorted(ev[2 * r].elapsed_time(ev[2 * r + 1]) for r in range(a.reps))
                 rec["ms_chunks_fused_pack"] = ms[len(ms) // 2]
             ranks.append(rec)
-            print(f"  P={P} rank {q}: rows={op.rows} halo={op.halo} chunks {times['chunks']:.3f} ms, "
+            print(f"  P={P} rank {q}: rows={op.rows} halo={op.halo} (received {op.n_recv}, ghosts {op.n_ghost} "
+                  f"<= degree {op.ghost_max_degree}) chunks {times['chunks']:.3f} ms (ghosts {times['ghosts']:.3f}), "
                   f"hub {times['hub']:.3f} ms", file=sys.stderr, flush=True)
             del op, src, dst
             torch.cuda.empty_cache()
         worst = max(ranks, key=lambda r: max(r["ms_hub"], r["ms_chunks"]))
-        out["worlds"][P] = {"ranks": ranks,
+        out["worlds"][f"{P}" if a.ghost == "auto" else f"{P}/ghost{ghost}"] = {"ranks": ranks,
                             "max_compute_ms": max(max(r["ms_hub"], r["ms_chunks"]) for r in ranks),
                             "mean_chunks_ms": sum(r["ms_chunks"] for r in ranks) / P,
                             "worst_rank": worst["rank"],
                             "max_halo_GB": max(r["halo_bytes"] for r in ranks) / 1e9}
-        print(f"P={P}: max compute {out['worlds'][P]['max_compute_ms']:.3f} ms "
+        W = out["worlds"][f"{P}" if a.ghost == "auto" else f"{P}/ghost{ghost}"]
+        print(f"P={P} ghost cap {ranks[0]['ghost_max_degree']}: max compute {W['max_compute_ms']:.3f} ms "
               f"(rank {worst['rank']}: chunks {worst['ms_chunks']:.3f}, hub {worst['ms_hub']:.3f}), "
-              f"mean chunks {out['worlds'][P]['mean_chunks_ms']:.3f} ms, max halo "
-              f"{out['worlds'][P]['max_halo_GB']:.2f} GB; pack {worst['ms_pack']:.3f} ms alone (index_select {worst['ms_pack_index_select']:.3f}), chunks+pack "
+              f"mean chunks {W['mean_chunks_ms']:.3f} ms, max received halo "
+              f"{W['max_halo_GB']:.2f} GB, busiest link {max(r['max_link_rows'] for r in ranks) * d * 4 / 1e9:.3f} GB; pack {worst['ms_pack']:.3f} ms alone (index_select {worst['ms_pack_index_select']:.3f}), chunks+pack "
               f"{worst['ms_chunks_with_pack']:.3f} ms", file=sys.stderr, flush=True)
     print(json.dumps(out), flush=True)
 
