@@ -7,8 +7,11 @@ and the same rows of every hop panel.  Two exchanges:
 * HaloPartitionedOperator (default): each rank receives only the remote rows its own rows
   reference, group by group (nnz-balanced row chunks + the hub rows), with one all_to_all_single
   per group on a communication stream as soon as that group's kernel is done -- overlapping the
-  later groups' kernels.  HaloWaveletFilter runs the wavelet basis' Chebyshev recurrence on the
-  same plan (one exchange per order).
+  later groups' kernels.  Low-degree halo rows whose neighbours are all local ("ghost rows") are
+  computed on the rank that needs them instead of received (the same CSR row, so the same bits):
+  a pair of GPUs shares one xGMI link, and on power-law graphs most of the halo is such rows.
+  HaloWaveletFilter runs the wavelet basis' Chebyshev recurrence on the same plan (one exchange per
+  order, no ghost rows).
 * RowPartitionedOperator: one padded all_gather_into_tensor of the whole panel per hop.
 
 In both, the local operator's column ids are remapped into the local panel layout with every
