@@ -4,7 +4,8 @@
 Launched by torchrun with P ranks, one per GPU (LOCAL_RANK).  It needs P GPUs: RCCL refuses two
 ranks on one card ("Duplicate GPU detected", seen on the one-GPU box), so on one GPU the N > 1 path
 is covered by the gloo tests and the virtual-rank GPU tests instead.  Every rank checks its rows of
-  * HaloPartitionedOperator.propagate (grouped all_to_all_single on the comm stream),
+  * HaloPartitionedOperator.propagate (grouped all_to_all_single on the comm stream; ghost rows
+    off, automatic and forced),
   * RowPartitionedOperator.propagate (all_gather_into_tensor),
   * HaloWaveletFilter.apply,
 bitwise against the single-GPU kernels (propagate on the whole graph / the virtual-rank wavelet
@@ -43,17 +44,18 @@ def main():
     ref = propagate(A, X, K)
     res = {"world": world, "n": n, "nnz": int(ix.numel()), "d": d, "K": K}
     ok = True
-    for chunks in (1, 4):
+    for chunks, ghost in ((1, 0), (4, None), (4, 16)):   # ghost rows off / auto cap / forced cap
         t0 = time.perf_counter()
-        op = HaloPartitionedOperator(ip, ix, vals, n, chunks=chunks, device=dev)
+        op = HaloPartitionedOperator(ip, ix, vals, n, chunks=chunks, device=dev, ghost_max_degree=ghost)
         panels = [op.new_panel(d) for _ in range(K + 1)]
         panels[0][: op.rows].copy_(X[op.r0:op.r1])
         for _ in range(2):                     # twice: the second run reuses streams and buffers
             op.propagate(panels[0], K, panels=panels)
         torch.cuda.synchronize()
         good = all(torch.equal(panels[k][: op.rows], ref[k][op.r0:op.r1]) for k in range(K + 1))
-        res[f"halo_chunks{chunks}"] = bool(good)
-        res[f"halo_chunks{chunks}_s"] = time.perf_counter() - t0
+        key = f"halo_chunks{chunks}_ghost{op.ghost_max_degree}" + ("auto" if ghost is None else "")
+        res[key] = bool(good)
+        res[key + "_s"] = time.perf_counter() - t0
         ok &= good
     op = RowPartitionedOperator(ip, ix, vals, n, device=dev)
     x_loc = op.new_panel(d)
