@@ -56,6 +56,9 @@ def parse():
     ap.add_argument("--nt-store", action="store_true")
     ap.add_argument("--exchange", default="halo", choices=["halo", "allgather"])
     ap.add_argument("--chunks", type=int, default=4, help="halo exchange groups per hop")
+    ap.add_argument("--exchange-x", action="store_true",
+                    help="halo exchange: receive hop 0's halo (X) from its owners instead of gathering "
+                         "it from the whole X every rank holds")
     ap.add_argument("--ghost-max-degree", type=int, default=None,
                     help="halo exchange: compute halo rows of at most this degree locally instead of "
                          "receiving them (default: the operator's cost model; 0 = off)")
@@ -377,10 +380,13 @@ def main():
         panels = [op.new_panel(d) for _ in range(K + 1)]
         panels[0][: op.rows].copy_(X[op.r0:op.r1])
         x_loc = panels[0]
+        # GraphOp.propagate takes the whole feature matrix; every rank holds it, so hop 0's halo
+        # is gathered locally (--exchange-x: from its owners, as when a rank holds only its rows)
+        x_full = None if a.exchange_x else X
         del X
 
         def step():
-            op.propagate(x_loc, K, panels=panels)
+            op.propagate(x_loc, K, panels=panels, x_full=x_full)
         # one hop's kernels also compute the ghost rows (the roofline counts that work)
         local_rows, local_nnz = op.rows + op.n_ghost, op.nnz_local + int(op._ghost_pos.numel())
 
@@ -453,7 +459,9 @@ def main():
         "config": {"workload": f"{a.config}-shaped K-hop propagate", "n_nodes": n, "nnz_ahat": nnz,
                    "d": d, "K": K, "normalization": "sym r=0.5",
                    "parallelism": f"row-partition x{world}" + (f" ({a.exchange} exchange)" if world > 1 else "")
-                   + (f", ghost rows <= degree {op.ghost_max_degree}" if world > 1 and a.exchange == "halo" else ""),
+                   + (f", ghost rows <= degree {op.ghost_max_degree}" if world > 1 and a.exchange == "halo" else "")
+                   + (", X whole on every rank (hop 0's halo gathered locally)" if world > 1 and a.exchange == "halo"
+                      and not a.exchange_x else ""),
                    "mode": "exact (bit-identical to reference)",
                    "outputs": ("all K+1 hop panels" if mode in ("panels", "auto") else
                                f"fused {a.aggregate} of hops 0..K (srgnn.aggregate, bit-exact vs the reference combine)"

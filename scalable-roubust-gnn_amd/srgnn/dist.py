@@ -363,6 +363,7 @@ class HaloPartitionedOperator:
         self.fused_pack = False
         # --- local operator over the panel rows [own | received (empty rows) | ghosts], columns
         # remapped into the same layout
+        self._halo_ids = torch.cat([need, gh]).contiguous()
         g2l = torch.full((n,), -1, dtype=torch.int64, device=dev)
         g2l[r0:r1] = torch.arange(self.rows, device=dev)
         g2l[need] = self.rows + torch.arange(self.n_recv, device=dev)
@@ -588,15 +589,31 @@ class HaloPartitionedOperator:
                 self._exchange_group(dst, g, packed)
         main.wait_stream(comm_s)     # also orders the next hop's writes into `packed` after these sends
 
-    def propagate(self, x_local: torch.Tensor, K: int, panels=None):
+    def halo_ids(self) -> torch.Tensor:
+        """Global row ids of the panel's halo rows, in panel order (received, then ghosts)."""
+        return self._halo_ids
+
+    def propagate(self, x_local: torch.Tensor, K: int, panels=None, x_full: torch.Tensor | None = None):
         """[X, ÂX, …, Â^K X] on this rank's rows: K+1 panels [rows + halo, d] (first `rows` are
-        this rank's rows in natural order)."""
+        this rank's rows in natural order).  x_full: the whole feature matrix [n, d] when this rank
+        holds it (as GraphOp.propagate's `feature` is given whole): hop 0's halo is then gathered
+        from it locally instead of exchanged; the results are the same bits."""
         d = x_local.shape[1]
         if panels is None:
             panels = [self.new_panel(d) for _ in range(K + 1)]
-        if x_local.data_ptr() != panels[0].data_ptr():
+        if x_full is not None:
+            if x_full.shape[0] != self.n or x_full.shape[1] != d:
+                raise ValueError(f"x_full must be [{self.n}, {d}], got {tuple(x_full.shape)}")
+            panels[0][: self.rows].copy_(x_full[self.r0:self.r1])
+            if self.halo:
+                if self._hip:
+                    from .spmm import gather_rows
+                    gather_rows(x_full, self._halo_ids, out=panels[0][self.rows:self.rows + self.halo])
+                else:
+                    panels[0][self.rows:self.rows + self.halo] = x_full.index_select(0, self._halo_ids)
+        elif x_local.data_ptr() != panels[0].data_ptr():
             panels[0][: self.rows].copy_(x_local[: self.rows])
-        if K > 0:
+        if K > 0 and x_full is None:
             self.exchange(panels[0], ghosts=True)
         for k in range(1, K + 1):
             self.hop(panels[k - 1], panels[k], exchange=k < K)    # the last hop's halo is never read

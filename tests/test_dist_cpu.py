@@ -82,7 +82,7 @@ def test_balanced_row_starts_and_remap():
     assert bool((m[1:] > m[:-1]).all())          # monotone: CSR order (and fma chains) preserved
 
 
-def _halo_worker(rank, world, port, out_path, chunks, ghost=None):
+def _halo_worker(rank, world, port, out_path, chunks, ghost=None, full_x=False):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     repo = os.path.dirname(here)
@@ -103,7 +103,7 @@ def _halo_worker(rank, world, port, out_path, chunks, ghost=None):
                                  device="cpu", ghost_max_degree=ghost)
     assert op.views[-1][1] > 0 or world > 2          # some hub rows exist at this threshold
     assert ghost is None or (op.n_ghost > 0) == (ghost > 0)
-    panels = op.propagate(x[op.r0:op.r1], 3)
+    panels = op.propagate(x[op.r0:op.r1], 3, x_full=x if full_x else None)
     rows = torch.tensor([op.rows])
     all_rows = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
     dist.all_gather(all_rows, rows)
@@ -119,12 +119,14 @@ def _halo_worker(rank, world, port, out_path, chunks, ghost=None):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,chunks,ghost", [(2, 3, None), (3, 2, None), (2, 2, 0), (3, 3, 16)])
-def test_halo_exchange_bitwise_equals_single(tmp_path, oracle_mod, world, chunks, ghost):
+@pytest.mark.parametrize("world,chunks,ghost,full_x", [(2, 3, None, False), (3, 2, None, False), (2, 2, 0, False),
+                                                      (3, 3, 16, False), (2, 2, None, True), (3, 2, 8, True)])
+def test_halo_exchange_bitwise_equals_single(tmp_path, oracle_mod, world, chunks, ghost, full_x):
     """Halo exchange (only referenced remote rows, grouped all_to_all_single; ghost rows computed
-    locally, exchanged once with X) over gloo ranks."""
+    locally, exchanged once with X -- or, with the whole X on every rank, gathered from it) over
+    gloo ranks."""
     out = str(tmp_path / "halo.npy")
-    mp.spawn(_halo_worker, args=(world, _free_port(), out, chunks, ghost), nprocs=world, join=True)
+    mp.spawn(_halo_worker, args=(world, _free_port(), out, chunks, ghost, full_x), nprocs=world, join=True)
     ip, ix, vals, x, n = _graph()
     want = oracle_mod.propagate(ip.numpy(), ix.numpy(), vals.numpy(), x.numpy(), 3)[3]
     np.testing.assert_array_equal(np.load(out), want)

@@ -44,16 +44,18 @@ def main():
     ref = propagate(A, X, K)
     res = {"world": world, "n": n, "nnz": int(ix.numel()), "d": d, "K": K}
     ok = True
-    for chunks, ghost in ((1, 0), (4, None), (4, 16)):   # ghost rows off / auto cap / forced cap
+    # ghost rows off / auto cap / forced cap; hop 0's halo exchanged or gathered from the whole X
+    for chunks, ghost, whole in ((1, 0, False), (4, None, False), (4, 16, False), (4, None, True)):
         t0 = time.perf_counter()
         op = HaloPartitionedOperator(ip, ix, vals, n, chunks=chunks, device=dev, ghost_max_degree=ghost)
         panels = [op.new_panel(d) for _ in range(K + 1)]
         panels[0][: op.rows].copy_(X[op.r0:op.r1])
         for _ in range(2):                     # twice: the second run reuses streams and buffers
-            op.propagate(panels[0], K, panels=panels)
+            op.propagate(panels[0], K, panels=panels, x_full=X if whole else None)
         torch.cuda.synchronize()
         good = all(torch.equal(panels[k][: op.rows], ref[k][op.r0:op.r1]) for k in range(K + 1))
-        key = f"halo_chunks{chunks}_ghost{op.ghost_max_degree}" + ("auto" if ghost is None else "")
+        key = f"halo_chunks{chunks}_ghost{op.ghost_max_degree}" + ("auto" if ghost is None else "") + \
+            ("_wholeX" if whole else "")
         res[key] = bool(good)
         res[key + "_s"] = time.perf_counter() - t0
         ok &= good
