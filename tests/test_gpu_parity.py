@@ -465,3 +465,28 @@ def test_gather_rows_equals_index_select(d):
     gather_rows(big[:, :d], torch.tensor([2, 0, 2], device="cuda"), out=out)
     torch.cuda.synchronize()
     assert torch.equal(out, big[[2, 0, 2], :d])
+
+
+@pytest.mark.parametrize("world,ghost", [(2, None), (4, 0), (8, 16)])
+def test_halo_whole_x_hop0_gather(world, ghost):
+    """propagate(x_full=X) on each virtual rank (K = 1: no exchange at all): hop 0's halo, ghost
+    rows included, is gathered from the whole X on the GPU, and hop 1's own rows (ghost kernels
+    included in the launch) are bitwise the single-device hop."""
+    from srgnn import synth
+    from srgnn.csr import DeviceCSR
+    from srgnn.dist import HaloPartitionedOperator
+    from srgnn.normalize import sym_norm_binary
+    from srgnn.spmm import propagate
+    n = 20000
+    u, v = synth.rmat_undirected_t(n, 150000, seed=24, device="cuda")
+    ip, ix = synth.symmetric_csr_t(n, u, v)
+    ip, ix, vals = sym_norm_binary(ip, ix, n, 0.5)
+    x = synth.uniform_features_t(n, 64, device="cuda")
+    want = propagate(DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, device="cuda"), x, 1)
+    for q in range(world):
+        op = HaloPartitionedOperator(ip, ix, vals, n, chunks=3, hub_threshold=300, device="cuda", rank=q,
+                                     world=world, ghost_max_degree=ghost)
+        panels = op.propagate(x[op.r0:op.r1], 1, x_full=x)
+        torch.cuda.synchronize()
+        assert torch.equal(panels[0][op.rows:], x.index_select(0, op.halo_ids()))
+        assert torch.equal(panels[1][: op.rows], want[1][op.r0:op.r1]), f"rank {q}/{world}"
