@@ -402,13 +402,17 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    ev_run = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev_run[0].record(stream)
     for _ in range(a.steps):
         step()
+    ev_run[1].record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    run_s = ev_run[0].elapsed_time(ev_run[1]) * 1e-3        # the timed steps, HIP events on the launch stream
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -436,7 +440,13 @@ def main():
         ev[2 * r + 1].record(stream)
     torch.cuda.synchronize()
     durs = [ev[2 * r].elapsed_time(ev[2 * r + 1]) * 1e-3 for r in range(a.roofline_reps)]
-    kern_s = float(np.mean(durs))
+    kern_isolated_s = float(np.mean(durs))
+    # one hop's launch duration: over the timed region itself on one GPU (K hop launches per step,
+    # back to back on the launch stream, so the events bracket exactly the kernels plus their
+    # few-microsecond gaps); on N GPUs the timed region also waits on the exchange, so the
+    # isolated launches above are the kernel's duration there
+    in_run = world == 1 and not a.aggregate and K > 0
+    kern_s = run_s / (a.steps * K) if in_run else kern_isolated_s
     b_alg = roofline.bytes_no_reuse(local_rows, local_nnz, d)
     achieved = b_alg / kern_s / 1e9
     peak = roofline.MI355X_HBM_PEAK_GBS
@@ -471,6 +481,9 @@ def main():
                      "frac": achieved / peak, "traffic": traffic,
                      "kernel": "k_spmm (+ k_spmm_hub beside it): one hop" + (" of rank 0's rows" if world > 1 else ""),
                      "kernel_ms": kern_s * 1e3,
+                     "kernel_ms_source": ("HIP events over the timed steps / (steps x K)" if in_run
+                                          else f"HIP events around {a.roofline_reps} isolated hop launches"),
+                     "kernel_ms_isolated": kern_isolated_s * 1e3,
                      # measured HBM bytes (PMC) per launch / the same launch duration: the share of
                      # the 8 TB/s peak the kernel actually moves (the no-reuse frac counts cache hits)
                      "traffic_frac": (traffic / kern_s / 1e9 / peak) if traffic else None,
