@@ -46,6 +46,15 @@ extern "C" {
 /* Diagnostic: keep one row per wave also for d <= 32 (the default runs 64 / S rows per wave,
  * S = the power of two >= d lanes per row).  Results are identical either way. */
 #define SRG_SPMM_WIDE_ROWS 0x4
+/* Diagnostic: hub workgroups always use 256-nonzero windows (72 KB of LDS, two per CU).  By default
+ * they do only when a launch has more hub workgroups than CUs.  Results are identical either way. */
+#define SRG_SPMM_HUB_W256 0x8
+/* The hub rows' workgroups are forked onto the library's per-device hub side stream and NOT
+ * joined back into `stream` before the call returns: later launches on `stream` run beside them
+ * (srgnn/dist.py issues the halo row chunks there).  The caller must srg_hub_join() a stream
+ * before anything reads the hub rows, and before the next NOJOIN fork on the device (one
+ * outstanding fork per device). */
+#define SRG_SPMM_HUB_NOJOIN 0x10u
 
 /* =============================================================================================
  * (A) drop-in entry points
@@ -185,6 +194,17 @@ int srg_segment_sum_f64(const int64_t* seg_ptr, const double* vals, int64_t n_se
  * dst row unwritten (no fault).  Asynchronous on `stream`. */
 int srg_gather_rows_f32(const float* src, int64_t lds, int64_t n_src, const int64_t* idx, int64_t n_idx,
                         float* dst, int64_t ldd, int32_t d, void* stream);
+
+/* Scheduling helper for a hub launch issued on ANOTHER stream than the launches that follow it
+ * (srgnn/dist.py: the halo exchange's hub group beside its row chunks): a single-wave kernel that
+ * holds `stream` for the hub dispatch delay (10 us, SRGNN_HUB_DISPATCH_DELAY_US), so that the hub
+ * workgroups (139 KB of LDS each) reach CUs before the next launch on `stream` fills them.
+ * srg_spmm_csr_f32 does the same internally when it forks its own hub rows. */
+int srg_hub_dispatch_delay(void* stream);
+
+/* `stream` waits (on the device, not the host) for the hub workgroups of the last
+ * SRG_SPMM_HUB_NOJOIN launch on the current device; no-op if none was forked. */
+int srg_hub_join(void* stream);
 
 /* Checks a device CSR: indptr[0] == 0, indptr non-decreasing, indptr[n_rows] == nnz, and every
  * column id in [0, n_cols).  Synchronous on `stream`.  Returns SRG_OK or SRG_ERR_INVALID. */

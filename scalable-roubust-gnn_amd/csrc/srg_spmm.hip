@@ -477,27 +477,36 @@ k_spmm(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
 // at 8.  Here the row's chain is fed from LDS by 8 producer waves:
 //   * windows of kHubW = 512 nonzeros, double-buffered tiles: while the consumer runs window h
 //     from one tile, the producers write window h+1 into the other (one barrier per window);
-//   * each producer lane gathers kHubUW = 8 dwordx4 (8 nonzeros' 128-byte slices per wave
+//   * each producer lane gathers W / 64 = 8 dwordx4 (8 nonzeros' 128-byte slices per wave
 //     instruction) per window into one of two register sets, so a window's gathers are issued
 //     two windows before they are written (~2 us of latency cover); the column ids / values of
 //     the next window are loaded one window ahead;
-//   * the tile is transposed, [32 columns][kHubLd] with the 4-nonzero group index XOR-swizzled
-//     per column group (conflict-free ds_write_b32 and ds_read_b128, see kHubLd);
+//   * the tile is transposed, [32 columns][W + 16] with the 4-nonzero group index XOR-swizzled
+//     per column group (conflict-free ds_write_b32 and ds_read_b128, see HubGeom);
 //   * the consumer wave (lanes 0..31, one column each) runs the 32 chains, 4 links per
 //     ds_read_b128, with a ring of three 16-link register sets so every LDS read is issued two
 //     sets (~32 links) before its fmas.
 // Still exactly one fma chain per output element, in CSR order.
 // ------------------------------------------------------------------------------------------------
 constexpr int kHubProducers = 8;
-constexpr int kHubW = 512;                                   // nonzeros per window
-constexpr int kHubUW = kHubW / (kHubProducers * 8);          // gathers per producer lane per window (8)
+constexpr int kHubW = 512;                                   // nonzeros per window (the default)
 constexpr int kHubThreads = 64 * (kHubProducers + 1);
-// floats per tile column: 528 == 16 (mod 64).  With the 4-link group index XOR-ed by (c >> 2) & 7,
+// Window geometry for W nonzeros per window.  W = 512 (139 KB of LDS, one workgroup per CU) is the
+// lowest-latency chain, for a few hub rows beside a big launch (one GPU).  W = 256 (72 KB) lets two
+// workgroups share a CU, for launches with more hub workgroups than CUs (the halo exchange's hub
+// group: hundreds of rows per rank), where the CUs' LDS, not one chain's latency, sets the time.
+// Floats per tile column: W + 16 == 16 (mod 64).  With the 4-link group index XOR-ed by (c >> 2) & 7,
 // both the producers' transposed ds_write_b32 (lanes: 4 nonzeros x 8 column chunks) and the
 // consumer's ds_read_b128 (lanes: 32 columns, 16-lane groups) are bank-conflict-free (exhaustive
 // check over all window offsets; the 4 (mod 64) stride of the first version made the reads 2-way)
-constexpr int kHubLd = kHubW + 16;
-constexpr int kHubTile = kSliceCols * kHubLd;                // floats per tile
+template <int W>
+struct HubGeom {
+    static constexpr int UW = W / (kHubProducers * 8);       // gathers per producer lane per window
+    static constexpr int LD = W + 16;
+    static constexpr int TILE = kSliceCols * LD;             // floats per tile
+    static constexpr size_t LDS_BYTES = (size_t)(2 * TILE + 2 * W) * sizeof(float);
+};
+constexpr int kHubWideLaunch = 256;   // more hub workgroups than this (the CU count) -> W = 256
 __device__ __forceinline__ int hub_swz(int c) { return (c >> 2) & 7; }
 constexpr int kHubL = 7;   // consumer: (tile, value) LDS read pairs in flight in a full window
 
@@ -505,7 +514,7 @@ constexpr int kHubL = 7;   // consumer: (tile, value) LDS read pairs in flight i
 // chains; 2 = the producers skip gathers and LDS writes; 3 = the consumer's fmas read registers
 // only (no LDS reads); 4 = producers gather but skip the LDS writes; 5 / 6 = the consumer reads
 // only the tile / only the values from LDS.
-template <bool SFULL, typename IP, int ABL = 0, bool SEND = false>
+template <bool SFULL, typename IP, int ABL = 0, bool SEND = false, int W = kHubW>
 __global__ void __launch_bounds__(kHubThreads)
 k_spmm_hub(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
            const float* __restrict__ vals, const int32_t* __restrict__ hub_rows, int n_slices,
@@ -514,8 +523,8 @@ k_spmm_hub(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
 {
     typedef typename Vec<float, 4>::type V4;
     extern __shared__ __attribute__((aligned(16))) float hub_lds[];
-    // [2 tiles][32 columns][kHubLd] then [2][kHubW] values
-    float* aval_base = hub_lds + 2 * kHubTile;
+    // [2 tiles][32 columns][HubGeom<W>::LD] then [2][W] values
+    float* aval_base = hub_lds + 2 * HubGeom<W>::TILE;
     const int item = blockIdx.x;
     const int row = hub_rows[item / n_slices];
     const int slice = item % n_slices;
@@ -523,7 +532,7 @@ k_spmm_hub(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
     const int lane = threadIdx.x & 63;
     const int64_t beg = indptr[row];
     const int64_t end = indptr[row + 1];
-    const int n_win = (int)((end - beg + kHubW - 1) / kHubW);
+    const int n_win = (int)((end - beg + W - 1) / W);
 
     if (wave == 0) {   // ---------------- consumer: 32 column chains ----------------
         const int c = lane & 31;
@@ -539,10 +548,10 @@ k_spmm_hub(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
         for (int h = 0; h < n_win; ++h) {
             __syncthreads();                      // window h is in tile h & 1
             if (lane < kSliceCols) {
-                const float* tcol = hub_lds + (h & 1) * kHubTile + c * kHubLd;
-                const float* av = aval_base + (h & 1) * kHubW;
-                const int64_t sb = beg + (int64_t)h * kHubW;
-                const int nb = (end - sb) < kHubW ? (int)(end - sb) : kHubW;
+                const float* tcol = hub_lds + (h & 1) * HubGeom<W>::TILE + c * HubGeom<W>::LD;
+                const float* av = aval_base + (h & 1) * W;
+                const int64_t sb = beg + (int64_t)h * W;
+                const int nb = (end - sb) < W ? (int)(end - sb) : W;
                 const int nc = nb / (4 * G);      // full 8-link sets
                 auto ld = [&](int set, V4 (&t)[G], V4 (&a)[G]) {
 #pragma unroll
@@ -562,16 +571,16 @@ k_spmm_hub(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
                     }
                 };
                 if (ABL == 1) continue;
-                if ((ABL == 0 || ABL == 2 || ABL == 4) && nb == kHubW) {
+                if ((ABL == 0 || ABL == 2 || ABL == 4) && nb == W) {
                     // full window, fully unrolled: every LDS read is a per-lane base (the XOR swizzle
                     // of group k & 7 folded in, hoisted per window) or the value base, plus an
                     // immediate offset -- no address arithmetic between the fmas.  A ring of kHubL
                     // (tile, value) read pairs in flight (2 * kHubL <= 15 = lgkmcnt's range).
                     // Same links, same order: the chain is unchanged.
-                    constexpr int NG = kHubW / 4;
+                    constexpr int NG = W / 4;
                     const float* tb[8];
 #pragma unroll
-                    for (int k = 0; k < 8; ++k) tb[k] = hub_lds + (h & 1) * kHubTile + c * kHubLd + ((k ^ sw) << 2);
+                    for (int k = 0; k < 8; ++k) tb[k] = hub_lds + (h & 1) * HubGeom<W>::TILE + c * HubGeom<W>::LD + ((k ^ sw) << 2);
                     auto rt = [&](int grp) { return *reinterpret_cast<const V4*>(tb[grp & 7] + (grp >> 3) * 32); };
                     auto ra = [&](int grp) { return *reinterpret_cast<const V4*>(av + (grp << 2)); };
                     V4 t[kHubL], a[kHubL];
@@ -663,38 +672,38 @@ k_spmm_hub(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
     const int qq = lane & 7;          // 16-byte chunk = columns qq*4 .. qq*4+3 of the slice
     const int qcol = slice * kSliceCols + qq * 4;
     const bool gact = SFULL || qcol < d;
-    V4 x0[kHubUW], x1[kHubUW];        // gathered windows, two register sets (even / odd windows)
-    float a0[kHubUW], a1[kHubUW];
-    int cn[kHubUW];                   // column ids / values of the next window to gather
-    float an[kHubUW];
+    V4 x0[HubGeom<W>::UW], x1[HubGeom<W>::UW];        // gathered windows, two register sets (even / odd windows)
+    float a0[HubGeom<W>::UW], a1[HubGeom<W>::UW];
+    int cn[HubGeom<W>::UW];                   // column ids / values of the next window to gather
+    float an[HubGeom<W>::UW];
     auto load_ids = [&](int w) {
-        const int64_t sb = beg + (int64_t)w * kHubW;
+        const int64_t sb = beg + (int64_t)w * W;
 #pragma unroll
-        for (int b = 0; b < kHubUW; ++b) {
-            int64_t jj = sb + (p * kHubUW + b) * 8 + g;
+        for (int b = 0; b < HubGeom<W>::UW; ++b) {
+            int64_t jj = sb + (p * HubGeom<W>::UW + b) * 8 + g;
             jj = jj < end ? jj : end - 1;
             cn[b] = indices[jj];
             an[b] = vals[jj];
         }
     };
-    auto gather = [&](V4 (&x)[kHubUW], float (&a)[kHubUW]) {
+    auto gather = [&](V4 (&x)[HubGeom<W>::UW], float (&a)[HubGeom<W>::UW]) {
 #pragma unroll
-        for (int b = 0; b < kHubUW; ++b) {
+        for (int b = 0; b < HubGeom<W>::UW; ++b) {
             x[b] = (gact && ABL != 2) ? gload<float, 4>(X + (int64_t)cn[b] * ldx + qcol) : vzero<float, 4>();
             a[b] = an[b];
         }
     };
-    auto put = [&](int w, const V4 (&x)[kHubUW], const float (&a)[kHubUW]) {
+    auto put = [&](int w, const V4 (&x)[HubGeom<W>::UW], const float (&a)[HubGeom<W>::UW]) {
         if (ABL == 2 || ABL == 4) return;
-        float* tile = hub_lds + (w & 1) * kHubTile;
-        float* av = aval_base + (w & 1) * kHubW;
+        float* tile = hub_lds + (w & 1) * HubGeom<W>::TILE;
+        float* av = aval_base + (w & 1) * W;
 #pragma unroll
-        for (int b = 0; b < kHubUW; ++b) {
-            const int nl = (p * kHubUW + b) * 8 + g;   // nonzero within the window
+        for (int b = 0; b < HubGeom<W>::UW; ++b) {
+            const int nl = (p * HubGeom<W>::UW + b) * 8 + g;   // nonzero within the window
 #pragma unroll
             for (int i = 0; i < 4; ++i) {             // transposed, swizzled: conflict-free
                 const int cc = qq * 4 + i;
-                tile[cc * kHubLd + ((((nl >> 2) ^ hub_swz(cc)) << 2) | (nl & 3))] = x[b][i];
+                tile[cc * HubGeom<W>::LD + ((((nl >> 2) ^ hub_swz(cc)) << 2) | (nl & 3))] = x[b][i];
             }
             if (qq == 0) av[nl] = a[b];
         }
@@ -724,7 +733,7 @@ k_spmm_hub(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
     // barrier count: 1 (prologue) + (n_win - 1) in the loop == the consumer's n_win
 }
 
-constexpr size_t kHubLdsBytes = (size_t)(2 * kHubTile + 2 * kHubW) * sizeof(float);
+constexpr size_t kHubLdsBytes = HubGeom<kHubW>::LDS_BYTES;
 
 // ------------------------------------------------------------------------------------------------
 // Chebyshev step with fused epilogue (wavelet basis)
@@ -1004,6 +1013,12 @@ __global__ void k_dispatch_delay(int us)
     while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(16);
 }
 
+int hub_delay_us()
+{
+    static const int us = [] { const char* e = getenv("SRGNN_HUB_DISPATCH_DELAY_US"); return e ? atoi(e) : 10; }();
+    return us;
+}
+
 // per-device side stream + fork/join events for the hub kernel (created once, never destroyed)
 struct SideStream {
     hipStream_t stream = nullptr;
@@ -1028,8 +1043,18 @@ int side_stream(SideStream** out)
         SRG_HIP_CHECK(hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming));
         SRG_HIP_CHECK(hipEventCreateWithFlags(&ss.join, hipEventDisableTiming));
         for (const void* fn : {(const void*)k_spmm_hub<true, int>, (const void*)k_spmm_hub<false, int>,
-                               (const void*)k_spmm_hub<true, int64_t>, (const void*)k_spmm_hub<false, int64_t>})
+                               (const void*)k_spmm_hub<true, int64_t>, (const void*)k_spmm_hub<false, int64_t>,
+                               (const void*)k_spmm_hub<true, int64_t, 0, true>,
+                               (const void*)k_spmm_hub<false, int64_t, 0, true>})
             SRG_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kHubLdsBytes));
+        for (const void* fn : {(const void*)k_spmm_hub<true, int, 0, false, 256>,
+                               (const void*)k_spmm_hub<false, int, 0, false, 256>,
+                               (const void*)k_spmm_hub<true, int64_t, 0, false, 256>,
+                               (const void*)k_spmm_hub<false, int64_t, 0, false, 256>,
+                               (const void*)k_spmm_hub<true, int64_t, 0, true, 256>,
+                               (const void*)k_spmm_hub<false, int64_t, 0, true, 256>})
+            SRG_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                              (int)HubGeom<256>::LDS_BYTES));
     }
     *out = &ss;
     return SRG_OK;
@@ -1081,19 +1106,26 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
             }
             hipLaunchKernelGGL(k, hgrid, dim3(kHubThreads), kHubLdsBytes, ss->stream, indptr, indices, vals,
                                order, n_slices, X, ldx, Y, ldy, d, acc, nt, epi);
-        } else if (sfull)
-            hipLaunchKernelGGL((k_spmm_hub<true, IP, 0, SEND>), hgrid, dim3(kHubThreads), kHubLdsBytes,
-                               ss->stream, indptr, indices, vals, order, n_slices, X, ldx, Y, ldy,
-                               d, acc, nt, epi);
-        else
-            hipLaunchKernelGGL((k_spmm_hub<false, IP, 0, SEND>), hgrid, dim3(kHubThreads), kHubLdsBytes,
-                               ss->stream, indptr, indices, vals, order, n_slices, X, ldx, Y, ldy,
-                               d, acc, nt, epi);
+        } else {
+            static const int wide_env = [] { const char* e = getenv("SRGNN_HUB_WIDE_LAUNCH"); return e ? atoi(e) : -1; }();
+            const int64_t wide = wide_env >= 0 ? wide_env : kHubWideLaunch;
+            const bool w256 = n_hub * n_slices > wide || (flags & SRG_SPMM_HUB_W256);
+#define SRG_LAUNCH_HUB(SF, WW)                                                                             \
+    hipLaunchKernelGGL((k_spmm_hub<SF, IP, 0, SEND, WW>), hgrid, dim3(kHubThreads), HubGeom<WW>::LDS_BYTES, \
+                       ss->stream, indptr, indices, vals, order, n_slices, X, ldx, Y, ldy, d, acc, nt, epi)
+            if (sfull) {
+                if (w256) SRG_LAUNCH_HUB(true, 256);
+                else SRG_LAUNCH_HUB(true, 512);
+            } else {
+                if (w256) SRG_LAUNCH_HUB(false, 256);
+                else SRG_LAUNCH_HUB(false, 512);
+            }
+#undef SRG_LAUNCH_HUB
+        }
         SRG_HIP_CHECK(hipGetLastError());
         SRG_HIP_CHECK(hipEventRecord(ss->join, ss->stream));
-        static const int delay_us = [] { const char* e = getenv("SRGNN_HUB_DISPATCH_DELAY_US"); return e ? atoi(e) : 10; }();
-        if (delay_us > 0) {
-            hipLaunchKernelGGL(k_dispatch_delay, dim3(1), dim3(64), 0, s, delay_us);
+        if (hub_delay_us() > 0) {
+            hipLaunchKernelGGL(k_dispatch_delay, dim3(1), dim3(64), 0, s, hub_delay_us());
             SRG_HIP_CHECK(hipGetLastError());
         }
     }
@@ -1153,7 +1185,7 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
 #undef SRG_LAUNCH_NARROW
         SRG_HIP_CHECK(hipGetLastError());
     }
-    if (ss) SRG_HIP_CHECK(hipStreamWaitEvent(s, ss->join, 0));   // join
+    if (ss && !(flags & SRG_SPMM_HUB_NOJOIN)) SRG_HIP_CHECK(hipStreamWaitEvent(s, ss->join, 0));   // join
     return SRG_OK;
 }
 
@@ -1521,6 +1553,29 @@ int srg_gather_rows_f32(const float* src, int64_t lds, int64_t n_src, const int6
 #undef SRG_GATHER_S
 #undef SRG_GATHER
     SRG_HIP_CHECK(hipGetLastError());
+    return ok();
+}
+
+int srg_hub_dispatch_delay(void* stream)
+{
+    if (hub_delay_us() > 0) {
+        hipLaunchKernelGGL(k_dispatch_delay, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream), hub_delay_us());
+        SRG_HIP_CHECK(hipGetLastError());
+    }
+    return ok();
+}
+
+int srg_hub_join(void* stream)
+{
+    int dev = 0;
+    SRG_HIP_CHECK(hipGetDevice(&dev));
+    if (dev < 0 || dev >= 64) return fail(SRG_ERR_HIP, "device id %d", dev);
+    hipEvent_t join = nullptr;
+    {
+        std::lock_guard<std::mutex> lock(g_side_mu);
+        join = g_side[dev].join;
+    }
+    if (join) SRG_HIP_CHECK(hipStreamWaitEvent(static_cast<hipStream_t>(stream), join, 0));
     return ok();
 }
 

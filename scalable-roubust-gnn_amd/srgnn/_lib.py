@@ -20,6 +20,8 @@ SRG_ERR_ALLOC = -3
 SRG_SPMM_ACCUMULATE = 0x1
 SRG_SPMM_NT_STORE = 0x2
 SRG_SPMM_WIDE_ROWS = 0x4
+SRG_SPMM_HUB_W256 = 0x8
+SRG_SPMM_HUB_NOJOIN = 0x10
 
 SRG_CHEBY_INIT = 0
 SRG_CHEBY_STEP = 1
@@ -45,6 +47,8 @@ EXPORTED_SYMBOLS = (
     "srg_tail_rowsum_f32",
     "srg_segment_sum_f64",
     "srg_gather_rows_f32",
+    "srg_hub_dispatch_delay",
+    "srg_hub_join",
     "srg_csr_validate",
     "srg_last_error",
     "srg_last_error_code",
@@ -98,6 +102,10 @@ def _declare(lib):
     lib.srg_segment_sum_f64.restype = ctypes.c_int
     lib.srg_gather_rows_f32.argtypes = [_p, _i64, _i64, _p, _i64, _p, _i64, _i32, _p]
     lib.srg_gather_rows_f32.restype = ctypes.c_int
+    lib.srg_hub_dispatch_delay.argtypes = [_p]
+    lib.srg_hub_dispatch_delay.restype = ctypes.c_int
+    lib.srg_hub_join.argtypes = [_p]
+    lib.srg_hub_join.restype = ctypes.c_int
     lib.srg_csr_validate.argtypes = [_p, _p, _i64, _i64, _i64, _p]
     lib.srg_csr_validate.restype = ctypes.c_int
     lib.srg_last_error.argtypes = []

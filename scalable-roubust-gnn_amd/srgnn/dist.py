@@ -416,7 +416,6 @@ class HaloPartitionedOperator:
             self._A = [(lip, lix, lvv, order) for (order, _, _, _) in self.views + [self.ghost_view]]
             self._spmm = local_spmm
         self._hip = local_spmm is None and dev.type == "cuda"      # the HIP kernels (fused pack possible)
-        self._streams = None
 
     # ------------------------------------------------------------------------------------------
     def new_panel(self, d: int) -> torch.Tensor:
@@ -436,7 +435,6 @@ class HaloPartitionedOperator:
             from .csr import DeviceCSR
             other._A = [DeviceCSR(a.indptr, a.indices, lvv, a.n_rows, a.n_cols, a.order, a.n_heavy, a.n_hub)
                         for a in self._A]
-        other._streams = None
         return other
 
     def _local_values(self, values: torch.Tensor) -> torch.Tensor:
@@ -452,16 +450,18 @@ class HaloPartitionedOperator:
             self._send_buf = torch.empty((self.send_offsets[-1], d), dtype=torch.float32, device=self.device)
         return self._send_buf
 
-    def _exchange_group(self, panel: torch.Tensor, g: int, packed: torch.Tensor | None = None):
+    def _exchange_group(self, panel: torch.Tensor, g: int, packed: torch.Tensor | None = None,
+                        async_op: bool = False):
         """all_to_all of group g's rows: from `packed` (the fused-pack buffer, already filled by
-        this group's kernels) or gathered from the panel's own rows here."""
+        this group's kernels) or gathered from the panel's own rows here (on the current stream).
+        async_op: returns (work, send) -- the caller waits on the work before the halo is read."""
         P, p = self.world, self.rank
         off = self.rows + self.group_offsets[g]
         out_splits = [self.recv_counts[g][q] for q in range(P)]
         in_splits = [self.send_counts[g][q] for q in range(P)]
         total_in = sum(out_splits)
         if P == 1 or (total_in == 0 and sum(in_splits) == 0 and not dist.is_initialized()):
-            return
+            return None
         recv = panel[off:off + total_in]
         if packed is not None:
             send = packed[self.send_offsets[g]:self.send_offsets[g + 1]]
@@ -475,7 +475,8 @@ class HaloPartitionedOperator:
             send = panel.new_zeros((0, panel.shape[1]))
         if self.virtual:
             raise RuntimeError("virtual shares exchange through simulate_halo_propagate()")
-        dist.all_to_all_single(recv, send, out_splits, in_splits, group=self.group)
+        work = dist.all_to_all_single(recv, send, out_splits, in_splits, group=self.group, async_op=async_op)
+        return (work, send) if async_op else None
 
     def _exchange_ghosts(self, panel: torch.Tensor):
         """all_to_all of the ghost rows (X's first exchange only: later hops compute them)."""
@@ -506,46 +507,55 @@ class HaloPartitionedOperator:
             self._exchange_ghosts(panel)
 
     def _launch_groups(self, src: torch.Tensor, dst: torch.Tensor, packed: torch.Tensor | None = None,
-                       ghosts: bool = True):
-        """dst[:rows] = local Â rows @ src: the hub group on its own stream (its kernel is a
-        latency-bound chain that runs beside the others), the row chunks in order on the current
-        stream, then (ghosts=True) the ghost rows into their halo slots of dst; with `packed`, the
-        kernels also store every row peers need into it (fused pack).
-        Returns the per-group completion events (CUDA) or None (CPU ranks)."""
+                       ghosts: bool = True, after_group=None):
+        """dst[:rows] = local Â rows @ src, everything on the current stream: the hub group's
+        workgroups forked onto the library's hub side stream (srg_spmm_csr_f32 with
+        SRG_SPMM_HUB_NOJOIN; they run beside the chunks), the row chunks in order, the ghost rows
+        into their halo slots of dst (ghosts=True), then the join of the hub side stream.
+        after_group(g) is called right after group g's launch (chunks in order, the hub group after
+        its join): the hop issues group g's exchange there.  With `packed`, the kernels also store
+        every row peers need into it (fused pack; the hub group then runs before the chunks).
+        No other stream is used: a second torch stream may share a hardware queue with this one,
+        and its waits would then stall the chunks behind the hub (measured: chunks + hub instead
+        of the longer of the two)."""
         gA = self._A[self.n_groups]
+        C = self.C
+        out = dst[: self.rows]
         if self.device.type != "cuda":
-            for g in range(self.n_groups):
+            for g in list(range(C)) + [C]:
                 if self.views[g][1]:
-                    self._spmm(self._A[g], src, dst[: self.rows])
+                    self._spmm(self._A[g], src, out)
             if ghosts and self.n_ghost:
                 self._spmm(gA, src, dst)
-            return None
-        if self._streams is None:
-            self._streams = (torch.cuda.Stream(self.device), torch.cuda.Stream(self.device))
-        hub_s = self._streams[0]
-        main = torch.cuda.current_stream(self.device)
-        C = self.C
-
-        def run(g):
-            if packed is None:
-                self._spmm(self._A[g], src, dst[: self.rows])
-            else:
-                from .spmm import spmm_send
-                spmm_send(self._A[g], src, dst[: self.rows], packed, self._send_ptr, self._send_slot)
-
-        done = [torch.cuda.Event() for _ in range(self.n_groups)]
-        hub_s.wait_stream(main)
+            if after_group is not None:
+                for g in list(range(C)) + [C]:
+                    after_group(g)
+            return
+        from . import _lib
+        from .spmm import spmm, spmm_send
+        fork = bool(self.views[C][1] and self.views[C][3] and self._hip and packed is None)
         if self.views[C][1]:
-            with torch.cuda.stream(hub_s):
-                run(C)
-        done[C].record(hub_s)
+            if packed is not None:
+                spmm_send(self._A[C], src, out, packed, self._send_ptr, self._send_slot)
+            elif fork:
+                spmm(self._A[C], src, out=out, hub_nojoin=True)
+            else:
+                self._spmm(self._A[C], src, out)
         for c in range(C):
             if self.views[c][1]:
-                run(c)
-            done[c].record(main)
-        if ghosts and self.n_ghost:      # after the chunks: their exchanges start first
+                if packed is not None:
+                    spmm_send(self._A[c], src, out, packed, self._send_ptr, self._send_slot)
+                else:
+                    self._spmm(self._A[c], src, out)
+            if after_group is not None:
+                after_group(c)
+        if ghosts and self.n_ghost:
             self._spmm(gA, src, dst)
-        return done
+        if fork:
+            _lib.check(_lib.lib().srg_hub_join(torch.cuda.current_stream(self.device).cuda_stream),
+                       "srg_hub_join")
+        if after_group is not None:
+            after_group(C)
 
     def compute_packed(self, src: torch.Tensor, dst: torch.Tensor) -> torch.Tensor:
         """compute() with the fused pack: returns the send buffer (all groups' rows peers need, in
@@ -553,41 +563,34 @@ class HaloPartitionedOperator:
         if not self._hip:
             raise RuntimeError("the fused pack needs the HIP kernels (a CUDA operator without local_spmm)")
         packed = self.send_buffer(src.shape[1])
-        done = self._launch_groups(src, dst, packed)
-        torch.cuda.current_stream(self.device).wait_event(done[self.C])
+        self._launch_groups(src, dst, packed)
         return packed
 
     def compute(self, src: torch.Tensor, dst: torch.Tensor, ghosts: bool = True):
         """dst[:rows] = local Â rows @ src (all groups, no exchange) and, with ghosts, the ghost
         rows of dst's halo; ordered on the current stream."""
-        done = self._launch_groups(src, dst, ghosts=ghosts)
-        if done is not None:
-            torch.cuda.current_stream(self.device).wait_event(done[self.C])
+        self._launch_groups(src, dst, ghosts=ghosts)
 
     def hop(self, src: torch.Tensor, dst: torch.Tensor, exchange: bool = True):
         """One hop: dst own rows from src, then (unless exchange=False, e.g. the last hop, whose halo
-        no later hop reads) dst's halo, group by group, each group's all_to_all_single issued on the
-        communication stream as soon as its kernel is done (overlapping the later groups)."""
+        no later hop reads) dst's halo, group by group: each group's rows are packed on the current
+        stream right after its kernel and sent with an asynchronous all_to_all_single (RCCL runs it
+        on its own stream while the later groups compute); the current stream waits for all of
+        them at the end of the hop."""
         packed = None
         if exchange and self.fused_pack and self.world > 1 and not self.virtual and self._hip:
             packed = self.send_buffer(src.shape[1])
-        done = self._launch_groups(src, dst, packed, ghosts=exchange)   # no later hop reads the last ghosts
-        if not exchange:
-            if done is not None:
-                torch.cuda.current_stream(self.device).wait_event(done[self.C])
+        if not exchange or self.world == 1 or self.device.type != "cuda":
+            self._launch_groups(src, dst, packed, ghosts=exchange)   # no later hop reads the last ghosts
+            if exchange:
+                self.exchange(dst)
             return
-        if done is None or self.world == 1:
-            if done is not None:
-                torch.cuda.current_stream(self.device).wait_event(done[self.C])
-            self.exchange(dst)
-            return
-        comm_s = self._streams[1]
-        main = torch.cuda.current_stream(self.device)
-        with torch.cuda.stream(comm_s):
-            for g in list(range(self.C)) + [self.C]:
-                comm_s.wait_event(done[g])
-                self._exchange_group(dst, g, packed)
-        main.wait_stream(comm_s)     # also orders the next hop's writes into `packed` after these sends
+        pending = []
+        self._launch_groups(src, dst, packed, ghosts=True,
+                            after_group=lambda g: pending.append(self._exchange_group(dst, g, packed, async_op=True)))
+        for item in pending:
+            if item is not None:
+                item[0].wait()        # the current stream waits for RCCL's stream (the CPU does not)
 
     def halo_ids(self) -> torch.Tensor:
         """Global row ids of the panel's halo rows, in panel order (received, then ghosts)."""

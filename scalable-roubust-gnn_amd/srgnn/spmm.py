@@ -33,9 +33,13 @@ def _check_panel(X: torch.Tensor, rows: int, name: str, d=None):
 
 
 def spmm(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor | None = None, accumulate: bool = False,
-         nt_store: bool = False, wide_rows: bool = False) -> torch.Tensor:
+         nt_store: bool = False, wide_rows: bool = False, hub_w256: bool = False,
+         hub_nojoin: bool = False) -> torch.Tensor:
     """out[r, :] (+)= A[r, :] @ X  for the rows of A (one hop; exact fma chains in CSR order).
-    wide_rows: diagnostic, one row per wave also for d <= 32 (same results)."""
+    wide_rows: diagnostic, one row per wave also for d <= 32; hub_w256: diagnostic, 256-nonzero
+    hub windows for any hub launch (same results either way).  hub_nojoin: A's hub rows are left
+    running on the library's side stream; the caller must call hub_join() on a stream before
+    reading them (srg_hub_join)."""
     _check_panel(X, A.n_cols, "X")
     d = X.shape[1]
     if out is None:
@@ -46,7 +50,8 @@ def spmm(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor | None = None, accumul
     if out.device != A.device or X.device != A.device:
         raise ValueError("A, X and out must be on the same device")
     flags = (_lib.SRG_SPMM_ACCUMULATE if accumulate else 0) | (_lib.SRG_SPMM_NT_STORE if nt_store else 0) | \
-        (_lib.SRG_SPMM_WIDE_ROWS if wide_rows else 0)
+        (_lib.SRG_SPMM_WIDE_ROWS if wide_rows else 0) | (_lib.SRG_SPMM_HUB_W256 if hub_w256 else 0) | \
+        (_lib.SRG_SPMM_HUB_NOJOIN if hub_nojoin else 0)
     rc = _lib.lib().srg_spmm_csr_f32(A.indptr.data_ptr(), A.indices.data_ptr(), A.values.data_ptr(),
                                      A.n_rows, A.order.data_ptr() if A.n_rows else None, A.n_hub,
                                      A.n_heavy,

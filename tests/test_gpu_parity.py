@@ -490,3 +490,34 @@ def test_halo_whole_x_hop0_gather(world, ghost):
         torch.cuda.synchronize()
         assert torch.equal(panels[0][op.rows:], x.index_select(0, op.halo_ids()))
         assert torch.equal(panels[1][: op.rows], want[1][op.r0:op.r1]), f"rank {q}/{world}"
+
+
+@pytest.mark.parametrize("name", ["rand_d128_r05", "rand_d36_ppr", "cora_sym_k3"])
+def test_hub_window_256_bit_exact(name, oracle_mod):
+    """Hub workgroups with 256-nonzero windows (two per CU; the default once a launch has more hub
+    workgroups than CUs) and with 512: every row a hub row, both bit-identical to the reference."""
+    from srgnn.spmm import spmm
+    c = G.Case(name)
+    if c.x().shape[1] % 4:
+        pytest.skip("hub workgroups need d % 4 == 0")
+    A = _csr(c, (0, 0))
+    assert A.n_hub == A.n_rows
+    X = torch.from_numpy(c.x()).cuda()
+    for w256 in (True, False):
+        y = spmm(A, X, hub_w256=w256)
+        c.check_hop(1, y.cpu().numpy())
+    # rows longer than one window (several 256-windows and a partial one)
+    from srgnn.csr import DeviceCSR
+    n, deg = 40, 1500
+    rng = np.random.default_rng(5)
+    ip = np.arange(n + 1, dtype=np.int64) * deg
+    ix = rng.integers(0, 3000, n * deg).astype(np.int32)
+    vv = rng.standard_normal(n * deg).astype(np.float32)
+    x = rng.standard_normal((3000, 64)).astype(np.float32)
+    B = DeviceCSR.from_tensors(ip, ix, vv, n_cols=3000, heavy_threshold=0, hub_threshold=0, device="cuda")
+    want = None
+    for w256 in (True, False):
+        y = spmm(B, torch.from_numpy(x).cuda(), hub_w256=w256).cpu().numpy()
+        want = y if want is None else want
+        assert np.array_equal(y, want)
+    assert np.array_equal(want, oracle_mod.spmm(ip, ix, vv, x))

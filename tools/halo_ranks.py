@@ -68,6 +68,16 @@ def main():
                 torch.cuda.synchronize()
                 ms = sorted(ev[2 * r].elapsed_time(ev[2 * r + 1]) for r in range(a.reps))
                 times[name] = ms[len(ms) // 2]
+            # the hop's own launch as it issues it: hub group on its side stream beside the chunks,
+            # then the ghost rows (the per-rank compute of one hop)
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * a.reps)]
+            for r in range(a.reps):
+                ev[2 * r].record()
+                op.compute(src, dst)
+                ev[2 * r + 1].record()
+            torch.cuda.synchronize()
+            ms = sorted(ev[2 * r].elapsed_time(ev[2 * r + 1]) for r in range(a.reps))
+            times["compute"] = ms[len(ms) // 2]
             # the send-side pack (index_select of the rows peers need, per group) alone, and the
             # chunks with each group's pack on a second stream as the real hop issues it
             for name, fn in (("pack_index_select", lambda t, i: t.index_select(0, i)), ("pack", gather_rows)):
@@ -109,7 +119,8 @@ def main():
                    "max_link_rows": max(sum(op.recv_counts[g][s] for g in range(G)) for s in range(P)),
                    "halo_bytes": op.n_recv * d * 4, "send_rows": int(sum(t.numel() for t in op.send_cat)),
                    "hub_rows": op.views[op.C][1],
-                   "ms_all_serial": times["all"], "ms_hub": times["hub"], "ms_chunks": times["chunks"]}
+                   "ms_all_serial": times["all"], "ms_hub": times["hub"], "ms_chunks": times["chunks"],
+                   "ms_compute": times["compute"]}
             if a.fused:
                 # the fused pack (srg_spmm_send_f32): the chunks' kernels store the send rows themselves
                 from srgnn.spmm import spmm_send
@@ -132,12 +143,14 @@ def main():
             torch.cuda.empty_cache()
         worst = max(ranks, key=lambda r: max(r["ms_hub"], r["ms_chunks"]))
         out["worlds"][f"{P}" if a.ghost == "auto" else f"{P}/ghost{ghost}"] = {"ranks": ranks,
+                            "max_hop_compute_ms": max(r["ms_compute"] for r in ranks),
                             "max_compute_ms": max(max(r["ms_hub"], r["ms_chunks"]) for r in ranks),
                             "mean_chunks_ms": sum(r["ms_chunks"] for r in ranks) / P,
                             "worst_rank": worst["rank"],
                             "max_halo_GB": max(r["halo_bytes"] for r in ranks) / 1e9}
         W = out["worlds"][f"{P}" if a.ghost == "auto" else f"{P}/ghost{ghost}"]
-        print(f"P={P} ghost cap {ranks[0]['ghost_max_degree']}: max compute {W['max_compute_ms']:.3f} ms "
+        print(f"P={P} ghost cap {ranks[0]['ghost_max_degree']}: hop compute {W['max_hop_compute_ms']:.3f} ms, "
+              f"max compute {W['max_compute_ms']:.3f} ms "
               f"(rank {worst['rank']}: chunks {worst['ms_chunks']:.3f}, hub {worst['ms_hub']:.3f}), "
               f"mean chunks {W['mean_chunks_ms']:.3f} ms, max received halo "
               f"{W['max_halo_GB']:.2f} GB, busiest link {max(r['max_link_rows'] for r in ranks) * d * 4 / 1e9:.3f} GB; pack {worst['ms_pack']:.3f} ms alone (index_select {worst['ms_pack_index_select']:.3f}), chunks+pack "
