@@ -303,14 +303,25 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
         log(f"note: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    # one rank per GPU.  SRGNN_DIST_BACKEND=gloo rehearses the N-rank path on fewer GPUs (ranks share
+    # devices round-robin; gloo moves the halo through the host, so its numbers are not a benchmark)
+    backend = os.environ.get("SRGNN_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+
+    def init_pg():
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     if a.op == "wavelet":
         if world > 1:
-            dist.init_process_group("nccl", device_id=dev)
+            init_pg()
         return run_wavelet(a, dev, world, rank)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        init_pg()
 
     from srgnn.csr import DeviceCSR
     from srgnn.spmm import propagate, spmm

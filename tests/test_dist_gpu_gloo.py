@@ -1,0 +1,65 @@
+"""The multi-GPU hop path on GPU ranks, rehearsed on ONE GPU: 2-3 processes share cuda:0 and talk
+over gloo (RCCL refuses two ranks on one GPU; gloo moves CUDA tensors through the host).  Every
+rank runs HaloPartitionedOperator.propagate exactly as on a multi-GPU node -- the hub fork without
+join, the packs and the asynchronous all_to_all per group, ghost rows, hop 0 exchanged or gathered
+from the whole X -- and its rows of every hop must be bitwise the single-GPU propagation."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, out_path, ghost, whole_x, chunks):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [os.path.join(os.path.dirname(here), "scalable-roubust-gnn_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from srgnn import synth
+    from srgnn.csr import DeviceCSR
+    from srgnn.dist import HaloPartitionedOperator
+    from srgnn.normalize import sym_norm_binary
+    from srgnn.spmm import propagate
+    dev = torch.device("cuda", 0)
+    n, K = 30000, 4
+    u, v = synth.rmat_undirected_t(n, 240000, seed=31, device=dev)
+    ip, ix = synth.symmetric_csr_t(n, u, v)
+    ip, ix, vals = sym_norm_binary(ip, ix, n, 0.5)
+    x = synth.uniform_features_t(n, 64, device=dev)
+    want = propagate(DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, device=dev), x, K)
+    op = HaloPartitionedOperator(ip, ix, vals, n, chunks=chunks, hub_threshold=400, device=dev,
+                                 ghost_max_degree=ghost)
+    ok = op.views[op.C][1] > 0 and (ghost is None or (op.n_ghost > 0) == (ghost > 0))
+    panels = [op.new_panel(64) for _ in range(K + 1)]
+    panels[0][: op.rows].copy_(x[op.r0:op.r1])
+    for _ in range(2):                          # twice: buffers and the hub side stream reused
+        op.propagate(panels[0], K, panels=panels, x_full=x if whole_x else None)
+    torch.cuda.synchronize()
+    ok = ok and all(torch.equal(panels[k][: op.rows], want[k][op.r0:op.r1]) for k in range(K + 1))
+    flags = [None] * world
+    dist.all_gather_object(flags, bool(ok))
+    if rank == 0:
+        np.save(out_path, np.array(flags))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,ghost,whole_x,chunks", [(2, None, False, 3), (3, 0, False, 2), (2, 16, True, 4),
+                                                         (3, None, True, 6)])
+def test_halo_hop_on_gpu_ranks_bitwise(tmp_path, world, ghost, whole_x, chunks):
+    out = str(tmp_path / "flags.npy")
+    mp.spawn(_worker, args=(world, _free_port(), out, ghost, whole_x, chunks), nprocs=world, join=True)
+    flags = np.load(out)
+    assert flags.all(), f"ranks disagree with one GPU: {flags.tolist()}"
