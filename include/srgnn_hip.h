@@ -195,13 +195,6 @@ int srg_segment_sum_f64(const int64_t* seg_ptr, const double* vals, int64_t n_se
 int srg_gather_rows_f32(const float* src, int64_t lds, int64_t n_src, const int64_t* idx, int64_t n_idx,
                         float* dst, int64_t ldd, int32_t d, void* stream);
 
-/* Scheduling helper for a hub launch issued on ANOTHER stream than the launches that follow it
- * (srgnn/dist.py: the halo exchange's hub group beside its row chunks): a single-wave kernel that
- * holds `stream` for the hub dispatch delay (10 us, SRGNN_HUB_DISPATCH_DELAY_US), so that the hub
- * workgroups (139 KB of LDS each) reach CUs before the next launch on `stream` fills them.
- * srg_spmm_csr_f32 does the same internally when it forks its own hub rows. */
-int srg_hub_dispatch_delay(void* stream);
-
 /* `stream` waits (on the device, not the host) for the hub workgroups of the last
  * SRG_SPMM_HUB_NOJOIN launch on the current device; no-op if none was forked. */
 int srg_hub_join(void* stream);

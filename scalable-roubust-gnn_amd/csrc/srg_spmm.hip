@@ -1556,15 +1556,6 @@ int srg_gather_rows_f32(const float* src, int64_t lds, int64_t n_src, const int6
     return ok();
 }
 
-int srg_hub_dispatch_delay(void* stream)
-{
-    if (hub_delay_us() > 0) {
-        hipLaunchKernelGGL(k_dispatch_delay, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream), hub_delay_us());
-        SRG_HIP_CHECK(hipGetLastError());
-    }
-    return ok();
-}
-
 int srg_hub_join(void* stream)
 {
     int dev = 0;

@@ -47,7 +47,6 @@ EXPORTED_SYMBOLS = (
     "srg_tail_rowsum_f32",
     "srg_segment_sum_f64",
     "srg_gather_rows_f32",
-    "srg_hub_dispatch_delay",
     "srg_hub_join",
     "srg_csr_validate",
     "srg_last_error",
@@ -102,8 +101,6 @@ def _declare(lib):
     lib.srg_segment_sum_f64.restype = ctypes.c_int
     lib.srg_gather_rows_f32.argtypes = [_p, _i64, _i64, _p, _i64, _p, _i64, _i32, _p]
     lib.srg_gather_rows_f32.restype = ctypes.c_int
-    lib.srg_hub_dispatch_delay.argtypes = [_p]
-    lib.srg_hub_dispatch_delay.restype = ctypes.c_int
     lib.srg_hub_join.argtypes = [_p]
     lib.srg_hub_join.restype = ctypes.c_int
     lib.srg_csr_validate.argtypes = [_p, _p, _i64, _i64, _i64, _p]
