@@ -275,6 +275,9 @@ class HaloPartitionedOperator:
             cb = _chunk_bounds(lip, C)
             for c in range(C):
                 grp[s0 + cb[c]:s0 + cb[c + 1]] = c
+            if q == p:
+                # local row range of each chunk (its hub rows included: they belong to group C)
+                self.chunk_ranges = [(cb[c], cb[c + 1]) for c in range(C)]
         grp[is_hub] = C
         self.n_groups = C + 1
         G = self.n_groups
@@ -592,6 +595,42 @@ class HaloPartitionedOperator:
             if item is not None:
                 item[0].wait()        # the current stream waits for RCCL's stream (the CPU does not)
 
+    def hop_with_epilogue(self, src: torch.Tensor, dst: torch.Tensor, epilogue):
+        """One exchange step whose own rows are finished by epilogue(a, b), an element-wise function
+        of rows [a, b) of the SpMM output (the Chebyshev recurrence of HaloWaveletFilter), before
+        peers receive them.  On the launch stream: the hub group forked (joined after chunk 0's
+        kernel, which it runs beside), then per chunk c its kernel, the epilogue over its row range
+        (hub rows in it included), its pack and an asynchronous all_to_all; the hub group's
+        exchange last; the stream waits for the collectives at the end.  GPU ranks with the HIP
+        kernels (no ghost rows: the epilogue covers own rows only)."""
+        if not (self._hip and self.world > 1 and not self.virtual) or self.n_ghost:
+            raise RuntimeError("hop_with_epilogue needs real GPU ranks with the HIP kernels and no ghost rows")
+        from . import _lib
+        from .spmm import spmm
+        out = dst[: self.rows]
+        C = self.C
+        fork = bool(self.views[C][1] and self.views[C][3])
+        if self.views[C][1]:
+            if fork:
+                spmm(self._A[C], src, out=out, hub_nojoin=True)
+            else:
+                self._spmm(self._A[C], src, out)
+        pending = []
+        for c in range(C):
+            if self.views[c][1]:
+                self._spmm(self._A[c], src, out)
+            if c == 0 and fork:
+                _lib.check(_lib.lib().srg_hub_join(torch.cuda.current_stream(self.device).cuda_stream),
+                           "srg_hub_join")
+            a, b = self.chunk_ranges[c]
+            if b > a:
+                epilogue(a, b)
+            pending.append(self._exchange_group(dst, c, async_op=True))
+        pending.append(self._exchange_group(dst, C, async_op=True))
+        for item in pending:
+            if item is not None:
+                item[0].wait()
+
     def halo_ids(self) -> torch.Tensor:
         """Global row ids of the panel's halo rows, in panel order (received, then ghosts)."""
         return self._halo_ids
@@ -718,29 +757,47 @@ class HaloWaveletFilter:
         self.coeffs = np.stack([heat_cheby_coeffs(t, self.lmax, order) for t in self.taus])
         self.rows, self.r0, self.r1 = self.opL.rows, self.opL.r0, self.opL.r1
         self._epi = epilogue or _epilogue_device
+        self.overlap = True      # real GPU ranks: each order's exchange overlapped chunk by chunk
 
     def new_panel(self, d):
         return self.opL.new_panel(d)
 
+    def _order(self, op, src, dst, epi, exchange: bool) -> bool:
+        """One Chebyshev order: dst = op @ src on the own rows, finished by epi(a, b) over row
+        ranges.  Real GPU ranks overlap it with dst's halo exchange chunk by chunk
+        (hop_with_epilogue); otherwise the whole epilogue runs after the SpMM and the caller
+        exchanges.  Returns whether the caller still has to exchange dst's halo."""
+        if exchange and op._hip and op.world > 1 and not op.virtual and self.overlap:
+            op.hop_with_epilogue(src, dst, epi)
+            return False
+        op.compute(src, dst)
+        epi(0, self.rows)
+        return exchange
+
     def steps(self, S_panel, work, R):
-        """Generator over the orders: yields after each order's local compute + epilogue with the
-        panel whose halo must be exchanged next (the caller exchanges it).  S_panel's halo must
-        already be filled; work = three [rows + halo, d] panels; R = [ns, rows, d]."""
+        """Generator over the orders: yields after an order's local compute + epilogue with the
+        panel whose halo the caller must exchange next (on real GPU ranks the orders exchange
+        their own halo, overlapped, and nothing is yielded).  S_panel's halo must already be
+        filled; work = three [rows + halo, d] panels; R = [ns, rows, d]."""
         ns, nc = self.coeffs.shape
-        r = self.rows
         t_old, t_cur = S_panel, work[0]
         free = list(work[1:])
-        self.opL.compute(S_panel, t_cur)
-        self._epi(t_cur[:r], S_panel[:r], None, 0, self.a1, self.a2, self.coeffs[:, 0], self.coeffs[:, 1], R)
-        yield t_cur
+        a1, a2, cf = self.a1, self.a2, self.coeffs
+
+        def epi_first(a, b, t=t_cur):
+            self._epi(t[a:b], S_panel[a:b], None, 0, a1, a2, cf[:, 0], cf[:, 1], R[:, a:b])
+        if self._order(self.opL, S_panel, t_cur, epi_first, exchange=nc > 2):
+            yield t_cur
         for k in range(2, nc):
             t_new = free.pop()
-            self.opF.compute(t_cur, t_new)
-            self._epi(t_new[:r], None, t_old[:r], 1, self.a1, self.a2, None, self.coeffs[:, k], R)
+
+            def epi_k(a, b, t=t_new, o=t_old, k=k):
+                self._epi(t[a:b], None, o[a:b], 1, a1, a2, None, cf[:, k], R[:, a:b])
+            more = self._order(self.opF, t_cur, t_new, epi_k, exchange=k + 1 < nc)
             if t_old is not S_panel:
                 free.append(t_old)
             t_old, t_cur = t_cur, t_new
-            if k + 1 < nc:
+            if more:
                 yield t_cur
 
     def apply(self, S_local: torch.Tensor) -> torch.Tensor:
