@@ -465,6 +465,14 @@ def main():
     peak = roofline.MI355X_HBM_PEAK_GBS
     traffic = pmc_traffic(a.config) if world == 1 else None
 
+    exchange_stats = {}
+    if world > 1 and a.exchange == "halo":
+        # per-hop exchange volume: max over ranks of the rows received and of the busiest peer link
+        link = max(sum(op.recv_counts[g][q] for g in range(op.n_groups)) for q in range(world))
+        st = torch.tensor([op.n_recv, link, op.n_ghost], dtype=torch.float64, device=dev)
+        dist.all_reduce(st, op=dist.ReduceOp.MAX)
+        exchange_stats = {"halo_rows_received_max": int(st[0]), "busiest_link_GB_per_hop": float(st[1]) * d * 4 / 1e9,
+                          "ghost_rows_max": int(st[2]), "halo_groups": op.n_groups}
     value = a.steps * K * nnz / dt
     res = {
         "metric": "propagated edges/sec (K-hop SpMM precompute)",
@@ -489,7 +497,8 @@ def main():
                    "outputs": ("all K+1 hop panels" if mode in ("panels", "auto") else
                                f"fused {a.aggregate} of hops 0..K (srgnn.aggregate, bit-exact vs the reference combine)"
                                if a.aggregate else "last hop only (2 ping-pong panels)")
-                   if world == 1 else "all K+1 hop panels (row slices)"},
+                   if world == 1 else "all K+1 hop panels (row slices)",
+                   **exchange_stats},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
                      "frac": achieved / peak, "traffic": traffic,
                      "kernel": "k_spmm (+ k_spmm_hub beside it): one hop" + (" of rank 0's rows" if world > 1 else ""),
