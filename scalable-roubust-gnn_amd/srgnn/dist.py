@@ -5,9 +5,9 @@ Rank p owns the contiguous row block [starts[p], starts[p+1]) of Â (blocks bala
 and the same rows of every hop panel.  Two exchanges:
 
 * HaloPartitionedOperator (default): each rank receives only the remote rows its own rows
-  reference, group by group (nnz-balanced row chunks + the hub rows), with one all_to_all_single
-  per group on a communication stream as soon as that group's kernel is done -- overlapping the
-  later groups' kernels.  Low-degree halo rows whose neighbours are all local ("ghost rows") are
+  reference, group by group (nnz-balanced row chunks + the hub rows), with one asynchronous
+  all_to_all_single per group issued as soon as that group's kernel is done -- RCCL runs it on its
+  own stream while the later groups compute.  Low-degree halo rows whose neighbours are all local ("ghost rows") are
   computed on the rank that needs them instead of received (the same CSR row, so the same bits):
   a pair of GPUs shares one xGMI link, and on power-law graphs most of the halo is such rows.
   HaloWaveletFilter runs the wavelet basis' Chebyshev recurrence on the same plan (one exchange per
@@ -231,10 +231,11 @@ class HaloPartitionedOperator:
         (source, id)], and the local operator (own rows and ghost rows) with its column ids
         remapped into it (each row's entries keep their CSR order, so every output element is the
         same fma chain as on one GPU).
-    Per hop k: the groups' kernels write the own part of panel k+1 (hub group on its own stream),
-    and as each group completes its rows that peers need are packed and exchanged with one
-    all_to_all_single (RCCL) on a communication stream, overlapping the next groups' kernels and
-    the ghost rows' kernel.  Only X's first exchange also carries the ghost rows.
+    Per hop k, all on the launch stream: the hub group's workgroups are forked onto the library's
+    hub side stream, the row chunks write the own part of panel k+1, and after each chunk its rows
+    that peers need are packed and sent with an asynchronous all_to_all_single (RCCL, overlapping
+    the next chunks and the ghost rows' kernel); the hub group is joined and exchanged last, and
+    the stream waits for the collectives.  Only X's first exchange also carries the ghost rows.
     """
 
     def __init__(self, indptr, indices, values, n: int, group=None, chunks: int = 4,

@@ -38,8 +38,8 @@ def spmm(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor | None = None, accumul
     """out[r, :] (+)= A[r, :] @ X  for the rows of A (one hop; exact fma chains in CSR order).
     wide_rows: diagnostic, one row per wave also for d <= 32; hub_w256: diagnostic, 256-nonzero
     hub windows for any hub launch (same results either way).  hub_nojoin: A's hub rows are left
-    running on the library's side stream; the caller must call hub_join() on a stream before
-    reading them (srg_hub_join)."""
+    running on the library's side stream; the caller must make a stream wait for them
+    (srg_hub_join) before reading them."""
     _check_panel(X, A.n_cols, "X")
     d = X.shape[1]
     if out is None:

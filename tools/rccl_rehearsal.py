@@ -4,7 +4,7 @@
 Launched by torchrun with P ranks, one per GPU (LOCAL_RANK).  It needs P GPUs: RCCL refuses two
 ranks on one card ("Duplicate GPU detected", seen on the one-GPU box), so on one GPU the N > 1 path
 is covered by the gloo tests and the virtual-rank GPU tests instead.  Every rank checks its rows of
-  * HaloPartitionedOperator.propagate (grouped all_to_all_single on the comm stream; ghost rows
+  * HaloPartitionedOperator.propagate (asynchronous all_to_all_single per group; ghost rows
     off, automatic and forced),
   * RowPartitionedOperator.propagate (all_gather_into_tensor),
   * HaloWaveletFilter.apply,
