@@ -240,7 +240,7 @@ class HaloPartitionedOperator:
 
     def __init__(self, indptr, indices, values, n: int, group=None, chunks: int = 4,
                  heavy_threshold=None, hub_threshold=None, device=None, rank=None, world=None,
-                 local_spmm=None, ghost_max_degree=None):
+                 local_spmm=None, ghost_max_degree=None, hub_launches=None):
         from .csr import DEFAULT_HEAVY_THRESHOLD, DEFAULT_HUB_THRESHOLD, auto_hub_threshold
         self.group = group
         self.virtual = rank is not None
@@ -263,7 +263,7 @@ class HaloPartitionedOperator:
         thr = torch.empty(P, dtype=torch.int64, device=dev)
         for q in range(P):
             nnz_q = int(gip[self.starts[q + 1]] - gip[self.starts[q]])
-            thr[q] = auto_hub_threshold(nnz_q, launches=max(1, int(chunks))) if hub_threshold is None else (
+            thr[q] = auto_hub_threshold(nnz_q, launches=max(1, int(hub_launches or chunks))) if hub_threshold is None else (
                 hub_threshold if hub_threshold >= 0 else (1 << 62))
         is_hub = deg > thr[owner]
         # chunk of every row (contiguous nnz-balanced ranges inside each owner's block)

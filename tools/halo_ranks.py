@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--d", type=int, default=None, help="feature width (default: the config's)")
     ap.add_argument("--fused", action="store_true", help="also time the opt-in fused pack (srg_spmm_send_f32)")
+    ap.add_argument("--hub-launches", type=int, default=None,
+                    help="launch count the hub threshold assumes (default: the chunk count)")
     ap.add_argument("--ghost", default="auto",
                     help="ghost row degree cap(s): 'auto' (the operator's cost model) or a comma list")
     a = ap.parse_args()
@@ -46,7 +48,7 @@ def main():
         ranks = []
         for q in range(P):
             op = HaloPartitionedOperator(ip, ix, vals, n, chunks=a.chunks, device=dev, rank=q, world=P,
-                                         ghost_max_degree=ghost)
+                                         ghost_max_degree=ghost, hub_launches=a.hub_launches)
             src = op.new_panel(d)
             src[: op.rows].copy_(x[op.r0:op.r1])
             src[op.rows:].uniform_(-1, 1)
