@@ -25,10 +25,18 @@ import torch
 import torch.distributed as dist
 
 
-def balanced_row_starts(indptr: torch.Tensor, parts: int):
-    """Row boundaries [0 = s_0 <= ... <= s_P = n] splitting the nonzeros as evenly as rows allow."""
+def balanced_row_starts(indptr: torch.Tensor, parts: int, giant_weight: float = 0.0, giant_threshold=None):
+    """Row boundaries [0 = s_0 <= ... <= s_P = n] splitting the nonzeros as evenly as rows allow.
+    giant_weight > 0: rows longer than giant_threshold count (1 + giant_weight) times their length,
+    so the rank holding a giant row (a latency-bound chain beside its other rows) gets fewer of
+    the others."""
     ip = indptr.to(torch.int64).cpu()
     n = ip.numel() - 1
+    if giant_weight > 0 and n > 0:
+        deg = ip[1:] - ip[:-1]
+        thr = int(giant_threshold) if giant_threshold is not None else max(2048, int(ip[-1]) // (1024 * parts))
+        extra = torch.where(deg > thr, (deg.double() * giant_weight).round().to(torch.int64), torch.zeros_like(deg))
+        ip = ip + torch.cat([torch.zeros(1, dtype=torch.int64), torch.cumsum(extra, 0)])
     nnz = int(ip[-1])
     targets = torch.tensor([(nnz * p) // parts for p in range(parts + 1)], dtype=torch.int64)
     starts = torch.searchsorted(ip, targets, right=False).clamp_(0, n)
@@ -148,6 +156,10 @@ def _chunk_bounds(indptr_local: torch.Tensor, chunks: int):
     return balanced_row_starts(indptr_local, chunks)
 
 
+# partition: rows longer than nnz / (1024 P) count (1 + GIANT_WEIGHT) times their length (0: plain
+# nnz balance)
+GIANT_WEIGHT = 0.0
+
 # ghost rows: candidates are scanned up to this degree; the automatic cap is chosen among these
 GHOST_SCAN_MAX = 64
 GHOST_CAPS = (0, 1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64)
@@ -240,7 +252,7 @@ class HaloPartitionedOperator:
 
     def __init__(self, indptr, indices, values, n: int, group=None, chunks: int = 4,
                  heavy_threshold=None, hub_threshold=None, device=None, rank=None, world=None,
-                 local_spmm=None, ghost_max_degree=None, hub_launches=None):
+                 local_spmm=None, ghost_max_degree=None, hub_launches=None, giant_weight=None):
         from .csr import DEFAULT_HEAVY_THRESHOLD, DEFAULT_HUB_THRESHOLD, auto_hub_threshold
         self.group = group
         self.virtual = rank is not None
@@ -252,7 +264,8 @@ class HaloPartitionedOperator:
         self.n = n
         gip = indptr.to(dev, torch.int64)
         gix = indices.to(dev)
-        self.starts = balanced_row_starts(gip, P)
+        self.giant_weight = GIANT_WEIGHT if giant_weight is None else float(giant_weight)
+        self.starts = balanced_row_starts(gip, P, giant_weight=self.giant_weight if P > 1 else 0.0)
         st = torch.tensor(self.starts, dtype=torch.int64, device=dev)
         self.nnz_total = int(gip[-1])
         deg = gip[1:] - gip[:-1]

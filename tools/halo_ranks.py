@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--fused", action="store_true", help="also time the opt-in fused pack (srg_spmm_send_f32)")
     ap.add_argument("--hub-launches", type=int, default=None,
                     help="launch count the hub threshold assumes (default: the chunk count)")
+    ap.add_argument("--giant-weight", type=float, default=None,
+                    help="partition weight of giant rows (default: srgnn.dist.GIANT_WEIGHT)")
     ap.add_argument("--ghost", default="auto",
                     help="ghost row degree cap(s): 'auto' (the operator's cost model) or a comma list")
     a = ap.parse_args()
@@ -48,7 +50,8 @@ def main():
         ranks = []
         for q in range(P):
             op = HaloPartitionedOperator(ip, ix, vals, n, chunks=a.chunks, device=dev, rank=q, world=P,
-                                         ghost_max_degree=ghost, hub_launches=a.hub_launches)
+                                         ghost_max_degree=ghost, hub_launches=a.hub_launches,
+                                         giant_weight=a.giant_weight)
             src = op.new_panel(d)
             src[: op.rows].copy_(x[op.r0:op.r1])
             src[op.rows:].uniform_(-1, 1)
