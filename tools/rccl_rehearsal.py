@@ -34,9 +34,17 @@ def main():
     world = int(os.environ["WORLD_SIZE"])
     rank = int(os.environ["RANK"])
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # SRGNN_DIST_BACKEND=gloo: a dry run of this script with ranks sharing the GPUs there are
+    # (gloo through the host; RCCL refuses two ranks on one GPU)
+    backend = os.environ.get("SRGNN_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    dist.init_process_group("nccl", device_id=dev)
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=dev)
+    else:
+        dist.init_process_group(backend)
     n, e, d, K = 60000, 700000, 64, 4
     ip, ix, vals, n, d, _ = graphs.build("arxiv", dev, n=n, n_edges=e, d=d)
     X = synth.uniform_features_t(n, d, device=dev)
