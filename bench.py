@@ -388,7 +388,8 @@ def main():
         op = HaloPartitionedOperator(ip, ix, vals, n, chunks=a.chunks, heavy_threshold=a.heavy_threshold,
                                      device=dev, ghost_max_degree=a.ghost_max_degree)
         log(f"rank {rank}: rows={op.rows} nnz={op.nnz_local} halo={op.halo} (received {op.n_recv}, "
-            f"ghosts {op.n_ghost} <= degree {op.ghost_max_degree}, {op._ghost_pos.numel()} ghost nnz) "
+            f"ghosts {op.n_ghost} <= degree {op.ghost_max_degree}, {op._ghost_pos.numel()} ghost nnz; "
+            f"link {op.link_bps / 1e9:.1f} GB/s) "
             f"hub_rows={op.views[-1][1]} groups={op.n_groups}")
         panels = [op.new_panel(d) for _ in range(K + 1)]
         panels[0][: op.rows].copy_(X[op.r0:op.r1])
@@ -472,7 +473,8 @@ def main():
         st = torch.tensor([op.n_recv, link, op.n_ghost], dtype=torch.float64, device=dev)
         dist.all_reduce(st, op=dist.ReduceOp.MAX)
         exchange_stats = {"halo_rows_received_max": int(st[0]), "busiest_link_GB_per_hop": float(st[1]) * d * 4 / 1e9,
-                          "ghost_rows_max": int(st[2]), "halo_groups": op.n_groups}
+                          "ghost_rows_max": int(st[2]), "halo_groups": op.n_groups,
+                          "link_GBps_measured_for_ghost_plan": op.link_bps / 1e9}
     value = a.steps * K * nnz / dt
     res = {
         "metric": "propagated edges/sec (K-hop SpMM precompute)",

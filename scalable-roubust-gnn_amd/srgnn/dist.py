@@ -203,11 +203,36 @@ def _ghost_candidates(gip, gix, deg, halo, s0: int, s1: int, n: int, max_degree:
     return ok
 
 
-def ghost_plan(halos, elig, deg, owner, gip, starts, caps=GHOST_CAPS):
+def measure_link_bps(group=None, device=None, mbytes_per_peer: int = 32, reps: int = 3) -> float:
+    """Per-link rate of this process group's all_to_all: every rank sends `mbytes_per_peer` to every
+    peer at once (as the halo exchange does), timed over `reps` calls after one warm-up; the
+    minimum over ranks (all_reduce), so every rank gets the same number.  Bytes per second per
+    peer link and direction."""
+    import time
+    P = dist.get_world_size(group)
+    n = max(1, mbytes_per_peer * (1 << 20) // 4)
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    send = torch.ones(P * n, dtype=torch.float32, device=dev)
+    recv = torch.empty_like(send)
+    dist.all_to_all_single(recv, send, group=group)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        dist.all_to_all_single(recv, send, group=group)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    rate = torch.tensor([n * 4 * reps / max(time.perf_counter() - t0, 1e-9)], dtype=torch.float64, device=dev)
+    dist.all_reduce(rate, op=dist.ReduceOp.MIN, group=group)
+    return float(rate.item())
+
+
+def ghost_plan(halos, elig, deg, owner, gip, starts, caps=GHOST_CAPS, link_bps=None):
     """The ghost degree cap minimising the modelled hop time max over ranks q of
-    max(q's SpMM incl. ghosts, q's busiest peer link), with the rates GHOST_GATHER_BPS /
-    GHOST_LINK_BPS.  Returns (cap, {cap: modelled seconds per byte of row}).  Deterministic
-    from the global plan, so every rank picks the same cap."""
+    max(q's SpMM incl. ghosts, q's busiest peer link), with the rates GHOST_GATHER_BPS and
+    `link_bps` (default GHOST_LINK_BPS).  Returns (cap, {cap: modelled seconds per byte of row}).
+    Deterministic from the global plan and the rates, so every rank picks the same cap."""
+    link_bps = GHOST_LINK_BPS if link_bps is None else float(link_bps)
     P = len(halos)
     model = {}
     for c in caps:
@@ -219,7 +244,7 @@ def ghost_plan(halos, elig, deg, owner, gip, starts, caps=GHOST_CAPS):
             nnz_q = int(gip[starts[q + 1]] - gip[starts[q]]) + int(dh[gmask].sum())
             recv = torch.bincount(owner[h[~gmask]], minlength=P)
             link = int(recv.max()) if recv.numel() else 0
-            worst = max(worst, nnz_q / GHOST_GATHER_BPS, link / GHOST_LINK_BPS)
+            worst = max(worst, nnz_q / GHOST_GATHER_BPS, link / link_bps)
         model[c] = worst
     best = min(caps, key=lambda c: (model[c], c))
     return best, model
@@ -252,7 +277,8 @@ class HaloPartitionedOperator:
 
     def __init__(self, indptr, indices, values, n: int, group=None, chunks: int = 4,
                  heavy_threshold=None, hub_threshold=None, device=None, rank=None, world=None,
-                 local_spmm=None, ghost_max_degree=None, hub_launches=None, giant_weight=None):
+                 local_spmm=None, ghost_max_degree=None, hub_launches=None, giant_weight=None,
+                 calibrate_link: bool = True):
         from .csr import DEFAULT_HEAVY_THRESHOLD, DEFAULT_HUB_THRESHOLD, auto_hub_threshold
         self.group = group
         self.virtual = rank is not None
@@ -316,8 +342,13 @@ class HaloPartitionedOperator:
             halos.append(hq)
             elig.append(_ghost_candidates(gip, gix, deg, hq, self.starts[q], self.starts[q + 1], n,
                                           GHOST_SCAN_MAX if ghost_max_degree is None else ghost_max_degree))
+        self.link_bps = GHOST_LINK_BPS
         if ghost_max_degree is None:
-            ghost_max_degree = ghost_plan(halos, elig, deg, owner, gip, self.starts)[0]
+            # the link rate the model uses: measured on this group's all_to_all when there is one
+            # (every rank gets the same minimum, so the same cap), else the assumed constant
+            if calibrate_link and P > 1 and not self.virtual and dist.is_initialized():
+                self.link_bps = measure_link_bps(group, dev)
+            ghost_max_degree = ghost_plan(halos, elig, deg, owner, gip, self.starts, link_bps=self.link_bps)[0]
         self.ghost_max_degree = int(ghost_max_degree)
         ghosts = [e & (deg[h] <= self.ghost_max_degree) for h, e in zip(halos, elig)]
         need = halos[p][~ghosts[p]]                                  # received: (group, source, id)
