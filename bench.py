@@ -55,9 +55,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--nt-store", action="store_true")
     ap.add_argument("--exchange", default="halo", choices=["halo", "allgather"])
-    ap.add_argument("--chunks", type=int, default=6,
-                    help="halo exchange groups per hop (row chunks; 4-8 cost the same compute, more "
-                         "chunks shorten the last group's exposed exchange)")
+    ap.add_argument("--chunks", type=int, default=None,
+                    help="halo exchange groups per hop (row chunks; default 4 at 2 GPUs, 6 above: the "
+                         "hop compute is within 3 %% over 2-8 chunks, more chunks shorten the last "
+                         "group's exposed exchange)")
     ap.add_argument("--exchange-x", action="store_true",
                     help="halo exchange: receive hop 0's halo (X) from its owners instead of gathering "
                          "it from the whole X every rank holds")
@@ -260,7 +261,7 @@ def run_wavelet_dist(a, dev, world, rank):
     ip, ix, lv, n, d, lmax = graphs.build_laplacian(a.config, dev, d=a.d)
     nnz = int(ix.numel())
     order = 3
-    f = HaloWaveletFilter(ip, ix, lv, n, [-0.5, 0.5], order=order, lmax=lmax, chunks=a.chunks,
+    f = HaloWaveletFilter(ip, ix, lv, n, [-0.5, 0.5], order=order, lmax=lmax, chunks=(a.chunks or (4 if world <= 2 else 6)),
                           heavy_threshold=a.heavy_threshold, device=dev)
     X = synth.uniform_features_t(n, d, seed=synth.FEATURE_SEED, device=dev)
     S_local = X[f.r0:f.r1].contiguous()
@@ -385,7 +386,7 @@ def main():
         local_rows, local_nnz = op.rows, op.nnz_local
     else:
         from srgnn.dist import HaloPartitionedOperator
-        op = HaloPartitionedOperator(ip, ix, vals, n, chunks=a.chunks, heavy_threshold=a.heavy_threshold,
+        op = HaloPartitionedOperator(ip, ix, vals, n, chunks=(a.chunks or (4 if world <= 2 else 6)), heavy_threshold=a.heavy_threshold,
                                      device=dev, ghost_max_degree=a.ghost_max_degree)
         log(f"rank {rank}: rows={op.rows} nnz={op.nnz_local} halo={op.halo} (received {op.n_recv}, "
             f"ghosts {op.n_ghost} <= degree {op.ghost_max_degree}, {op._ghost_pos.numel()} ghost nnz; "
