@@ -147,6 +147,34 @@ def test_accumulate_and_nt_store_flags(oracle_mod):
         np.testing.assert_array_equal(Y.cpu().numpy(), ref, err_msg=str(thr))
 
 
+@pytest.mark.parametrize("thr", THRESHOLDS)
+@pytest.mark.parametrize("name", ["rand_d128_r05", "cora_sym_k3", "rand_d7_r03"])
+def test_column_blocked_chain_continuation(name, thr):
+    """ACCUMULATE continues a row's fma chain from the stored fp32 value: Â's columns are sorted
+    (utils.py:81-93), so running the entries of B column blocks in ascending order (block 0 from
+    +0.0f, the rest with ACCUMULATE) is bitwise the one-pass hop and so the reference's product
+    (tools/colblock_probe.py measures this form at full size)."""
+    from srgnn.csr import DeviceCSR
+    from srgnn.spmm import spmm
+    c = G.Case(name)
+    ip, ix, v = (np.asarray(a) for a in c.ahat())
+    assert all(np.all(np.diff(ix[ip[i]:ip[i + 1]]) > 0) for i in range(c.n))
+    X = torch.from_numpy(c.x()).cuda()
+    heavy, hub = thr
+    row = np.repeat(np.arange(c.n), np.diff(ip))
+    for B in (2, 3, 7):
+        blk = (ix.astype(np.int64) * B) // c.n
+        Y = torch.empty_like(X)
+        for b in range(B):
+            m = blk == b
+            bip = np.concatenate([[0], np.cumsum(np.bincount(row[m], minlength=c.n))])
+            Ab = DeviceCSR.from_tensors(bip, ix[m], v[m], n_cols=c.n, heavy_threshold=heavy,
+                                        hub_threshold=hub, device="cuda")
+            spmm(Ab, X, out=Y, accumulate=b > 0)
+        torch.cuda.synchronize()
+        c.check_hop(1, Y.cpu().numpy())
+
+
 def test_strided_panels_and_row_blocks(oracle_mod):
     """Leading dimensions > d and a row block with rebased indptr (the multi-GPU layout)."""
     from srgnn.spmm import spmm

@@ -87,3 +87,22 @@ def test_aggregation_plan_equals_reference_message_ops(oracle_mod, name):
         else:
             out = run_steps_np(AG.combine_steps(mode, terms, div), hops, c.n, hops[0].shape[1])
         c.check_output(key, out)
+
+
+@pytest.mark.parametrize("name", ["rand_d128_r05", "cora_sym_k3", "rand_d7_r03"])
+def test_column_blocked_chain_continuation_oracle(oracle_mod, name):
+    """The exactness argument behind tools/colblock_probe.py, on the reference's own hops: with
+    sorted columns, B ascending column-block passes (the first from +0.0f, the rest accumulating
+    into the stored fp32 partial) reproduce the reference's one-pass product bit for bit."""
+    c = G.Case(name)
+    ip, ix, v = (np.asarray(a) for a in c.ahat())
+    x = c.x()
+    row = np.repeat(np.arange(c.n), np.diff(ip))
+    for B in (2, 5):
+        blk = (ix.astype(np.int64) * B) // c.n
+        y = None
+        for b in range(B):
+            m = blk == b
+            bip = np.concatenate([[0], np.cumsum(np.bincount(row[m], minlength=c.n))])
+            y = oracle_mod.spmm(bip, ix[m], v[m].astype(np.float32), x, out=y, accumulate=b > 0)
+        c.check_hop(1, y)
