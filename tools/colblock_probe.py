@@ -9,6 +9,8 @@ one-pass hop (checked here).  Each pass gathers only from an X slice of n/B rows
 Infinity Cache once B is large enough; the price is one extra read + write of Y per extra pass.
 
     python tools/colblock_probe.py [--config products] [--blocks 1,2,3,4,5,6,8] [--reps 7]  -> JSON
+
+A block count may repeat (--blocks 1,2,1,2): ms_per_hop keeps one median per occurrence.
 """
 import argparse
 import json
@@ -75,12 +77,12 @@ def main():
     Y = torch.empty_like(x)
     for B in [int(s) for s in a.blocks.split(",")]:
         As = column_blocks(ip, ix, vals, n, B)
-        res["ms_per_hop"][B] = time_blocks(As, x, Y if B > 1 else Y1, a.reps)
+        res["ms_per_hop"].setdefault(B, []).append(time_blocks(As, x, Y if B > 1 else Y1, a.reps))
         if B > 1:
             res["bitwise_equal"][B] = bool(torch.equal(Y, Y1))
         del As
         torch.cuda.empty_cache()
-        print(json.dumps({"B": B, "ms": res["ms_per_hop"][B], "eq": res["bitwise_equal"].get(B)}), flush=True)
+        print(json.dumps({"B": B, "ms": res["ms_per_hop"][B][-1], "eq": res["bitwise_equal"].get(B)}), flush=True)
     print(json.dumps(res), flush=True)
 
 
