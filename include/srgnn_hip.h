@@ -20,7 +20,12 @@
  *   - CSR: int64 row pointers (nnz may exceed 2^31), int32 column ids, row-major dense panels with
  *     explicit leading dimensions (64-bit element offsets: N*d may exceed 2^31).
  *   - Column ids are trusted on (B): validate a matrix once with srg_csr_validate() before use.
- *   - `stream` is a hipStream_t passed as void* (NULL = the null stream).
+ *   - `stream` is a hipStream_t passed as void* (NULL = the null stream).  Every launch of an entry
+ *     goes to the device `stream` belongs to (the current device for the null stream); the entry
+ *     makes that device current for its duration and restores the caller's afterwards.
+ *   - Threads: entries may be called concurrently from several host threads.  Hub rows fork onto a
+ *     library-owned side stream per (device, caller stream) with its own fork / join events; the
+ *     fork sequence is serialised by a library mutex.
  */
 #ifndef SRGNN_HIP_H_
 #define SRGNN_HIP_H_
@@ -49,11 +54,11 @@ extern "C" {
 /* Diagnostic: hub workgroups always use 256-nonzero windows (72 KB of LDS, two per CU).  By default
  * they do only when a launch has more hub workgroups than CUs.  Results are identical either way. */
 #define SRG_SPMM_HUB_W256 0x8
-/* The hub rows' workgroups are forked onto the library's per-device hub side stream and NOT
- * joined back into `stream` before the call returns: later launches on `stream` run beside them
- * (srgnn/dist.py issues the halo row chunks there).  The caller must srg_hub_join() a stream
- * before anything reads the hub rows, and before the next NOJOIN fork on the device (one
- * outstanding fork per device). */
+/* The hub rows' workgroups are forked onto the library's hub side stream of (device, `stream`) and
+ * NOT joined back into `stream` before the call returns: later launches on `stream` run beside
+ * them (srgnn/dist.py issues the halo row chunks there).  The caller must srg_hub_join(stream)
+ * before anything reads the hub rows, and before the next NOJOIN fork from the same stream (one
+ * outstanding fork per caller stream). */
 #define SRG_SPMM_HUB_NOJOIN 0x10u
 
 /* =============================================================================================
@@ -195,8 +200,8 @@ int srg_segment_sum_f64(const int64_t* seg_ptr, const double* vals, int64_t n_se
 int srg_gather_rows_f32(const float* src, int64_t lds, int64_t n_src, const int64_t* idx, int64_t n_idx,
                         float* dst, int64_t ldd, int32_t d, void* stream);
 
-/* `stream` waits (on the device, not the host) for the hub workgroups of the last
- * SRG_SPMM_HUB_NOJOIN launch on the current device; no-op if none was forked. */
+/* `stream` waits (on the device, not the host) for the hub workgroups of the last hub launch
+ * forked from `stream` (an SRG_SPMM_HUB_NOJOIN one); no-op if none was forked. */
 int srg_hub_join(void* stream);
 
 /* Checks a device CSR: indptr[0] == 0, indptr non-decreasing, indptr[n_rows] == nnz, and every

@@ -28,7 +28,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
+#include <utility>
 #include <vector>
 
 #include "srgnn_hip.h"
@@ -1019,21 +1021,49 @@ int hub_delay_us()
     return us;
 }
 
-// per-device side stream + fork/join events for the hub kernel (created once, never destroyed)
+// Hub side streams.  One per (device, caller stream), created on first use and never destroyed,
+// each with its own fork / join events: callers on different streams never share events.  The
+// whole fork sequence of a launch (record fork, side-stream wait, hub launch, record join, main
+// launch, join wait) runs under g_side_mu, so host threads sharing one caller stream cannot
+// interleave their records either.  SRG_SPMM_HUB_NOJOIN leaves the join to srg_hub_join(stream),
+// which waits on the same (device, stream) entry's join event.
 struct SideStream {
     hipStream_t stream = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
 };
 std::mutex g_side_mu;
-SideStream g_side[64];
+std::map<std::pair<int, hipStream_t>, SideStream> g_side;   // guarded by g_side_mu
+bool g_side_attr[64] = {};                                     // per-device kernel attributes set
 
-int side_stream(SideStream** out)
+// Sets the hub kernels' dynamic-LDS limit on the current device (attributes are per device).
+template <typename IP>
+int hub_attrs()
+{
+    for (const void* fn : {(const void*)k_spmm_hub<true, IP>, (const void*)k_spmm_hub<false, IP>,
+                           (const void*)k_spmm_hub<true, IP, 0, true>, (const void*)k_spmm_hub<false, IP, 0, true>,
+                           (const void*)k_spmm_hub<true, IP, 1>, (const void*)k_spmm_hub<true, IP, 2>,
+                           (const void*)k_spmm_hub<true, IP, 3>, (const void*)k_spmm_hub<true, IP, 4>,
+                           (const void*)k_spmm_hub<true, IP, 5>, (const void*)k_spmm_hub<true, IP, 6>})
+        SRG_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kHubLdsBytes));
+    for (const void* fn : {(const void*)k_spmm_hub<true, IP, 0, false, 256>, (const void*)k_spmm_hub<false, IP, 0, false, 256>,
+                           (const void*)k_spmm_hub<true, IP, 0, true, 256>, (const void*)k_spmm_hub<false, IP, 0, true, 256>})
+        SRG_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)HubGeom<256>::LDS_BYTES));
+    return SRG_OK;
+}
+
+// The side stream of (current device, caller); the caller holds g_side_mu.
+int side_stream_locked(hipStream_t caller, SideStream** out)
 {
     int dev = 0;
     SRG_HIP_CHECK(hipGetDevice(&dev));
     if (dev < 0 || dev >= 64) return fail(SRG_ERR_HIP, "device id %d", dev);
-    std::lock_guard<std::mutex> lock(g_side_mu);
-    SideStream& ss = g_side[dev];
+    if (!g_side_attr[dev]) {
+        int rc = hub_attrs<int>();
+        if (!rc) rc = hub_attrs<int64_t>();
+        if (rc) return rc;
+        g_side_attr[dev] = true;
+    }
+    SideStream& ss = g_side[std::make_pair(dev, caller)];
     if (!ss.stream) {
         // highest queue priority: the hub workgroups (9 waves, ~136 KB LDS each) must get CUs
         // before the main launch's many small blocks occupy them all
@@ -1042,23 +1072,43 @@ int side_stream(SideStream** out)
         SRG_HIP_CHECK(hipStreamCreateWithPriority(&ss.stream, hipStreamNonBlocking, greatest));
         SRG_HIP_CHECK(hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming));
         SRG_HIP_CHECK(hipEventCreateWithFlags(&ss.join, hipEventDisableTiming));
-        for (const void* fn : {(const void*)k_spmm_hub<true, int>, (const void*)k_spmm_hub<false, int>,
-                               (const void*)k_spmm_hub<true, int64_t>, (const void*)k_spmm_hub<false, int64_t>,
-                               (const void*)k_spmm_hub<true, int64_t, 0, true>,
-                               (const void*)k_spmm_hub<false, int64_t, 0, true>})
-            SRG_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kHubLdsBytes));
-        for (const void* fn : {(const void*)k_spmm_hub<true, int, 0, false, 256>,
-                               (const void*)k_spmm_hub<false, int, 0, false, 256>,
-                               (const void*)k_spmm_hub<true, int64_t, 0, false, 256>,
-                               (const void*)k_spmm_hub<false, int64_t, 0, false, 256>,
-                               (const void*)k_spmm_hub<true, int64_t, 0, true, 256>,
-                               (const void*)k_spmm_hub<false, int64_t, 0, true, 256>})
-            SRG_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                              (int)HubGeom<256>::LDS_BYTES));
     }
     *out = &ss;
     return SRG_OK;
 }
+
+// Makes the device of `s` current for the lifetime of the guard (the null stream means the
+// current device), so every launch, event and side stream of an entry point belongs to the
+// device the caller's stream lives on.
+struct DeviceGuard {
+    int prev = -1, dev = -1, rc = SRG_OK;
+    explicit DeviceGuard(hipStream_t s)
+    {
+        // no usable device: leave it to the entry point (argument checks and empty problems
+        // need none; its first HIP call reports the error)
+        hipError_t e = hipGetDevice(&prev);
+        if (e != hipSuccess) { (void)hipGetLastError(); prev = -1; return; }
+        dev = prev;
+        if (s) {
+            hipDevice_t d = 0;
+            e = hipStreamGetDevice(s, &d);
+            if (e != hipSuccess) { rc = fail(SRG_ERR_HIP, "hipStreamGetDevice failed: %s", hipGetErrorString(e)); return; }
+            dev = (int)d;
+        }
+        if (dev != prev) {
+            e = hipSetDevice(dev);
+            if (e != hipSuccess) { rc = fail(SRG_ERR_HIP, "hipSetDevice(%d) failed: %s", dev, hipGetErrorString(e)); dev = prev; }
+        }
+    }
+    ~DeviceGuard()
+    {
+        if (prev >= 0 && dev != prev) (void)hipSetDevice(prev);
+    }
+};
+
+#define SRG_DEVICE_GUARD(stream)                                   \
+    DeviceGuard guard_(static_cast<hipStream_t>(stream));          \
+    if (guard_.rc) return guard_.rc
 
 template <typename IP, bool SEND = false>
 int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int64_t n_rows,
@@ -1085,8 +1135,10 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
     const bool sfull = d % kSliceCols == 0;
 
     SideStream* ss = nullptr;
+    std::unique_lock<std::mutex> side_lock(g_side_mu, std::defer_lock);
     if (n_hub > 0) {   // fork: hub blocks run beside the main launch
-        int rc = side_stream(&ss);
+        side_lock.lock();
+        int rc = side_stream_locked(s, &ss);
         if (rc) return rc;
         SRG_HIP_CHECK(hipEventRecord(ss->fork, s));
         SRG_HIP_CHECK(hipStreamWaitEvent(ss->stream, ss->fork, 0));
@@ -1096,14 +1148,6 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
             auto k = abl == 1 ? k_spmm_hub<true, IP, 1> : abl == 2 ? k_spmm_hub<true, IP, 2>
                    : abl == 3 ? k_spmm_hub<true, IP, 3> : abl == 4 ? k_spmm_hub<true, IP, 4>
                    : abl == 5 ? k_spmm_hub<true, IP, 5> : k_spmm_hub<true, IP, 6>;
-            static bool attr = false;
-            if (!attr) {
-                for (auto f : {k_spmm_hub<true, IP, 1>, k_spmm_hub<true, IP, 2>, k_spmm_hub<true, IP, 3>,
-                               k_spmm_hub<true, IP, 4>, k_spmm_hub<true, IP, 5>, k_spmm_hub<true, IP, 6>})
-                    SRG_HIP_CHECK(hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                      (int)kHubLdsBytes));
-                attr = true;
-            }
             hipLaunchKernelGGL(k, hgrid, dim3(kHubThreads), kHubLdsBytes, ss->stream, indptr, indices, vals,
                                order, n_slices, X, ldx, Y, ldy, d, acc, nt, epi);
         } else {
@@ -1366,6 +1410,7 @@ int srg_spmm_csr_f32(const int64_t* indptr, const int32_t* indices, const float*
                      const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t d, uint32_t flags,
                      void* stream)
 {
+    SRG_DEVICE_GUARD(stream);
     int rc = check_spmm_args(indptr, indices, values, n_rows, X, ldx, Y, ldy, d);
     if (rc) return rc;
     rc = launch_spmm<int64_t>(indptr, indices, values, n_rows, row_order, n_hub, n_heavy, X, ldx, Y, ldy, d, flags,
@@ -1378,6 +1423,7 @@ int srg_spmm_agg_f32(const int64_t* indptr, const int32_t* indices, const float*
                      const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t d, uint32_t flags,
                      float* agg, int64_t lda, float w, int agg_init, void* stream)
 {
+    SRG_DEVICE_GUARD(stream);
     int rc = check_spmm_args(indptr, indices, values, n_rows, X, ldx, Y, ldy, d);
     if (rc) return rc;
     if (n_rows > 0 && d > 0 && (!agg || lda < d))
@@ -1394,6 +1440,7 @@ int srg_spmm_send_f32(const int64_t* indptr, const int32_t* indices, const float
                       float* send, int64_t lds, const int64_t* send_ptr, const int32_t* send_slot,
                       void* stream)
 {
+    SRG_DEVICE_GUARD(stream);
     int rc = check_spmm_args(indptr, indices, values, n_rows, X, ldx, Y, ldy, d);
     if (rc) return rc;
     if (n_rows > 0 && d > 0 && send && (lds < d || !send_ptr || !send_slot))
@@ -1411,6 +1458,7 @@ int srg_propagate_khop_f32(const int64_t* indptr, const int32_t* indices, const 
                            int64_t n_heavy, float* const* panels,
                            int64_t ld, int32_t d, int32_t K, uint32_t flags, void* stream)
 {
+    SRG_DEVICE_GUARD(stream);
     if (K < 0) return fail(SRG_ERR_INVALID, "K=%d < 0", K);
     if (K > 0 && !panels) return fail(SRG_ERR_INVALID, "null panels");
     for (int k = 0; k <= K; ++k)
@@ -1433,6 +1481,7 @@ int srg_cheby_step_f64(const int64_t* indptr, const int32_t* indices, const doub
                        double a2, const double* coef_prev, const double* coef, int32_t n_scales,
                        double* R, int64_t r_stride, void* stream)
 {
+    SRG_DEVICE_GUARD(stream);
     return launch_cheby<double>(indptr, indices, values, n_rows, row_order, Tc, To, Tn, ld, d, mode,
                                 a1, a2, coef_prev, coef, n_scales, R, r_stride,
                                 static_cast<hipStream_t>(stream));
@@ -1444,6 +1493,7 @@ int srg_cheby_step_f32(const int64_t* indptr, const int32_t* indices, const floa
                        const float* coef_prev, const float* coef, int32_t n_scales, float* R,
                        int64_t r_stride, void* stream)
 {
+    SRG_DEVICE_GUARD(stream);
     return launch_cheby<float>(indptr, indices, values, n_rows, row_order, Tc, To, Tn, ld, d, mode,
                                a1, a2, coef_prev, coef, n_scales, R, r_stride,
                                static_cast<hipStream_t>(stream));
@@ -1454,6 +1504,7 @@ int srg_cheby_epilogue_f32(float* Tn, int64_t ldn, const float* Tc, int64_t ldc,
                            const float* coef_prev, const float* coef, int32_t n_scales, float* R,
                            int64_t ldr, int64_t r_stride, void* stream)
 {
+    SRG_DEVICE_GUARD(stream);
     if (mode != SRG_CHEBY_INIT && mode != SRG_CHEBY_STEP)
         return fail(SRG_ERR_INVALID, "cheby mode %d", mode);
     if (n_scales < 1 || n_scales > 8) return fail(SRG_ERR_INVALID, "n_scales=%d not in [1,8]", n_scales);
@@ -1479,6 +1530,7 @@ int srg_cheby_epilogue_f32(float* Tn, int64_t ldn, const float* Tc, int64_t ldc,
 int srg_hop_accumulate_f32(float* agg, int64_t lda, const float* y, int64_t ldy, int64_t n_rows,
                            int32_t d, float w, int mode, void* stream)
 {
+    SRG_DEVICE_GUARD(stream);
     if (mode != SRG_ACC_INIT && mode != SRG_ACC_ADD && mode != SRG_ACC_DIV)
         return fail(SRG_ERR_INVALID, "accumulate mode %d", mode);
     if (n_rows < 0 || d < 0 || lda < d || (mode != SRG_ACC_DIV && ldy < d))
@@ -1496,6 +1548,7 @@ int srg_hop_accumulate_f32(float* agg, int64_t lda, const float* y, int64_t ldy,
 int srg_tail_record_f32(float* hist, const float* y, int64_t ldy, int32_t d, int64_t flat_start,
                         int32_t len, float w, void* stream)
 {
+    SRG_DEVICE_GUARD(stream);
     if (d <= 0 || ldy < d || flat_start < 0 || len < 0 || len > SRG_TAIL_MAX)
         return fail(SRG_ERR_INVALID, "bad tail d=%d ldy=%lld flat_start=%lld len=%d", d, (long long)ldy,
                     (long long)flat_start, len);
@@ -1510,6 +1563,7 @@ int srg_tail_record_f32(float* hist, const float* y, int64_t ldy, int32_t d, int
 int srg_tail_rowsum_f32(float* agg, int64_t lda, int32_t d, int64_t flat_start, int32_t len,
                         const float* hist, int32_t n_terms, void* stream)
 {
+    SRG_DEVICE_GUARD(stream);
     if (d <= 0 || lda < d || flat_start < 0 || len < 0 || len > SRG_TAIL_MAX || n_terms < 0)
         return fail(SRG_ERR_INVALID, "bad tail d=%d lda=%lld flat_start=%lld len=%d n_terms=%d", d,
                     (long long)lda, (long long)flat_start, len, n_terms);
@@ -1524,6 +1578,7 @@ int srg_tail_rowsum_f32(float* agg, int64_t lda, int32_t d, int64_t flat_start, 
 int srg_gather_rows_f32(const float* src, int64_t lds, int64_t n_src, const int64_t* idx, int64_t n_idx,
                         float* dst, int64_t ldd, int32_t d, void* stream)
 {
+    SRG_DEVICE_GUARD(stream);
     if (n_idx < 0 || n_src < 0 || d < 0 || (d > 0 && (lds < d || ldd < d)))
         return fail(SRG_ERR_INVALID, "bad gather shape n_idx=%lld n_src=%lld d=%d lds=%lld ldd=%lld",
                     (long long)n_idx, (long long)n_src, d, (long long)lds, (long long)ldd);
@@ -1558,20 +1613,17 @@ int srg_gather_rows_f32(const float* src, int64_t lds, int64_t n_src, const int6
 
 int srg_hub_join(void* stream)
 {
-    int dev = 0;
-    SRG_HIP_CHECK(hipGetDevice(&dev));
-    if (dev < 0 || dev >= 64) return fail(SRG_ERR_HIP, "device id %d", dev);
-    hipEvent_t join = nullptr;
-    {
-        std::lock_guard<std::mutex> lock(g_side_mu);
-        join = g_side[dev].join;
-    }
-    if (join) SRG_HIP_CHECK(hipStreamWaitEvent(static_cast<hipStream_t>(stream), join, 0));
+    SRG_DEVICE_GUARD(stream);
+    std::lock_guard<std::mutex> lock(g_side_mu);
+    auto it = g_side.find(std::make_pair(guard_.dev, static_cast<hipStream_t>(stream)));
+    if (it != g_side.end() && it->second.join)
+        SRG_HIP_CHECK(hipStreamWaitEvent(static_cast<hipStream_t>(stream), it->second.join, 0));
     return ok();
 }
 
 int srg_segment_sum_f64(const int64_t* seg_ptr, const double* vals, int64_t n_seg, double* out, void* stream)
 {
+    SRG_DEVICE_GUARD(stream);
     if (n_seg < 0) return fail(SRG_ERR_INVALID, "n_seg=%lld < 0", (long long)n_seg);
     if (n_seg == 0) return ok();
     if (!seg_ptr || !out) return fail(SRG_ERR_INVALID, "null pointer");
@@ -1585,6 +1637,7 @@ int srg_segment_sum_f64(const int64_t* seg_ptr, const double* vals, int64_t n_se
 int srg_csr_validate(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t nnz,
                      int64_t n_cols, void* stream)
 {
+    SRG_DEVICE_GUARD(stream);
     if (n_rows < 0 || nnz < 0 || n_cols < 0) return fail(SRG_ERR_INVALID, "negative size");
     if (!indptr) return fail(SRG_ERR_INVALID, "null indptr");
     if (nnz > 0 && !indices) return fail(SRG_ERR_INVALID, "null indices");

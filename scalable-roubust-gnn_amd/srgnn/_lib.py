@@ -9,6 +9,8 @@ import ctypes
 import os
 import threading
 
+import torch
+
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("SRGNN_HIP_LIB", os.path.join(_PKG_ROOT, "lib", "libsrgnn_hip.so"))
 
@@ -140,6 +142,24 @@ def last_error() -> str:
 def check(rc: int, what: str) -> None:
     if rc != SRG_OK:
         raise SrgError(f"{what} failed ({rc}): {last_error()}")
+
+
+def stream(device) -> int:
+    """torch's current HIP stream of `device` as the C-ABI's stream argument (0 = the null stream,
+    i.e. that of the CURRENT device: run the call under on_device(device), as call() does)."""
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def call(device, name: str, *args) -> None:
+    """Runs entry point `name` with `device` current (the library resolves its side streams and
+    the null stream from the current device) and raises SrgError on a failed status."""
+    fn = getattr(lib(), name)
+    device = torch.device(device)
+    if device.index is not None and device.index != torch.cuda.current_device():
+        with torch.cuda.device(device):
+            check(fn(*args), name)
+    else:
+        check(fn(*args), name)
 
 
 def version() -> str:

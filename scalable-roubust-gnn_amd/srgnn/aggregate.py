@@ -125,7 +125,7 @@ class _DeviceSteps:
         self.n, self.d, self.device = n, d, device
         self.slots = {}
         self.pool = []
-        self.stream = torch.cuda.current_stream(device).cuda_stream
+        self.stream = _lib.stream(device)
         self.ts, self.tl = tail_range(n, d)
         self.hist = None
 
@@ -134,11 +134,9 @@ class _DeviceSteps:
                                                              device=self.device)
 
     def _acc(self, agg, y, w, mode):
-        rc = _lib.lib().srg_hop_accumulate_f32(agg.data_ptr(), agg.stride(0),
-                                               y.data_ptr() if y is not None else None,
-                                               y.stride(0) if y is not None else agg.stride(0),
-                                               self.n, self.d, float(w), mode, self.stream)
-        _lib.check(rc, "srg_hop_accumulate_f32")
+        _lib.call(self.device, "srg_hop_accumulate_f32", agg.data_ptr(), agg.stride(0),
+                  y.data_ptr() if y is not None else None, y.stride(0) if y is not None else agg.stride(0),
+                  self.n, self.d, float(w), mode, self.stream)
 
     def run(self, s, hop_panel=None):
         kind = s[0]
@@ -169,16 +167,14 @@ class _DeviceSteps:
                 if self.hist is not None:
                     grown[: self.hist.shape[0]].copy_(self.hist)
                 self.hist = grown
-            rc = _lib.lib().srg_tail_record_f32(self.hist[t].data_ptr(), hop_panel.data_ptr(), hop_panel.stride(0),
-                                                self.d, self.ts, self.tl, float(s[2]), self.stream)
-            _lib.check(rc, "srg_tail_record_f32")
+            _lib.call(self.device, "srg_tail_record_f32", self.hist[t].data_ptr(), hop_panel.data_ptr(),
+                      hop_panel.stride(0), self.d, self.ts, self.tl, float(s[2]), self.stream)
         elif kind == "rowsum":
             if self.tl == 0 or s[1] == 0:
                 return
             agg = self.result()
-            rc = _lib.lib().srg_tail_rowsum_f32(agg.data_ptr(), agg.stride(0), self.d, self.ts, self.tl,
-                                                self.hist.data_ptr(), s[1], self.stream)
-            _lib.check(rc, "srg_tail_rowsum_f32")
+            _lib.call(self.device, "srg_tail_rowsum_f32", agg.data_ptr(), agg.stride(0), self.d, self.ts, self.tl,
+                      self.hist.data_ptr(), s[1], self.stream)
         else:
             raise ValueError(f"unknown step {s!r}")
 

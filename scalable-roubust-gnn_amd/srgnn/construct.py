@@ -26,9 +26,8 @@ from .normalize import degree_powers
 def segment_sum_device(seg_ptr: torch.Tensor, vals: torch.Tensor) -> torch.Tensor:
     n_seg = seg_ptr.numel() - 1
     out = torch.empty(n_seg, dtype=torch.float64, device=vals.device)
-    rc = _lib.lib().srg_segment_sum_f64(seg_ptr.data_ptr(), vals.data_ptr() if vals.numel() else None,
-                                        n_seg, out.data_ptr(), torch.cuda.current_stream(vals.device).cuda_stream)
-    _lib.check(rc, "srg_segment_sum_f64")
+    _lib.call(vals.device, "srg_segment_sum_f64", seg_ptr.data_ptr(), vals.data_ptr() if vals.numel() else None,
+              n_seg, out.data_ptr(), _lib.stream(vals.device))
     return out
 
 

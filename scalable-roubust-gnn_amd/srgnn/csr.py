@@ -94,9 +94,8 @@ class DeviceCSR:
             raise ValueError(f"indices ({ix.numel()}) and values ({vv.numel()}) differ in length")
         ip, ix, vv = ip.contiguous(), ix.contiguous(), vv.contiguous()
         if validate:
-            stream = torch.cuda.current_stream(device).cuda_stream
-            _lib.check(_lib.lib().srg_csr_validate(ip.data_ptr(), ix.data_ptr(), n_rows, ix.numel(),
-                                                   n_cols, stream), "srg_csr_validate")
+            _lib.call(device, "srg_csr_validate", ip.data_ptr(), ix.data_ptr(), n_rows, ix.numel(), n_cols,
+                      _lib.stream(device))
         order, n_heavy, n_hub = make_schedule(ip, heavy_threshold, hub_threshold)
         return cls(ip, ix, vv, n_rows, int(n_cols), order, n_heavy, n_hub)
 

@@ -453,10 +453,8 @@ class HaloPartitionedOperator:
             from .spmm import spmm
             if dev.type == "cuda":
                 from . import _lib
-                _lib.check(_lib.lib().srg_csr_validate(lip.data_ptr(), lix.data_ptr(), self.rows + self.halo,
-                                                       lix.numel(), self.ncols_local,
-                                                       torch.cuda.current_stream(dev).cuda_stream),
-                           "srg_csr_validate")
+                _lib.call(dev, "srg_csr_validate", lip.data_ptr(), lix.data_ptr(), self.rows + self.halo,
+                          lix.numel(), self.ncols_local, _lib.stream(dev))
             self._A = [DeviceCSR(lip, lix, lvv, n_g, self.ncols_local, order, n_heavy, n_hub)
                        for (order, n_g, n_heavy, n_hub) in self.views + [self.ghost_view]]
             self._spmm = lambda A, X, out: spmm(A, X, out=out)
@@ -600,8 +598,7 @@ class HaloPartitionedOperator:
         if ghosts and self.n_ghost:
             self._spmm(gA, src, dst)
         if fork:
-            _lib.check(_lib.lib().srg_hub_join(torch.cuda.current_stream(self.device).cuda_stream),
-                       "srg_hub_join")
+            _lib.call(self.device, "srg_hub_join", _lib.stream(self.device))
         if after_group is not None:
             after_group(C)
 
@@ -665,8 +662,7 @@ class HaloPartitionedOperator:
             if self.views[c][1]:
                 self._spmm(self._A[c], src, out)
             if c == 0 and fork:
-                _lib.check(_lib.lib().srg_hub_join(torch.cuda.current_stream(self.device).cuda_stream),
-                           "srg_hub_join")
+                _lib.call(self.device, "srg_hub_join", _lib.stream(self.device))
             a, b = self.chunk_ranges[c]
             if b > a:
                 epilogue(a, b)
@@ -761,13 +757,10 @@ def _epilogue_device(Tn, Tc, To, mode, a1, a2, coef_prev, coef, R):
     n, w = Tn.shape
     ct = ctypes.c_float
     cp = (ct * ns)(*coef_prev) if coef_prev is not None else None
-    rc = _lib.lib().srg_cheby_epilogue_f32(Tn.data_ptr(), Tn.stride(0), Tc.data_ptr() if Tc is not None else None,
-                                           Tc.stride(0) if Tc is not None else w,
-                                           To.data_ptr() if To is not None else None,
-                                           To.stride(0) if To is not None else w, n, w, mode, a1, a2, cp,
-                                           (ct * ns)(*coef), ns, R.data_ptr(), R.stride(1), R.stride(0),
-                                           torch.cuda.current_stream(Tn.device).cuda_stream)
-    _lib.check(rc, "srg_cheby_epilogue_f32")
+    _lib.call(Tn.device, "srg_cheby_epilogue_f32", Tn.data_ptr(), Tn.stride(0),
+              Tc.data_ptr() if Tc is not None else None, Tc.stride(0) if Tc is not None else w,
+              To.data_ptr() if To is not None else None, To.stride(0) if To is not None else w, n, w, mode,
+              a1, a2, cp, (ct * ns)(*coef), ns, R.data_ptr(), R.stride(1), R.stride(0), _lib.stream(Tn.device))
 
 
 class HaloWaveletFilter:

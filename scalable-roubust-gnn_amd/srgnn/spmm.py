@@ -13,8 +13,7 @@ from . import _lib
 from .csr import DeviceCSR
 
 
-def _stream(device):
-    return torch.cuda.current_stream(device).cuda_stream
+_stream = _lib.stream
 
 
 def _check_panel(X: torch.Tensor, rows: int, name: str, d=None):
@@ -28,6 +27,9 @@ def _check_panel(X: torch.Tensor, rows: int, name: str, d=None):
         raise ValueError(f"{name} has {X.shape[0]} rows, need {rows}")
     if X.stride(1) != 1:
         raise ValueError(f"{name} must be row-major with unit column stride")
+    if X.shape[0] > 1 and X.stride(0) < X.shape[1]:
+        raise ValueError(f"{name} rows overlap (stride(0)={X.stride(0)} < {X.shape[1]} columns): "
+                         "pass a contiguous tensor, not an expanded / broadcast one")
     if d is not None and X.shape[1] != d:
         raise ValueError(f"{name} has {X.shape[1]} columns, expected {d}")
 
@@ -52,12 +54,9 @@ def spmm(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor | None = None, accumul
     flags = (_lib.SRG_SPMM_ACCUMULATE if accumulate else 0) | (_lib.SRG_SPMM_NT_STORE if nt_store else 0) | \
         (_lib.SRG_SPMM_WIDE_ROWS if wide_rows else 0) | (_lib.SRG_SPMM_HUB_W256 if hub_w256 else 0) | \
         (_lib.SRG_SPMM_HUB_NOJOIN if hub_nojoin else 0)
-    rc = _lib.lib().srg_spmm_csr_f32(A.indptr.data_ptr(), A.indices.data_ptr(), A.values.data_ptr(),
-                                     A.n_rows, A.order.data_ptr() if A.n_rows else None, A.n_hub,
-                                     A.n_heavy,
-                                     X.data_ptr(), X.stride(0), out.data_ptr(), out.stride(0), d, flags,
-                                     _stream(X.device))
-    _lib.check(rc, "srg_spmm_csr_f32")
+    _lib.call(X.device, "srg_spmm_csr_f32", A.indptr.data_ptr(), A.indices.data_ptr(), A.values.data_ptr(),
+              A.n_rows, A.order.data_ptr() if A.n_rows else None, A.n_hub, A.n_heavy, X.data_ptr(),
+              X.stride(0), out.data_ptr(), out.stride(0), d, flags, _stream(X.device))
     return out
 
 
@@ -72,12 +71,10 @@ def spmm_agg(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, agg: torch.Tensor
     if not (out.device == X.device == agg.device == A.device):
         raise ValueError("A, X, out and agg must be on the same device")
     flags = _lib.SRG_SPMM_NT_STORE if nt_store else 0
-    rc = _lib.lib().srg_spmm_agg_f32(A.indptr.data_ptr(), A.indices.data_ptr(), A.values.data_ptr(),
-                                     A.n_rows, A.order.data_ptr() if A.n_rows else None, A.n_hub, A.n_heavy,
-                                     X.data_ptr(), X.stride(0), out.data_ptr(), out.stride(0), d, flags,
-                                     agg.data_ptr(), agg.stride(0), float(w), 1 if init else 0,
-                                     _stream(X.device))
-    _lib.check(rc, "srg_spmm_agg_f32")
+    _lib.call(X.device, "srg_spmm_agg_f32", A.indptr.data_ptr(), A.indices.data_ptr(), A.values.data_ptr(),
+              A.n_rows, A.order.data_ptr() if A.n_rows else None, A.n_hub, A.n_heavy, X.data_ptr(),
+              X.stride(0), out.data_ptr(), out.stride(0), d, flags, agg.data_ptr(), agg.stride(0),
+              float(w), 1 if init else 0, _stream(X.device))
     return out
 
 
@@ -97,13 +94,12 @@ def spmm_send(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, send: torch.Tens
         raise ValueError("send_ptr must be int64 [rows + 1] (indexed by A's row ids) and send_slot int32, on A's device")
     if send_slot.numel() and send.shape[0] == 0:
         raise ValueError("send slots into an empty send buffer")
-    rc = _lib.lib().srg_spmm_send_f32(A.indptr.data_ptr(), A.indices.data_ptr(), A.values.data_ptr(),
-                                      A.n_rows, A.order.data_ptr() if A.n_rows else None, A.n_hub, A.n_heavy,
-                                      X.data_ptr(), X.stride(0), out.data_ptr(), out.stride(0), d, 0,
-                                      send.data_ptr() if send.numel() else None, max(send.stride(0), d),
-                                      send_ptr.data_ptr(), send_slot.data_ptr() if send_slot.numel() else None,
-                                      _stream(X.device))
-    _lib.check(rc, "srg_spmm_send_f32")
+    _lib.call(X.device, "srg_spmm_send_f32", A.indptr.data_ptr(), A.indices.data_ptr(), A.values.data_ptr(),
+              A.n_rows, A.order.data_ptr() if A.n_rows else None, A.n_hub, A.n_heavy, X.data_ptr(),
+              X.stride(0), out.data_ptr(), out.stride(0), d, 0,
+              send.data_ptr() if send.numel() else None, send.stride(0) if send.shape[0] > 1 else d,
+              send_ptr.data_ptr(), send_slot.data_ptr() if send_slot.numel() else None,
+              _stream(X.device))
     return out
 
 
@@ -119,10 +115,9 @@ def gather_rows(src: torch.Tensor, idx: torch.Tensor, out: torch.Tensor | None =
     if out is None:
         out = torch.empty((idx.numel(), d), dtype=torch.float32, device=src.device)
     _check_panel(out, idx.numel(), "out", d)
-    rc = _lib.lib().srg_gather_rows_f32(src.data_ptr(), max(src.stride(0), d), src.shape[0],
-                                        idx.data_ptr() if idx.numel() else None, idx.numel(),
-                                        out.data_ptr(), max(out.stride(0), d), d, _stream(src.device))
-    _lib.check(rc, "srg_gather_rows_f32")
+    _lib.call(src.device, "srg_gather_rows_f32", src.data_ptr(), src.stride(0) if src.shape[0] > 1 else d,
+              src.shape[0], idx.data_ptr() if idx.numel() else None, idx.numel(), out.data_ptr(),
+              out.stride(0) if out.shape[0] > 1 else d, d, _stream(src.device))
     return out
 
 
@@ -153,11 +148,9 @@ def propagate(A: DeviceCSR, X: torch.Tensor, K: int, panels: list | None = None,
             raise ValueError("all panels must share one leading dimension")
     arr = (ctypes.c_void_p * (K + 1))(*[p.data_ptr() for p in panels])
     flags = _lib.SRG_SPMM_NT_STORE if nt_store else 0
-    rc = _lib.lib().srg_propagate_khop_f32(A.indptr.data_ptr(), A.indices.data_ptr(),
-                                           A.values.data_ptr(), n,
-                                           A.order.data_ptr() if n else None, A.n_hub, A.n_heavy,
-                                           arr, ld, d, K, flags, _stream(X.device))
-    _lib.check(rc, "srg_propagate_khop_f32")
+    _lib.call(X.device, "srg_propagate_khop_f32", A.indptr.data_ptr(), A.indices.data_ptr(),
+              A.values.data_ptr(), n, A.order.data_ptr() if n else None, A.n_hub, A.n_heavy, arr, ld, d,
+              K, flags, _stream(X.device))
     if panels[0] is not X0 and X is not X0:
         panels = [X0] + list(panels[1:])
     return panels

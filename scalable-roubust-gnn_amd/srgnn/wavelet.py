@@ -190,16 +190,15 @@ class HeatWaveletFilter:
         ns, nc = self.coeffs.shape
         f64 = self.dtype == torch.float64
         ct = ctypes.c_double if f64 else ctypes.c_float
-        fn = _lib.lib().srg_cheby_step_f64 if f64 else _lib.lib().srg_cheby_step_f32
-        stream = torch.cuda.current_stream(S.device).cuda_stream
+        name = "srg_cheby_step_f64" if f64 else "srg_cheby_step_f32"
+        stream = _lib.stream(S.device)
 
         def launch(vals, Tc, To, Tn, mode, coef_prev, coef):
             cp = self._coef(ct, coef_prev) if coef_prev is not None else None
-            rc = fn(self.indptr.data_ptr(), self.indices.data_ptr(), vals.data_ptr(), n,
-                    self.order.data_ptr(), Tc.data_ptr(), To.data_ptr() if To is not None else None,
-                    Tn.data_ptr(), d, d, mode, self.a1, self.a2, cp, self._coef(ct, coef), ns,
-                    R.data_ptr(), n * d, stream)
-            _lib.check(rc, fn.__name__)
+            _lib.call(S.device, name, self.indptr.data_ptr(), self.indices.data_ptr(), vals.data_ptr(), n,
+                      self.order.data_ptr(), Tc.data_ptr(), To.data_ptr() if To is not None else None,
+                      Tn.data_ptr(), d, d, mode, self.a1, self.a2, cp, self._coef(ct, coef), ns,
+                      R.data_ptr(), n * d, stream)
 
         # T_{k-1}, T_k and the free panel rotate through three buffers (S itself is never written)
         t_old, t_cur = S, torch.empty_like(S)
@@ -222,17 +221,16 @@ class HeatWaveletFilter:
         n, w = Sb.shape
         ns, nc = self.coeffs.shape
         ct = ctypes.c_float
-        fn = _lib.lib().srg_cheby_epilogue_f32
-        stream = torch.cuda.current_stream(Sb.device).cuda_stream
+        stream = _lib.stream(Sb.device)
         Lm, Fm = self._csr(self.lvals), self._csr(self.fvals)
 
         def epi(Tn, Tc, To, mode, coef_prev, coef):
             cp = self._coef(ct, coef_prev) if coef_prev is not None else None
-            rc = fn(Tn.data_ptr(), Tn.stride(0), Tc.data_ptr() if Tc is not None else None,
-                    Tc.stride(0) if Tc is not None else w, To.data_ptr() if To is not None else None,
-                    To.stride(0) if To is not None else w, n, w, mode, self.a1, self.a2, cp,
-                    self._coef(ct, coef), ns, Rb.data_ptr(), Rb.stride(1), Rb.stride(0), stream)
-            _lib.check(rc, "srg_cheby_epilogue_f32")
+            _lib.call(Sb.device, "srg_cheby_epilogue_f32", Tn.data_ptr(), Tn.stride(0),
+                      Tc.data_ptr() if Tc is not None else None, Tc.stride(0) if Tc is not None else w,
+                      To.data_ptr() if To is not None else None, To.stride(0) if To is not None else w, n, w,
+                      mode, self.a1, self.a2, cp, self._coef(ct, coef), ns, Rb.data_ptr(), Rb.stride(1),
+                      Rb.stride(0), stream)
 
         t_old, t_cur = Sb, work[0]
         free = list(work[1:])
