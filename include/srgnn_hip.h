@@ -191,6 +191,17 @@ int srg_tail_rowsum_f32(float* agg, int64_t lda, int32_t d, int64_t flat_start, 
  * -- the order in which scipy merges duplicate entries of adj + I and sums the rows for the
  * degrees.  seg_ptr has n_seg + 1 entries; all pointers are device pointers. */
 int srg_segment_sum_f64(const int64_t* seg_ptr, const double* vals, int64_t n_seg, double* out, void* stream);
+/* The same in fp32: the directed families' fp32 normalisations (SSRG/operators/utils.py:195-424:
+ * torch_scatter.scatter_add over fp32 edge weights, a sequential sum in element order). */
+int srg_segment_sum_f32(const int64_t* seg_ptr, const float* vals, int64_t n_seg, float* out, void* stream);
+
+/* fp64 Y = A * X (X [rows of A's columns, d], ldx; Y [n_rows, d], ldy) in scipy's csr_matvec(s)
+ * order (each element from 0, adding the separately rounded product of every stored entry in
+ * storage order): the W @ x step of the fast PPR power iteration in
+ * adj_to_fast_ppr_approx_symmetric_norm (SSRG/operators/utils.py:284-291) and the stationary
+ * distribution of the two-order operator (:338-356).  Not a hop kernel. */
+int srg_spmm_csr_f64(const int64_t* indptr, const int32_t* indices, const double* values, int64_t n_rows,
+                     const double* X, int64_t ldx, double* Y, int64_t ldy, int32_t d, void* stream);
 
 /* Row gather, the send-side pack of the multi-GPU halo exchange (srgnn/dist.py; no reference
  * counterpart -- the reference is single process): dst[i, :] = src[idx[i], :] for i < n_idx, a C

@@ -7,6 +7,8 @@ does, and it must not be used as a fallback.
   sym_norm        restates adj_to_symmetric_norm      SSRG/operators/utils.py:81-93
   spmm / propagate restate FloatCSRMulDenseOMP + the   SSRG/operators/csrc/matmul.c:23-40,
                   GraphOp hop loop                     SSRG/operators/base_operator.py:19-36
+  spmm64          fp64 product in scipy's csr_matvecs order (the directed families' power iterations)
+  segment_sum     sequential per-segment sums (scatter_add / duplicate merges), any float dtype
   ref_spmm        the reference's own matmul.c, compiled from its source by oracle/Makefile into
                   oracle/_ref/libmatmul_ref.so (the shipped prebuilt libmatmul.so is never loaded)
   combine         restates MessageOp.combine for last / sum / mean / simple_weighted with the same
@@ -177,6 +179,32 @@ def propagate(indptr, indices, values, X, K):
     out = [np.asarray(X, dtype=np.float32)]
     for _ in range(K):
         out.append(spmm(indptr, indices, values, out[-1]))
+    return out
+
+
+def spmm64(indptr, indices, values, X):
+    """fp64 Y = A @ X in scipy's csr_matvecs order: each element from 0, adding the separately
+    rounded products in storage order (C oracle)."""
+    indptr = np.ascontiguousarray(indptr, dtype=np.int64)
+    indices = np.ascontiguousarray(indices, dtype=np.int32)
+    values = np.ascontiguousarray(values, dtype=np.float64)
+    X2 = np.ascontiguousarray(np.asarray(X, dtype=np.float64).reshape(np.shape(X)[0], -1))
+    n_rows, d = indptr.size - 1, X2.shape[1]
+    out = np.zeros((n_rows, d), dtype=np.float64)
+    lib().srg_oracle_spmm_f64(_ptr(indptr), _ptr(indices), _ptr(values), n_rows, _ptr(X2), d, _ptr(out), d, d)
+    return out.reshape((n_rows,) + tuple(np.shape(X)[1:]))
+
+
+def segment_sum(ptr, vals):
+    """out[s] = ((0 + v[p[s]]) + v[p[s]+1]) + ..., left to right in vals' dtype (torch_scatter's
+    scatter_add / scipy's duplicate merge order); vectorised across segments."""
+    ptr = np.asarray(ptr, dtype=np.int64)
+    vals = np.asarray(vals)
+    lens = np.diff(ptr)
+    out = np.zeros(lens.size, dtype=vals.dtype)
+    for k in range(int(lens.max()) if lens.size else 0):
+        live = lens > k
+        out[live] = out[live] + vals[ptr[:-1][live] + k]
     return out
 
 

@@ -948,15 +948,37 @@ __global__ void k_tail_rowsum(float* __restrict__ agg, int64_t lda, int d, int64
 // construct_adj on the device: sequential fp64 segment sums (duplicate merging and row degrees in
 // storage order, starting from +0 -- scipy's csr_binop / csr_matvec accumulation order)
 // ------------------------------------------------------------------------------------------------
+template <typename T>
 __global__ void __launch_bounds__(256)
-k_segment_sum_f64(const int64_t* __restrict__ seg_ptr, const double* __restrict__ vals, int64_t n_seg,
-                  double* __restrict__ out)
+k_segment_sum(const int64_t* __restrict__ seg_ptr, const T* __restrict__ vals, int64_t n_seg,
+              T* __restrict__ out)
 {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n_seg; s += stride) {
-        double acc = 0.0;
-        for (int64_t j = seg_ptr[s]; j < seg_ptr[s + 1]; ++j) acc = __dadd_rn(acc, vals[j]);
+        T acc = T(0);
+        for (int64_t j = seg_ptr[s]; j < seg_ptr[s + 1]; ++j) acc = e_add(acc, vals[j]);
         out[s] = acc;
+    }
+}
+
+// fp64 product Y = A * X in scipy's csr_matvec(s) order (sparsetools csr.h): each element starts
+// from 0 and adds the separately rounded product of every stored entry, in storage order.  One
+// thread per output element (row-major, so neighbouring threads share a row's entries); used by
+// the construct_adj power iterations (srgnn/directed.py), not by the hop loop.
+__global__ void __launch_bounds__(256)
+k_spmm_f64(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
+           const double* __restrict__ vals, int64_t n_rows, const double* __restrict__ X, int64_t ldx,
+           double* __restrict__ Y, int64_t ldy, int d)
+{
+    const int64_t total = n_rows * (int64_t)d;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += stride) {
+        const int64_t row = e / d;
+        const int c = (int)(e - row * d);
+        double acc = 0.0;
+        for (int64_t j = indptr[row]; j < indptr[row + 1]; ++j)
+            acc = __dadd_rn(acc, __dmul_rn(vals[j], X[(int64_t)indices[j] * ldx + c]));
+        Y[row * ldy + c] = acc;
     }
 }
 
@@ -1621,15 +1643,47 @@ int srg_hub_join(void* stream)
     return ok();
 }
 
-int srg_segment_sum_f64(const int64_t* seg_ptr, const double* vals, int64_t n_seg, double* out, void* stream)
+}  // extern "C"
+
+namespace {
+template <typename T>
+int launch_segment_sum(const int64_t* seg_ptr, const T* vals, int64_t n_seg, T* out, void* stream)
 {
     SRG_DEVICE_GUARD(stream);
     if (n_seg < 0) return fail(SRG_ERR_INVALID, "n_seg=%lld < 0", (long long)n_seg);
     if (n_seg == 0) return ok();
     if (!seg_ptr || !out) return fail(SRG_ERR_INVALID, "null pointer");
     const unsigned blocks = (unsigned)std::min<int64_t>((n_seg + 255) / 256, 1 << 16);
-    hipLaunchKernelGGL(k_segment_sum_f64, dim3(blocks), dim3(256), 0, static_cast<hipStream_t>(stream),
+    hipLaunchKernelGGL(k_segment_sum<T>, dim3(blocks), dim3(256), 0, static_cast<hipStream_t>(stream),
                        seg_ptr, vals, n_seg, out);
+    SRG_HIP_CHECK(hipGetLastError());
+    return ok();
+}
+}  // namespace
+
+extern "C" {
+
+int srg_segment_sum_f64(const int64_t* seg_ptr, const double* vals, int64_t n_seg, double* out, void* stream)
+{
+    return launch_segment_sum<double>(seg_ptr, vals, n_seg, out, stream);
+}
+
+int srg_segment_sum_f32(const int64_t* seg_ptr, const float* vals, int64_t n_seg, float* out, void* stream)
+{
+    return launch_segment_sum<float>(seg_ptr, vals, n_seg, out, stream);
+}
+
+int srg_spmm_csr_f64(const int64_t* indptr, const int32_t* indices, const double* values, int64_t n_rows,
+                     const double* X, int64_t ldx, double* Y, int64_t ldy, int32_t d, void* stream)
+{
+    SRG_DEVICE_GUARD(stream);
+    int rc = check_spmm_args(indptr, indices, values, n_rows, X, ldx, Y, ldy, d);
+    if (rc) return rc;
+    if (n_rows == 0 || d == 0) return ok();
+    const int64_t total = n_rows * (int64_t)d;
+    const unsigned blocks = (unsigned)std::min<int64_t>((total + 255) / 256, 1 << 20);
+    hipLaunchKernelGGL(k_spmm_f64, dim3(blocks), dim3(256), 0, static_cast<hipStream_t>(stream),
+                       indptr, indices, values, n_rows, X, ldx, Y, ldy, d);
     SRG_HIP_CHECK(hipGetLastError());
     return ok();
 }

@@ -1,8 +1,8 @@
 """Reference-compatible helpers of the propagation path (mirror of SSRG/operators/utils.py).
 
 Same names, argument meaning and error behaviour as the reference; the SpMM runs on the GPU through
-libsrgnn_hip.so instead of libmatmul.so.  Only the hot-path subset is provided here (the directed /
-magnetic / PPR-approximation normalisations at utils.py:95-424 are out of scope).
+libsrgnn_hip.so instead of libmatmul.so.  The directed-family normalisations (utils.py:95-424) are
+built on the GPU by srgnn.directed and returned as scipy matrices, as the reference returns them.
 """
 from __future__ import annotations
 
@@ -91,6 +91,70 @@ def adj_to_symmetric_norm(adj, r):
     scaled = a_hat @ sp.diags(left)
     # transpose, then scale column j by right[j]
     return scaled.transpose() @ sp.diags(right)
+
+
+def _coo_of(adj):
+    """The reference reads adj.row / adj.col / adj.data (a coo_matrix, utils.py:97-98, 197-198)."""
+    if not isinstance(adj, sp.coo_matrix):
+        adj = sp.coo_matrix(adj)
+    return adj.row, adj.col, adj.data, adj.shape[0]
+
+
+def _scipy(csr, n):
+    from srgnn.construct import to_scipy
+    return to_scipy(*csr, n)
+
+
+def adj_to_directed_symmetric_mag_norm(adj, r, q):
+    """Magnetic Laplacian normalisation, utils.py:95-138: (real, imag) csr_matrix parts of
+    D_s^(r-1) (A_s + I) D_s^(-r) * exp(i 2 pi q (A - A^T)), A_s = (A + A^T) / 2 (GPU, bit-identical)."""
+    from srgnn.directed import magnetic_norm
+    row, col, data, n = _coo_of(adj)
+    re, im = magnetic_norm(row, col, data, n, r, q)
+    return _scipy(re, n), _scipy(im, n)
+
+
+def PyGSD_adj_to_directed_symmetric_mag_norm(adj, r, q):
+    """utils.py:140-193 (PyTorch Geometric Signed Directed's variant: no self-loops in the degrees,
+    L = I - A_norm scaled by 2 / lambda_max with lambda_max = 2, a second set of -1 loops on the
+    real part).  GPU; bit-identical except, in a row of more than 16 stored entries that also stores
+    a self-loop, the last bit of that diagonal entry (scipy sums its three duplicates in the order
+    its introsort leaves them)."""
+    from srgnn.directed import pygsd_magnetic_norm
+    row, col, data, n = _coo_of(adj)
+    re, im = pygsd_magnetic_norm(row, col, data, n, r, q)
+    return _scipy(re, n), _scipy(im, n)
+
+
+def adj_to_un_in_out_dir_symmetric_norm(adj, r):
+    """utils.py:195-260: (un, in, out) csr_matrix operators.  un is bit-identical; in / out come from
+    the dense P^T P and P P^T (P = D^-1 (A + I)), here fp64 GEMMs on the GPU rounded to fp32, so
+    they match the reference's fp32 sgemm values to a few ulps (same sparsity)."""
+    from srgnn.directed import in_out_norm
+    row, col, _, n = _coo_of(adj)
+    un, i, o = in_out_norm(row, col, n, r)
+    return _scipy(un, n), _scipy(i, n), _scipy(o, n)
+
+
+def adj_to_fast_ppr_approx_symmetric_norm(adj, r, ppr_alpha, max_iter=100):
+    """utils.py:262-322: the symmetric normalisation of (Pi^1/2 P Pi^-1/2 + Pi^-1/2 P^T Pi^1/2) / 2,
+    Pi from the reference's power iteration (fp64 on the GPU; its dot product and norm are BLAS
+    reductions in the reference, so values agree to a few fp32 ulps, same sparsity)."""
+    from srgnn.directed import fast_ppr_norm
+    row, col, _, n = _coo_of(adj)
+    return _scipy(fast_ppr_norm(row, col, n, r, ppr_alpha, max_iter), n)
+
+
+def adj_to_slow_first_second_ppr_approx_symmetric_norm(adj, r, ppr_alpha):
+    """utils.py:324-424: (first-order, second-order) csr_matrix operators.  The stationary
+    distribution comes from a fp64 power iteration on the GPU instead of the reference's fp32 dense
+    eigendecomposition (scipy.linalg.eig of a float32 matrix), so the first-order values differ from
+    the reference's by that eigenvector's fp32 error (up to ~5e-4 relative on Cora); the
+    second-order operator matches to a few ulps (fp64 GEMMs vs the reference's sgemm)."""
+    from srgnn.directed import two_order_norm
+    row, col, _, n = _coo_of(adj)
+    one, two = two_order_norm(row, col, n, r, ppr_alpha)
+    return _scipy(one, n), _scipy(two, n)
 
 
 def one_dim_weighted_add(feat_list, weight_list):

@@ -48,6 +48,8 @@ EXPORTED_SYMBOLS = (
     "srg_tail_record_f32",
     "srg_tail_rowsum_f32",
     "srg_segment_sum_f64",
+    "srg_segment_sum_f32",
+    "srg_spmm_csr_f64",
     "srg_gather_rows_f32",
     "srg_hub_join",
     "srg_csr_validate",
@@ -101,6 +103,10 @@ def _declare(lib):
     lib.srg_tail_rowsum_f32.restype = ctypes.c_int
     lib.srg_segment_sum_f64.argtypes = [_p, _p, _i64, _p, _p]
     lib.srg_segment_sum_f64.restype = ctypes.c_int
+    lib.srg_segment_sum_f32.argtypes = [_p, _p, _i64, _p, _p]
+    lib.srg_segment_sum_f32.restype = ctypes.c_int
+    lib.srg_spmm_csr_f64.argtypes = [_p, _p, _p, _i64, _p, _i64, _p, _i64, _i32, _p]
+    lib.srg_spmm_csr_f64.restype = ctypes.c_int
     lib.srg_gather_rows_f32.argtypes = [_p, _i64, _i64, _p, _i64, _p, _i64, _i32, _p]
     lib.srg_gather_rows_f32.restype = ctypes.c_int
     lib.srg_hub_join.argtypes = [_p]
