@@ -158,7 +158,7 @@ def test_segment_sum_f32_equals_oracle(oracle_mod):
     rng = np.random.default_rng(5)
     lens = rng.integers(0, 40, 500)
     ptr = np.r_[0, np.cumsum(lens)]
-    v = (rng.standard_normal(ptr[-1]) * 10 ** rng.integers(-3, 4, ptr[-1])).astype(np.float32)
+    v = (rng.standard_normal(ptr[-1]) * 10.0 ** rng.integers(-3, 4, ptr[-1])).astype(np.float32)
     dev = _dev()
     got = segment_sum(torch.from_numpy(ptr).to(dev), torch.from_numpy(v).to(dev))
     assert got.dtype == torch.float32
