@@ -48,8 +48,9 @@ extern "C" {
  * (SSRG/operators/csrc/matmul.c:23-40) given a zeroed answer (SSRG/operators/utils.py:38). */
 #define SRG_SPMM_ACCUMULATE 0x1u   /* chains start from Y's current content (matmul.c contract) */
 #define SRG_SPMM_NT_STORE 0x2u     /* non-temporal stores of Y */
-/* Diagnostic: keep one row per wave also for d <= 32 (the default runs 64 / S rows per wave,
- * S = the power of two >= d lanes per row).  Results are identical either way. */
+/* Diagnostic: one light row per wave.  By default d <= 32 runs 64 / S rows per wave (S = the power
+ * of two >= d lanes per row), and d = 64 / 128 / 256 runs 4 light rows per wave (16 lanes per row,
+ * 16-byte column chunks).  Results are identical either way. */
 #define SRG_SPMM_WIDE_ROWS 0x4
 /* Diagnostic: hub workgroups always use 256-nonzero windows (72 KB of LDS, two per CU).  By default
  * they do only when a launch has more hub workgroups than CUs.  Results are identical either way. */

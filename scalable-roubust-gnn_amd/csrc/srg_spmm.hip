@@ -419,7 +419,85 @@ __device__ __forceinline__ void narrow_rows(const IP* __restrict__ indptr, const
     }
 }
 
-template <int VEC, int U, int UH, bool FULL, bool SFULL, typename IP, int NS = 0, bool SEND = false>
+// Light rows of wide panels (d = LQ * 4 * S, S = 64 / LR): one wave runs LR rows at once, S lanes
+// per row, each lane LQ 16-byte column chunks (chunk q of lane l: columns q*4S + 4l .. +3, so the S
+// lanes of a row read 16*S contiguous bytes per gather).  A one-row wave walks its row's short
+// stream through a chain of dependent loads (schedule slot -> row pointers -> column ids -> X) and
+// the phase is bound by how many rows are in flight, not by bytes; LR rows per wave multiply that.
+// Each lane loads its own row's (column id, value) entries (the S lanes of a row share the address),
+// then U gathers per row in flight, then the fma links in CSR order.  Entries past a row's end are
+// skipped (never folded in as 0*x).  Still one sequential fma chain per output element.
+template <int LR, int LQ, int U, typename IP, bool SEND>
+__device__ __forceinline__ void packed_rows(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
+                                            const float* __restrict__ vals, const int32_t* __restrict__ order,
+                                            int n_rows, int first, const float* __restrict__ X, int64_t ldx,
+                                            float* __restrict__ Y, int64_t ldy, int accumulate, int nt,
+                                            const Epi& epi)
+{
+    typedef typename Vec<float, 4>::type V4;
+    constexpr int S = 64 / LR;
+    const int lane = threadIdx.x & 63;
+    const int g = lane / S, l = lane % S;
+    const int slot = first + g;
+    const bool rv = slot < n_rows;
+    const int row = rv ? (order ? order[slot] : slot) : 0;
+    const int64_t beg = rv ? (int64_t)indptr[row] : 0;
+    const int len = rv ? (int)((int64_t)indptr[row + 1] - beg) : 0;
+    int maxlen = len;
+#pragma unroll
+    for (int off = S; off < 64; off <<= 1) {
+        const int o = __shfl_xor(maxlen, off);
+        maxlen = o > maxlen ? o : maxlen;
+    }
+    maxlen = __builtin_amdgcn_readfirstlane(maxlen);
+    float* __restrict__ yrow = Y + (int64_t)row * ldy;
+    float* __restrict__ arow = epi.agg ? epi.agg + (int64_t)row * epi.lda : nullptr;
+    V4 acc[LQ], aprev[LQ];
+#pragma unroll
+    for (int q = 0; q < LQ; ++q) {
+        const int col = q * 4 * S + 4 * l;
+        acc[q] = (accumulate && rv) ? vload<float, 4>(yrow + col) : vzero<float, 4>();
+        aprev[q] = (arow && !epi.init && rv) ? vload<float, 4>(arow + col) : vzero<float, 4>();
+    }
+    for (int j = 0; j < maxlen; j += U) {
+        int cv[U];
+        float av[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool ok = j + u < len;
+            const int64_t p = beg + (ok ? j + u : 0);
+            cv[u] = ok ? indices[p] : 0;
+            av[u] = ok ? vals[p] : 0.0f;
+        }
+        __builtin_amdgcn_sched_barrier(0);   // every id load ahead of the first gather
+        V4 x[U][LQ];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int q = 0; q < LQ; ++q)
+                x[u][q] = (j + u < len) ? gload<float, 4>(X + (int64_t)cv[u] * ldx + q * 4 * S + 4 * l)
+                                        : vzero<float, 4>();
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (j + u < len)
+#pragma unroll
+                for (int q = 0; q < LQ; ++q) chain<float, 4>(acc[q], av[u], x[u][q]);
+    }
+    if (!rv) return;
+#pragma unroll
+    for (int q = 0; q < LQ; ++q) {
+        const int col = q * 4 * S + 4 * l;
+        vstore<float, 4>(yrow + col, acc[q], nt != 0);
+        if (arow) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) aprev[q][i] = __fadd_rn(aprev[q][i], __fmul_rn(epi.w, acc[q][i]));
+            vstore<float, 4>(arow + col, aprev[q], false);
+        }
+        if constexpr (SEND) send_row<4>(epi, row, col, acc[q]);
+    }
+}
+
+template <int VEC, int U, int UH, bool FULL, bool SFULL, typename IP, int NS = 0, bool SEND = false, int LR = 0, int LQ = 1>
 __global__ void __launch_bounds__(kBlock)
 k_spmm(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
        const float* __restrict__ vals, const int32_t* __restrict__ order, int n_rows, int n_heavy,
@@ -437,6 +515,12 @@ k_spmm(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
         const int row = order[item / n_slices];
         slice_wave<UH, SFULL, IP, SEND>(indptr, indices, vals, row, item % n_slices, X, ldx, Y, ldy, d,
                            accumulate, nt, lds + wib * 2 * 256, epi);
+        return;
+    }
+    if constexpr (LR > 0) {   // wide panel: LR light rows per wave
+        const int first = __builtin_amdgcn_readfirstlane((bid - nb_heavy) * kWavesPerBlock + wib) * LR + n_heavy;
+        if (first >= n_rows) return;
+        packed_rows<LR, LQ, U, IP, SEND>(indptr, indices, vals, order, n_rows, first, X, ldx, Y, ldy, accumulate, nt, epi);
         return;
     }
     if constexpr (NS > 0) {   // narrow panel: 64 / NS light rows per wave
@@ -1037,6 +1121,29 @@ __global__ void k_dispatch_delay(int us)
     while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(16);
 }
 
+// Light rows per wave for wide panels (packed_rows): SRGNN_PACKED_ROWS = 0 (one row per wave), 2, 4
+// or 8; SRGNN_PACKED_U = gathers in flight per row (2, 4 or 8).  Results are identical for every setting.
+constexpr int kPackedRowsDefault = 4;
+constexpr int kPackedUDefault = 4;
+int packed_rows_setting()
+{
+    static const int v = [] {
+        const char* e = getenv("SRGNN_PACKED_ROWS");
+        const int x = e ? atoi(e) : kPackedRowsDefault;
+        return (x == 2 || x == 4 || x == 8) ? x : 0;
+    }();
+    return v;
+}
+int packed_u_setting()
+{
+    static const int v = [] {
+        const char* e = getenv("SRGNN_PACKED_U");
+        const int x = e ? atoi(e) : kPackedUDefault;
+        return (x == 2 || x == 4 || x == 8) ? x : kPackedUDefault;
+    }();
+    return v;
+}
+
 int hub_delay_us()
 {
     static const int us = [] { const char* e = getenv("SRGNN_HUB_DISPATCH_DELAY_US"); return e ? atoi(e) : 10; }();
@@ -1202,7 +1309,19 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
     const int64_t n_light = m_rows - n_heavy;
     // narrow panels: S lanes per row (power of two >= d), 64 / S rows per wave
     const int ns = (d <= 32 && !(flags & SRG_SPMM_WIDE_ROWS)) ? (d <= 1 ? 1 : d <= 2 ? 2 : d <= 4 ? 4 : d <= 8 ? 8 : d <= 16 ? 16 : 32) : 0;
-    const int64_t rows_per_block = (int64_t)kWavesPerBlock * (ns ? 64 / ns : 1);
+    // wide panels: LR light rows per wave (packed_rows) when the column tiles line up
+    int lr = 0, lq = 0;
+    if (!ns && !(flags & SRG_SPMM_WIDE_ROWS)) {
+        lr = packed_rows_setting();
+        const int S = lr ? 64 / lr : 0;
+        lq = lr ? d / (4 * S) : 0;
+        const bool ok = lr && d % (4 * S) == 0 && (lq == 1 || lq == 2 || lq == 4) && ldx % 4 == 0 &&
+                        ldy % 4 == 0 && aligned(X, 16) && aligned(Y, 16) &&
+                        (!epi.agg || (epi.lda % 4 == 0 && aligned(epi.agg, 16))) &&
+                        (!epi.send || (epi.lds % 4 == 0 && aligned(epi.send, 16)));
+        if (!ok) lr = lq = 0;
+    }
+    const int64_t rows_per_block = (int64_t)kWavesPerBlock * (ns ? 64 / ns : lr ? lr : 1);
     const int64_t blocks = nb_heavy + (n_light + rows_per_block - 1) / rows_per_block;
     if (blocks > INT32_MAX) return fail(SRG_ERR_INVALID, "grid too large");
     int vec = pick_vec(d, ldx, ldy, X, Y, sizeof(float));
@@ -1221,7 +1340,29 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
     hipLaunchKernelGGL((k_spmm<1, kUnroll, kUnrollHeavy, false, SF, IP, NSV, SEND>), grid, dim3(kBlock), 0, s, \
                        indptr, indices, vals, morder, nr, nh, n_slices, nb_heavy, X, ldx, Y, ldy,     \
                        d, acc, nt, bb, epi)
-        if (ns == 32) {
+#define SRG_LAUNCH_PACKED(LRV, LQV, UV)                                                              \
+    hipLaunchKernelGGL((k_spmm<1, UV, kUnrollHeavy, false, true, IP, 0, SEND, LRV, LQV>), grid, dim3(kBlock), 0, s, \
+                       indptr, indices, vals, morder, nr, nh, n_slices, nb_heavy, X, ldx, Y, ldy,     \
+                       d, acc, nt, bb, epi)
+#define SRG_LAUNCH_PACKED_U(LRV, LQV)                                                                 \
+    do {                                                                                              \
+        if (packed_u_setting() == 4) SRG_LAUNCH_PACKED(LRV, LQV, 4);                                  \
+        else if (packed_u_setting() == 2) SRG_LAUNCH_PACKED(LRV, LQV, 2);                             \
+        else SRG_LAUNCH_PACKED(LRV, LQV, 8);                                                          \
+    } while (0)
+        if (lr == 2) {
+            if (lq == 1) SRG_LAUNCH_PACKED_U(2, 1);
+            else if (lq == 2) SRG_LAUNCH_PACKED_U(2, 2);
+            else SRG_LAUNCH_PACKED_U(2, 4);
+        } else if (lr == 4) {
+            if (lq == 1) SRG_LAUNCH_PACKED_U(4, 1);
+            else if (lq == 2) SRG_LAUNCH_PACKED_U(4, 2);
+            else SRG_LAUNCH_PACKED_U(4, 4);
+        } else if (lr == 8) {
+            if (lq == 1) SRG_LAUNCH_PACKED_U(8, 1);
+            else if (lq == 2) SRG_LAUNCH_PACKED_U(8, 2);
+            else SRG_LAUNCH_PACKED_U(8, 4);
+        } else if (ns == 32) {
             if (sfull) SRG_LAUNCH_NARROW(32, true);
             else SRG_LAUNCH_NARROW(32, false);
         } else if (ns == 16) {
@@ -1249,6 +1390,8 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
         }
 #undef SRG_LAUNCH_SPMM
 #undef SRG_LAUNCH_NARROW
+#undef SRG_LAUNCH_PACKED
+#undef SRG_LAUNCH_PACKED_U
         SRG_HIP_CHECK(hipGetLastError());
     }
     if (ss && !(flags & SRG_SPMM_HUB_NOJOIN)) SRG_HIP_CHECK(hipStreamWaitEvent(s, ss->join, 0));   // join

@@ -38,7 +38,8 @@ def spmm(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor | None = None, accumul
          nt_store: bool = False, wide_rows: bool = False, hub_w256: bool = False,
          hub_nojoin: bool = False) -> torch.Tensor:
     """out[r, :] (+)= A[r, :] @ X  for the rows of A (one hop; exact fma chains in CSR order).
-    wide_rows: diagnostic, one row per wave also for d <= 32; hub_w256: diagnostic, 256-nonzero
+    wide_rows: diagnostic, one row per wave for every light row (no narrow or packed rows);
+    hub_w256: diagnostic, 256-nonzero
     hub windows for any hub launch (same results either way).  hub_nojoin: A's hub rows are left
     running on the library's side stream; the caller must make a stream wait for them
     (srg_hub_join) before reading them."""

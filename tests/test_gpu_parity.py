@@ -446,6 +446,48 @@ def test_narrow_rows_per_wave_bit_exact(oracle_mod, thr, d):
     assert torch.equal(out, y) and torch.equal(agg, 1.0 + 0.25 * y)
 
 
+@pytest.mark.parametrize("thr", [(-1, -1), (None, None), (4, 64)])
+@pytest.mark.parametrize("d,ld", [(64, 64), (128, 128), (128, 132), (256, 256), (192, 192), (96, 100), (200, 200)])
+def test_packed_light_rows_bit_exact(oracle_mod, thr, d, ld):
+    """Wide panels: 4 light rows per wave (packed path; d = 64 / 128 / 256 with 16-byte aligned
+    rows, the others fall back) == one row per wave == the oracle, bit for bit, including
+    ACCUMULATE, the fused aggregation and halo-pack epilogues and strided panels."""
+    from srgnn import synth
+    from srgnn.csr import DeviceCSR
+    from srgnn.spmm import spmm, spmm_agg, spmm_send
+    n = 3000
+    u, v = synth.rmat_undirected_t(n, 24000, seed=50 + d)
+    ip, ix = synth.symmetric_csr_t(n, u, v)
+    vals = torch.from_numpy(np.random.default_rng(d).random(ix.numel()).astype(np.float32) - 0.5)
+    A = DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, heavy_threshold=thr[0], hub_threshold=thr[1], device="cuda")
+    wide = torch.from_numpy(np.random.default_rng(3).standard_normal((n, ld)).astype(np.float32)).cuda()
+    X = wide[:, :d]
+    y = spmm(A, X)
+    np.testing.assert_array_equal(y.cpu().numpy(),
+                                  oracle_mod.spmm(ip.numpy(), ix.numpy(), vals.numpy(), X.cpu().numpy()))
+    assert torch.equal(spmm(A, X, wide_rows=True), y)
+    y2, y3 = y.clone(), y.clone()
+    spmm(A, X, out=y2, accumulate=True)
+    spmm(A, X, out=y3, accumulate=True, wide_rows=True)
+    assert torch.equal(y2, y3)
+    agg = torch.full_like(y, 2.0)
+    out = torch.empty_like(y)
+    spmm_agg(A, X, out, agg, -0.5, False)
+    assert torch.equal(out, y) and torch.equal(agg, 2.0 + (-0.5) * y)
+    # halo pack: every third row stored into two send slots
+    rows = torch.arange(n)
+    cnt = ((rows % 3) == 0).to(torch.int64) * 2
+    ptr = torch.zeros(n + 1, dtype=torch.int64)
+    ptr[1:] = torch.cumsum(cnt, 0)
+    slot = torch.randperm(int(ptr[-1]), generator=torch.Generator().manual_seed(d)).to(torch.int32)
+    send = torch.full((int(ptr[-1]), d), float("nan"), device="cuda")
+    out2 = torch.empty_like(y)
+    spmm_send(A, X, out2, send, ptr.cuda(), slot.cuda())
+    assert torch.equal(out2, y)
+    src = torch.repeat_interleave(rows, cnt).cuda()
+    assert torch.equal(send[slot.long().cuda()], y[src])
+
+
 def test_papers100M_scale_sampled_rows_bit_exact(oracle_mod):
     """The papers100M-shaped graph on one GPU (111 M rows, 3.34e9 nonzeros: indptr beyond 2^31,
     launches chunked beyond 2^32 lanes): one hop checked bit for bit on 2000 sampled rows plus the
