@@ -49,8 +49,8 @@ extern "C" {
 #define SRG_SPMM_ACCUMULATE 0x1u   /* chains start from Y's current content (matmul.c contract) */
 #define SRG_SPMM_NT_STORE 0x2u     /* non-temporal stores of Y */
 /* Diagnostic: one light row per wave.  By default d <= 32 runs 64 / S rows per wave (S = the power
- * of two >= d lanes per row), and d = 64 / 128 / 256 runs 4 light rows per wave (16 lanes per row,
- * 16-byte column chunks).  Results are identical either way. */
+ * of two >= d lanes per row), and d = 64 / 128 / 256 runs 512 / d light rows per wave (two 16-byte
+ * column chunks per lane).  Results are identical either way. */
 #define SRG_SPMM_WIDE_ROWS 0x4
 /* Diagnostic: hub workgroups always use 256-nonzero windows (72 KB of LDS, two per CU).  By default
  * they do only when a launch has more hub workgroups than CUs.  Results are identical either way. */

@@ -1121,18 +1121,22 @@ __global__ void k_dispatch_delay(int us)
     while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(16);
 }
 
-// Light rows per wave for wide panels (packed_rows): SRGNN_PACKED_ROWS = 0 (one row per wave), 2, 4
-// or 8; SRGNN_PACKED_U = gathers in flight per row (2, 4 or 8).  Results are identical for every setting.
-constexpr int kPackedRowsDefault = 4;
+// Light rows per wave for wide panels (packed_rows).  Default: 512 / d rows, so that every lane holds
+// two 16-byte column chunks (d = 128: 4 rows, 16 lanes each; d = 256: 2 rows of 32 lanes; measured
+// best, profiles/r02_ab_d256.txt: 4 rows at d = 256 are 2 % slower than one row per wave).
+// SRGNN_PACKED_ROWS = 0 (one row per wave), 2, 4 or 8 overrides it; SRGNN_PACKED_U = gathers in
+// flight per row (2, 4 or 8).  Results are identical for every setting.
 constexpr int kPackedUDefault = 4;
-int packed_rows_setting()
+int packed_rows_setting(int d)
 {
     static const int v = [] {
         const char* e = getenv("SRGNN_PACKED_ROWS");
-        const int x = e ? atoi(e) : kPackedRowsDefault;
+        if (!e) return -1;
+        const int x = atoi(e);
         return (x == 2 || x == 4 || x == 8) ? x : 0;
     }();
-    return v;
+    if (v >= 0) return v;
+    return d == 64 ? 8 : d == 128 ? 4 : d == 256 ? 2 : 0;
 }
 int packed_u_setting()
 {
@@ -1312,7 +1316,7 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
     // wide panels: LR light rows per wave (packed_rows) when the column tiles line up
     int lr = 0, lq = 0;
     if (!ns && !(flags & SRG_SPMM_WIDE_ROWS)) {
-        lr = packed_rows_setting();
+        lr = packed_rows_setting(d);
         const int S = lr ? 64 / lr : 0;
         lq = lr ? d / (4 * S) : 0;
         const bool ok = lr && d % (4 * S) == 0 && (lq == 1 || lq == 2 || lq == 4) && ldx % 4 == 0 &&

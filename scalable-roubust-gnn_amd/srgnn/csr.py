@@ -12,7 +12,7 @@ A `DeviceCSR` holds the normalised adjacency Â of `GraphOp.construct_adj`
                                      n_heavy rows with more than `heavy_threshold` (one wave per
                                        32-column slice),
                                      then the rest (row waves: one row per wave, or 64 / S
-                                       rows for d <= 32, 4 rows for d = 64 / 128 / 256)
+                                       rows for d <= 32, 512 / d rows for d = 64 / 128 / 256)
 
 The schedule never changes results -- every output element stays one fma chain in CSR order -- it
 only decides which wave works on what and when (power-law hubs start first).
@@ -28,7 +28,7 @@ import torch
 from . import _lib
 
 # Rows longer than this take the slice-wave path; shorter ones the row path, packed 4 rows per wave
-# for wide panels (d = 64, 128, 256).  96 measured best with packing (profiles/r02_ab_heavy_*.txt:
+# for wide panels (512 / d rows at d = 64, 128, 256).  96 measured best with packing (profiles/r02_ab_heavy_*.txt:
 # products hop 7.93 ms vs 8.03 at 32, arxiv 0.168 vs 0.185; papers100M and RMAT-26 gain too).
 DEFAULT_HEAVY_THRESHOLD = int(os.environ.get("SRGNN_HEAVY_THRESHOLD", "96"))
 # "auto": rows whose slice-wave time (~40 ns per nonzero, measured) would exceed about half of the
