@@ -216,7 +216,7 @@ def run_wavelet(a, dev, world=1, rank=0):
     dt = time.perf_counter() - t0
     # roofline: one order's SpMM launch at the block width (HIP events on the launch stream)
     stream = torch.cuda.current_stream(dev)
-    Fm = DeviceCSR(filt.indptr, filt.indices, filt.fvals, n, n, filt.order, filt.n_heavy, filt.n_hub)
+    Fm = filt._csr(filt.fvals)
     tb = torch.empty((n, cb), dtype=torch.float32, device=dev)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * a.roofline_reps)]
     for r in range(a.roofline_reps):

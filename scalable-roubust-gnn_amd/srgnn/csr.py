@@ -27,10 +27,15 @@ import torch
 
 from . import _lib
 
-# Rows longer than this take the slice-wave path; shorter ones the row path, packed 4 rows per wave
-# for wide panels (512 / d rows at d = 64, 128, 256).  96 measured best with packing (profiles/r02_ab_heavy_*.txt:
-# products hop 7.93 ms vs 8.03 at 32, arxiv 0.168 vs 0.185; papers100M and RMAT-26 gain too).
-DEFAULT_HEAVY_THRESHOLD = int(os.environ.get("SRGNN_HEAVY_THRESHOLD", "96"))
+# Rows longer than the heavy threshold take the slice-wave path; shorter ones the row path (packed
+# 512 / d rows per wave at d = 64, 128, 256).  "auto" (default): auto_heavy_threshold(nnz).
+_HEAVY_ENV = os.environ.get("SRGNN_HEAVY_THRESHOLD", "auto")
+DEFAULT_HEAVY_THRESHOLD = None if _HEAVY_ENV == "auto" else int(_HEAVY_ENV)
+# Narrow panels (d <= 32) run their light rows as 64 / S single-lane-per-column rows per wave, whose
+# cost per nonzero is a full dependent gather: they keep the slice waves from 32 up (profiles/
+# r02_ab_auto.txt: d = 8 hop 3.34 ms at 32 vs 3.76 at the wide auto threshold; the RMAT-26 wavelet
+# in 32-column blocks 63.8 vs 98.9 ms per block).  Used when the wide threshold is automatic.
+NARROW_HEAVY_THRESHOLD = int(os.environ.get("SRGNN_NARROW_HEAVY_THRESHOLD", "32"))
 # "auto": rows whose slice-wave time (~40 ns per nonzero, measured) would exceed about half of the
 # expected hop time (~nnz / 13.5e9 s at the measured hop rate) go to the hub path:
 # threshold = nnz // 1024, at least 8192.  Products on 1 GPU -> only the top hub; 1/8 of it -> ~15 K.
@@ -47,6 +52,18 @@ def auto_hub_threshold(nnz: int, launches: int = 1) -> int:
     (profiles/r01_sweep_hub_threshold_*.json): products 123,209 (only the top row) is best;
     arxiv 2,048-4,096 run a hop in 0.208 ms vs 0.236 ms at the former floor of 8,192."""
     return max(2048, int(nnz) // (1024 * max(1, int(launches))))
+
+
+def auto_heavy_threshold(nnz: int, launches: int = 1) -> int:
+    """Row length above which a row is cut into 32-column slice waves instead of running in a packed
+    row wave.  A packed row wave costs ~3 instructions per (nonzero, row) against ~13 for the four
+    slice waves of a row, but a row's latency grows with its length (one dependent gather round per
+    4 nonzeros): a row should be sliced once it would take about a fifth of its launch.  That is
+    nnz / (60000 * launches), floor 96.  Sweeps (profiles/r02_packed_sweep_breakdown.jsonl,
+    r02_ab_big.txt): products best at 2048 (7.42 ms per hop vs 7.92 at 96, 8.78 at 16384 where the
+    longest packed rows become the tail), arxiv at 96-128, papers100M and RMAT-26 flat over
+    20000-110000 and 2 % faster than at 96."""
+    return max(96, int(nnz) // (60000 * max(1, int(launches))))
 
 
 def _dev(device):
@@ -68,6 +85,12 @@ class DeviceCSR:
     order: torch.Tensor
     n_heavy: int
     n_hub: int = 0
+    n_heavy_narrow: int | None = None    # slice-wave rows for d <= 32 (None: n_heavy)
+
+    def heavy(self, d: int) -> int:
+        """The slice-wave row count for a panel of d columns (same order, a longer prefix of it
+        for narrow panels)."""
+        return self.n_heavy_narrow if (d <= 32 and self.n_heavy_narrow is not None) else self.n_heavy
 
     @property
     def nnz(self) -> int:
@@ -101,7 +124,8 @@ class DeviceCSR:
             _lib.call(device, "srg_csr_validate", ip.data_ptr(), ix.data_ptr(), n_rows, ix.numel(), n_cols,
                       _lib.stream(device))
         order, n_heavy, n_hub = make_schedule(ip, heavy_threshold, hub_threshold)
-        return cls(ip, ix, vv, n_rows, int(n_cols), order, n_heavy, n_hub)
+        return cls(ip, ix, vv, n_rows, int(n_cols), order, n_heavy, n_hub,
+                   narrow_heavy(ip, n_hub) if _auto_heavy(heavy_threshold) else None)
 
     @classmethod
     def from_scipy(cls, adj, heavy_threshold=None, device=None):
@@ -119,7 +143,20 @@ class DeviceCSR:
         ip = ip - base
         order, n_heavy, n_hub = make_schedule(ip, heavy_threshold, hub_threshold)
         return DeviceCSR(ip.contiguous(), self.indices[base:end], self.values[base:end],
-                         r1 - r0, self.n_cols, order, n_heavy, n_hub)
+                         r1 - r0, self.n_cols, order, n_heavy, n_hub,
+                         narrow_heavy(ip, n_hub) if _auto_heavy(heavy_threshold) else None)
+
+
+def _auto_heavy(heavy_threshold) -> bool:
+    return heavy_threshold is None and DEFAULT_HEAVY_THRESHOLD is None
+
+
+def narrow_heavy(indptr: torch.Tensor, n_hub: int, threshold: int | None = None) -> int:
+    """Slice-wave rows of the schedule for narrow panels: rows longer than NARROW_HEAVY_THRESHOLD,
+    hubs excluded (they lead the same decreasing-length order)."""
+    t = NARROW_HEAVY_THRESHOLD if threshold is None else threshold
+    deg = indptr[1:] - indptr[:-1]
+    return max(0, int((deg > t).sum().item()) - int(n_hub)) if deg.numel() else 0
 
 
 def make_schedule(indptr: torch.Tensor, heavy_threshold=None, hub_threshold=None):
@@ -128,6 +165,8 @@ def make_schedule(indptr: torch.Tensor, heavy_threshold=None, hub_threshold=None
     more than heavy_threshold.  A negative threshold disables that group."""
     if heavy_threshold is None:
         heavy_threshold = DEFAULT_HEAVY_THRESHOLD
+    if heavy_threshold is None:
+        heavy_threshold = auto_heavy_threshold(int(indptr[-1]) if indptr.numel() else 0)
     if hub_threshold is None:
         hub_threshold = DEFAULT_HUB_THRESHOLD
     if hub_threshold is None:

@@ -279,7 +279,8 @@ class HaloPartitionedOperator:
                  heavy_threshold=None, hub_threshold=None, device=None, rank=None, world=None,
                  local_spmm=None, ghost_max_degree=None, hub_launches=None, giant_weight=None,
                  calibrate_link: bool = True):
-        from .csr import DEFAULT_HEAVY_THRESHOLD, DEFAULT_HUB_THRESHOLD, auto_hub_threshold
+        from .csr import (DEFAULT_HEAVY_THRESHOLD, DEFAULT_HUB_THRESHOLD, NARROW_HEAVY_THRESHOLD,
+                          auto_heavy_threshold, auto_hub_threshold)
         self.group = group
         self.virtual = rank is not None
         self.rank = rank if rank is not None else (dist.get_rank(group) if dist.is_initialized() else 0)
@@ -430,8 +431,13 @@ class HaloPartitionedOperator:
         # --- per-group row schedules (local row ids; long rows first)
         lgrp = grp[r0:r1]
         ldeg = deg[r0:r1]
-        heavy_t = DEFAULT_HEAVY_THRESHOLD if heavy_threshold is None else heavy_threshold
+        if heavy_threshold is None:
+            heavy_threshold = DEFAULT_HEAVY_THRESHOLD
+        # per launch: the rank's nonzeros split over its row chunks, as for the hub threshold
+        auto_heavy = heavy_threshold is None
+        heavy_t = auto_heavy_threshold(int(lip[self.rows]), launches=C) if auto_heavy else heavy_threshold
         self.views = []
+        narrow = []           # slice-wave rows of each view for narrow panels (d <= 32), automatic only
         for g in range(G):
             rows_g = torch.nonzero(lgrp == g).flatten()
             rows_g = rows_g[torch.sort(ldeg[rows_g], descending=True, stable=True).indices]
@@ -442,11 +448,13 @@ class HaloPartitionedOperator:
                 n_hub = 0
                 n_heavy = int((ldeg[rows_g] > heavy_t).sum()) if heavy_t >= 0 else 0
             self.views.append((rows_g.to(torch.int32).contiguous(), n_g, n_heavy, n_hub))
+            narrow.append(int((ldeg[rows_g] > NARROW_HEAVY_THRESHOLD).sum()) if auto_heavy and g != C else None)
         # the ghost rows: one more launch (no exchange), panel rows rows + n_recv + i
         gsort = torch.sort(gdeg, descending=True, stable=True)
         g_rows = (self.rows + self.n_recv + gsort.indices).to(torch.int32).contiguous()
         g_heavy = int((gsort.values > heavy_t).sum()) if heavy_t >= 0 else 0
         self.ghost_view = (g_rows, self.n_ghost, g_heavy, 0)
+        narrow.append(int((gsort.values > NARROW_HEAVY_THRESHOLD).sum()) if auto_heavy else None)
         self._lip, self._lix, self._lvv = lip, lix, lvv
         if local_spmm is None:
             from .csr import DeviceCSR
@@ -455,8 +463,8 @@ class HaloPartitionedOperator:
                 from . import _lib
                 _lib.call(dev, "srg_csr_validate", lip.data_ptr(), lix.data_ptr(), self.rows + self.halo,
                           lix.numel(), self.ncols_local, _lib.stream(dev))
-            self._A = [DeviceCSR(lip, lix, lvv, n_g, self.ncols_local, order, n_heavy, n_hub)
-                       for (order, n_g, n_heavy, n_hub) in self.views + [self.ghost_view]]
+            self._A = [DeviceCSR(lip, lix, lvv, n_g, self.ncols_local, order, n_heavy, n_hub, nn)
+                       for (order, n_g, n_heavy, n_hub), nn in zip(self.views + [self.ghost_view], narrow)]
             self._spmm = lambda A, X, out: spmm(A, X, out=out)
         else:
             self._A = [(lip, lix, lvv, order) for (order, _, _, _) in self.views + [self.ghost_view]]
@@ -479,7 +487,8 @@ class HaloPartitionedOperator:
             other._A = [(a[0], a[1], lvv, a[3]) for a in self._A]
         else:
             from .csr import DeviceCSR
-            other._A = [DeviceCSR(a.indptr, a.indices, lvv, a.n_rows, a.n_cols, a.order, a.n_heavy, a.n_hub)
+            other._A = [DeviceCSR(a.indptr, a.indices, lvv, a.n_rows, a.n_cols, a.order, a.n_heavy, a.n_hub,
+                                  a.n_heavy_narrow)
                         for a in self._A]
         return other
 

@@ -56,7 +56,7 @@ def spmm(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor | None = None, accumul
         (_lib.SRG_SPMM_WIDE_ROWS if wide_rows else 0) | (_lib.SRG_SPMM_HUB_W256 if hub_w256 else 0) | \
         (_lib.SRG_SPMM_HUB_NOJOIN if hub_nojoin else 0)
     _lib.call(X.device, "srg_spmm_csr_f32", A.indptr.data_ptr(), A.indices.data_ptr(), A.values.data_ptr(),
-              A.n_rows, A.order.data_ptr() if A.n_rows else None, A.n_hub, A.n_heavy, X.data_ptr(),
+              A.n_rows, A.order.data_ptr() if A.n_rows else None, A.n_hub, A.heavy(d), X.data_ptr(),
               X.stride(0), out.data_ptr(), out.stride(0), d, flags, _stream(X.device))
     return out
 
@@ -73,7 +73,7 @@ def spmm_agg(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, agg: torch.Tensor
         raise ValueError("A, X, out and agg must be on the same device")
     flags = _lib.SRG_SPMM_NT_STORE if nt_store else 0
     _lib.call(X.device, "srg_spmm_agg_f32", A.indptr.data_ptr(), A.indices.data_ptr(), A.values.data_ptr(),
-              A.n_rows, A.order.data_ptr() if A.n_rows else None, A.n_hub, A.n_heavy, X.data_ptr(),
+              A.n_rows, A.order.data_ptr() if A.n_rows else None, A.n_hub, A.heavy(d), X.data_ptr(),
               X.stride(0), out.data_ptr(), out.stride(0), d, flags, agg.data_ptr(), agg.stride(0),
               float(w), 1 if init else 0, _stream(X.device))
     return out
@@ -96,7 +96,7 @@ def spmm_send(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, send: torch.Tens
     if send_slot.numel() and send.shape[0] == 0:
         raise ValueError("send slots into an empty send buffer")
     _lib.call(X.device, "srg_spmm_send_f32", A.indptr.data_ptr(), A.indices.data_ptr(), A.values.data_ptr(),
-              A.n_rows, A.order.data_ptr() if A.n_rows else None, A.n_hub, A.n_heavy, X.data_ptr(),
+              A.n_rows, A.order.data_ptr() if A.n_rows else None, A.n_hub, A.heavy(d), X.data_ptr(),
               X.stride(0), out.data_ptr(), out.stride(0), d, 0,
               send.data_ptr() if send.numel() else None, send.stride(0) if send.shape[0] > 1 else d,
               send_ptr.data_ptr(), send_slot.data_ptr() if send_slot.numel() else None,
@@ -150,7 +150,7 @@ def propagate(A: DeviceCSR, X: torch.Tensor, K: int, panels: list | None = None,
     arr = (ctypes.c_void_p * (K + 1))(*[p.data_ptr() for p in panels])
     flags = _lib.SRG_SPMM_NT_STORE if nt_store else 0
     _lib.call(X.device, "srg_propagate_khop_f32", A.indptr.data_ptr(), A.indices.data_ptr(),
-              A.values.data_ptr(), n, A.order.data_ptr() if n else None, A.n_hub, A.n_heavy, arr, ld, d,
+              A.values.data_ptr(), n, A.order.data_ptr() if n else None, A.n_hub, A.heavy(d), arr, ld, d,
               K, flags, _stream(X.device))
     if panels[0] is not X0 and X is not X0:
         panels = [X0] + list(panels[1:])

@@ -29,7 +29,7 @@ import scipy.sparse as sp
 import torch
 
 from . import _lib
-from .csr import DeviceCSR, make_schedule
+from .csr import DeviceCSR, _auto_heavy, make_schedule, narrow_heavy
 
 
 def laplacian_from_adj(adj: sp.spmatrix) -> sp.csr_matrix:
@@ -150,6 +150,7 @@ class HeatWaveletFilter:
         del diag, l64
         self.lvals = lvals.to(dtype)
         self.order, self.n_heavy, self.n_hub = make_schedule(self.indptr, heavy_threshold, hub_threshold)
+        self.n_heavy_narrow = narrow_heavy(self.indptr, self.n_hub) if _auto_heavy(heavy_threshold) else None
 
     def _coef(self, ct, vals):
         return (ct * len(vals))(*vals)
@@ -213,7 +214,8 @@ class HeatWaveletFilter:
         return R
 
     def _csr(self, vals):
-        return DeviceCSR(self.indptr, self.indices, vals, self.n, self.n, self.order, self.n_heavy, self.n_hub)
+        return DeviceCSR(self.indptr, self.indices, vals, self.n, self.n, self.order, self.n_heavy, self.n_hub,
+                         self.n_heavy_narrow)
 
     def _apply_split(self, Sb, Rb, work):
         """One column block: Sb [n, w] and Rb [ns, n, w] may be strided views."""
