@@ -1136,7 +1136,11 @@ int packed_rows_setting(int d)
         return (x == 2 || x == 4 || x == 8) ? x : 0;
     }();
     if (v >= 0) return v;
-    return d == 64 ? 8 : d == 128 ? 4 : d == 256 ? 2 : 0;
+    // d = 32 (8 rows of 8 lanes, one chunk each) measured even with the narrow path on products
+    // (3.46 vs 3.42 ms per hop) and within 3 % on the RMAT-26 wavelet blocks: off unless asked for
+    // (SRGNN_PACKED_D32=1; profiles/r02_ab_d32.txt)
+    static const bool d32 = [] { const char* e = getenv("SRGNN_PACKED_D32"); return e ? atoi(e) != 0 : false; }();
+    return d == 32 ? (d32 ? 8 : 0) : d == 64 ? 8 : d == 128 ? 4 : d == 256 ? 2 : 0;
 }
 int packed_u_setting()
 {
@@ -1311,20 +1315,20 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
     const int64_t m_rows = n_rows - n_hub;
     const int nb_heavy = (int)((n_heavy * n_slices + kWavesPerBlock - 1) / kWavesPerBlock);
     const int64_t n_light = m_rows - n_heavy;
-    // narrow panels: S lanes per row (power of two >= d), 64 / S rows per wave
-    const int ns = (d <= 32 && !(flags & SRG_SPMM_WIDE_ROWS)) ? (d <= 1 ? 1 : d <= 2 ? 2 : d <= 4 ? 4 : d <= 8 ? 8 : d <= 16 ? 16 : 32) : 0;
-    // wide panels: LR light rows per wave (packed_rows) when the column tiles line up
+    // light rows: LR rows per wave (packed_rows) when the column tiles line up; else, for d <= 32,
+    // 64 / S rows per wave (narrow_rows); else one row per wave
     int lr = 0, lq = 0;
-    if (!ns && !(flags & SRG_SPMM_WIDE_ROWS)) {
-        lr = packed_rows_setting(d);
-        const int S = lr ? 64 / lr : 0;
-        lq = lr ? d / (4 * S) : 0;
-        const bool ok = lr && d % (4 * S) == 0 && (lq == 1 || lq == 2 || lq == 4) && ldx % 4 == 0 &&
+    if (!(flags & SRG_SPMM_WIDE_ROWS)) {
+        const int cand = packed_rows_setting(d);
+        const int S = cand ? 64 / cand : 0;
+        const int q = cand ? d / (4 * S) : 0;
+        const bool ok = cand && d % (4 * S) == 0 && (q == 1 || q == 2 || q == 4) && ldx % 4 == 0 &&
                         ldy % 4 == 0 && aligned(X, 16) && aligned(Y, 16) &&
                         (!epi.agg || (epi.lda % 4 == 0 && aligned(epi.agg, 16))) &&
                         (!epi.send || (epi.lds % 4 == 0 && aligned(epi.send, 16)));
-        if (!ok) lr = lq = 0;
+        if (ok) { lr = cand; lq = q; }
     }
+    const int ns = (!lr && d <= 32 && !(flags & SRG_SPMM_WIDE_ROWS)) ? (d <= 1 ? 1 : d <= 2 ? 2 : d <= 4 ? 4 : d <= 8 ? 8 : d <= 16 ? 16 : 32) : 0;
     const int64_t rows_per_block = (int64_t)kWavesPerBlock * (ns ? 64 / ns : lr ? lr : 1);
     const int64_t blocks = nb_heavy + (n_light + rows_per_block - 1) / rows_per_block;
     if (blocks > INT32_MAX) return fail(SRG_ERR_INVALID, "grid too large");
