@@ -55,6 +55,8 @@ _STUBS = {
         "import torch\n"
         "def coalesce(index, value, m, n, op='add'):\n"
         "    assert op == 'add'\n"
+        "    if index.shape[1] == 0:\n"
+        "        return index, value\n"
         "    row, col = index[0], index[1]\n"
         "    key = n * row + col\n"
         "    key, perm = key.sort(stable=True)\n"
@@ -153,12 +155,28 @@ def main():
     graphs["cora"] = (adj, synth.uniform_features_np(adj.shape[0], 24, seed=80), 3)
     adj = directed_random(90, 0.06, seed=500)
     graphs["rand"] = (adj, synth.uniform_features_np(90, 16, seed=81), 3)
+    # edge cases: a single node with a self-loop; one directed edge plus an isolated node; no edges
+    graphs["tiny1"] = (sp.csr_matrix(np.array([[2.0]])), synth.uniform_features_np(1, 4, seed=82), 2)
+    graphs["tiny3"] = (sp.csr_matrix(np.array([[0.0, 1.5, 0.0], [0.0, 0.0, 0.0], [0.0, 0.0, 0.0]])),
+                       synth.uniform_features_np(3, 4, seed=83), 2)
+    graphs["empty4"] = (sp.csr_matrix((4, 4)), synth.uniform_features_np(4, 4, seed=84), 2)
     for gname, (adj, X, K) in graphs.items():
         for key, (_, _, kw) in OPS.items():
-            if gname == "cora" and key == "mag_lap_q01_r03":
+            if gname != "rand" and key == "mag_lap_q01_r03":
                 continue
             op = classes[key](K, **kw)
-            lists = op.propagate(adj, X)
+            try:
+                lists = op.propagate(adj, X)
+            except Exception as e:  # noqa: BLE001 -- the reference's own failure is the fixture
+                name = f"dir_{gname}_{key}"
+                manifest[name] = {"n": adj.shape[0], "d": X.shape[1], "k": K, "op": "directed_error",
+                                  "operator": key, "class": OPS[key][1], "kwargs": kw, "error": type(e).__name__,
+                                  "message": str(e)[:200]}
+                np.savez_compressed(os.path.join(MG.OUT, f"{name}.npz"),
+                                    adj_indptr=adj.indptr.astype(np.int64), adj_indices=adj.indices.astype(np.int32),
+                                    adj_data=adj.data.astype(np.float64), x=X)
+                print(name, "raises", type(e).__name__, str(e)[:80], flush=True)
+                continue
             if key in ("mag_lap", "mag_lap_q01_r03", "mag_comppr"):
                 mats = {"real": op.real_adj, "imag": op.imag_adj}
             elif key == "two_dir":
