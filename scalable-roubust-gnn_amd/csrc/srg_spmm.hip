@@ -259,6 +259,14 @@ constexpr int64_t kMaxLaunchBlocks = int64_t(1) << 23;
 // Both roles produce bit-identical results (one fma chain per output element, CSR order).
 // ------------------------------------------------------------------------------------------------
 constexpr int kSliceCols = 32;
+// LDS tiles per slice wave (8 nonzeros x 32 columns, 1 KB each).  One suffices: a wave's LDS
+// operations complete in issue order, so the next group's write cannot overtake this group's reads.
+// Two (the round-1 layout) cost 8 KB per k_spmm block, which beside the hub group's 72 KB workgroups
+// (halo exchange) left room for only two row blocks per CU.
+#ifndef SRG_SLICE_LDS_BUFS
+#define SRG_SLICE_LDS_BUFS 1
+#endif
+constexpr int kSliceLdsBufs = SRG_SLICE_LDS_BUFS;
 
 // Epilogues of the SpMM kernels (every output element y a kernel stores may also go to):
 //  * fused hop aggregation (srgnn.aggregate): with agg != nullptr it is folded into the accumulator
@@ -331,7 +339,7 @@ __device__ __forceinline__ void slice_wave(const IP* __restrict__ indptr,
             const int64_t jb = j + b * 8;
             if (jb >= end) break;                               // wave-uniform
             const int nb = (end - jb) < 8 ? (int)(end - jb) : 8;
-            float* slot = lds + (b & 1) * 256;
+            float* slot = lds + (kSliceLdsBufs == 2 ? (b & 1) * 256 : 0);
             *reinterpret_cast<V4*>(slot + lane * 4) = x[b];     // tile [g][32 cols]
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -506,7 +514,7 @@ k_spmm(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
 {
     typedef typename Vec<float, VEC>::type V;
     const int bid = block_base + (int)blockIdx.x;
-    __shared__ __attribute__((aligned(16))) float lds[kWavesPerBlock * 2 * 256];
+    __shared__ __attribute__((aligned(16))) float lds[kWavesPerBlock * kSliceLdsBufs * 256];
     const int lane = threadIdx.x & 63;
     const int wib = threadIdx.x >> 6;
     if (bid < nb_heavy) {
@@ -514,7 +522,7 @@ k_spmm(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
         if (item >= n_heavy * n_slices) return;
         const int row = order[item / n_slices];
         slice_wave<UH, SFULL, IP, SEND>(indptr, indices, vals, row, item % n_slices, X, ldx, Y, ldy, d,
-                           accumulate, nt, lds + wib * 2 * 256, epi);
+                           accumulate, nt, lds + wib * kSliceLdsBufs * 256, epi);
         return;
     }
     if constexpr (LR > 0) {   // wide panel: LR light rows per wave
