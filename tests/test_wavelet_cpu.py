@@ -111,3 +111,40 @@ def test_l1_normalization_restatement_matches_sklearn():
             got.data[lo:hi] = (M.data[lo:hi].astype(np.float64) / acc).astype(np.float32)
     want = normalize(M, norm="l1", axis=1)
     np.testing.assert_array_equal(got.data, want.data)
+
+
+def _wavelet_golden(name):
+    import golden_cases as G
+    z = np.load(f"{G.GOLDEN}/{name}.npz", allow_pickle=False)
+    n = z["adj_indptr"].size - 1
+    adj = sp.csr_matrix((z["adj_data"], z["adj_indices"], z["adj_indptr"]), shape=(n, n))
+    return z, adj, n
+
+
+@pytest.mark.parametrize("name", ["wav_rand", "wav_cora"])
+def test_oracle_wavelet_basis_equals_reference_spectral_model(oracle_mod, name):
+    """phi and phi^-1 of the REFERENCE's own SpectralModel.preprocess (tests/golden/make_golden_wavelet.py:
+    real networkx, its impulse batches, threshold, float32 blocks and sklearn normalisation; pygsp
+    restated) equal the oracle's restatement bit for bit, with the fixture's lmax."""
+    from sklearn.preprocessing import normalize
+    z, adj, n = _wavelet_golden(name)
+    lmax, scale, order, tol = float(z["lmax"]), float(z["scale"]), int(z["order"]), float(z["tolerance"])
+    L = oracle_mod.laplacian(adj.indptr, adj.indices, adj.data, n)
+    Lh = W.laplacian_from_adj(adj)
+    assert np.array_equal(Lh.indptr, L[0]) and np.array_equal(Lh.indices, L[1]) and np.array_equal(Lh.data, L[2])
+    coeffs = np.stack([oracle_mod.cheby_coeffs(t, lmax, order) for t in (-scale, scale)])
+    blocks = [[], []]
+    for c0 in range(0, n, 1000):
+        w = min(1000, n - c0)
+        S = np.zeros((n, w))
+        S[np.arange(c0, c0 + w), np.arange(w)] = 1
+        R = oracle_mod.cheby_op(L, coeffs, S, lmax)
+        for s in range(2):
+            sub = R[s].copy()
+            sub[sub < tol] = 0
+            blocks[s].append(sp.csr_matrix(sub.astype(np.float32)))
+    for s in range(2):
+        phi = normalize(sp.hstack(blocks[s]).tocsr(), norm="l1", axis=1)
+        np.testing.assert_array_equal(phi.indptr, z[f"phi{s}_indptr"])
+        np.testing.assert_array_equal(phi.indices, z[f"phi{s}_indices"])
+        assert np.array_equal(phi.data, z[f"phi{s}_data"])

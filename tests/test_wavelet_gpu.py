@@ -150,3 +150,26 @@ def test_halo_wavelet_virtual_ranks_bitwise(world, chunks):
     want = one.apply(S, split=True)
     got = simulate_halo_wavelet(ip, ix, lv, n, S, [-0.5, 0.5], 3, lmax, world, chunks=chunks, device="cuda")
     assert torch.equal(got, want)
+
+
+@pytest.mark.parametrize("name", ["wav_rand", "wav_cora"])
+def test_wavelet_basis_equals_reference_spectral_model(name):
+    """The GPU wavelet basis against the REFERENCE's own SpectralModel.preprocess (golden wav_*,
+    pygsp restated in the fixture generator): phi and phi^-1 bit for bit (fp64 recurrence, threshold,
+    fp32 blocks, L1 normalisation), processed_feature = [X | relu(phi phi^-1 X)] within 1e-5 of its
+    scale (the reference forms phi phi^-1 with a sparse-sparse product first; here phi (phi^-1 X))."""
+    import golden_cases as G
+    from srgnn.wavelet import spectral_features
+    z = np.load(f"{G.GOLDEN}/{name}.npz", allow_pickle=False)
+    n = z["adj_indptr"].size - 1
+    adj = sp.csr_matrix((z["adj_data"], z["adj_indices"], z["adj_indptr"]), shape=(n, n))
+    feat, phi, phi_inv, lmax = spectral_features(adj, z["x"], float(z["scale"]), int(z["order"]),
+                                                 float(z["tolerance"]), lmax=float(z["lmax"]), device="cuda")
+    for s, m in enumerate((phi, phi_inv)):
+        m = sp.csr_matrix(m)
+        np.testing.assert_array_equal(m.indptr, z[f"phi{s}_indptr"])
+        np.testing.assert_array_equal(m.indices, z[f"phi{s}_indices"])
+        assert np.array_equal(m.data, z[f"phi{s}_data"]), f"phi{s} values differ"
+    want = z["processed_feature"]
+    assert feat.shape == want.shape and feat.dtype == torch.float32
+    np.testing.assert_allclose(feat.numpy(), want, rtol=1e-5, atol=1e-5 * np.abs(want).max())
