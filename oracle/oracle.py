@@ -16,8 +16,10 @@ does, and it must not be used as a fallback.
                                                  SSRG/operators/utils.py:426-437
   laplacian, cheby_coeffs, cheby_op
                   restate the wavelet basis' pygsp calls (SSRG/models/base_scalable/
-                  base_model.py:180-191, 236-265): PARITY UNPINNED -- pygsp is not in the
-                  reference tree nor installed here; validated against a dense eigendecomposition.
+                  base_model.py:180-191, 236-265); pygsp is not in the reference tree nor installed
+                  here.  Pinned on the reference's own SpectralModel.preprocess run with pygsp
+                  restated (tests/golden/wav_*.npz, bit-identical phi / phi^-1) and validated
+                  against a dense eigendecomposition.
 
 Pinning: sym_norm/spmm/propagate are checked against tests/golden/*.npz, produced by running the
 reference's own Python operators (tests/golden/make_golden.py), and spmm against ref_spmm.
@@ -224,7 +226,7 @@ def ref_spmm(indptr, indices, values, X):
 
 
 # ------------------------------------------------------------------------------------------------
-# wavelet basis (parity unpinned: restates pygsp 0.5.x)
+# wavelet basis (restates pygsp 0.5.x; pinned by tests/golden/wav_*.npz from the reference's SpectralModel)
 # ------------------------------------------------------------------------------------------------
 def laplacian(indptr, indices, data, n):
     """Combinatorial Laplacian L = D - W of nx.Graph(adj) (base_model.py:181-183): W is the

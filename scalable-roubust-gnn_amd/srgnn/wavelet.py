@@ -15,8 +15,9 @@ load-balanced SpMM (slice waves, hub workgroups) plus srg_cheby_epilogue_f32 -- 
 the fused kernel -- and the panel can be filtered in column blocks (`col_block`) so that
 billion-edge graphs with d = 256 fit in HBM (R is written in place, no block copies).
 
-pygsp is not available offline: the restatement follows pygsp 0.5.x semantics and is validated
-against a dense eigendecomposition (tests) -- parity with the reference is unpinned.  lmax is an
+pygsp is not available offline: the restatement follows pygsp 0.5.x semantics.  phi and phi^-1 are
+bit-identical to the reference's own SpectralModel.preprocess run with pygsp restated
+(tests/golden/wav_*.npz) and validated against a dense eigendecomposition.  lmax is an
 explicit input (pygsp's ARPACK estimate uses a random start vector); `estimate_lmax` gives the
 same estimator (eigsh, tol 5e-3, x1.01) with a fixed start vector.
 """
@@ -300,8 +301,8 @@ def spectral_features(adj: sp.spmatrix, feature, scale: float = 0.5, order: int 
 
     The reference forms the product matrix phi phi^-1 with torch_sparse.spspmm and then multiplies
     X; here phi (phi^-1 X) is two exact-chain SpMMs on the GPU (no SpGEMM, no N x N product).
-    Same value up to floating-point association -- parity unpinned (torch_sparse is absent), the
-    tests compare against a dense fp64 evaluation."""
+    Same value up to floating-point association: the tests compare against the reference's
+    processed_feature (tests/golden/wav_*.npz) within 1e-5 and against a dense fp64 evaluation."""
     from .csr import DeviceCSR
     from .spmm import spmm
     phi, phi_inv, lmax = wavelet_basis(adj, scale, order, tolerance, lmax, batch, device)
