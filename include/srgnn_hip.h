@@ -221,6 +221,45 @@ int srg_hub_join(void* stream);
 int srg_csr_validate(const int64_t* indptr, const int32_t* indices, int64_t n_rows,
                      int64_t nnz, int64_t n_cols, void* stream);
 
+/* ---- multi-GPU: communicators and the row-partitioned K-hop propagation ---------------------------
+ * SURVEY.md §8(b) item 5, for C / C++ hosts (the Python package drives the same kernels through
+ * torch.distributed: srgnn/dist.py).  RCCL is loaded at run time.  Rank r owns rows
+ * [row_starts[r], row_starts[r+1]) of Â and of every hop panel; per hop the blocks are exchanged
+ * with grouped ncclSend / ncclRecv to every peer (variable block sizes) and each rank multiplies its
+ * rows by the gathered panel (srg_spmm_csr_f32).  Every hop is bitwise the one-GPU hop (each row's
+ * fma chain is unchanged).  Replaces the reference's single-process hop loop,
+ * SSRG/operators/base_operator.py:32-35. */
+typedef struct srg_comm srg_comm;
+#define SRG_COMM_ID_BYTES 128
+/* RCCL unique id (SRG_COMM_ID_BYTES bytes) to share out of band before srg_comm_init_rank. */
+int srg_comm_unique_id(void* id_out);
+/* One rank per process: `device` is this process's HIP device. */
+int srg_comm_init_rank(int nranks, const void* id, int rank, int device, srg_comm** comm);
+/* One process driving ndev devices (devices == NULL: 0 .. ndev-1); rank i = devices[i]. */
+int srg_comm_init_all(int ndev, const int* devices, srg_comm** comm);
+int srg_comm_destroy(srg_comm* comm);
+int srg_comm_size(const srg_comm* comm);
+
+/* One local rank's share (device pointers on `device`). */
+typedef struct {
+    int device;
+    const int64_t* indptr;        /* [n_rows + 1], rebased to 0 */
+    const int32_t* indices;       /* global column ids (rows of the gathered panel) */
+    const float* values;
+    int64_t row0, n_rows;         /* must equal the rank's row_starts block */
+    const int32_t* row_order;     /* optional schedule, as srg_spmm_csr_f32 */
+    int64_t n_hub, n_heavy;
+    float* x_full;                /* [row_starts[P], ld] gather buffer */
+    float* const* panels;         /* HOST array of K + 1 pointers, each [n_rows, ld]; panels[0] = own X rows */
+    void* stream;                 /* hipStream_t of `device` (NULL: its null stream) */
+} srg_shard_f32;
+
+/* panels[k] = (rank's rows of Â) * (panel k-1 gathered from every rank), k = 1..K, for every local
+ * shard (shards[i] belongs to the communicator's i-th local rank).  Asynchronous on each shard's
+ * stream; the exchange is a grouped RCCL call across the local ranks. */
+int srg_dist_propagate_khop_f32(srg_comm* comm, const srg_shard_f32* shards, int n_shards,
+                                const int64_t* row_starts, int64_t ld, int32_t d, int32_t K);
+
 /* ---- diagnostics ----------------------------------------------------------------------------- */
 const char* srg_last_error(void);   /* thread-local message of the last failure ("" if none) */
 int srg_last_error_code(void);      /* thread-local status of the last call (SRG_OK if fine)  */

@@ -1875,6 +1875,11 @@ int srg_csr_validate(const int64_t* indptr, const int32_t* indices, int64_t n_ro
 
 const char* srg_last_error(void) { return g_err_msg; }
 int srg_last_error_code(void) { return g_err_code; }
+// the communicator entries (srg_comm.hip) report through the same thread-local status
+__attribute__((visibility("hidden"))) void srg_set_error(int code, const char* msg)
+{
+    (void)fail(code, "%s", msg);
+}
 void srg_clear_error(void) { (void)ok(); }
 const char* srg_version(void) { return "srgnn_hip " SRG_GIT_REV " gfx950"; }
 

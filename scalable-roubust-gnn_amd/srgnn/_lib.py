@@ -53,6 +53,12 @@ EXPORTED_SYMBOLS = (
     "srg_gather_rows_f32",
     "srg_hub_join",
     "srg_csr_validate",
+    "srg_comm_unique_id",
+    "srg_comm_init_rank",
+    "srg_comm_init_all",
+    "srg_comm_destroy",
+    "srg_comm_size",
+    "srg_dist_propagate_khop_f32",
     "srg_last_error",
     "srg_last_error_code",
     "srg_clear_error",
@@ -113,6 +119,18 @@ def _declare(lib):
     lib.srg_hub_join.restype = ctypes.c_int
     lib.srg_csr_validate.argtypes = [_p, _p, _i64, _i64, _i64, _p]
     lib.srg_csr_validate.restype = ctypes.c_int
+    lib.srg_comm_unique_id.argtypes = [_p]
+    lib.srg_comm_unique_id.restype = ctypes.c_int
+    lib.srg_comm_init_rank.argtypes = [ctypes.c_int, _p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_p)]
+    lib.srg_comm_init_rank.restype = ctypes.c_int
+    lib.srg_comm_init_all.argtypes = [ctypes.c_int, _p, ctypes.POINTER(_p)]
+    lib.srg_comm_init_all.restype = ctypes.c_int
+    lib.srg_comm_destroy.argtypes = [_p]
+    lib.srg_comm_destroy.restype = ctypes.c_int
+    lib.srg_comm_size.argtypes = [_p]
+    lib.srg_comm_size.restype = ctypes.c_int
+    lib.srg_dist_propagate_khop_f32.argtypes = [_p, _p, ctypes.c_int, _p, _i64, _i32, _i32]
+    lib.srg_dist_propagate_khop_f32.restype = ctypes.c_int
     lib.srg_last_error.argtypes = []
     lib.srg_last_error.restype = ctypes.c_char_p
     lib.srg_last_error_code.argtypes = []
@@ -166,6 +184,17 @@ def call(device, name: str, *args) -> None:
             check(fn(*args), name)
     else:
         check(fn(*args), name)
+
+
+def call_host(name: str, *args) -> None:
+    """Entry points that choose their devices themselves (srg_comm_*, srg_dist_propagate_khop_f32:
+    every shard names its device) -- no device guard; raises SrgError on a failed status."""
+    check(getattr(lib(), name)(*args), name)
+
+
+def query(name: str, *args) -> int:
+    """An entry point that returns a value, not a status (srg_comm_size)."""
+    return getattr(lib(), name)(*args)
 
 
 def version() -> str:

@@ -163,3 +163,34 @@ def test_segment_sum_f32_equals_oracle(oracle_mod):
     got = segment_sum(torch.from_numpy(ptr).to(dev), torch.from_numpy(v).to(dev))
     assert got.dtype == torch.float32
     assert np.array_equal(got.cpu().numpy(), oracle_mod.segment_sum(ptr, v))
+
+
+UTILS = {"mag_lap": "adj_to_directed_symmetric_mag_norm", "mag_lap_q01_r03": "adj_to_directed_symmetric_mag_norm",
+         "pygsd_mag": "PyGSD_adj_to_directed_symmetric_mag_norm", "two_dir": "adj_to_un_in_out_dir_symmetric_norm",
+         "fast_ppr": "adj_to_fast_ppr_approx_symmetric_norm",
+         "two_order": "adj_to_slow_first_second_ppr_approx_symmetric_norm"}
+
+
+@pytest.mark.parametrize("name", [k for k in directed_cases() if G.manifest()[k]["operator"] in UTILS])
+def test_operators_utils_normalisations(name):
+    """operators.utils' reference-named functions (utils.py:95-424): coo input, scipy csr output with the
+    reference's dtypes, the same values (bit-identical or within the stated tolerance)."""
+    import operators.utils as U
+    c = G.Case(name)
+    op, kw = c.meta["operator"], c.meta["kwargs"]
+    fn = getattr(U, UTILS[op])
+    args = [kw["r"]] + ([kw["q"]] if "q" in kw else []) + ([kw["ppr_alpha"]] if "ppr_alpha" in kw else [])
+    out = fn(c.adj().tocoo(), *args)
+    out = out if isinstance(out, tuple) else (out,)
+    for m, got in zip(c.meta["matrices"], out):
+        assert isinstance(got, sp.csr_matrix)
+        np.testing.assert_array_equal(got.indptr, c[f"m_{m}_indptr"])
+        np.testing.assert_array_equal(got.indices, c[f"m_{m}_indices"])
+        want = c[f"m_{m}_data"]
+        assert got.data.dtype == want.dtype
+        if op in ("mag_lap", "mag_lap_q01_r03") or (op == "two_dir" and m == "un"):
+            assert np.array_equal(got.data.view(np.uint8), want.view(np.uint8))
+        elif op == "pygsd_mag":
+            np.testing.assert_allclose(got.data, want, rtol=0, atol=4.5e-16)
+        else:
+            np.testing.assert_allclose(got.data, want, rtol=1e-3 if (op == "two_order" and m == "one") else 2e-6)
