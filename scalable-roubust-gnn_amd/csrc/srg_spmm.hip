@@ -505,7 +505,8 @@ __device__ __forceinline__ void packed_rows(const IP* __restrict__ indptr, const
     }
 }
 
-template <int VEC, int U, int UH, bool FULL, bool SFULL, typename IP, int NS = 0, bool SEND = false, int LR = 0, int LQ = 1>
+template <int VEC, int U, int UH, bool FULL, bool SFULL, typename IP, int NS = 0, bool SEND = false, int LR = 0, int LQ = 1,
+          bool XH = false>
 __global__ void __launch_bounds__(kBlock)
 k_spmm(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
        const float* __restrict__ vals, const int32_t* __restrict__ order, int n_rows, int n_heavy,
@@ -518,6 +519,18 @@ k_spmm(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
     const int lane = threadIdx.x & 63;
     const int wib = threadIdx.x >> 6;
     if (bid < nb_heavy) {
+        if constexpr (XH) {
+            // XCD-aware slice waves: blocks are dealt round-robin over the 8 XCDs (b and b + 8 share
+            // one), so block b takes slice (b % 8) % n_slices of 4 rows: an XCD's L2 then holds one
+            // slice of the X rows these waves gather.  Groups of 8 blocks cover 8 / n_slices row
+            // groups x every slice.
+            const int per = 8 / n_slices, x = bid & 7;
+            const int item = __builtin_amdgcn_readfirstlane(((bid >> 3) * per + x / n_slices) * kWavesPerBlock + wib);
+            if (item >= n_heavy) return;
+            slice_wave<UH, SFULL, IP, SEND>(indptr, indices, vals, order[item], x % n_slices, X, ldx, Y, ldy, d,
+                                            accumulate, nt, lds + wib * kSliceLdsBufs * 256, epi);
+            return;
+        }
         const int item = __builtin_amdgcn_readfirstlane(bid * kWavesPerBlock + wib);
         if (item >= n_heavy * n_slices) return;
         const int row = order[item / n_slices];
@@ -1150,6 +1163,12 @@ int packed_rows_setting(int d)
     static const bool d32 = [] { const char* e = getenv("SRGNN_PACKED_D32"); return e ? atoi(e) != 0 : false; }();
     return d == 32 ? (d32 ? 8 : 0) : d == 64 ? 8 : d == 128 ? 4 : d == 256 ? 2 : 0;
 }
+// XCD-aware slice waves (k_spmm<..., XH>): SRGNN_XCD_HEAVY=1.  Results are identical either way.
+bool xcd_heavy_setting()
+{
+    static const bool v = [] { const char* e = getenv("SRGNN_XCD_HEAVY"); return e ? atoi(e) != 0 : false; }();
+    return v;
+}
 int packed_u_setting()
 {
     static const int v = [] {
@@ -1338,7 +1357,16 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
     }
     const int ns = (!lr && d <= 32 && !(flags & SRG_SPMM_WIDE_ROWS)) ? (d <= 1 ? 1 : d <= 2 ? 2 : d <= 4 ? 4 : d <= 8 ? 8 : d <= 16 ? 16 : 32) : 0;
     const int64_t rows_per_block = (int64_t)kWavesPerBlock * (ns ? 64 / ns : lr ? lr : 1);
-    const int64_t blocks = nb_heavy + (n_light + rows_per_block - 1) / rows_per_block;
+    // XCD-aware slice waves (k_spmm<..., XH>) with packed light rows, 2 / 4 / 8 slices
+    const bool xh = xcd_heavy_setting() && lr && (n_slices == 2 || n_slices == 4 || n_slices == 8);
+    int nb_heavy_launch = nb_heavy;
+    if (xh) {
+        const int64_t per = 8 / n_slices;
+        const int64_t bh = ((n_heavy + kWavesPerBlock - 1) / kWavesPerBlock + per - 1) / per * 8;
+        if (bh > INT32_MAX) return fail(SRG_ERR_INVALID, "grid too large");
+        nb_heavy_launch = (int)bh;
+    }
+    const int64_t blocks = nb_heavy_launch + (n_light + rows_per_block - 1) / rows_per_block;
     if (blocks > INT32_MAX) return fail(SRG_ERR_INVALID, "grid too large");
     int vec = pick_vec(d, ldx, ldy, X, Y, sizeof(float));
     if (epi.send) vec = std::min(vec, pick_vec(d, epi.lds, epi.lds, epi.send, epi.send, sizeof(float)));
@@ -1357,9 +1385,16 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
                        indptr, indices, vals, morder, nr, nh, n_slices, nb_heavy, X, ldx, Y, ldy,     \
                        d, acc, nt, bb, epi)
 #define SRG_LAUNCH_PACKED(LRV, LQV, UV)                                                              \
-    hipLaunchKernelGGL((k_spmm<1, UV, kUnrollHeavy, false, true, IP, 0, SEND, LRV, LQV>), grid, dim3(kBlock), 0, s, \
-                       indptr, indices, vals, morder, nr, nh, n_slices, nb_heavy, X, ldx, Y, ldy,     \
-                       d, acc, nt, bb, epi)
+    do {                                                                                              \
+        if (xh)                                                                                       \
+            hipLaunchKernelGGL((k_spmm<1, UV, kUnrollHeavy, false, true, IP, 0, SEND, LRV, LQV, true>), grid, dim3(kBlock), \
+                               0, s, indptr, indices, vals, morder, nr, nh, n_slices, nb_heavy_launch, X, ldx, Y, ldy, \
+                               d, acc, nt, bb, epi);                                                  \
+        else                                                                                          \
+            hipLaunchKernelGGL((k_spmm<1, UV, kUnrollHeavy, false, true, IP, 0, SEND, LRV, LQV>), grid, dim3(kBlock), 0, s, \
+                               indptr, indices, vals, morder, nr, nh, n_slices, nb_heavy, X, ldx, Y, ldy, \
+                               d, acc, nt, bb, epi);                                                  \
+    } while (0)
 #define SRG_LAUNCH_PACKED_U(LRV, LQV)                                                                 \
     do {                                                                                              \
         if (packed_u_setting() == 4) SRG_LAUNCH_PACKED(LRV, LQV, 4);                                  \
