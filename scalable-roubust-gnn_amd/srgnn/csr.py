@@ -58,12 +58,14 @@ def auto_heavy_threshold(nnz: int, launches: int = 1) -> int:
     """Row length above which a row is cut into 32-column slice waves instead of running in a packed
     row wave.  A packed row wave costs ~3 instructions per (nonzero, row) against ~13 for the four
     slice waves of a row, but a row's latency grows with its length (one dependent gather round per
-    4 nonzeros): a row should be sliced once it would take about a fifth of its launch.  That is
-    nnz / (60000 * launches), floor 96.  Sweeps (profiles/r02_packed_sweep_breakdown.jsonl,
-    r02_ab_big.txt): products best at 2048 (7.42 ms per hop vs 7.92 at 96, 8.78 at 16384 where the
-    longest packed rows become the tail), arxiv at 96-128, papers100M and RMAT-26 flat over
-    20000-110000 and 2 % faster than at 96."""
-    return max(96, int(nnz) // (60000 * max(1, int(launches))))
+    4 nonzeros), so the longest rows must be sliced.  The slice waves are XCD-aware (each XCD's L2
+    caches one column slice of the rows they gather), which makes slices cheaper in bytes than
+    packed rows.  nnz / (150000 * launches), floor 96.  Sweeps: with XCD-aware slices products is
+    flat at 7.18-7.23 ms per hop over 128-1024 and 7.31 at 2102 (profiles/r02_ab_xh*.txt); without
+    them it was best at 2048 (7.42 ms vs 7.92 at 96, 8.78 at 16384, where the longest packed rows
+    become the tail; r02_packed_sweep_breakdown.jsonl).  arxiv is best at 96-128.  papers100M and
+    RMAT-26 are flat over 20000-110000 and slower at 2048 (r02_ab_big.txt, r02_ab_xh2.txt)."""
+    return max(96, int(nnz) // (150000 * max(1, int(launches))))
 
 
 def _dev(device):
