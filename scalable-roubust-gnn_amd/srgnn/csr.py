@@ -60,12 +60,13 @@ def auto_heavy_threshold(nnz: int, launches: int = 1) -> int:
     slice waves of a row, but a row's latency grows with its length (one dependent gather round per
     4 nonzeros), so the longest rows must be sliced.  The slice waves are XCD-aware (each XCD's L2
     caches one column slice of the rows they gather), which makes slices cheaper in bytes than
-    packed rows.  nnz / (150000 * launches), floor 96.  Sweeps: with XCD-aware slices products is
+    packed rows.  nnz / (100000 * launches), floor 96.  Sweeps: with XCD-aware slices products is
     flat at 7.18-7.23 ms per hop over 128-1024 and 7.31 at 2102 (profiles/r02_ab_xh*.txt); without
     them it was best at 2048 (7.42 ms vs 7.92 at 96, 8.78 at 16384, where the longest packed rows
     become the tail; r02_packed_sweep_breakdown.jsonl).  arxiv is best at 96-128.  papers100M and
-    RMAT-26 are flat over 20000-110000 and slower at 2048 (r02_ab_big.txt, r02_ab_xh2.txt)."""
-    return max(96, int(nnz) // (150000 * max(1, int(launches))))
+    RMAT-26 are flat over 20000-110000 and slower at 2048 (r02_ab_big.txt, r02_ab_xh2.txt); at
+    nnz / 150000 RMAT-26 (d = 256, 14,800) took 331 ms per hop against 318-321 at 20,000-37,000."""
+    return max(96, int(nnz) // (100000 * max(1, int(launches))))
 
 
 def _dev(device):
