@@ -69,6 +69,9 @@ def parse():
                     help="khop: the K-hop propagate (GraphOp.propagate); wavelet: the heat-wavelet "
                          "Chebyshev filter bank (order 3, scales -0.5/+0.5) applied to the feature panel")
     ap.add_argument("--col-block", type=int, default=None, help="wavelet: column block width")
+    ap.add_argument("--fused-epilogue", action="store_true",
+                    help="wavelet: one srg_spmm_cheby_f32 launch per order (two work panels) instead of the "
+                         "SpMM + epilogue launches (three work panels); same bits, measured slower")
     ap.add_argument("--aggregate", default=None, choices=["sum", "mean", "weighted"],
                     help="one GPU: fused hop aggregation (SGC/SSGC/GBP precompute) instead of the K+1 "
                          "panels: sum / mean over hops 0..K, or GBP weights alpha(1-alpha)^k, alpha 0.15")
@@ -186,7 +189,8 @@ def run_wavelet(a, dev, world=1, rank=0):
         return run_wavelet_dist(a, dev, world, rank)
     from srgnn import wavelet as W
     from srgnn.csr import DeviceCSR
-    from srgnn.spmm import spmm
+    from srgnn import _lib
+    from srgnn.spmm import spmm, spmm_cheby
     t_build = time.perf_counter()
     ip, ix, lv, n, d, lmax = graphs.build_laplacian(a.config, dev, d=a.d)
     nnz = int(ix.numel())
@@ -199,13 +203,17 @@ def run_wavelet(a, dev, world=1, rank=0):
     torch.cuda.empty_cache()          # the builders' temporaries
     free, _ = torch.cuda.mem_get_info(dev)
     cb = a.col_block or d
-    while not a.col_block and cb > 8 and 3 * n * cb * 4 > 0.9 * free:
+    fused = a.fused_epilogue
+    n_work = filt.work_panels(fused)
+    # widest block whose work panels fit beside what is resident (1 GiB kept free): wide blocks
+    # gather more bytes per nonzero (RMAT-26: 64 columns 1.37 s per step, 32 columns 1.87 s)
+    while not a.col_block and cb > 8 and n_work * n * cb * 4 > free - 2 ** 30:
         cb //= 2
     log(f"wavelet {a.config}: n={n} nnz(L)={nnz} d={d} lmax={lmax} col_block={cb} "
         f"hub={filt.n_hub} heavy={filt.n_heavy} built in {time.perf_counter() - t_build:.1f}s")
 
     def step():
-        filt.apply(X, col_block=cb, out=R)
+        filt.apply(X, col_block=cb, out=R, fused_epilogue=fused)
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
@@ -214,19 +222,27 @@ def run_wavelet(a, dev, world=1, rank=0):
         step()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    # roofline: one order's SpMM launch at the block width (HIP events on the launch stream)
+    # roofline: one order's launch at the block width (HIP events on the launch stream): a
+    # Chebyshev step (srg_spmm_cheby_f32, T_{k+1} over T_{k-1}) with the fused epilogue, else the
+    # SpMM launch of the split path
     stream = torch.cuda.current_stream(dev)
     Fm = filt._csr(filt.fvals)
-    tb = torch.empty((n, cb), dtype=torch.float32, device=dev)
+    tb = torch.zeros((n, cb), dtype=torch.float32, device=dev)
+    ns = len(filt.taus)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * a.roofline_reps)]
     for r in range(a.roofline_reps):
         ev[2 * r].record(stream)
-        spmm(Fm, X[:, :cb], out=tb)
+        if fused:
+            spmm_cheby(Fm, X[:, :cb], tb, _lib.SRG_CHEBY_STEP, filt.a1, filt.a2, tb, None, filt.coeffs[:, 2],
+                       R[:, :, :cb])
+        else:
+            spmm(Fm, X[:, :cb], out=tb)
         ev[2 * r + 1].record(stream)
     torch.cuda.synchronize()
     kern_s = float(np.mean([ev[2 * r].elapsed_time(ev[2 * r + 1]) * 1e-3 for r in range(a.roofline_reps)]))
     del tb
-    b_alg = roofline.bytes_no_reuse(n, nnz, cb)
+    # the fused step also reads T_{k-1} and reads + writes every scale's output once
+    b_alg = roofline.bytes_no_reuse(n, nnz, cb) + (n * cb * 4 * (1 + 2 * ns) if fused else 0)
     achieved = b_alg / kern_s / 1e9
     res = {
         "metric": "propagated edges/sec (wavelet-basis Chebyshev propagation)",
@@ -238,10 +254,13 @@ def run_wavelet(a, dev, world=1, rank=0):
         "config": {"workload": f"{a.config}-shaped heat-wavelet filter bank", "n_nodes": n, "nnz_L": nnz,
                    "d": d, "chebyshev_order": order, "scales": [-0.5, 0.5], "lmax": lmax,
                    "col_block": cb, "parallelism": "x1",
-                   "mode": "fp32 (split path bit-identical to the fused Chebyshev kernel)"},
+                   "mode": ("fp32, one load-balanced launch per order with the Chebyshev epilogue fused"
+                            if fused else "fp32, split path (SpMM + epilogue launches)")
+                           + " (bit-identical to the fused Chebyshev kernel)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": roofline.MI355X_HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / roofline.MI355X_HBM_PEAK_GBS, "traffic": None,
-                     "kernel": f"k_spmm: one Chebyshev order's SpMM over a {cb}-column block",
+                     "kernel": (f"k_spmm with the Chebyshev epilogue: one order over a {cb}-column block" if fused
+                                else f"k_spmm: one Chebyshev order's SpMM over a {cb}-column block"),
                      "kernel_ms": kern_s * 1e3, "algorithmic_bytes_per_launch": b_alg,
                      "compulsory_bytes_per_launch": roofline.bytes_compulsory(n, nnz, cb, n_cols=n)},
         "cpu_baseline": None,

@@ -143,6 +143,19 @@ int srg_cheby_epilogue_f32(float* Tn, int64_t ldn, const float* Tc, int64_t ldc,
                            const float* coef_prev, const float* coef, int32_t n_scales, float* R,
                            int64_t ldr, int64_t r_stride, void* stream);
 
+/* The split path's two launches in one: srg_spmm_csr_f32 of Tc into Tn (load-balanced: slice waves,
+ * packed light rows, hub workgroups) with srg_cheby_epilogue_f32's arithmetic fused into the
+ * store, so Tn receives the next T directly -- bit-identical to the split path.  Tn may be To
+ * itself (same leading dimension): every element of T_{k-1} is read by its one owner before it is
+ * overwritten, so an order of any depth needs two work panels.  Tn must not alias Tc, R no panel;
+ * flags as srg_spmm_csr_f32 without SRG_SPMM_ACCUMULATE.  coef_prev / coef are host arrays. */
+int srg_spmm_cheby_f32(const int64_t* indptr, const int32_t* indices, const float* values,
+                       int64_t n_rows, const int32_t* row_order, int64_t n_hub, int64_t n_heavy,
+                       const float* Tc, int64_t ldc, float* Tn, int64_t ldn, int32_t d, uint32_t flags,
+                       int mode, float a1, float a2, const float* To, int64_t ldo, const float* coef_prev,
+                       const float* coef, int32_t n_scales, float* R, int64_t ldr, int64_t r_stride,
+                       void* stream);
+
 /* Hop aggregation without the K+1 panels (fused precompute of SGC / SSGC / GBP).  The reference
  * combines the hop list on the host (SSRG/operators/message_operator/{sum,mean,simple_weighted}_
  * message_op.py; operators/utils.py:426-437 one_dim_weighted_add); the host side plans the same

@@ -274,7 +274,19 @@ constexpr int kSliceLdsBufs = SRG_SLICE_LDS_BUFS;
 //    following srg_hop_accumulate_f32 step, without re-reading Y;
 //  * fused halo pack (srgnn.dist): with send != nullptr row r is also stored into the send-buffer
 //    rows send_slot[send_ptr[r] .. send_ptr[r+1]) (one per peer that needs it), so the exchange
-//    reads a ready buffer instead of gathering the rows again.
+//    reads a ready buffer instead of gathering the rows again;
+//  * fused Chebyshev step (srgnn.wavelet, srg_spmm_cheby_f32): y = A*T_k becomes T_{k+1} before it
+//    is stored and every scale's output is updated, with k_cheby_epilogue's arithmetic --
+//      INIT: T1 = (y - a2*T0) / a1,  R_s = (c0_s/2)*T0 + c1_s*T1   (T0 = X, the gathered panel)
+//      STEP: T_{k+1} = y - T_{k-1},  R_s += ck_s*T_{k+1}
+//    T0 / T_{k-1} is read before the chain (its latency hides under the gathers).  Y may alias
+//    T_{k-1}: every element is read and then written by its one owner, and no wave gathers it, so
+//    a step needs two work panels instead of three and one panel pass less than the split path.
+template <typename T> struct ChebyCoef {
+    T prev[8];   // c0_s / 2 (INIT only)
+    T cur[8];    // c1_s (INIT) or ck_s (STEP)
+};
+
 struct Epi {
     float* agg;
     int64_t lda;
@@ -284,12 +296,22 @@ struct Epi {
     int64_t lds;
     const int64_t* send_ptr;
     const int32_t* send_slot;
+    // fused Chebyshev step (EX == kEpiCheby only)
+    const float* cto;     // T_{k-1} (STEP)
+    int64_t ldo;
+    float* R;             // R_s = R + s * r_stride, rows ldr apart
+    int64_t ldr, r_stride;
+    int cmode, ns;
+    float a1, a2;
+    ChebyCoef<float> cf;
 };
 
-// SEND is a template parameter and every call site sits under `if constexpr (SEND)`: a runtime
-// branch cost the plain kernels ~20 %, and even an empty inlined call (the reference-bound acc)
-// changed the gather loop's schedule (+10 % per hop on products); guarded, the SEND=false kernels
-// are instruction-for-instruction the plain ones.
+// Epilogue kinds (template parameter EX of the SpMM kernels).  Every call site sits under
+// `if constexpr`: a runtime branch cost the plain kernels ~20 %, and even an empty inlined call
+// (the reference-bound acc) changed the gather loop's schedule (+10 % per hop on products);
+// guarded, the kEpiPlain kernels are instruction-for-instruction the plain ones.
+constexpr int kEpiPlain = 0, kEpiSend = 1, kEpiCheby = 2;
+
 template <int VEC>
 __device__ __forceinline__ void send_row(const Epi& e, int row, int col, const typename Vec<float, VEC>::type& v)
 {
@@ -298,7 +320,71 @@ __device__ __forceinline__ void send_row(const Epi& e, int row, int col, const t
         vstore<float, VEC>(e.send + (int64_t)e.send_slot[s] * e.lds + col, v, false);
 }
 
-template <int UH, bool SFULL, typename IP, bool SEND>
+// Operands of the Chebyshev epilogue at (row, col), loaded before the chain so that their latency
+// hides under the gathers (loaded after it, the R round trips were the end of every light row:
+// +40 % per order on products): T0 = X (INIT) or T_{k-1} (STEP), and in a step the current
+// outputs of the first kChebyPre scales (further scales are read after the chain).
+constexpr int kChebyPre = 2;
+template <int VEC> struct ChebyOps {
+    typename Vec<float, VEC>::type pre, r[kChebyPre];
+};
+
+template <int VEC>
+__device__ __forceinline__ void cheby_load(const Epi& e, int row, int col, const float* __restrict__ X, int64_t ldx,
+                                           ChebyOps<VEC>& o)
+{
+    if (e.cmode == SRG_CHEBY_INIT) {
+        o.pre = vload<float, VEC>(X + (int64_t)row * ldx + col);
+    } else {
+        o.pre = vload<float, VEC>(e.cto + (int64_t)row * e.ldo + col);
+        const float* rr = e.R + (int64_t)row * e.ldr + col;
+#pragma unroll
+        for (int s = 0; s < kChebyPre; ++s)
+            if (s < e.ns) o.r[s] = vload<float, VEC>(rr + s * e.r_stride);
+    }
+}
+
+// acc = A*T_k at (row, col) becomes T_{k+1}; R_s updated (k_cheby_epilogue's operations, in order).
+template <int VEC>
+__device__ __forceinline__ void cheby_epi(const Epi& e, int row, int col, typename Vec<float, VEC>::type& acc,
+                                          const ChebyOps<VEC>& o)
+{
+    typedef typename Vec<float, VEC>::type V;
+    V t;
+    float* rr = e.R + (int64_t)row * e.ldr + col;
+    if (e.cmode == SRG_CHEBY_INIT) {
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) elem(t, i) = e_div(e_sub(elem(acc, i), e_mul(e.a2, elem(o.pre, i))), e.a1);
+        for (int s = 0; s < e.ns; ++s) {
+            V r;
+#pragma unroll
+            for (int i = 0; i < VEC; ++i)
+                elem(r, i) = e_add(e_mul(e.cf.prev[s], elem(o.pre, i)), e_mul(e.cf.cur[s], elem(t, i)));
+            vstore<float, VEC>(rr + s * e.r_stride, r, false);
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) elem(t, i) = e_sub(elem(acc, i), elem(o.pre, i));
+#pragma unroll
+        for (int s = 0; s < kChebyPre; ++s) {
+            if (s < e.ns) {
+                V r = o.r[s];
+#pragma unroll
+                for (int i = 0; i < VEC; ++i) elem(r, i) = e_add(elem(r, i), e_mul(e.cf.cur[s], elem(t, i)));
+                vstore<float, VEC>(rr + s * e.r_stride, r, false);
+            }
+        }
+        for (int s = kChebyPre; s < e.ns; ++s) {
+            V r = vload<float, VEC>(rr + s * e.r_stride);
+#pragma unroll
+            for (int i = 0; i < VEC; ++i) elem(r, i) = e_add(elem(r, i), e_mul(e.cf.cur[s], elem(t, i)));
+            vstore<float, VEC>(rr + s * e.r_stride, r, false);
+        }
+    }
+    acc = t;
+}
+
+template <int UH, bool SFULL, typename IP, int EX>
 __device__ __forceinline__ void slice_wave(const IP* __restrict__ indptr,
                                            const int32_t* __restrict__ indices,
                                            const float* __restrict__ vals, int row, int slice,
@@ -317,6 +403,9 @@ __device__ __forceinline__ void slice_wave(const IP* __restrict__ indptr,
     float acc = 0.0f;
     if (accumulate && cact) acc = yrow[ccol];
     const float aprev = (epi.agg && !epi.init && cact) ? epi.agg[(int64_t)row * epi.lda + ccol] : 0.0f;
+    [[maybe_unused]] ChebyOps<1> cop;
+    if constexpr (EX == kEpiCheby)
+        if (cact) cheby_load<1>(epi, row, ccol, X, ldx, cop);
     const int64_t beg = indptr[row];
     const int64_t end = indptr[row + 1];
     for (int64_t j = beg; j < end; j += 8 * UH) {
@@ -358,12 +447,13 @@ __device__ __forceinline__ void slice_wave(const IP* __restrict__ indptr,
         }
     }
     if (cact) {
+        if constexpr (EX == kEpiCheby) cheby_epi<1>(epi, row, ccol, acc, cop);
         if (nt)
             __builtin_nontemporal_store(acc, yrow + ccol);
         else
             yrow[ccol] = acc;
         if (epi.agg) epi.agg[(int64_t)row * epi.lda + ccol] = __fadd_rn(aprev, __fmul_rn(epi.w, acc));
-        if constexpr (SEND) send_row<1>(epi, row, ccol, acc);
+        if constexpr (EX == kEpiSend) send_row<1>(epi, row, ccol, acc);
     }
 }
 
@@ -373,7 +463,7 @@ __device__ __forceinline__ void slice_wave(const IP* __restrict__ indptr,
 // address, one instruction for the whole wave -- then U gathers in flight, then U fma links.
 // Rows come from the degree-sorted schedule, so the R rows of a wave have similar lengths.
 // Still one sequential fma chain per output element, in CSR order.
-template <int S, int U, typename IP, bool SEND>
+template <int S, int U, typename IP, int EX>
 __device__ __forceinline__ void narrow_rows(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
                                             const float* __restrict__ vals, const int32_t* __restrict__ order,
                                             int n_rows, int first, const float* __restrict__ X, int64_t ldx,
@@ -398,6 +488,9 @@ __device__ __forceinline__ void narrow_rows(const IP* __restrict__ indptr, const
     float* __restrict__ yrow = Y + (int64_t)row * ldy;
     float acc = (accumulate && act) ? yrow[c] : 0.0f;
     const float aprev = (epi.agg && !epi.init && act) ? epi.agg[(int64_t)row * epi.lda + c] : 0.0f;
+    [[maybe_unused]] ChebyOps<1> cop;
+    if constexpr (EX == kEpiCheby)
+        if (act) cheby_load<1>(epi, row, c, X, ldx, cop);
     for (int j = 0; j < maxlen; j += U) {
         int cv[U];
         float av[U];
@@ -418,12 +511,13 @@ __device__ __forceinline__ void narrow_rows(const IP* __restrict__ indptr, const
             if (act && j + u < len) acc = __builtin_fmaf(av[u], x[u], acc);
     }
     if (act) {
+        if constexpr (EX == kEpiCheby) cheby_epi<1>(epi, row, c, acc, cop);
         if (nt)
             __builtin_nontemporal_store(acc, yrow + c);
         else
             yrow[c] = acc;
         if (epi.agg) epi.agg[(int64_t)row * epi.lda + c] = __fadd_rn(aprev, __fmul_rn(epi.w, acc));
-        if constexpr (SEND) send_row<1>(epi, row, c, acc);
+        if constexpr (EX == kEpiSend) send_row<1>(epi, row, c, acc);
     }
 }
 
@@ -435,7 +529,7 @@ __device__ __forceinline__ void narrow_rows(const IP* __restrict__ indptr, const
 // Each lane loads its own row's (column id, value) entries (the S lanes of a row share the address),
 // then U gathers per row in flight, then the fma links in CSR order.  Entries past a row's end are
 // skipped (never folded in as 0*x).  Still one sequential fma chain per output element.
-template <int LR, int LQ, int U, typename IP, bool SEND>
+template <int LR, int LQ, int U, typename IP, int EX>
 __device__ __forceinline__ void packed_rows(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
                                             const float* __restrict__ vals, const int32_t* __restrict__ order,
                                             int n_rows, int first, const float* __restrict__ X, int64_t ldx,
@@ -459,13 +553,18 @@ __device__ __forceinline__ void packed_rows(const IP* __restrict__ indptr, const
     }
     maxlen = __builtin_amdgcn_readfirstlane(maxlen);
     float* __restrict__ yrow = Y + (int64_t)row * ldy;
-    float* __restrict__ arow = epi.agg ? epi.agg + (int64_t)row * epi.lda : nullptr;
+    // the Chebyshev epilogue never aggregates nor accumulates (its entry rejects both): dropping
+    // them statically keeps its registers (the prefetched operands) within 5 waves per SIMD
+    float* __restrict__ arow = (EX != kEpiCheby && epi.agg) ? epi.agg + (int64_t)row * epi.lda : nullptr;
     V4 acc[LQ], aprev[LQ];
+    [[maybe_unused]] ChebyOps<4> cop[LQ];
 #pragma unroll
     for (int q = 0; q < LQ; ++q) {
         const int col = q * 4 * S + 4 * l;
-        acc[q] = (accumulate && rv) ? vload<float, 4>(yrow + col) : vzero<float, 4>();
+        acc[q] = (EX != kEpiCheby && accumulate && rv) ? vload<float, 4>(yrow + col) : vzero<float, 4>();
         aprev[q] = (arow && !epi.init && rv) ? vload<float, 4>(arow + col) : vzero<float, 4>();
+        if constexpr (EX == kEpiCheby)
+            if (rv) cheby_load<4>(epi, row, col, X, ldx, cop[q]);
     }
     for (int j = 0; j < maxlen; j += U) {
         int cv[U];
@@ -495,17 +594,18 @@ __device__ __forceinline__ void packed_rows(const IP* __restrict__ indptr, const
 #pragma unroll
     for (int q = 0; q < LQ; ++q) {
         const int col = q * 4 * S + 4 * l;
+        if constexpr (EX == kEpiCheby) cheby_epi<4>(epi, row, col, acc[q], cop[q]);
         vstore<float, 4>(yrow + col, acc[q], nt != 0);
         if (arow) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) aprev[q][i] = __fadd_rn(aprev[q][i], __fmul_rn(epi.w, acc[q][i]));
             vstore<float, 4>(arow + col, aprev[q], false);
         }
-        if constexpr (SEND) send_row<4>(epi, row, col, acc[q]);
+        if constexpr (EX == kEpiSend) send_row<4>(epi, row, col, acc[q]);
     }
 }
 
-template <int VEC, int U, int UH, bool FULL, bool SFULL, typename IP, int NS = 0, bool SEND = false, int LR = 0, int LQ = 1,
+template <int VEC, int U, int UH, bool FULL, bool SFULL, typename IP, int NS = 0, int EX = kEpiPlain, int LR = 0, int LQ = 1,
           bool XH = false>
 __global__ void __launch_bounds__(kBlock)
 k_spmm(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
@@ -527,27 +627,27 @@ k_spmm(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
             const int per = 8 / n_slices, x = bid & 7;
             const int item = __builtin_amdgcn_readfirstlane(((bid >> 3) * per + x / n_slices) * kWavesPerBlock + wib);
             if (item >= n_heavy) return;
-            slice_wave<UH, SFULL, IP, SEND>(indptr, indices, vals, order[item], x % n_slices, X, ldx, Y, ldy, d,
+            slice_wave<UH, SFULL, IP, EX>(indptr, indices, vals, order[item], x % n_slices, X, ldx, Y, ldy, d,
                                             accumulate, nt, lds + wib * kSliceLdsBufs * 256, epi);
             return;
         }
         const int item = __builtin_amdgcn_readfirstlane(bid * kWavesPerBlock + wib);
         if (item >= n_heavy * n_slices) return;
         const int row = order[item / n_slices];
-        slice_wave<UH, SFULL, IP, SEND>(indptr, indices, vals, row, item % n_slices, X, ldx, Y, ldy, d,
+        slice_wave<UH, SFULL, IP, EX>(indptr, indices, vals, row, item % n_slices, X, ldx, Y, ldy, d,
                            accumulate, nt, lds + wib * kSliceLdsBufs * 256, epi);
         return;
     }
     if constexpr (LR > 0) {   // wide panel: LR light rows per wave
         const int first = __builtin_amdgcn_readfirstlane((bid - nb_heavy) * kWavesPerBlock + wib) * LR + n_heavy;
         if (first >= n_rows) return;
-        packed_rows<LR, LQ, U, IP, SEND>(indptr, indices, vals, order, n_rows, first, X, ldx, Y, ldy, accumulate, nt, epi);
+        packed_rows<LR, LQ, U, IP, EX>(indptr, indices, vals, order, n_rows, first, X, ldx, Y, ldy, accumulate, nt, epi);
         return;
     }
     if constexpr (NS > 0) {   // narrow panel: 64 / NS light rows per wave
         const int first = __builtin_amdgcn_readfirstlane((bid - nb_heavy) * kWavesPerBlock + wib) * (64 / NS) + n_heavy;
         if (first >= n_rows) return;
-        narrow_rows<NS, U, IP, SEND>(indptr, indices, vals, order, n_rows, first, X, ldx, Y, ldy, d, accumulate, nt, epi);
+        narrow_rows<NS, U, IP, EX>(indptr, indices, vals, order, n_rows, first, X, ldx, Y, ldy, d, accumulate, nt, epi);
         return;
     }
     const int w = __builtin_amdgcn_readfirstlane((bid - nb_heavy) * kWavesPerBlock + wib) + n_heavy;
@@ -558,20 +658,24 @@ k_spmm(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
         const int col = c0 + lane * VEC;
         const bool act = col < d;
         V acc = vzero<float, VEC>();
-        if (accumulate && (FULL || act)) acc = vload<float, VEC>(yrow + col);
+        if (EX != kEpiCheby && accumulate && (FULL || act)) acc = vload<float, VEC>(yrow + col);
         // the accumulator row is loaded before the chain, so its latency hides under the gathers
         V aprev = vzero<float, VEC>();
-        float* arow = epi.agg ? epi.agg + (int64_t)row * epi.lda : nullptr;
+        float* arow = (EX != kEpiCheby && epi.agg) ? epi.agg + (int64_t)row * epi.lda : nullptr;
         if (arow && !epi.init && (FULL || act)) aprev = vload<float, VEC>(arow + col);
+        [[maybe_unused]] ChebyOps<VEC> cop;
+        if constexpr (EX == kEpiCheby)
+            if (FULL || act) cheby_load<VEC>(epi, row, col, X, ldx, cop);
         row_gather<float, VEC, U, FULL, IP>(acc, indptr, indices, vals, row, X, ldx, col, act);
         if (FULL || act) {
+            if constexpr (EX == kEpiCheby) cheby_epi<VEC>(epi, row, col, acc, cop);
             vstore<float, VEC>(yrow + col, acc, nt != 0);
             if (arow) {
 #pragma unroll
                 for (int i = 0; i < VEC; ++i) elem(aprev, i) = __fadd_rn(elem(aprev, i), __fmul_rn(epi.w, elem(acc, i)));
                 vstore<float, VEC>(arow + col, aprev, false);
             }
-            if constexpr (SEND) send_row<VEC>(epi, row, col, acc);
+            if constexpr (EX == kEpiSend) send_row<VEC>(epi, row, col, acc);
         }
     }
 }
@@ -621,7 +725,7 @@ constexpr int kHubL = 7;   // consumer: (tile, value) LDS read pairs in flight i
 // chains; 2 = the producers skip gathers and LDS writes; 3 = the consumer's fmas read registers
 // only (no LDS reads); 4 = producers gather but skip the LDS writes; 5 / 6 = the consumer reads
 // only the tile / only the values from LDS.
-template <bool SFULL, typename IP, int ABL = 0, bool SEND = false, int W = kHubW>
+template <bool SFULL, typename IP, int ABL = 0, int EX = kEpiPlain, int W = kHubW>
 __global__ void __launch_bounds__(kHubThreads)
 k_spmm_hub(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
            const float* __restrict__ vals, const int32_t* __restrict__ hub_rows, int n_slices,
@@ -649,6 +753,9 @@ k_spmm_hub(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
         float acc = 0.0f;
         if (accumulate && cact) acc = yrow[ccol];
         const float aprev = (epi.agg && !epi.init && cact) ? epi.agg[(int64_t)row * epi.lda + ccol] : 0.0f;
+        [[maybe_unused]] ChebyOps<1> cop;
+        if constexpr (EX == kEpiCheby)
+            if (cact) cheby_load<1>(epi, row, ccol, X, ldx, cop);
         const int sw = hub_swz(c);
         constexpr int G = 2;                      // groups of 4 links per register set (8 links)
         V4 tA[G], aA[G], tB[G], aB[G], tC[G], aC[G], tD[G], aD[G];
@@ -763,12 +870,13 @@ k_spmm_hub(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
             }
         }
         if (cact) {
+            if constexpr (EX == kEpiCheby) cheby_epi<1>(epi, row, ccol, acc, cop);
             if (nt)
                 __builtin_nontemporal_store(acc, yrow + ccol);
             else
                 yrow[ccol] = acc;
             if (epi.agg) epi.agg[(int64_t)row * epi.lda + ccol] = __fadd_rn(aprev, __fmul_rn(epi.w, acc));
-            if constexpr (SEND) send_row<1>(epi, row, ccol, acc);
+            if constexpr (EX == kEpiSend) send_row<1>(epi, row, ccol, acc);
         }
         return;
     }
@@ -845,11 +953,6 @@ constexpr size_t kHubLdsBytes = HubGeom<kHubW>::LDS_BYTES;
 // ------------------------------------------------------------------------------------------------
 // Chebyshev step with fused epilogue (wavelet basis)
 // ------------------------------------------------------------------------------------------------
-template <typename T> struct ChebyCoef {
-    T prev[8];   // c0_s / 2 (INIT only)
-    T cur[8];    // c1_s (INIT) or ck_s (STEP)
-};
-
 template <typename T, int VEC, int U>
 __global__ void __launch_bounds__(kBlock)
 k_cheby(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
@@ -1206,13 +1309,15 @@ template <typename IP>
 int hub_attrs()
 {
     for (const void* fn : {(const void*)k_spmm_hub<true, IP>, (const void*)k_spmm_hub<false, IP>,
-                           (const void*)k_spmm_hub<true, IP, 0, true>, (const void*)k_spmm_hub<false, IP, 0, true>,
+                           (const void*)k_spmm_hub<true, IP, 0, kEpiSend>, (const void*)k_spmm_hub<false, IP, 0, kEpiSend>,
+                           (const void*)k_spmm_hub<true, IP, 0, kEpiCheby>, (const void*)k_spmm_hub<false, IP, 0, kEpiCheby>,
                            (const void*)k_spmm_hub<true, IP, 1>, (const void*)k_spmm_hub<true, IP, 2>,
                            (const void*)k_spmm_hub<true, IP, 3>, (const void*)k_spmm_hub<true, IP, 4>,
                            (const void*)k_spmm_hub<true, IP, 5>, (const void*)k_spmm_hub<true, IP, 6>})
         SRG_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kHubLdsBytes));
     for (const void* fn : {(const void*)k_spmm_hub<true, IP, 0, false, 256>, (const void*)k_spmm_hub<false, IP, 0, false, 256>,
-                           (const void*)k_spmm_hub<true, IP, 0, true, 256>, (const void*)k_spmm_hub<false, IP, 0, true, 256>})
+                           (const void*)k_spmm_hub<true, IP, 0, kEpiSend, 256>, (const void*)k_spmm_hub<false, IP, 0, kEpiSend, 256>,
+                           (const void*)k_spmm_hub<true, IP, 0, kEpiCheby, 256>, (const void*)k_spmm_hub<false, IP, 0, kEpiCheby, 256>})
         SRG_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)HubGeom<256>::LDS_BYTES));
     return SRG_OK;
 }
@@ -1276,7 +1381,7 @@ struct DeviceGuard {
     DeviceGuard guard_(static_cast<hipStream_t>(stream));          \
     if (guard_.rc) return guard_.rc
 
-template <typename IP, bool SEND = false>
+template <typename IP, int EX = kEpiPlain>
 int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int64_t n_rows,
                 const int32_t* order, int64_t n_hub, int64_t n_heavy, const float* X, int64_t ldx,
                 float* Y, int64_t ldy, int d, uint32_t flags, hipStream_t s,
@@ -1310,7 +1415,7 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
         SRG_HIP_CHECK(hipStreamWaitEvent(ss->stream, ss->fork, 0));
         const dim3 hgrid((unsigned)(n_hub * n_slices));
         static const int abl = [] { const char* e = getenv("SRGNN_HUB_ABLATION"); return e ? atoi(e) : 0; }();
-        if (!SEND && sfull && abl >= 1 && abl <= 6) {
+        if (EX == kEpiPlain && sfull && abl >= 1 && abl <= 6) {
             auto k = abl == 1 ? k_spmm_hub<true, IP, 1> : abl == 2 ? k_spmm_hub<true, IP, 2>
                    : abl == 3 ? k_spmm_hub<true, IP, 3> : abl == 4 ? k_spmm_hub<true, IP, 4>
                    : abl == 5 ? k_spmm_hub<true, IP, 5> : k_spmm_hub<true, IP, 6>;
@@ -1321,7 +1426,7 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
             const int64_t wide = wide_env >= 0 ? wide_env : kHubWideLaunch;
             const bool w256 = n_hub * n_slices > wide || (flags & SRG_SPMM_HUB_W256);
 #define SRG_LAUNCH_HUB(SF, WW)                                                                             \
-    hipLaunchKernelGGL((k_spmm_hub<SF, IP, 0, SEND, WW>), hgrid, dim3(kHubThreads), HubGeom<WW>::LDS_BYTES, \
+    hipLaunchKernelGGL((k_spmm_hub<SF, IP, 0, EX, WW>), hgrid, dim3(kHubThreads), HubGeom<WW>::LDS_BYTES, \
                        ss->stream, indptr, indices, vals, order, n_slices, X, ldx, Y, ldy, d, acc, nt, epi)
             if (sfull) {
                 if (w256) SRG_LAUNCH_HUB(true, 256);
@@ -1354,7 +1459,9 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
         const bool ok = cand && d % (4 * S) == 0 && (q == 1 || q == 2 || q == 4) && ldx % 4 == 0 &&
                         ldy % 4 == 0 && aligned(X, 16) && aligned(Y, 16) &&
                         (!epi.agg || (epi.lda % 4 == 0 && aligned(epi.agg, 16))) &&
-                        (!epi.send || (epi.lds % 4 == 0 && aligned(epi.send, 16)));
+                        (!epi.send || (epi.lds % 4 == 0 && aligned(epi.send, 16))) &&
+                        (EX != kEpiCheby || (epi.ldo % 4 == 0 && aligned(epi.cto, 16) && epi.ldr % 4 == 0 &&
+                                             epi.r_stride % 4 == 0 && aligned(epi.R, 16)));
         if (ok) { lr = cand; lq = q; }
     }
     const int ns = (!lr && d <= 32 && !(flags & SRG_SPMM_WIDE_ROWS)) ? (d <= 1 ? 1 : d <= 2 ? 2 : d <= 4 ? 4 : d <= 8 ? 8 : d <= 16 ? 16 : 32) : 0;
@@ -1373,27 +1480,31 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
     int vec = pick_vec(d, ldx, ldy, X, Y, sizeof(float));
     if (epi.send) vec = std::min(vec, pick_vec(d, epi.lds, epi.lds, epi.send, epi.send, sizeof(float)));
     if (epi.agg) vec = std::min(vec, pick_vec(d, epi.lda, epi.lda, epi.agg, epi.agg, sizeof(float)));
+    if (EX == kEpiCheby) {
+        vec = std::min(vec, pick_vec(d, epi.ldo, epi.ldr, epi.cto, epi.R, sizeof(float)));
+        while (vec > 1 && epi.r_stride % vec) vec /= 2;
+    }
     const int nr = (int)m_rows, nh = (int)n_heavy;
     for (int64_t b0 = 0; b0 < blocks; b0 += kMaxLaunchBlocks) {
         const dim3 grid((unsigned)std::min<int64_t>(kMaxLaunchBlocks, blocks - b0));
         const int bb = (int)b0;
 #define SRG_LAUNCH_SPMM(V, F, SF)                                                               \
-    hipLaunchKernelGGL((k_spmm<V, kUnroll, kUnrollHeavy, F, SF, IP, 0, SEND>), grid, dim3(kBlock), 0, s,     \
+    hipLaunchKernelGGL((k_spmm<V, kUnroll, kUnrollHeavy, F, SF, IP, 0, EX>), grid, dim3(kBlock), 0, s,     \
                        indptr, indices, vals, morder, nr, nh, n_slices, nb_heavy, X, ldx, Y, ldy, \
                        d, acc, nt, bb, epi)
         const bool full = d % (64 * vec) == 0;        // implies d % 32 == 0
 #define SRG_LAUNCH_NARROW(NSV, SF)                                                                 \
-    hipLaunchKernelGGL((k_spmm<1, kUnroll, kUnrollHeavy, false, SF, IP, NSV, SEND>), grid, dim3(kBlock), 0, s, \
+    hipLaunchKernelGGL((k_spmm<1, kUnroll, kUnrollHeavy, false, SF, IP, NSV, EX>), grid, dim3(kBlock), 0, s, \
                        indptr, indices, vals, morder, nr, nh, n_slices, nb_heavy, X, ldx, Y, ldy,     \
                        d, acc, nt, bb, epi)
 #define SRG_LAUNCH_PACKED(LRV, LQV, UV)                                                              \
     do {                                                                                              \
         if (xh)                                                                                       \
-            hipLaunchKernelGGL((k_spmm<1, UV, kUnrollHeavy, false, true, IP, 0, SEND, LRV, LQV, true>), grid, dim3(kBlock), \
+            hipLaunchKernelGGL((k_spmm<1, UV, kUnrollHeavy, false, true, IP, 0, EX, LRV, LQV, true>), grid, dim3(kBlock), \
                                0, s, indptr, indices, vals, morder, nr, nh, n_slices, nb_heavy_launch, X, ldx, Y, ldy, \
                                d, acc, nt, bb, epi);                                                  \
         else                                                                                          \
-            hipLaunchKernelGGL((k_spmm<1, UV, kUnrollHeavy, false, true, IP, 0, SEND, LRV, LQV>), grid, dim3(kBlock), 0, s, \
+            hipLaunchKernelGGL((k_spmm<1, UV, kUnrollHeavy, false, true, IP, 0, EX, LRV, LQV>), grid, dim3(kBlock), 0, s, \
                                indptr, indices, vals, morder, nr, nh, n_slices, nb_heavy, X, ldx, Y, ldy, \
                                d, acc, nt, bb, epi);                                                  \
     } while (0)
@@ -1663,11 +1774,54 @@ int srg_spmm_send_f32(const int64_t* indptr, const int32_t* indices, const float
     if (rc) return rc;
     if (n_rows > 0 && d > 0 && send && (lds < d || !send_ptr || !send_slot))
         return fail(SRG_ERR_INVALID, "send buffer: lds=%lld < d=%d or null slot map", (long long)lds, d);
-    rc = send ? launch_spmm<int64_t, true>(indptr, indices, values, n_rows, row_order, n_hub, n_heavy, X, ldx, Y, ldy,
+    rc = send ? launch_spmm<int64_t, kEpiSend>(indptr, indices, values, n_rows, row_order, n_hub, n_heavy, X, ldx, Y, ldy,
                                            d, flags, static_cast<hipStream_t>(stream),
                                            Epi{nullptr, 0, 0.0f, 0, send, lds, send_ptr, send_slot})
               : launch_spmm<int64_t>(indptr, indices, values, n_rows, row_order, n_hub, n_heavy, X, ldx, Y, ldy, d,
                                      flags, static_cast<hipStream_t>(stream));
+    return rc ? rc : ok();
+}
+
+int srg_spmm_cheby_f32(const int64_t* indptr, const int32_t* indices, const float* values,
+                       int64_t n_rows, const int32_t* row_order, int64_t n_hub, int64_t n_heavy,
+                       const float* Tc, int64_t ldc, float* Tn, int64_t ldn, int32_t d, uint32_t flags,
+                       int mode, float a1, float a2, const float* To, int64_t ldo, const float* coef_prev,
+                       const float* coef, int32_t n_scales, float* R, int64_t ldr, int64_t r_stride,
+                       void* stream)
+{
+    SRG_DEVICE_GUARD(stream);
+    int rc = check_spmm_args(indptr, indices, values, n_rows, Tc, ldc, Tn, ldn, d);
+    if (rc) return rc;
+    if (mode != SRG_CHEBY_INIT && mode != SRG_CHEBY_STEP) return fail(SRG_ERR_INVALID, "cheby mode %d", mode);
+    if (n_scales < 1 || n_scales > 8) return fail(SRG_ERR_INVALID, "n_scales=%d not in [1,8]", n_scales);
+    if (!coef || (mode == SRG_CHEBY_INIT && !coef_prev)) return fail(SRG_ERR_INVALID, "null coefficient array");
+    if (flags & SRG_SPMM_ACCUMULATE) return fail(SRG_ERR_INVALID, "the Chebyshev epilogue starts every chain from 0");
+    if (n_rows == 0 || d == 0) return ok();
+    if (!R || ldr < d) return fail(SRG_ERR_INVALID, "R=%p ldr=%lld < d=%d", (void*)R, (long long)ldr, d);
+    if (n_scales > 1 && r_stride < n_rows * ldr && r_stride > -n_rows * ldr)
+        return fail(SRG_ERR_INVALID, "r_stride overlaps the scale panels");
+    if (mode == SRG_CHEBY_STEP && (!To || ldo < d))
+        return fail(SRG_ERR_INVALID, "step needs To with ldo >= d (To=%p ldo=%lld)", (const void*)To, (long long)ldo);
+    if (Tn == Tc) return fail(SRG_ERR_INVALID, "Tn must not alias Tc (its rows are gathered)");
+    if (mode == SRG_CHEBY_STEP && To == Tn && ldo != ldn)
+        return fail(SRG_ERR_INVALID, "Tn may alias To only with the same leading dimension");
+    if (R == Tn || R == Tc || (mode == SRG_CHEBY_STEP && R == To)) return fail(SRG_ERR_INVALID, "R must not alias a T panel");
+    Epi e{};
+    e.cto = mode == SRG_CHEBY_STEP ? To : nullptr;
+    e.ldo = mode == SRG_CHEBY_STEP ? ldo : 0;
+    e.R = R;
+    e.ldr = ldr;
+    e.r_stride = r_stride;
+    e.cmode = mode;
+    e.ns = n_scales;
+    e.a1 = a1;
+    e.a2 = a2;
+    for (int i = 0; i < 8; ++i) {
+        e.cf.prev[i] = (mode == SRG_CHEBY_INIT && i < n_scales) ? 0.5f * coef_prev[i] : 0.0f;
+        e.cf.cur[i] = i < n_scales ? coef[i] : 0.0f;
+    }
+    rc = launch_spmm<int64_t, kEpiCheby>(indptr, indices, values, n_rows, row_order, n_hub, n_heavy, Tc, ldc, Tn, ldn,
+                                         d, flags, static_cast<hipStream_t>(stream), e);
     return rc ? rc : ok();
 }
 

@@ -45,6 +45,7 @@ EXPORTED_SYMBOLS = (
     "srg_hop_accumulate_f32",
     "srg_spmm_agg_f32",
     "srg_spmm_send_f32",
+    "srg_spmm_cheby_f32",
     "srg_tail_record_f32",
     "srg_tail_rowsum_f32",
     "srg_segment_sum_f64",
@@ -101,6 +102,9 @@ def _declare(lib):
     lib.srg_spmm_send_f32.argtypes = [_p, _p, _p, _i64, _p, _i64, _i64, _p, _i64, _p, _i64, _i32, ctypes.c_uint32,
                                       _p, _i64, _p, _p, _p]
     lib.srg_spmm_send_f32.restype = ctypes.c_int
+    lib.srg_spmm_cheby_f32.argtypes = [_p, _p, _p, _i64, _p, _i64, _i64, _p, _i64, _p, _i64, _i32, ctypes.c_uint32,
+                                       ctypes.c_int, _f32, _f32, _p, _i64, _p, _p, _i32, _p, _i64, _i64, _p]
+    lib.srg_spmm_cheby_f32.restype = ctypes.c_int
     lib.srg_hop_accumulate_f32.argtypes = [_p, _i64, _p, _i64, _i64, _i32, _f32, ctypes.c_int, _p]
     lib.srg_hop_accumulate_f32.restype = ctypes.c_int
     lib.srg_tail_record_f32.argtypes = [_p, _p, _i64, _i32, _i64, _i32, _f32, _p]

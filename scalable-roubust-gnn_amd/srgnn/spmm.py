@@ -104,6 +104,37 @@ def spmm_send(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, send: torch.Tens
     return out
 
 
+def spmm_cheby(A: DeviceCSR, Tc: torch.Tensor, out: torch.Tensor, mode: int, a1: float, a2: float,
+               To: torch.Tensor | None, coef_prev, coef, R: torch.Tensor) -> torch.Tensor:
+    """One Chebyshev order in one launch (srg_spmm_cheby_f32): y = A @ Tc becomes, before it is stored,
+    INIT: out = (y - a2*Tc) / a1, R[s] = (coef_prev[s]/2)*Tc + coef[s]*out;
+    STEP: out = y - To,           R[s] += coef[s]*out
+    -- srg_spmm_csr_f32 followed by srg_cheby_epilogue_f32, bit for bit.  `out` may be `To` itself
+    (each element of To is read by its owner before it is overwritten).  R: [n_scales, rows, d],
+    strided views allowed (row-major rows)."""
+    _check_panel(Tc, A.n_cols, "Tc")
+    d = Tc.shape[1]
+    _check_panel(out, A.n_rows, "out", d)
+    if To is not None:
+        _check_panel(To, A.n_rows, "To", d)
+    if not isinstance(R, torch.Tensor) or R.dtype != torch.float32 or R.dim() != 3 or R.shape[1] < A.n_rows \
+            or R.shape[2] != d or R.stride(2) != 1 or R.device != A.device:
+        raise ValueError("R must be a float32 [n_scales, rows, d] tensor with unit column stride on A's device")
+    if not (Tc.device == out.device == A.device) or (To is not None and To.device != A.device):
+        raise ValueError("A and the panels must be on the same device")
+    ns = R.shape[0]
+    if len(coef) != ns or (mode == _lib.SRG_CHEBY_INIT and (coef_prev is None or len(coef_prev) != ns)):
+        raise ValueError("one coefficient per scale")
+    cur = (ctypes.c_float * ns)(*[float(c) for c in coef])
+    prev = (ctypes.c_float * ns)(*[float(c) for c in coef_prev]) if coef_prev is not None else None
+    _lib.call(Tc.device, "srg_spmm_cheby_f32", A.indptr.data_ptr(), A.indices.data_ptr(), A.values.data_ptr(),
+              A.n_rows, A.order.data_ptr() if A.n_rows else None, A.n_hub, A.heavy(d), Tc.data_ptr(),
+              Tc.stride(0), out.data_ptr(), out.stride(0), d, 0, mode, float(a1), float(a2),
+              To.data_ptr() if To is not None else None, To.stride(0) if To is not None else 0,
+              prev, cur, ns, R.data_ptr(), R.stride(1), R.stride(0), _stream(Tc.device))
+    return out
+
+
 def gather_rows(src: torch.Tensor, idx: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     """out[i] = src[idx[i]] (srg_gather_rows_f32; the halo exchange's send-side pack), the same rows
     as src.index_select(0, idx).  idx: int64 on src's device, every entry in [0, src.shape[0])."""

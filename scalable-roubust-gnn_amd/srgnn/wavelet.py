@@ -157,9 +157,13 @@ class HeatWaveletFilter:
         return (ct * len(vals))(*vals)
 
     def apply(self, S: torch.Tensor, col_block: int | None = None, split: bool | None = None,
-              out: torch.Tensor | None = None) -> torch.Tensor:
+              out: torch.Tensor | None = None, fused_epilogue: bool = False) -> torch.Tensor:
         """[n_scales, n, d] filter outputs for the panel S [n, d] (device tensor).  fp32 defaults to
-        the split path (load-balanced SpMM + epilogue), in column blocks of `col_block`."""
+        the split path (load-balanced SpMM + epilogue), in column blocks of `col_block`.
+        fused_epilogue (split path): each order is one srg_spmm_cheby_f32 launch writing T_{k+1}
+        over T_{k-1}, so a block needs two work panels instead of three.  Same bits either way;
+        slower where measured (the epilogue's row accesses follow the schedule's row order instead
+        of streaming: products 10.5 vs 9.0 ms per order), so only for when memory is short."""
         if not S.is_cuda or S.shape[0] != self.n or S.dim() != 2:
             raise ValueError("S must be a [n, d] device tensor")
         if split is None:
@@ -180,11 +184,12 @@ class HeatWaveletFilter:
                     raise ValueError("the fused path needs contiguous S and out")
             return self._apply_fused(S, R)
         cb = d if not col_block else min(int(col_block), d)
-        work = [torch.empty((n, cb), dtype=torch.float32, device=S.device) for _ in range(3 if self.coeffs.shape[1] > 2 else 1)]
+        work = [torch.empty((n, cb), dtype=torch.float32, device=S.device)
+                for _ in range(self.work_panels(fused_epilogue))]
         for c0 in range(0, d, cb):
             w = min(cb, d - c0)
             self._apply_split(S[:, c0:c0 + w], R[:, :, c0:c0 + w],
-                              [t.view(-1)[: n * w].view(n, w) for t in work])
+                              [t.view(-1)[: n * w].view(n, w) for t in work], fused_epilogue)
         return R
 
     def _apply_fused(self, S, R):
@@ -218,14 +223,30 @@ class HeatWaveletFilter:
         return DeviceCSR(self.indptr, self.indices, vals, self.n, self.n, self.order, self.n_heavy, self.n_hub,
                          self.n_heavy_narrow)
 
-    def _apply_split(self, Sb, Rb, work):
+    def work_panels(self, fused_epilogue: bool = False) -> int:
+        """[n, column block] work panels the split path needs: T_1 alone for order 1; T_{k-1} and
+        T_k with the fused epilogue (T_{k+1} overwrites T_{k-1}); one more for the SpMM's raw
+        output without it."""
+        return 1 if self.coeffs.shape[1] <= 2 else (2 if fused_epilogue else 3)
+
+    def _apply_split(self, Sb, Rb, work, fused_epilogue: bool = False):
         """One column block: Sb [n, w] and Rb [ns, n, w] may be strided views."""
-        from .spmm import spmm
+        from .spmm import spmm, spmm_cheby
         n, w = Sb.shape
         ns, nc = self.coeffs.shape
         ct = ctypes.c_float
         stream = _lib.stream(Sb.device)
         Lm, Fm = self._csr(self.lvals), self._csr(self.fvals)
+        if fused_epilogue:
+            t_old, t_cur = Sb, work[0]
+            spmm_cheby(Lm, Sb, t_cur, _lib.SRG_CHEBY_INIT, self.a1, self.a2, None, self.coeffs[:, 0],
+                       self.coeffs[:, 1], Rb)
+            for k in range(2, nc):
+                t_new = work[1] if t_old is Sb else t_old      # T_{k+1} over T_{k-1} (never over S)
+                spmm_cheby(Fm, t_cur, t_new, _lib.SRG_CHEBY_STEP, self.a1, self.a2, t_old, None,
+                           self.coeffs[:, k], Rb)
+                t_old, t_cur = t_cur, t_new
+            return
 
         def epi(Tn, Tc, To, mode, coef_prev, coef):
             cp = self._coef(ct, coef_prev) if coef_prev is not None else None

@@ -4,6 +4,8 @@ fp64: the kernel follows the oracle's operation order (sequential CSR chains of 
 and add, uncontracted epilogue), so results are compared BIT FOR BIT.  fp32: normwise relative
 error <= 1e-5 against the fp64 oracle.  (Parity with pygsp itself is unpinned; see
 tests/test_wavelet_cpu.py for the oracle's validation against a dense eigendecomposition.)"""
+import ctypes
+
 import numpy as np
 import pytest
 import scipy.sparse as sp
@@ -98,10 +100,14 @@ def test_spectral_features_vs_dense_fp64(oracle_mod):
 
 
 @pytest.mark.parametrize("thr", [(None, None), (0, -1), (-1, -1), (4, 40)])
-@pytest.mark.parametrize("d,cb", [(128, None), (100, 32), (256, 64), (36, 8)])
+@pytest.mark.parametrize("d,cb", [(128, None), (100, 32), (256, 64), (36, 8), (130, None), (96, None), (64, 16)])
 def test_split_path_bit_identical_to_fused(d, cb, thr):
-    """fp32 split path (load-balanced SpMM + srg_cheby_epilogue_f32, column blocks writing into
-    strided views of R) == the fused srg_cheby_step_f32 kernel, bit for bit."""
+    """fp32 split path (load-balanced SpMM with the Chebyshev epilogue fused into its store,
+    srg_spmm_cheby_f32, T_{k+1} written over T_{k-1}; and the two-launch form, SpMM +
+    srg_cheby_epilogue_f32; column blocks writing into strided views of R) == the fused
+    srg_cheby_step_f32 kernel, bit for bit.  The shapes reach every store site: packed light rows
+    (d = 64 / 128 / 256 blocks), narrow rows (blocks of 4 / 8 / 16 / 32), row waves with 2- and
+    1-wide lanes (130, 96), slice waves and hub workgroups (thresholds)."""
     from srgnn import wavelet as W
     a = graphs()["rmat3000"]
     L = W.laplacian_from_adj(a)
@@ -111,12 +117,46 @@ def test_split_path_bit_identical_to_fused(d, cb, thr):
     fused = f.apply(S, split=False)
     split = f.apply(S, split=True, col_block=cb)
     assert torch.equal(fused, split)
+    one_launch = f.apply(S, split=True, col_block=cb, fused_epilogue=True)
+    assert torch.equal(fused, one_launch)
     # into a caller-provided stack, and from a strided column window of a wider panel
     wide = torch.zeros((a.shape[0], d + 12), device="cuda")
     wide[:, 4:4 + d] = S
-    out = torch.full((3, a.shape[0], d), float("nan"), device="cuda")
-    f.apply(wide[:, 4:4 + d], split=True, col_block=cb, out=out)
-    assert torch.equal(fused, out)
+    for fe in (True, False):
+        out = torch.full((3, a.shape[0], d), float("nan"), device="cuda")
+        f.apply(wide[:, 4:4 + d], split=True, col_block=cb, out=out, fused_epilogue=fe)
+        assert torch.equal(fused, out)
+
+
+def test_spmm_cheby_in_place_and_argument_checks():
+    """srg_spmm_cheby_f32 directly: a step written over T_{k-1} equals the step into a fresh panel
+    and the two-launch form; aliasing and flag misuse are rejected before any launch."""
+    from srgnn import _lib, wavelet as W
+    from srgnn.spmm import spmm, spmm_cheby
+    a = graphs()["rmat3000"]
+    L = W.laplacian_from_adj(a)
+    f = W.HeatWaveletFilter(L, [-0.5, 0.5], order=3, lmax=None, dtype=torch.float32, device="cuda")
+    n = a.shape[0]
+    rng = np.random.default_rng(11)
+    Tc, To = (torch.from_numpy(rng.standard_normal((n, 128)).astype(np.float32)).cuda() for _ in range(2))
+    Fm = f._csr(f.fvals)
+    R0 = torch.from_numpy(rng.standard_normal((2, n, 128)).astype(np.float32)).cuda()
+    fresh, Rf = torch.empty_like(To), R0.clone()
+    spmm_cheby(Fm, Tc, fresh, _lib.SRG_CHEBY_STEP, f.a1, f.a2, To, None, f.coeffs[:, 2], Rf)
+    inplace, Ri = To.clone(), R0.clone()
+    spmm_cheby(Fm, Tc, inplace, _lib.SRG_CHEBY_STEP, f.a1, f.a2, inplace, None, f.coeffs[:, 2], Ri)
+    y, Rs = spmm(Fm, Tc), R0.clone()
+    cp = (ctypes.c_float * 2)(*f.coeffs[:, 2])
+    _lib.call(y.device, "srg_cheby_epilogue_f32", y.data_ptr(), 128, None, 128, To.data_ptr(), 128, n, 128,
+              _lib.SRG_CHEBY_STEP, f.a1, f.a2, None, cp, 2, Rs.data_ptr(), 128, n * 128, _lib.stream(y.device))
+    assert torch.equal(fresh, inplace) and torch.equal(fresh, y)
+    assert torch.equal(Rf, Ri) and torch.equal(Rf, Rs)
+    with pytest.raises(_lib.SrgError, match="alias Tc"):
+        spmm_cheby(Fm, Tc, Tc, _lib.SRG_CHEBY_STEP, f.a1, f.a2, To, None, f.coeffs[:, 2], Rf)
+    with pytest.raises(_lib.SrgError, match="must not alias a T panel"):
+        spmm_cheby(Fm, Tc, fresh, _lib.SRG_CHEBY_STEP, f.a1, f.a2, To, None, f.coeffs[:1, 2], fresh.view(1, n, 128))
+    with pytest.raises(_lib.SrgError, match="needs To"):
+        spmm_cheby(Fm, Tc, fresh, _lib.SRG_CHEBY_STEP, f.a1, f.a2, None, None, f.coeffs[:, 2], Rf)
 
 
 def test_device_built_filter_equals_host_built():
