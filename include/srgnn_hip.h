@@ -138,6 +138,16 @@ int srg_cheby_step_f32(const int64_t* indptr, const int32_t* indices, const floa
  * epilogue turning Tn = A*Tc into the next T and updating R -- bit-identical to
  * srg_cheby_step_f32 (same fma chain, same epilogue arithmetic).  Every panel has its own leading
  * dimension (column blocks of S and R without copies); R_s = R + s*r_stride, rows ldr apart. */
+/* Two-pass-saving modes of the epilogue (the split path of an order >= 2 filter):
+ *   SRG_CHEBY_INIT_T (order 1):     Tn = (A*Tc - a2*Tc) / a1; R untouched (coef unused)
+ *   SRG_CHEBY_STEP_FIRST (order 2): Tn = A*Tc - To with To = T0, Tc = T1;
+ *                                   R_s = ((c0_s/2)*T0 + c1_s*T1) + c2_s*Tn
+ *                                   coef_prev = [c0_0..c0_{ns-1}, c1_0..c1_{ns-1}], coef = c2
+ *   | SRG_CHEBY_NO_T (any step):    Tn is not stored (the last order: no later step reads it)
+ * INIT_T then STEP_FIRST gives the same bits as INIT then STEP (same operations, same order). */
+#define SRG_CHEBY_INIT_T 2
+#define SRG_CHEBY_STEP_FIRST 3
+#define SRG_CHEBY_NO_T 0x10
 int srg_cheby_epilogue_f32(float* Tn, int64_t ldn, const float* Tc, int64_t ldc, const float* To,
                            int64_t ldo, int64_t n_rows, int32_t d, int mode, float a1, float a2,
                            const float* coef_prev, const float* coef, int32_t n_scales, float* R,

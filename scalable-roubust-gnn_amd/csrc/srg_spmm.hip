@@ -283,8 +283,9 @@ constexpr int kSliceLdsBufs = SRG_SLICE_LDS_BUFS;
 //    T_{k-1}: every element is read and then written by its one owner, and no wave gathers it, so
 //    a step needs two work panels instead of three and one panel pass less than the split path.
 template <typename T> struct ChebyCoef {
-    T prev[8];   // c0_s / 2 (INIT only)
-    T cur[8];    // c1_s (INIT) or ck_s (STEP)
+    T prev[8];   // c0_s / 2 (INIT, STEP_FIRST)
+    T cur[8];    // c1_s (INIT) or ck_s (STEP, STEP_FIRST)
+    T mid[8];    // c1_s (STEP_FIRST only)
 };
 
 struct Epi {
@@ -1006,6 +1007,9 @@ k_cheby(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
 // Chebyshev epilogue after a load-balanced SpMM (fp32, large graphs): Tn holds acc = A*Tc (the
 // same fma chain k_cheby forms, so results are bit-identical to the fused kernel) and becomes
 // Tn; every panel has its own leading dimension, so column blocks of S and R need no copies.
+// INIT_T / STEP_FIRST defer the INIT's scale outputs to the first step, which forms them from T0,
+// T1 and T2 with the same operations in the same order (R = ((c0/2) T0 + c1 T1) + c2 T2), and
+// SRG_CHEBY_NO_T leaves T_{k+1} unstored in the last order: 4 panel passes less per order-3 block.
 __global__ void __launch_bounds__(256)
 k_cheby_epilogue(float* __restrict__ Tn, int64_t ldn, const float* __restrict__ Tc, int64_t ldc,
                  const float* __restrict__ To, int64_t ldo, int64_t n_rows, int d, int mode, float a1,
@@ -1014,23 +1018,31 @@ k_cheby_epilogue(float* __restrict__ Tn, int64_t ldn, const float* __restrict__ 
 {
     const int lane = threadIdx.x & 63;
     const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
+    const bool store_t = !(mode & SRG_CHEBY_NO_T);
+    const int m = mode & 0xf;
     for (int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); r < n_rows; r += waves) {
         float* tn = Tn + r * ldn;
         float* rr = R + r * ldr;
         for (int c = lane; c < d; c += 64) {
             const float acc = tn[c];
             float t;
-            if (mode == SRG_CHEBY_INIT) {
+            if (m == SRG_CHEBY_INIT || m == SRG_CHEBY_INIT_T) {
                 const float tc = Tc[r * ldc + c];
                 t = e_div(e_sub(acc, e_mul(a2, tc)), a1);
+                if (m == SRG_CHEBY_INIT)
+                    for (int s = 0; s < n_scales; ++s)
+                        rr[s * r_stride + c] = e_add(e_mul(cf.prev[s], tc), e_mul(cf.cur[s], t));
+            } else if (m == SRG_CHEBY_STEP_FIRST) {
+                const float t0 = To[r * ldo + c], t1 = Tc[r * ldc + c];
+                t = e_sub(acc, t0);
                 for (int s = 0; s < n_scales; ++s)
-                    rr[s * r_stride + c] = e_add(e_mul(cf.prev[s], tc), e_mul(cf.cur[s], t));
+                    rr[s * r_stride + c] = e_add(e_add(e_mul(cf.prev[s], t0), e_mul(cf.mid[s], t1)), e_mul(cf.cur[s], t));
             } else {
                 t = e_sub(acc, To[r * ldo + c]);
                 for (int s = 0; s < n_scales; ++s)
                     rr[s * r_stride + c] = e_add(rr[s * r_stride + c], e_mul(cf.cur[s], t));
             }
-            tn[c] = t;
+            if (store_t) tn[c] = t;
         }
     }
 }
@@ -1877,20 +1889,28 @@ int srg_cheby_epilogue_f32(float* Tn, int64_t ldn, const float* Tc, int64_t ldc,
                            int64_t ldr, int64_t r_stride, void* stream)
 {
     SRG_DEVICE_GUARD(stream);
-    if (mode != SRG_CHEBY_INIT && mode != SRG_CHEBY_STEP)
+    const int m = mode & ~SRG_CHEBY_NO_T;
+    if (m != SRG_CHEBY_INIT && m != SRG_CHEBY_STEP && m != SRG_CHEBY_INIT_T && m != SRG_CHEBY_STEP_FIRST)
         return fail(SRG_ERR_INVALID, "cheby mode %d", mode);
+    const bool init = m == SRG_CHEBY_INIT || m == SRG_CHEBY_INIT_T;
+    const bool needs_r = m != SRG_CHEBY_INIT_T;
     if (n_scales < 1 || n_scales > 8) return fail(SRG_ERR_INVALID, "n_scales=%d not in [1,8]", n_scales);
-    if (!coef || (mode == SRG_CHEBY_INIT && !coef_prev)) return fail(SRG_ERR_INVALID, "null coefficient array");
-    if (n_rows < 0 || d < 0 || ldn < d || ldr < d || (mode == SRG_CHEBY_INIT ? ldc < d : ldo < d))
+    if ((needs_r && !coef) || ((m == SRG_CHEBY_INIT || m == SRG_CHEBY_STEP_FIRST) && !coef_prev))
+        return fail(SRG_ERR_INVALID, "null coefficient array");
+    if (n_rows < 0 || d < 0 || ldn < d || (needs_r && ldr < d) || (init ? ldc < d : ldo < d) ||
+        (m == SRG_CHEBY_STEP_FIRST && ldc < d))
         return fail(SRG_ERR_INVALID, "bad shape n_rows=%lld d=%d", (long long)n_rows, d);
-    if (n_scales > 1 && r_stride < n_rows * ldr && r_stride > -n_rows * ldr)
+    if (needs_r && n_scales > 1 && r_stride < n_rows * ldr && r_stride > -n_rows * ldr)
         return fail(SRG_ERR_INVALID, "r_stride overlaps the scale panels");
     if (n_rows == 0 || d == 0) return ok();
-    if (!Tn || !R || (mode == SRG_CHEBY_INIT ? !Tc : !To)) return fail(SRG_ERR_INVALID, "null panel");
+    if (!Tn || (needs_r && !R) || (init ? !Tc : !To) || (m == SRG_CHEBY_STEP_FIRST && !Tc))
+        return fail(SRG_ERR_INVALID, "null panel");
     ChebyCoef<float> cf;
     for (int i = 0; i < 8; ++i) {
-        cf.prev[i] = (mode == SRG_CHEBY_INIT && i < n_scales) ? 0.5f * coef_prev[i] : 0.0f;
-        cf.cur[i] = i < n_scales ? coef[i] : 0.0f;
+        const bool on = i < n_scales;
+        cf.prev[i] = ((m == SRG_CHEBY_INIT || m == SRG_CHEBY_STEP_FIRST) && on) ? 0.5f * coef_prev[i] : 0.0f;
+        cf.mid[i] = (m == SRG_CHEBY_STEP_FIRST && on) ? coef_prev[n_scales + i] : 0.0f;
+        cf.cur[i] = (needs_r && on) ? coef[i] : 0.0f;
     }
     const unsigned blocks = (unsigned)std::min<int64_t>((n_rows + 3) / 4, 256 * 16);
     hipLaunchKernelGGL(k_cheby_epilogue, dim3(blocks), dim3(256), 0, static_cast<hipStream_t>(stream),

@@ -24,6 +24,7 @@ same estimator (eigsh, tol 5e-3, x1.01) with a fixed start vector.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 import scipy.sparse as sp
@@ -150,6 +151,9 @@ class HeatWaveletFilter:
         self.fvals = ((2.0 / self.a1) * torch.where(diag, l64 - self.a2, l64)).to(dtype)
         del diag, l64
         self.lvals = lvals.to(dtype)
+        # split path: the lean epilogue sequence (SRG_CHEBY_INIT_T / STEP_FIRST / NO_T); False runs
+        # INIT + STEP epilogues (same bits; SRGNN_WAVELET_LEAN=0 for A/B runs)
+        self.lean_epilogue = os.environ.get("SRGNN_WAVELET_LEAN", "1") != "0"
         self.order, self.n_heavy, self.n_hub = make_schedule(self.indptr, heavy_threshold, hub_threshold)
         self.n_heavy_narrow = narrow_heavy(self.indptr, self.n_hub) if _auto_heavy(heavy_threshold) else None
 
@@ -250,20 +254,32 @@ class HeatWaveletFilter:
 
         def epi(Tn, Tc, To, mode, coef_prev, coef):
             cp = self._coef(ct, coef_prev) if coef_prev is not None else None
+            cc = self._coef(ct, coef) if coef is not None else None
             _lib.call(Sb.device, "srg_cheby_epilogue_f32", Tn.data_ptr(), Tn.stride(0),
                       Tc.data_ptr() if Tc is not None else None, Tc.stride(0) if Tc is not None else w,
                       To.data_ptr() if To is not None else None, To.stride(0) if To is not None else w, n, w,
-                      mode, self.a1, self.a2, cp, self._coef(ct, coef), ns, Rb.data_ptr(), Rb.stride(1),
-                      Rb.stride(0), stream)
+                      mode, self.a1, self.a2, cp, cc, ns, Rb.data_ptr(), Rb.stride(1), Rb.stride(0), stream)
 
+        # lean epilogues (order >= 2): order 1 stores T1 only, order 2 forms R from T0, T1, T2 at
+        # once, the last order does not store its T -- the same operations in the same order as
+        # INIT + STEP..., four panel passes less for order 3
+        lean = self.lean_epilogue and nc > 2
         t_old, t_cur = Sb, work[0]
         free = list(work[1:])
         spmm(Lm, Sb, out=t_cur)
-        epi(t_cur, Sb, None, _lib.SRG_CHEBY_INIT, self.coeffs[:, 0], self.coeffs[:, 1])
+        if lean:
+            epi(t_cur, Sb, None, _lib.SRG_CHEBY_INIT_T, None, None)
+        else:
+            epi(t_cur, Sb, None, _lib.SRG_CHEBY_INIT, self.coeffs[:, 0], self.coeffs[:, 1])
         for k in range(2, nc):
             t_new = free.pop()
             spmm(Fm, t_cur, out=t_new)
-            epi(t_new, None, t_old, _lib.SRG_CHEBY_STEP, None, self.coeffs[:, k])
+            last = _lib.SRG_CHEBY_NO_T if lean and k == nc - 1 else 0
+            if lean and k == 2:
+                epi(t_new, t_cur, t_old, _lib.SRG_CHEBY_STEP_FIRST | last,
+                    np.concatenate([self.coeffs[:, 0], self.coeffs[:, 1]]), self.coeffs[:, 2])
+            else:
+                epi(t_new, None, t_old, _lib.SRG_CHEBY_STEP | last, None, self.coeffs[:, k])
             if t_old is not Sb:
                 free.append(t_old)
             t_old, t_cur = t_cur, t_new

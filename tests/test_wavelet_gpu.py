@@ -128,6 +128,25 @@ def test_split_path_bit_identical_to_fused(d, cb, thr):
         assert torch.equal(fused, out)
 
 
+@pytest.mark.parametrize("order", [1, 2, 3, 5])
+@pytest.mark.parametrize("cb", [None, 32])
+def test_lean_epilogue_bit_identical(order, cb):
+    """Split path with the lean epilogue sequence (order 1 stores T1 only, order 2 forms R from
+    T0, T1, T2, the last order stores no T) == the INIT + STEP epilogues == the fused kernel."""
+    from srgnn import wavelet as W
+    a = graphs()["rmat3000"]
+    L = W.laplacian_from_adj(a)
+    f = W.HeatWaveletFilter(L, [-0.5, 0.5, 1.5], order=order, lmax=None, dtype=torch.float32, device="cuda",
+                            heavy_threshold=40, hub_threshold=400)
+    S = torch.from_numpy(np.random.default_rng(order).standard_normal((a.shape[0], 96)).astype(np.float32)).cuda()
+    fused = f.apply(S, split=False)
+    f.lean_epilogue = True
+    lean = f.apply(S, split=True, col_block=cb)
+    f.lean_epilogue = False
+    plain = f.apply(S, split=True, col_block=cb)
+    assert torch.equal(fused, lean) and torch.equal(fused, plain)
+
+
 def test_spmm_cheby_in_place_and_argument_checks():
     """srg_spmm_cheby_f32 directly: a step written over T_{k-1} equals the step into a fresh panel
     and the two-launch form; aliasing and flag misuse are rejected before any launch."""
