@@ -765,11 +765,12 @@ def _epilogue_device(Tn, Tc, To, mode, a1, a2, coef_prev, coef, R):
     ns = R.shape[0]
     n, w = Tn.shape
     ct = ctypes.c_float
-    cp = (ct * ns)(*coef_prev) if coef_prev is not None else None
+    cp = (ct * len(coef_prev))(*coef_prev) if coef_prev is not None else None
+    cc = (ct * ns)(*coef) if coef is not None else None
     _lib.call(Tn.device, "srg_cheby_epilogue_f32", Tn.data_ptr(), Tn.stride(0),
               Tc.data_ptr() if Tc is not None else None, Tc.stride(0) if Tc is not None else w,
               To.data_ptr() if To is not None else None, To.stride(0) if To is not None else w, n, w, mode,
-              a1, a2, cp, (ct * ns)(*coef), ns, R.data_ptr(), R.stride(1), R.stride(0), _lib.stream(Tn.device))
+              a1, a2, cp, cc, ns, R.data_ptr(), R.stride(1), R.stride(0), _lib.stream(Tn.device))
 
 
 class HaloWaveletFilter:
@@ -830,16 +831,28 @@ class HaloWaveletFilter:
         t_old, t_cur = S_panel, work[0]
         free = list(work[1:])
         a1, a2, cf = self.a1, self.a2, self.coeffs
+        # the lean epilogue sequence of HeatWaveletFilter's split path (same bits): order 1 stores
+        # T1 only, order 2 forms R from T0, T1, T2, the last order stores no T (its halo is never
+        # exchanged)
+        lean = nc > 2
 
         def epi_first(a, b, t=t_cur):
-            self._epi(t[a:b], S_panel[a:b], None, 0, a1, a2, cf[:, 0], cf[:, 1], R[:, a:b])
+            if lean:
+                self._epi(t[a:b], S_panel[a:b], None, 2, a1, a2, None, None, R[:, a:b])
+            else:
+                self._epi(t[a:b], S_panel[a:b], None, 0, a1, a2, cf[:, 0], cf[:, 1], R[:, a:b])
         if self._order(self.opL, S_panel, t_cur, epi_first, exchange=nc > 2):
             yield t_cur
         for k in range(2, nc):
             t_new = free.pop()
 
-            def epi_k(a, b, t=t_new, o=t_old, k=k):
-                self._epi(t[a:b], None, o[a:b], 1, a1, a2, None, cf[:, k], R[:, a:b])
+            def epi_k(a, b, t=t_new, o=t_old, c=t_cur, k=k):
+                last = 0x10 if k == nc - 1 else 0
+                if k == 2:
+                    self._epi(t[a:b], c[a:b], o[a:b], 3 | last, a1, a2, np.concatenate([cf[:, 0], cf[:, 1]]),
+                              cf[:, 2], R[:, a:b])
+                else:
+                    self._epi(t[a:b], None, o[a:b], 1 | last, a1, a2, None, cf[:, k], R[:, a:b])
             more = self._order(self.opF, t_cur, t_new, epi_k, exchange=k + 1 < nc)
             if t_old is not S_panel:
                 free.append(t_old)

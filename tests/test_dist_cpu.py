@@ -223,17 +223,26 @@ def test_ghost_plan_cost_model():
 
 
 def _cpu_epilogue(Tn, Tc, To, mode, a1, a2, coef_prev, coef, R):
-    """srg_cheby_epilogue_f32's arithmetic in torch fp32 (CPU ranks)."""
+    """srg_cheby_epilogue_f32's arithmetic in torch fp32 (CPU ranks), every mode: INIT (0), STEP
+    (1), INIT_T (2), STEP_FIRST (3), with the NO_T flag (0x10)."""
     a1, a2 = torch.tensor(a1, dtype=torch.float32), torch.tensor(a2, dtype=torch.float32)
-    if mode == 0:
+    f32 = lambda v: torch.tensor(v, dtype=torch.float32)  # noqa: E731
+    m, ns = mode & 0xF, R.shape[0]
+    if m in (0, 2):
         t = (Tn - a2 * Tc) / a1
-        for s in range(R.shape[0]):
-            R[s] = (0.5 * torch.tensor(coef_prev[s], dtype=torch.float32)) * Tc + torch.tensor(coef[s], dtype=torch.float32) * t
+        if m == 0:
+            for s in range(ns):
+                R[s] = (0.5 * f32(coef_prev[s])) * Tc + f32(coef[s]) * t
+    elif m == 3:
+        t = Tn - To
+        for s in range(ns):
+            R[s] = ((0.5 * f32(coef_prev[s])) * To + f32(coef_prev[ns + s]) * Tc) + f32(coef[s]) * t
     else:
         t = Tn - To
-        for s in range(R.shape[0]):
-            R[s] = R[s] + torch.tensor(coef[s], dtype=torch.float32) * t
-    Tn.copy_(t)
+        for s in range(ns):
+            R[s] = R[s] + f32(coef[s]) * t
+    if not mode & 0x10:
+        Tn.copy_(t)
 
 
 def _wavelet_graph():
