@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--nt-store", action="store_true")
+    ap.add_argument("--col-blocks", type=int, default=None,
+                    help="column blocks per hop on one GPU (default: srgnn.spmm.auto_col_blocks; 1 = one launch)")
     ap.add_argument("--exchange", default="halo", choices=["halo", "allgather"])
     ap.add_argument("--chunks", type=int, default=None,
                     help="halo exchange groups per hop (row chunks; default 4 at 2 GPUs, 6 above: the "
@@ -167,13 +169,15 @@ def cpu_baseline(ip, ix, vals, x_host, n, d, budget_s):
                       f"buffers, OMP_NUM_THREADS={threads}, {dt:.1f} s; value_1thread on a row block"}
 
 
-def pmc_traffic(config, kernel_hint="k_spmm"):
+def pmc_traffic(config, kernel_hint="k_spmm", launches_per_hop=1):
     path = os.path.join(HERE, "profiles", f"pmc_{config}.json")
     if not os.path.exists(path):
         return None
     try:
         with open(path) as f:
             rec = json.load(f)
+        if int(rec.get("launches_per_hop", 1)) != int(launches_per_hop):
+            return None       # measured with another hop layout
         return float(rec["hbm_bytes_per_launch"])
     except Exception:  # noqa: BLE001
         return None
@@ -344,7 +348,7 @@ def main():
         init_pg()
 
     from srgnn.csr import DeviceCSR
-    from srgnn.spmm import propagate, spmm
+    from srgnn.spmm import auto_col_blocks, hop, propagate, spmm
 
     t_build = time.perf_counter()
     ip, ix, vals, n, d, K = graphs.build(a.config, dev, d=a.d)
@@ -358,11 +362,14 @@ def main():
     mode = a.mode
     if world == 1:
         A = DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, heavy_threshold=a.heavy_threshold, device=dev)
-        log(f"schedule: n_hub={A.n_hub} n_heavy={A.n_heavy}")
         if mode == "auto":
             free, _ = torch.cuda.mem_get_info(dev)
             mode = "panels" if K * n * d * 4 < 0.9 * free else "last"
             log(f"mode {mode}: {K} panels need {K * n * d * 4 / 1e9:.1f} GB, {free / 1e9:.1f} GB free")
+        col_blocks = a.col_blocks if a.col_blocks is not None else auto_col_blocks(A, d)
+        if col_blocks > 1 and (a.aggregate or mode != "panels" or not A.column_blocks(col_blocks)):
+            col_blocks = 1          # the fused aggregation and the last-hop mode run one launch per hop
+        log(f"schedule: n_hub={A.n_hub} n_heavy={A.n_heavy} column blocks per hop={col_blocks}")
         if a.aggregate:
             from srgnn.aggregate import combine_plan, combine_steps, propagate_aggregate
 
@@ -382,7 +389,7 @@ def main():
             panels = [X] + [buf[k] for k in range(K)]
 
             def step():
-                propagate(A, X, K, panels=panels, nt_store=a.nt_store)
+                propagate(A, X, K, panels=panels, nt_store=a.nt_store, col_blocks=col_blocks)
         else:
             from srgnn.aggregate import propagate_aggregate
             panels = [X, None]
@@ -391,7 +398,9 @@ def main():
                 panels[1] = None
                 panels[1] = propagate_aggregate(A, X, K, last_only=True)
         local_rows, local_nnz = n, nnz
-    elif a.exchange == "allgather":
+    else:
+        col_blocks = 1
+    if world > 1 and a.exchange == "allgather":
         from srgnn.dist import RowPartitionedOperator
         op = RowPartitionedOperator(ip, ix, vals, n, heavy_threshold=a.heavy_threshold, device=dev)
         A = op.A
@@ -403,7 +412,7 @@ def main():
         def step():
             op.propagate(x_loc, K, panels=panels)
         local_rows, local_nnz = op.rows, op.nnz_local
-    else:
+    elif world > 1:
         from srgnn.dist import HaloPartitionedOperator
         op = HaloPartitionedOperator(ip, ix, vals, n, chunks=(a.chunks or (4 if world <= 2 else 6)), heavy_threshold=a.heavy_threshold,
                                      device=dev, ghost_max_degree=a.ghost_max_degree)
@@ -457,7 +466,7 @@ def main():
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * a.roofline_reps)]
     if world == 1:
         def one_hop():
-            spmm(A, panels[0], out=panels[1], nt_store=a.nt_store)
+            hop(A, panels[0], panels[1], nt_store=a.nt_store, col_blocks=col_blocks)
         if panels[1] is None:
             panels[1] = torch.empty_like(X)
     elif a.exchange == "allgather":
@@ -484,7 +493,7 @@ def main():
     b_alg = roofline.bytes_no_reuse(local_rows, local_nnz, d)
     achieved = b_alg / kern_s / 1e9
     peak = roofline.MI355X_HBM_PEAK_GBS
-    traffic = pmc_traffic(a.config) if world == 1 else None
+    traffic = pmc_traffic(a.config, launches_per_hop=col_blocks) if world == 1 else None
 
     exchange_stats = {}
     if world > 1 and a.exchange == "halo":
@@ -511,6 +520,7 @@ def main():
         "data": f"synthetic (R-MAT power-law graph with the {a.config} node/edge counts, U[-1,1) features)",
         "config": {"workload": f"{a.config}-shaped K-hop propagate", "n_nodes": n, "nnz_ahat": nnz,
                    "d": d, "K": K, "normalization": "sym r=0.5",
+                   **({"column_blocks_per_hop": col_blocks} if world == 1 else {}),
                    "parallelism": f"row-partition x{world}" + (f" ({a.exchange} exchange)" if world > 1 else "")
                    + (f", ghost rows <= degree {op.ghost_max_degree}" if world > 1 and a.exchange == "halo" else "")
                    + (", X whole on every rank (hop 0's halo gathered locally)" if world > 1 and a.exchange == "halo"
@@ -523,8 +533,11 @@ def main():
                    **exchange_stats},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
                      "frac": achieved / peak, "traffic": traffic,
-                     "kernel": "k_spmm (+ k_spmm_hub beside it): one hop" + (" of rank 0's rows" if world > 1 else ""),
+                     "kernel": "k_spmm (+ k_spmm_hub beside it): one hop" + (" of rank 0's rows" if world > 1 else "")
+                     + (f" = {col_blocks} column-block launches (bitwise the one-launch hop)" if col_blocks > 1 else ""),
                      "kernel_ms": kern_s * 1e3,
+                     "launches_per_hop": col_blocks,
+                     "kernel_ms_per_launch": kern_s * 1e3 / col_blocks,
                      "kernel_ms_source": ("HIP events over the timed steps / (steps x K)" if in_run
                                           else f"HIP events around {a.roofline_reps} isolated hop launches"),
                      "kernel_ms_isolated": kern_isolated_s * 1e3,

@@ -20,7 +20,7 @@ only decides which wave works on what and when (power-law hubs start first).
 from __future__ import annotations
 
 import os
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 
 import numpy as np
 import torch
@@ -89,6 +89,7 @@ class DeviceCSR:
     n_heavy: int
     n_hub: int = 0
     n_heavy_narrow: int | None = None    # slice-wave rows for d <= 32 (None: n_heavy)
+    _blocks: dict = field(default_factory=dict, repr=False, compare=False)   # column_blocks() cache
 
     def heavy(self, d: int) -> int:
         """The slice-wave row count for a panel of d columns (same order, a longer prefix of it
@@ -137,6 +138,45 @@ class DeviceCSR:
                                 np.asarray(adj.indices, dtype=np.int32),
                                 np.asarray(adj.data),   # cast to fp32 on the device (round to nearest, as astype)
                                 n_cols=adj.shape[1], heavy_threshold=heavy_threshold, device=device)
+
+    def column_blocks(self, B: int):
+        """B operators over the same rows: block b holds each row's entries whose column ids lie in
+        [b * n_cols // B, (b + 1) * n_cols // B), in their stored order (each with its own
+        schedule), or None when some row's entries are not in block order.
+
+        A hop is then block 0 from +0.0f and blocks 1..B-1 with ACCUMULATE: each output element is
+        the same fma chain over the same entries in the same order, continued from the fp32 value
+        the previous block stored, so the result is bitwise the one-launch hop.  Â from
+        construct_adj has sorted column ids (utils.py:81-93 builds a canonical transpose); a CSR
+        with unsorted rows may not be cut (None).  Cached per B."""
+        B = int(B)
+        if B in self._blocks:
+            return self._blocks[B]
+        if B < 2 or self.n_rows == 0 or self.nnz == 0:
+            self._blocks[B] = None
+            return None
+        ip, ix, n = self.indptr, self.indices, self.n_cols
+        row = torch.repeat_interleave(torch.arange(self.n_rows, device=ip.device, dtype=torch.int32),
+                                      ip[1:] - ip[:-1])
+        blk = ((ix.to(torch.int64) * B) // n).to(torch.int8)
+        same_row = row[1:] == row[:-1]
+        if bool(((blk[1:] < blk[:-1]) & same_row).any()):
+            self._blocks[B] = None
+            return None
+        del same_row
+        out = []
+        for b in range(B):
+            m = blk == b
+            cnt = torch.bincount(row[m], minlength=self.n_rows)
+            bip = torch.zeros(self.n_rows + 1, dtype=torch.int64, device=ip.device)
+            torch.cumsum(cnt, 0, out=bip[1:])
+            del cnt
+            order, n_heavy, n_hub = make_schedule(bip)
+            out.append(DeviceCSR(bip, ix[m].contiguous(), self.values[m].contiguous(), self.n_rows, n, order,
+                                 n_heavy, n_hub, narrow_heavy(bip, n_hub)))
+            del m
+        self._blocks[B] = out
+        return out
 
     def rows(self, r0: int, r1: int, heavy_threshold=None, hub_threshold=None) -> "DeviceCSR":
         """Row block [r0, r1) with rebased row pointers (global column ids kept)."""

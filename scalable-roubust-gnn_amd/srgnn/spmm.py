@@ -6,6 +6,7 @@ on torch's current HIP stream of the operand's device, so torch events / synchro
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -14,6 +15,35 @@ from .csr import DeviceCSR
 
 
 _stream = _lib.stream
+
+# Column-blocked hops (DeviceCSR.column_blocks): B launches per hop, each gathering from one
+# contiguous slice of X's rows, so the caches hold a larger share of the rows a launch reads.
+# Measured (profiles/r02_colblock_*.json): products (X 1.25 GB) 7.12 vs 7.35 ms per hop at B = 2,
+# 7.28 at 3; arxiv (X 87 MB, already cache-resident) 0.221 vs 0.166 ms.  "auto" takes B = 2 for
+# panels of 512 MiB .. 16 GiB; SRGNN_COL_BLOCKS=<B> forces B.
+_COL_BLOCKS_ENV = os.environ.get("SRGNN_COL_BLOCKS", "auto")
+
+
+def auto_col_blocks(A: DeviceCSR, d: int) -> int:
+    """Column blocks per hop for a panel of d columns (1 = the one-launch hop)."""
+    if _COL_BLOCKS_ENV != "auto":
+        return max(1, int(_COL_BLOCKS_ENV))
+    panel = A.n_cols * d * 4
+    return 2 if d >= 64 and (512 << 20) <= panel <= (16 << 30) else 1
+
+
+def hop(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, nt_store: bool = False, col_blocks=None) -> torch.Tensor:
+    """out = A @ X (one hop, exact), column-blocked when auto_col_blocks (or `col_blocks`) says so
+    and A's rows allow it; bitwise the same either way."""
+    d = X.shape[1]
+    B = auto_col_blocks(A, d) if col_blocks is None else int(col_blocks)
+    blocks = A.column_blocks(B) if B > 1 else None
+    if not blocks:
+        return spmm(A, X, out=out, nt_store=nt_store)
+    spmm(blocks[0], X, out=out, nt_store=nt_store)
+    for Ab in blocks[1:]:
+        spmm(Ab, X, out=out, accumulate=True, nt_store=nt_store)
+    return out
 
 
 def _check_panel(X: torch.Tensor, rows: int, name: str, d=None):
@@ -154,11 +184,12 @@ def gather_rows(src: torch.Tensor, idx: torch.Tensor, out: torch.Tensor | None =
 
 
 def propagate(A: DeviceCSR, X: torch.Tensor, K: int, panels: list | None = None,
-              nt_store: bool = False) -> list:
+              nt_store: bool = False, col_blocks=None) -> list:
     """[X, ÂX, …, Â^K X] as device tensors (panels[0] is X itself, like the reference's list).
 
     Device-resident form of GraphOp.propagate's hop loop (SSRG/operators/base_operator.py:32-35):
-    the K hops run back to back on the GPU with no host round trips."""
+    the K hops run back to back on the GPU with no host round trips (srg_propagate_khop_f32, or
+    hop() per hop when the hops are column-blocked)."""
     if A.n_rows != A.n_cols:
         raise ValueError("propagate needs a square operator")
     _check_panel(X, A.n_rows, "X")
@@ -178,11 +209,16 @@ def propagate(A: DeviceCSR, X: torch.Tensor, K: int, panels: list | None = None,
         _check_panel(p, n, f"panels[{k}]", d)
         if p.stride(0) != ld:
             raise ValueError("all panels must share one leading dimension")
-    arr = (ctypes.c_void_p * (K + 1))(*[p.data_ptr() for p in panels])
-    flags = _lib.SRG_SPMM_NT_STORE if nt_store else 0
-    _lib.call(X.device, "srg_propagate_khop_f32", A.indptr.data_ptr(), A.indices.data_ptr(),
-              A.values.data_ptr(), n, A.order.data_ptr() if n else None, A.n_hub, A.heavy(d), arr, ld, d,
-              K, flags, _stream(X.device))
+    B = auto_col_blocks(A, d) if col_blocks is None else int(col_blocks)
+    if K > 0 and B > 1 and A.column_blocks(B):
+        for k in range(1, K + 1):
+            hop(A, panels[k - 1], panels[k], nt_store=nt_store, col_blocks=B)
+    else:
+        arr = (ctypes.c_void_p * (K + 1))(*[p.data_ptr() for p in panels])
+        flags = _lib.SRG_SPMM_NT_STORE if nt_store else 0
+        _lib.call(X.device, "srg_propagate_khop_f32", A.indptr.data_ptr(), A.indices.data_ptr(),
+                  A.values.data_ptr(), n, A.order.data_ptr() if n else None, A.n_hub, A.heavy(d), arr, ld, d,
+                  K, flags, _stream(X.device))
     if panels[0] is not X0 and X is not X0:
         panels = [X0] + list(panels[1:])
     return panels

@@ -175,6 +175,41 @@ def test_column_blocked_chain_continuation(name, thr):
         c.check_hop(1, Y.cpu().numpy())
 
 
+@pytest.mark.parametrize("B", [2, 3, 5])
+@pytest.mark.parametrize("name", G.names("norm"))
+def test_propagate_column_blocked_bit_exact(name, B):
+    """The product path's column-blocked hops (DeviceCSR.column_blocks + propagate(col_blocks=B):
+    B launches per hop, each block with its own schedule) == the reference's hops, bit for bit."""
+    from srgnn.spmm import hop, propagate
+    c = G.Case(name)
+    A = _csr(c, (None, None))
+    blocks = A.column_blocks(B)
+    assert blocks is not None and len(blocks) == B and sum(b.nnz for b in blocks) == A.nnz
+    X = torch.from_numpy(c.x()).cuda()
+    hops = propagate(A, X, c.k, col_blocks=B)
+    torch.cuda.synchronize()
+    for k in range(1, c.k + 1):
+        c.check_hop(k, hops[k].cpu().numpy())
+    one = hop(A, X, torch.empty_like(X), col_blocks=B)
+    c.check_hop(1, one.cpu().numpy())
+
+
+@pytest.mark.parametrize("name", G.names("raw"))
+def test_column_blocks_refused_for_unordered_rows(name):
+    """A CSR whose rows are not in column-block order cannot be cut (the chain order would change):
+    column_blocks returns None and the hop runs as one launch, still bit-exact."""
+    from srgnn.csr import DeviceCSR
+    from srgnn.spmm import hop
+    c = G.Case(name)
+    a = c.adj()
+    ip, ix = np.asarray(a.indptr), np.asarray(a.indices)
+    A = DeviceCSR.from_tensors(ip, ix, a.data.astype(np.float32), n_cols=c.n, device="cuda")
+    blk_sorted = all(np.all(np.diff((ix[ip[i]:ip[i + 1]].astype(np.int64) * 2) // c.n) >= 0) for i in range(c.n))
+    assert (A.column_blocks(2) is not None) == blk_sorted
+    Y = hop(A, torch.from_numpy(c.x()).cuda(), torch.empty((c.n, c.x().shape[1]), device="cuda"), col_blocks=2)
+    c.check_hop(1, Y.cpu().numpy())
+
+
 def test_strided_panels_and_row_blocks(oracle_mod):
     """Leading dimensions > d and a row block with rebased indptr (the multi-GPU layout)."""
     from srgnn.spmm import spmm

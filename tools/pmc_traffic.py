@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Per-launch HBM traffic of the SpMM kernel from rocprofv3 --pmc runs of tools/spmm_probe.py.
+"""Per-hop HBM traffic of the SpMM kernel from rocprofv3 --pmc runs of tools/spmm_probe.py (a hop
+is one launch, or one per column block; the "_per_launch" keys hold per-hop sums).
 
     python tools/pmc_traffic.py --fetch DIR --write DIR [--hits DIR] --probe probe.json --out OUT.json
 
@@ -17,13 +18,16 @@ import json
 import os
 
 
-def per_launch(d, counters, kernel_sub="k_spmm"):
+def per_launch(d, counters, kernel_sub="k_spmm<", hops=None):
+    """Median over the main k_spmm dispatches (hub workgroups excluded) of each counter, or with
+    `hops`, the sum over all of them divided by the hop count (column-blocked hops are several
+    launches).  Returns {counter: (value, dispatches)}."""
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     vals = {}
     for f in files:
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                if kernel_sub not in row.get("Kernel_Name", ""):
+                if kernel_sub not in row.get("Kernel_Name", "") or "k_spmm_hub" in row.get("Kernel_Name", ""):
                     continue
                 name = row.get("Counter_Name")
                 if name not in counters:
@@ -35,7 +39,7 @@ def per_launch(d, counters, kernel_sub="k_spmm"):
         v = sorted(x for (n, _, _), x in vals.items() if n == c)
         if not v:
             raise SystemExit(f"no {c} rows for {kernel_sub} under {d}")
-        out[c] = (v[len(v) // 2], len(v))
+        out[c] = (sum(v) / hops if hops else v[len(v) // 2], len(v))
     return out
 
 
@@ -48,15 +52,18 @@ def main():
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     probe = json.load(open(a.probe))
-    f = per_launch(a.fetch, ["FETCH_SIZE"])["FETCH_SIZE"]
-    w = per_launch(a.write, ["WRITE_SIZE"])["WRITE_SIZE"]
-    rec = {"config": probe["config"], "kernel": "k_spmm (one hop)", "n_heavy": probe.get("n_heavy"),
-           "launches": f[1],
+    hops = probe["reps"]
+    f = per_launch(a.fetch, ["FETCH_SIZE"], hops=hops)["FETCH_SIZE"]
+    w = per_launch(a.write, ["WRITE_SIZE"], hops=hops)["WRITE_SIZE"]
+    B = probe.get("launches_per_hop", 1)
+    rec = {"config": probe["config"], "kernel": f"k_spmm (one hop: {B} launch{'es' if B > 1 else ''}, "
+                                               "hub workgroups excluded)", "n_heavy": probe.get("n_heavy"),
+           "launches": f[1], "launches_per_hop": B,
            "fetch_size_kib": f[0], "write_size_kib": w[0],
            "hbm_read_bytes_per_launch": 2.0 * f[0] * 1024, "hbm_write_bytes_per_launch": w[0] * 1024}
     rec["hbm_bytes_per_launch"] = rec["hbm_read_bytes_per_launch"] + rec["hbm_write_bytes_per_launch"]
     if a.hits:
-        h = per_launch(a.hits, ["TCC_HIT_sum", "TCC_MISS_sum"])
+        h = per_launch(a.hits, ["TCC_HIT_sum", "TCC_MISS_sum"], hops=hops)
         hit, miss = h["TCC_HIT_sum"][0], h["TCC_MISS_sum"][0]
         rec["l2_hit_rate"] = hit / (hit + miss)
         rec["l2_miss_bytes_per_launch"] = miss * 128.0

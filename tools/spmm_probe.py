@@ -20,13 +20,14 @@ import torch  # noqa: E402
 
 from srgnn import graphs, roofline, synth  # noqa: E402
 from srgnn.csr import DeviceCSR  # noqa: E402
-from srgnn.spmm import spmm  # noqa: E402
+from srgnn.spmm import auto_col_blocks, hop  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="products")
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--identity", action="store_true")
 ap.add_argument("--heavy-threshold", type=int, default=None)
+ap.add_argument("--col-blocks", type=int, default=None, help="column blocks per hop (default: auto_col_blocks)")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 if a.identity:
@@ -39,13 +40,15 @@ else:
 A = DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, heavy_threshold=a.heavy_threshold, device=dev)
 X = synth.uniform_features_t(n, d, device=dev)
 Y = torch.empty_like(X)
+B = 1 if a.identity else (a.col_blocks if a.col_blocks is not None else auto_col_blocks(A, d))
+B = B if B > 1 and A.column_blocks(B) else 1
 torch.cuda.synchronize()
 for _ in range(a.reps):
-    spmm(A, X, out=Y)
+    hop(A, X, Y, col_blocks=B)      # one hop = B k_spmm launches (column blocks), same bits
 torch.cuda.synchronize()
 nnz = A.nnz
 print(json.dumps({"config": "identity" if a.identity else a.config, "n": n, "nnz": nnz, "d": d,
-                  "reps": a.reps, "n_heavy": A.n_heavy, "n_hub": A.n_hub,
+                  "reps": a.reps, "launches_per_hop": B, "n_heavy": A.n_heavy, "n_hub": A.n_hub,
                   "algorithmic_bytes": roofline.bytes_no_reuse(n, nnz, d),
                   "compulsory_bytes": roofline.bytes_compulsory(n, nnz, d),
                   "x_read_bytes": n * 4 * d, "y_write_bytes": n * 4 * d,
