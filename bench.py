@@ -367,8 +367,8 @@ def main():
             mode = "panels" if K * n * d * 4 < 0.9 * free else "last"
             log(f"mode {mode}: {K} panels need {K * n * d * 4 / 1e9:.1f} GB, {free / 1e9:.1f} GB free")
         col_blocks = a.col_blocks if a.col_blocks is not None else auto_col_blocks(A, d)
-        if col_blocks > 1 and (a.aggregate or mode != "panels" or not A.column_blocks(col_blocks)):
-            col_blocks = 1          # the fused aggregation and the last-hop mode run one launch per hop
+        if col_blocks > 1 and not A.column_blocks(col_blocks):
+            col_blocks = 1
         log(f"schedule: n_hub={A.n_hub} n_heavy={A.n_heavy} column blocks per hop={col_blocks}")
         if a.aggregate:
             from srgnn.aggregate import combine_plan, combine_steps, propagate_aggregate
@@ -383,7 +383,7 @@ def main():
 
             def step():
                 panels[1] = None
-                panels[1] = propagate_aggregate(A, X, K, steps_plan)
+                panels[1] = propagate_aggregate(A, X, K, steps_plan, col_blocks=col_blocks)
         elif mode == "panels":
             buf = torch.empty((K, n, d), dtype=torch.float32, device=dev)
             panels = [X] + [buf[k] for k in range(K)]
@@ -396,7 +396,7 @@ def main():
 
             def step():
                 panels[1] = None
-                panels[1] = propagate_aggregate(A, X, K, last_only=True)
+                panels[1] = propagate_aggregate(A, X, K, last_only=True, col_blocks=col_blocks)
         local_rows, local_nnz = n, nnz
     else:
         col_blocks = 1

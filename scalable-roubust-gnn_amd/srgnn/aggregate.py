@@ -27,7 +27,7 @@ import torch
 
 from . import _lib
 from .csr import DeviceCSR
-from .spmm import spmm, spmm_agg
+from .spmm import hop, spmm, spmm_agg  # noqa: F401
 
 
 def _slice_indices(n: int, start, end):
@@ -227,12 +227,12 @@ def schedule(steps):
 
 
 def propagate_aggregate(A: DeviceCSR, X: torch.Tensor, K: int, steps=None, last_only: bool = False,
-                        fuse: bool = True):
+                        fuse: bool = True, col_blocks=None):
     """Runs hops 1..K of Â on the device panel X ([n, d], row-major) with two ping-pong panels and
     executes `steps` (combine_steps) as each hop appears; returns the aggregated panel, or Â^K X
     when last_only.  Hops beyond the last one a step needs are not computed.  With `fuse`, a hop's
     first accumulation step runs in the SpMM's epilogue (srg_spmm_agg_f32: same arithmetic, one
-    panel pass less)."""
+    panel pass less).  col_blocks: column blocks per hop (spmm.hop; None = auto_col_blocks)."""
     n, d = X.shape
     if A.n_rows != n or A.n_cols != n:
         raise ValueError("propagate_aggregate needs a square operator matching X")
@@ -258,12 +258,12 @@ def propagate_aggregate(A: DeviceCSR, X: torch.Tensor, K: int, steps=None, last_
             g = groups[k] if ex is not None and k < len(groups) else []
             if fuse and g and g[0][0] == "acc" and g[0][1] == 0:
                 agg, init = ex.fused_target(g[0])
-                spmm_agg(A, cur, nxt, agg, g[0][3], init)
+                hop(A, cur, nxt, col_blocks=col_blocks, agg=(agg, g[0][3], init))
                 cur = nxt
                 for s_ in g[1:]:
                     ex.run(s_, cur if step_hop(s_) is not None else None)
             else:
-                spmm(A, cur, out=nxt)
+                hop(A, cur, nxt, col_blocks=col_blocks)
                 cur = nxt
                 consume(k, cur)
     if last_only:

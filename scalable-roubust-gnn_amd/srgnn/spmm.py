@@ -32,17 +32,19 @@ def auto_col_blocks(A: DeviceCSR, d: int) -> int:
     return 2 if d >= 64 and (512 << 20) <= panel <= (16 << 30) else 1
 
 
-def hop(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, nt_store: bool = False, col_blocks=None) -> torch.Tensor:
+def hop(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, nt_store: bool = False, col_blocks=None,
+        agg=None) -> torch.Tensor:
     """out = A @ X (one hop, exact), column-blocked when auto_col_blocks (or `col_blocks`) says so
-    and A's rows allow it; bitwise the same either way."""
+    and A's rows allow it; bitwise the same either way.  agg = (panel, w, init): the aggregation
+    step fused into the (last) launch's epilogue, as spmm_agg."""
     d = X.shape[1]
     B = auto_col_blocks(A, d) if col_blocks is None else int(col_blocks)
-    blocks = A.column_blocks(B) if B > 1 else None
-    if not blocks:
-        return spmm(A, X, out=out, nt_store=nt_store)
-    spmm(blocks[0], X, out=out, nt_store=nt_store)
-    for Ab in blocks[1:]:
-        spmm(Ab, X, out=out, accumulate=True, nt_store=nt_store)
+    blocks = (A.column_blocks(B) if B > 1 else None) or [A]
+    for b, Ab in enumerate(blocks):
+        if agg is not None and b == len(blocks) - 1:
+            spmm_agg(Ab, X, out, agg[0], agg[1], agg[2], nt_store=nt_store, accumulate=b > 0)
+        else:
+            spmm(Ab, X, out=out, accumulate=b > 0, nt_store=nt_store)
     return out
 
 
@@ -92,16 +94,17 @@ def spmm(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor | None = None, accumul
 
 
 def spmm_agg(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, agg: torch.Tensor, w: float, init: bool,
-             nt_store: bool = False) -> torch.Tensor:
+             nt_store: bool = False, accumulate: bool = False) -> torch.Tensor:
     """out = A @ X and, fused into the same kernels' epilogue, agg = (0 if init else agg) + w * out
-    (srg_spmm_agg_f32; the arithmetic of spmm followed by one srg_hop_accumulate_f32 step)."""
+    (srg_spmm_agg_f32; the arithmetic of spmm followed by one srg_hop_accumulate_f32 step).
+    accumulate: the chains continue from out's content (the last block of a column-blocked hop)."""
     _check_panel(X, A.n_cols, "X")
     d = X.shape[1]
     _check_panel(out, A.n_rows, "out", d)
     _check_panel(agg, A.n_rows, "agg", d)
     if not (out.device == X.device == agg.device == A.device):
         raise ValueError("A, X, out and agg must be on the same device")
-    flags = _lib.SRG_SPMM_NT_STORE if nt_store else 0
+    flags = (_lib.SRG_SPMM_NT_STORE if nt_store else 0) | (_lib.SRG_SPMM_ACCUMULATE if accumulate else 0)
     _lib.call(X.device, "srg_spmm_agg_f32", A.indptr.data_ptr(), A.indices.data_ptr(), A.values.data_ptr(),
               A.n_rows, A.order.data_ptr() if A.n_rows else None, A.n_hub, A.heavy(d), X.data_ptr(),
               X.stride(0), out.data_ptr(), out.stride(0), d, flags, agg.data_ptr(), agg.stride(0),

@@ -53,6 +53,31 @@ def test_fused_combine_bit_exact(oracle_mod, name, K):
         np.testing.assert_array_equal(got, want, err_msg=f"{name} K={K} {msg.aggr_type} {msg.start}:{msg.end}")
 
 
+@pytest.mark.parametrize("B", [2, 3])
+@pytest.mark.parametrize("name", ["cora_sym_k3", "rand_d130_r1", "rand_d36_ppr"])
+def test_propagate_aggregate_column_blocked_bit_exact(oracle_mod, name, B):
+    """Column-blocked hops in the fused aggregation (spmm.hop: blocks with ACCUMULATE, the
+    aggregation epilogue in the last block's launch) == the reference's combine, bit for bit."""
+    from srgnn.aggregate import combine_plan, combine_steps, propagate_aggregate
+    from srgnn.csr import DeviceCSR
+    c = G.Case(name)
+    ip, ix, v = c.ahat()
+    x = c.x()
+    K = 5
+    hops = oracle_mod.propagate(ip, ix, v, x, K)
+    A = DeviceCSR.from_tensors(ip, ix, v, n_cols=c.n, device="cuda")
+    assert A.column_blocks(B) is not None
+    X = torch.from_numpy(x).cuda()
+    for msg in _ops(K):
+        mode, terms, div = combine_plan(msg, K + 1)
+        if mode == "last":
+            got = propagate_aggregate(A, X, K, last_only=True, col_blocks=B)
+        else:
+            got = propagate_aggregate(A, X, K, combine_steps(mode, terms, div), col_blocks=B)
+        np.testing.assert_array_equal(got.cpu().numpy(), _expected(oracle_mod, msg, hops),
+                                      err_msg=f"{name} B={B} {msg.aggr_type} {msg.start}:{msg.end}")
+
+
 def test_graphop_propagate_aggregate_matches_aggregate_of_propagate():
     """operators API: GraphOp.propagate_aggregate(adj, x, msg) == msg.aggregate(GraphOp.propagate(adj, x))."""
     from operators.graph_operator.symmetrical_simgraph_laplacian_operator import SymLaplacianGraphOp
