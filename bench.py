@@ -194,7 +194,7 @@ def run_wavelet(a, dev, world=1, rank=0):
     from srgnn import wavelet as W
     from srgnn.csr import DeviceCSR
     from srgnn import _lib
-    from srgnn.spmm import spmm, spmm_cheby
+    from srgnn.spmm import auto_col_blocks, hop, spmm_cheby
     t_build = time.perf_counter()
     ip, ix, lv, n, d, lmax = graphs.build_laplacian(a.config, dev, d=a.d)
     nnz = int(ix.numel())
@@ -231,6 +231,8 @@ def run_wavelet(a, dev, world=1, rank=0):
     # SpMM launch of the split path
     stream = torch.cuda.current_stream(dev)
     Fm = filt._csr(filt.fvals)
+    B = auto_col_blocks(Fm, cb)
+    B = 1 if fused or B < 2 or not Fm.column_blocks(B) else B
     tb = torch.zeros((n, cb), dtype=torch.float32, device=dev)
     ns = len(filt.taus)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * a.roofline_reps)]
@@ -240,7 +242,7 @@ def run_wavelet(a, dev, world=1, rank=0):
             spmm_cheby(Fm, X[:, :cb], tb, _lib.SRG_CHEBY_STEP, filt.a1, filt.a2, tb, None, filt.coeffs[:, 2],
                        R[:, :, :cb])
         else:
-            spmm(Fm, X[:, :cb], out=tb)
+            hop(Fm, X[:, :cb], tb)
         ev[2 * r + 1].record(stream)
     torch.cuda.synchronize()
     kern_s = float(np.mean([ev[2 * r].elapsed_time(ev[2 * r + 1]) * 1e-3 for r in range(a.roofline_reps)]))
@@ -265,7 +267,7 @@ def run_wavelet(a, dev, world=1, rank=0):
                      "frac": achieved / roofline.MI355X_HBM_PEAK_GBS, "traffic": None,
                      "kernel": (f"k_spmm with the Chebyshev epilogue: one order over a {cb}-column block" if fused
                                 else f"k_spmm: one Chebyshev order's SpMM over a {cb}-column block"),
-                     "kernel_ms": kern_s * 1e3, "algorithmic_bytes_per_launch": b_alg,
+                     "kernel_ms": kern_s * 1e3, "launches_per_hop": B, "algorithmic_bytes_per_launch": b_alg,
                      "compulsory_bytes_per_launch": roofline.bytes_compulsory(n, nnz, cb, n_cols=n)},
         "cpu_baseline": None,
     }

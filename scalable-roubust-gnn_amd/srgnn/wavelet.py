@@ -224,8 +224,13 @@ class HeatWaveletFilter:
         return R
 
     def _csr(self, vals):
-        return DeviceCSR(self.indptr, self.indices, vals, self.n, self.n, self.order, self.n_heavy, self.n_hub,
-                         self.n_heavy_narrow)
+        """The operator with values `vals` (L or F), built once per value array so that its column
+        blocks (spmm.hop) are cut once."""
+        cache = self.__dict__.setdefault("_csr_cache", {})
+        if id(vals) not in cache:
+            cache[id(vals)] = DeviceCSR(self.indptr, self.indices, vals, self.n, self.n, self.order, self.n_heavy,
+                                        self.n_hub, self.n_heavy_narrow)
+        return cache[id(vals)]
 
     def work_panels(self, fused_epilogue: bool = False) -> int:
         """[n, column block] work panels the split path needs: T_1 alone for order 1; T_{k-1} and
@@ -235,7 +240,7 @@ class HeatWaveletFilter:
 
     def _apply_split(self, Sb, Rb, work, fused_epilogue: bool = False):
         """One column block: Sb [n, w] and Rb [ns, n, w] may be strided views."""
-        from .spmm import spmm, spmm_cheby
+        from .spmm import hop, spmm_cheby
         n, w = Sb.shape
         ns, nc = self.coeffs.shape
         ct = ctypes.c_float
@@ -266,14 +271,14 @@ class HeatWaveletFilter:
         lean = self.lean_epilogue and nc > 2
         t_old, t_cur = Sb, work[0]
         free = list(work[1:])
-        spmm(Lm, Sb, out=t_cur)
+        hop(Lm, Sb, t_cur)                 # column-blocked where spmm.auto_col_blocks says so
         if lean:
             epi(t_cur, Sb, None, _lib.SRG_CHEBY_INIT_T, None, None)
         else:
             epi(t_cur, Sb, None, _lib.SRG_CHEBY_INIT, self.coeffs[:, 0], self.coeffs[:, 1])
         for k in range(2, nc):
             t_new = free.pop()
-            spmm(Fm, t_cur, out=t_new)
+            hop(Fm, t_cur, t_new)
             last = _lib.SRG_CHEBY_NO_T if lean and k == nc - 1 else 0
             if lean and k == 2:
                 epi(t_new, t_cur, t_old, _lib.SRG_CHEBY_STEP_FIRST | last,

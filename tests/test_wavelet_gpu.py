@@ -147,6 +147,21 @@ def test_lean_epilogue_bit_identical(order, cb):
     assert torch.equal(fused, lean) and torch.equal(fused, plain)
 
 
+@pytest.mark.parametrize("B", ["2", "3"])
+def test_split_path_column_blocked_bit_identical(monkeypatch, B):
+    """The split path's SpMMs as column-blocked hops (spmm.hop, forced here; automatic for panels of
+    512 MiB .. 16 GiB) == the fused kernel, bit for bit."""
+    from srgnn import spmm as S_, wavelet as W
+    monkeypatch.setattr(S_, "_COL_BLOCKS_ENV", B)
+    a = graphs()["rmat3000"]
+    L = W.laplacian_from_adj(a)
+    f = W.HeatWaveletFilter(L, [-0.5, 0.5], order=3, lmax=None, dtype=torch.float32, device="cuda",
+                            heavy_threshold=40, hub_threshold=400)
+    assert f._csr(f.fvals).column_blocks(int(B)) is not None
+    S = torch.from_numpy(np.random.default_rng(9).standard_normal((a.shape[0], 128)).astype(np.float32)).cuda()
+    assert torch.equal(f.apply(S, split=False), f.apply(S, split=True, col_block=64))
+
+
 def test_spmm_cheby_in_place_and_argument_checks():
     """srg_spmm_cheby_f32 directly: a step written over T_{k-1} equals the step into a fresh panel
     and the two-launch form; aliasing and flag misuse are rejected before any launch."""
