@@ -61,6 +61,10 @@ extern "C" {
  * before anything reads the hub rows, and before the next NOJOIN fork from the same stream (one
  * outstanding fork per caller stream). */
 #define SRG_SPMM_HUB_NOJOIN 0x10u
+/* Packed light rows keep 2 gathers per row in flight instead of 4: better for the short rows of a
+ * column block (srgnn.spmm.hop passes it for column-blocked hops; products 7.15 -> 7.01 ms per hop),
+ * worse for whole rows.  Results are identical either way. */
+#define SRG_SPMM_PACKED_U2 0x20u
 
 /* =============================================================================================
  * (A) drop-in entry points

@@ -1497,6 +1497,7 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
         while (vec > 1 && epi.r_stride % vec) vec /= 2;
     }
     const int nr = (int)m_rows, nh = (int)n_heavy;
+    const int pu = (flags & SRG_SPMM_PACKED_U2) ? 2 : packed_u_setting();
     for (int64_t b0 = 0; b0 < blocks; b0 += kMaxLaunchBlocks) {
         const dim3 grid((unsigned)std::min<int64_t>(kMaxLaunchBlocks, blocks - b0));
         const int bb = (int)b0;
@@ -1522,8 +1523,8 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
     } while (0)
 #define SRG_LAUNCH_PACKED_U(LRV, LQV)                                                                 \
     do {                                                                                              \
-        if (packed_u_setting() == 4) SRG_LAUNCH_PACKED(LRV, LQV, 4);                                  \
-        else if (packed_u_setting() == 2) SRG_LAUNCH_PACKED(LRV, LQV, 2);                             \
+        if (pu == 4) SRG_LAUNCH_PACKED(LRV, LQV, 4);                                                  \
+        else if (pu == 2) SRG_LAUNCH_PACKED(LRV, LQV, 2);                                             \
         else SRG_LAUNCH_PACKED(LRV, LQV, 8);                                                          \
     } while (0)
         if (lr == 2) {

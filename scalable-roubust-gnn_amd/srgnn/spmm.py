@@ -22,6 +22,10 @@ _stream = _lib.stream
 # 7.28 at 3; arxiv (X 87 MB, already cache-resident) 0.221 vs 0.166 ms.  "auto" takes B = 2 for
 # panels of 512 MiB .. 16 GiB; SRGNN_COL_BLOCKS=<B> forces B.
 _COL_BLOCKS_ENV = os.environ.get("SRGNN_COL_BLOCKS", "auto")
+# column blocks' launches keep 2 gathers per packed light row in flight (SRG_SPMM_PACKED_U2) for
+# d >= 128: products 7.15 -> 7.03 ms per hop, d = 256 +1.3 %, d = 64 -3 % (so not there);
+# SRGNN_BLOCK_U2=0 turns it off (A/B, profiles/r02_ab_col_blocks.txt)
+_U2_BLOCKED = os.environ.get("SRGNN_BLOCK_U2", "1") != "0"
 
 
 def auto_col_blocks(A: DeviceCSR, d: int) -> int:
@@ -40,11 +44,14 @@ def hop(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, nt_store: bool = False
     d = X.shape[1]
     B = auto_col_blocks(A, d) if col_blocks is None else int(col_blocks)
     blocks = (A.column_blocks(B) if B > 1 else None) or [A]
+    # a block's rows are short: 2 gathers per packed row in flight (d >= 128: 4 or 2 rows per wave;
+    # at d = 64, 8 rows per wave, it is 3 % slower)
+    u2 = len(blocks) > 1 and d >= 128 and _U2_BLOCKED
     for b, Ab in enumerate(blocks):
         if agg is not None and b == len(blocks) - 1:
-            spmm_agg(Ab, X, out, agg[0], agg[1], agg[2], nt_store=nt_store, accumulate=b > 0)
+            spmm_agg(Ab, X, out, agg[0], agg[1], agg[2], nt_store=nt_store, accumulate=b > 0, packed_u2=u2)
         else:
-            spmm(Ab, X, out=out, accumulate=b > 0, nt_store=nt_store)
+            spmm(Ab, X, out=out, accumulate=b > 0, nt_store=nt_store, packed_u2=u2)
     return out
 
 
@@ -68,7 +75,7 @@ def _check_panel(X: torch.Tensor, rows: int, name: str, d=None):
 
 def spmm(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor | None = None, accumulate: bool = False,
          nt_store: bool = False, wide_rows: bool = False, hub_w256: bool = False,
-         hub_nojoin: bool = False) -> torch.Tensor:
+         hub_nojoin: bool = False, packed_u2: bool = False) -> torch.Tensor:
     """out[r, :] (+)= A[r, :] @ X  for the rows of A (one hop; exact fma chains in CSR order).
     wide_rows: diagnostic, one row per wave for every light row (no narrow or packed rows);
     hub_w256: diagnostic, 256-nonzero
@@ -86,7 +93,7 @@ def spmm(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor | None = None, accumul
         raise ValueError("A, X and out must be on the same device")
     flags = (_lib.SRG_SPMM_ACCUMULATE if accumulate else 0) | (_lib.SRG_SPMM_NT_STORE if nt_store else 0) | \
         (_lib.SRG_SPMM_WIDE_ROWS if wide_rows else 0) | (_lib.SRG_SPMM_HUB_W256 if hub_w256 else 0) | \
-        (_lib.SRG_SPMM_HUB_NOJOIN if hub_nojoin else 0)
+        (_lib.SRG_SPMM_HUB_NOJOIN if hub_nojoin else 0) | (_lib.SRG_SPMM_PACKED_U2 if packed_u2 else 0)
     _lib.call(X.device, "srg_spmm_csr_f32", A.indptr.data_ptr(), A.indices.data_ptr(), A.values.data_ptr(),
               A.n_rows, A.order.data_ptr() if A.n_rows else None, A.n_hub, A.heavy(d), X.data_ptr(),
               X.stride(0), out.data_ptr(), out.stride(0), d, flags, _stream(X.device))
@@ -94,7 +101,7 @@ def spmm(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor | None = None, accumul
 
 
 def spmm_agg(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, agg: torch.Tensor, w: float, init: bool,
-             nt_store: bool = False, accumulate: bool = False) -> torch.Tensor:
+             nt_store: bool = False, accumulate: bool = False, packed_u2: bool = False) -> torch.Tensor:
     """out = A @ X and, fused into the same kernels' epilogue, agg = (0 if init else agg) + w * out
     (srg_spmm_agg_f32; the arithmetic of spmm followed by one srg_hop_accumulate_f32 step).
     accumulate: the chains continue from out's content (the last block of a column-blocked hop)."""
@@ -104,7 +111,8 @@ def spmm_agg(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, agg: torch.Tensor
     _check_panel(agg, A.n_rows, "agg", d)
     if not (out.device == X.device == agg.device == A.device):
         raise ValueError("A, X, out and agg must be on the same device")
-    flags = (_lib.SRG_SPMM_NT_STORE if nt_store else 0) | (_lib.SRG_SPMM_ACCUMULATE if accumulate else 0)
+    flags = (_lib.SRG_SPMM_NT_STORE if nt_store else 0) | (_lib.SRG_SPMM_ACCUMULATE if accumulate else 0) | \
+        (_lib.SRG_SPMM_PACKED_U2 if packed_u2 else 0)
     _lib.call(X.device, "srg_spmm_agg_f32", A.indptr.data_ptr(), A.indices.data_ptr(), A.values.data_ptr(),
               A.n_rows, A.order.data_ptr() if A.n_rows else None, A.n_hub, A.heavy(d), X.data_ptr(),
               X.stride(0), out.data_ptr(), out.stride(0), d, flags, agg.data_ptr(), agg.stride(0),
