@@ -158,7 +158,10 @@ class DeviceCSR:
         ip, ix, n = self.indptr, self.indices, self.n_cols
         row = torch.repeat_interleave(torch.arange(self.n_rows, device=ip.device, dtype=torch.int32),
                                       ip[1:] - ip[:-1])
-        blk = ((ix.to(torch.int64) * B) // n).to(torch.int8)
+        # block ids in int32 arithmetic where it cannot overflow (billion-entry CSRs: no int64 copy)
+        wide = ix.to(torch.int64) if n * B >= 2 ** 31 else ix
+        blk = torch.div(wide * B, n, rounding_mode="floor").to(torch.int8)
+        del wide
         same_row = row[1:] == row[:-1]
         if bool(((blk[1:] < blk[:-1]) & same_row).any()):
             self._blocks[B] = None
@@ -167,12 +170,14 @@ class DeviceCSR:
         out = []
         for b in range(B):
             m = blk == b
-            cnt = torch.bincount(row[m], minlength=self.n_rows)
+            cnt = torch.zeros(self.n_rows, dtype=torch.int64, device=ip.device)
+            for c0 in range(0, m.numel(), _CHUNK):
+                cnt += torch.bincount(row[c0:c0 + _CHUNK][m[c0:c0 + _CHUNK]].to(torch.int64), minlength=self.n_rows)
             bip = torch.zeros(self.n_rows + 1, dtype=torch.int64, device=ip.device)
             torch.cumsum(cnt, 0, out=bip[1:])
             del cnt
             order, n_heavy, n_hub = make_schedule(bip)
-            out.append(DeviceCSR(bip, ix[m].contiguous(), self.values[m].contiguous(), self.n_rows, n, order,
+            out.append(DeviceCSR(bip, _masked(ix, m), _masked(self.values, m), self.n_rows, n, order,
                                  n_heavy, n_hub, narrow_heavy(bip, n_hub)))
             del m
         self._blocks[B] = out
@@ -188,6 +193,17 @@ class DeviceCSR:
         return DeviceCSR(ip.contiguous(), self.indices[base:end], self.values[base:end],
                          r1 - r0, self.n_cols, order, n_heavy, n_hub,
                          narrow_heavy(ip, n_hub) if _auto_heavy(heavy_threshold) else None)
+
+
+# boolean selections and bincounts go in chunks: past ~2^31 entries torch's nonzero overflows
+_CHUNK = 1 << 28
+
+
+def _masked(t: torch.Tensor, m: torch.Tensor) -> torch.Tensor:
+    """t[m] for 1-D t and mask m of any length (chunked)."""
+    if t.numel() <= _CHUNK:
+        return t[m].contiguous()
+    return torch.cat([t[c0:c0 + _CHUNK][m[c0:c0 + _CHUNK]] for c0 in range(0, t.numel(), _CHUNK)])
 
 
 def _auto_heavy(heavy_threshold) -> bool:
