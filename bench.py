@@ -213,6 +213,7 @@ def run_wavelet(a, dev, world=1, rank=0):
     # gather more bytes per nonzero (RMAT-26: 64 columns 1.37 s per step, 32 columns 1.87 s)
     while not a.col_block and cb > 8 and n_work * n * cb * 4 > free - 2 ** 30:
         cb //= 2
+    filt.prepare_column_blocks(cb, hops=order * (d // cb) * (a.steps + a.warmup))
     log(f"wavelet {a.config}: n={n} nnz(L)={nnz} d={d} lmax={lmax} col_block={cb} "
         f"hub={filt.n_hub} heavy={filt.n_heavy} built in {time.perf_counter() - t_build:.1f}s")
 
@@ -368,7 +369,8 @@ def main():
             free, _ = torch.cuda.mem_get_info(dev)
             mode = "panels" if K * n * d * 4 < 0.9 * free else "last"
             log(f"mode {mode}: {K} panels need {K * n * d * 4 / 1e9:.1f} GB, {free / 1e9:.1f} GB free")
-        col_blocks = a.col_blocks if a.col_blocks is not None else auto_col_blocks(A, d)
+        # the operator serves every warm-up and timed step: cut it once here when that amortises
+        col_blocks = a.col_blocks if a.col_blocks is not None else auto_col_blocks(A, d, hops=K * (a.steps + a.warmup))
         if col_blocks > 1 and not A.column_blocks(col_blocks):
             col_blocks = 1
         log(f"schedule: n_hub={A.n_hub} n_heavy={A.n_heavy} column blocks per hop={col_blocks}")

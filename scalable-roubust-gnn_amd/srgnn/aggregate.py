@@ -238,6 +238,9 @@ def propagate_aggregate(A: DeviceCSR, X: torch.Tensor, K: int, steps=None, last_
         raise ValueError("propagate_aggregate needs a square operator matching X")
     if X.dim() != 2 or X.dtype != torch.float32 or X.stride(1) != 1 or X.stride(0) < d:
         raise ValueError("X must be a row-major float32 [n, d] device panel")
+    if col_blocks is None:
+        from .spmm import auto_col_blocks
+        col_blocks = auto_col_blocks(A, d, hops=K)
     groups, trailing = schedule(steps or [])
     if len(groups) > K + 1:
         raise ValueError("hop index out of range")

@@ -28,12 +28,22 @@ _COL_BLOCKS_ENV = os.environ.get("SRGNN_COL_BLOCKS", "auto")
 _U2_BLOCKED = os.environ.get("SRGNN_BLOCK_U2", "1") != "0"
 
 
-def auto_col_blocks(A: DeviceCSR, d: int) -> int:
-    """Column blocks per hop for a panel of d columns (1 = the one-launch hop)."""
+# Cutting an operator costs about as much as 50 hops gain (products: 21 ms against 0.39 ms per hop,
+# tools/probes/colblock_build_time.py): it is cut for a run of at least this many hops, or when
+# its blocks already exist (a reused operator: bench.py cuts once up front).
+MIN_HOPS_TO_CUT = 48
+
+
+def auto_col_blocks(A: DeviceCSR, d: int, hops: int | None = None) -> int:
+    """Column blocks per hop for a panel of d columns (1 = the one-launch hop): 2 for panels of
+    512 MiB .. 16 GiB at d >= 64, if A's blocks exist or `hops` hops will amortise cutting it."""
     if _COL_BLOCKS_ENV != "auto":
         return max(1, int(_COL_BLOCKS_ENV))
     panel = A.n_cols * d * 4
-    return 2 if d >= 64 and (512 << 20) <= panel <= (16 << 30) else 1
+    B = 2 if d >= 64 and (512 << 20) <= panel <= (16 << 30) else 1
+    if B > 1 and B not in A._blocks and (hops is None or hops < MIN_HOPS_TO_CUT):
+        return 1
+    return B
 
 
 def hop(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, nt_store: bool = False, col_blocks=None,
@@ -220,7 +230,7 @@ def propagate(A: DeviceCSR, X: torch.Tensor, K: int, panels: list | None = None,
         _check_panel(p, n, f"panels[{k}]", d)
         if p.stride(0) != ld:
             raise ValueError("all panels must share one leading dimension")
-    B = auto_col_blocks(A, d) if col_blocks is None else int(col_blocks)
+    B = auto_col_blocks(A, d, hops=K) if col_blocks is None else int(col_blocks)
     if K > 0 and B > 1 and A.column_blocks(B):
         for k in range(1, K + 1):
             hop(A, panels[k - 1], panels[k], nt_store=nt_store, col_blocks=B)

@@ -232,6 +232,18 @@ class HeatWaveletFilter:
                                         self.n_hub, self.n_heavy_narrow)
         return cache[id(vals)]
 
+    def prepare_column_blocks(self, width: int, hops: int) -> int:
+        """Cut L and F into column blocks (spmm.hop) when `hops` SpMMs over panels `width` columns
+        wide amortise it (spmm.auto_col_blocks); returns the blocks per SpMM."""
+        from .spmm import auto_col_blocks
+        B = 1
+        for vals in (self.lvals, self.fvals):
+            A = self._csr(vals)
+            B = auto_col_blocks(A, width, hops=hops)
+            if B > 1 and not A.column_blocks(B):
+                B = 1
+        return B
+
     def work_panels(self, fused_epilogue: bool = False) -> int:
         """[n, column block] work panels the split path needs: T_1 alone for order 1; T_{k-1} and
         T_k with the fused epilogue (T_{k+1} overwrites T_{k-1}); one more for the SpMM's raw
