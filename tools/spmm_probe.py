@@ -40,7 +40,8 @@ else:
 A = DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, heavy_threshold=a.heavy_threshold, device=dev)
 X = synth.uniform_features_t(n, d, device=dev)
 Y = torch.empty_like(X)
-B = 1 if a.identity else (a.col_blocks if a.col_blocks is not None else auto_col_blocks(A, d))
+# the probe stands for a long run of hops (bench.py's operator serves every step): the panel rule alone
+B = 1 if a.identity else (a.col_blocks if a.col_blocks is not None else auto_col_blocks(A, d, hops=1 << 30))
 B = B if B > 1 and A.column_blocks(B) else 1
 torch.cuda.synchronize()
 for _ in range(a.reps):
