@@ -183,6 +183,30 @@ def pmc_traffic(config, kernel_hint="k_spmm", launches_per_hop=1):
         return None
 
 
+def reference_hops(ip, ix, vals, n, X, K, dev):
+    """Hop 1 and hop K of the whole graph computed by this rank alone with the one-GPU kernels
+    (bitwise the 1-GPU bench, and so the reference's product): an N-GPU run checks its own rows
+    against them after the timed steps, so the first run over RCCL on a node also proves the
+    exchange bitwise.  None when three whole panels do not fit in half of the free memory."""
+    from srgnn.csr import DeviceCSR
+    from srgnn.spmm import spmm
+    free, _ = torch.cuda.mem_get_info(dev)
+    if K < 1 or 3 * n * X.shape[1] * 4 > 0.5 * free:
+        return None
+    A = DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, device=dev, validate=False)
+    bufs = [torch.empty_like(X), torch.empty_like(X)]
+    out, cur = {}, X
+    for k in range(1, K + 1):
+        nxt = bufs[(k - 1) % 2] if k > 1 or K == 1 else torch.empty_like(X)
+        spmm(A, cur, out=nxt)
+        if k == 1:
+            out[1] = nxt
+        cur = nxt
+    out[K] = cur
+    torch.cuda.synchronize()
+    return out
+
+
 def run_wavelet(a, dev, world=1, rank=0):
     """SpectralModel's wavelet operator (SSRG/models/base_scalable/base_model.py:180-265) on the
     config's graph: R_s = sum_k c_{s,k} T_k(L~) X for tau = -0.5, +0.5, Chebyshev order 3, fp32.
@@ -363,6 +387,7 @@ def main():
 
     stream = torch.cuda.current_stream(dev)
     mode = a.mode
+    ref_full = reference_hops(ip, ix, vals, n, X, K, dev) if world > 1 else None
     if world == 1:
         A = DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, heavy_threshold=a.heavy_threshold, device=dev)
         if mode == "auto":
@@ -437,6 +462,11 @@ def main():
         # one hop's kernels also compute the ghost rows (the roofline counts that work)
         local_rows, local_nnz = op.rows + op.n_ghost, op.nnz_local + int(op._ghost_pos.numel())
 
+    refs = None
+    if ref_full is not None:     # this rank's rows of the 1-GPU hops, checked after the timed steps
+        refs = {k: v[op.r0:op.r1].clone() for k, v in ref_full.items()}
+    del ref_full
+    torch.cuda.empty_cache()
     host_copy = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         host_copy = (ip.cpu().numpy(), ix.cpu().numpy(), vals.cpu().numpy(), X.cpu().numpy())
@@ -464,6 +494,16 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+
+    parity = None
+    if world > 1:
+        # the N-GPU hops of this rank's rows against the 1-GPU kernels on the whole graph, bit for bit
+        ok = refs is not None and all(torch.equal(panels[k][: op.rows], v) for k, v in refs.items())
+        flags = torch.tensor([int(refs is not None), int(ok)], dtype=torch.int32, device=dev)
+        dist.all_reduce(flags, op=dist.ReduceOp.MIN)
+        parity = ({"hops_checked": sorted(refs), "bitwise_equal_to_1gpu": bool(flags[1].item()), "ranks": world}
+                  if flags[0].item() else {"skipped": "the whole graph's panels do not fit beside a rank's share"})
+        del refs
 
     # roofline: average duration of one hop's SpMM launches on this rank (HIP events on the
     # launch stream; the hub side stream is joined back into it by the library)
@@ -553,6 +593,8 @@ def main():
                                                                               n_cols=n)},
         "cpu_baseline": None,
     }
+    if parity is not None:
+        res["parity_vs_1gpu"] = parity
     if host_copy is not None:
         log("cpu baseline ...")
         ipn, ixn, vn, xn = host_copy
