@@ -315,9 +315,19 @@ def run_wavelet_dist(a, dev, world, rank):
                           heavy_threshold=a.heavy_threshold, device=dev)
     X = synth.uniform_features_t(n, d, seed=synth.FEATURE_SEED, device=dev)
     S_local = X[f.r0:f.r1].contiguous()
+    # this rank's rows of the one-GPU filter bank on the whole graph, checked after the timed steps
+    ref = None
+    free, _ = torch.cuda.mem_get_info(dev)
+    if 6 * n * d * 4 < 0.5 * free:
+        from srgnn import wavelet as W
+        one = W.HeatWaveletFilter.from_device(ip, ix, lv, n, [-0.5, 0.5], order=order, lmax=lmax,
+                                              dtype=torch.float32, heavy_threshold=a.heavy_threshold)
+        ref = one.apply(X)[:, f.r0:f.r1].clone()
+        del one
     del X, ip, ix, lv
     torch.cuda.empty_cache()
     log(f"rank {rank}: wavelet rows={f.rows} halo={f.opL.halo} built in {time.perf_counter() - t_build:.1f}s")
+    R = None
     for _ in range(a.warmup):
         f.apply(S_local)
     torch.cuda.synchronize()
@@ -325,13 +335,18 @@ def run_wavelet_dist(a, dev, world, rank):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        f.apply(S_local)
+        R = f.apply(S_local)
     torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
     t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
+    ok = ref is not None and R is not None and torch.equal(R, ref)
+    flags = torch.tensor([int(ref is not None), int(ok)], dtype=torch.int32, device=dev)
+    dist.all_reduce(flags, op=dist.ReduceOp.MIN)
+    parity = ({"outputs_checked": "every scale, this rank's rows", "bitwise_equal_to_1gpu": bool(flags[1].item()),
+               "ranks": world} if flags[0].item() else {"skipped": "the whole graph's panels do not fit beside a rank's share"})
     res = {"metric": "propagated edges/sec (wavelet-basis Chebyshev propagation)",
            "value": a.steps * order * nnz / dt, "unit": "propagated edges/s", "n_gpus": world,
            "steps": a.steps, "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True,
@@ -340,7 +355,7 @@ def run_wavelet_dist(a, dev, world, rank):
            "config": {"workload": f"{a.config}-shaped heat-wavelet filter bank", "n_nodes": n, "nnz_L": nnz, "d": d,
                       "chebyshev_order": order, "scales": [-0.5, 0.5], "lmax": lmax,
                       "parallelism": f"row-partition x{world} (halo exchange per order)"},
-           "roofline": None, "cpu_baseline": None}
+           "roofline": None, "cpu_baseline": None, "parity_vs_1gpu": parity}
     if rank == 0:
         print(json.dumps(res), flush=True)
     dist.barrier()
