@@ -192,6 +192,21 @@ int srg_spmm_agg_f32(const int64_t* indptr, const int32_t* indices, const float*
                      const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t d, uint32_t flags,
                      float* agg, int64_t lda, float w, int agg_init, void* stream);
 
+/* One column block of a hop over ROW SPANS: row r's entries are [row_beg[r], row_end[r]) of the
+ * shared indices / values arrays (both int64 [n_rows]), otherwise srg_spmm_csr_f32 (agg == NULL)
+ * or srg_spmm_agg_f32 (agg != NULL).  When every row of Â holds sorted column ids (utils.py:81-93
+ * builds them so), the entries of row r whose ids fall in a column block are one span of the row,
+ * so block b of a hop is this call with row_beg = split_b, row_end = split_{b+1} (split_0 =
+ * indptr[0:n], split_B = indptr[1:n+1]): no copy of the ids or values.  Block 0 runs from +0.0f,
+ * blocks 1.. with SRG_SPMM_ACCUMULATE continue every chain from the fp32 value the previous block
+ * stored -- the same fmas in the same order as the one-launch hop, so the same bits.  row_order /
+ * n_hub / n_heavy schedule the spans' lengths.  Replaces one call of csr_sparse_dense_matmul
+ * (SSRG/operators/utils.py:17-47) inside GraphOp.propagate's hop loop (base_operator.py:33-35). */
+int srg_spmm_span_f32(const int64_t* row_beg, const int64_t* row_end, const int32_t* indices,
+                      const float* values, int64_t n_rows, const int32_t* row_order, int64_t n_hub,
+                      int64_t n_heavy, const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t d,
+                      uint32_t flags, float* agg, int64_t lda, float w, int agg_init, void* stream);
+
 /* srg_spmm_csr_f32 with the halo pack of the multi-GPU exchange fused into its epilogue
  * (srgnn/dist.py HaloPartitionedOperator; no reference counterpart -- the reference is single
  * process): every row r it computes is also stored, unchanged, into the send-buffer rows
@@ -242,6 +257,15 @@ int srg_gather_rows_f32(const float* src, int64_t lds, int64_t n_src, const int6
 /* `stream` waits (on the device, not the host) for the hub workgroups of the last hub launch
  * forked from `stream` (an SRG_SPMM_HUB_NOJOIN one); no-op if none was forked. */
 int srg_hub_join(void* stream);
+
+/* Column-block split points of a device CSR for srg_spmm_span_f32 (asynchronous on `stream`):
+ * splits[(b-1) * n_rows + r] = the first entry of row r with column id >= ceil(b * n_cols / n_blocks)
+ * (binary search over the row's sorted ids), b = 1 .. n_blocks-1; splits: int64 [(n_blocks-1) * n_rows].
+ * For any row the split points lie in [indptr[r], indptr[r+1]] and never decrease with b, so the
+ * spans partition every row in CSR order and the blocked hop stays exact even for unsorted rows
+ * (which only lose the blocks' locality).  n_blocks in [2, 64]. */
+int srg_csr_col_splits(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t n_cols,
+                       int32_t n_blocks, int64_t* splits, void* stream);
 
 /* Checks a device CSR: indptr[0] == 0, indptr non-decreasing, indptr[n_rows] == nnz, and every
  * column id in [0, n_cols).  Synchronous on `stream`.  Returns SRG_OK or SRG_ERR_INVALID. */

@@ -177,17 +177,23 @@ constexpr int kBlock = 64 * kWavesPerBlock;
 // (never folded in as 0*x: that would flip -0.0 sums and turn inf/nan inputs into nan).
 // FULL: every lane of the wave owns columns (d is a multiple of 64*VEC), so no lane predicates.
 // ------------------------------------------------------------------------------------------------
-template <typename T, int VEC, int U, bool FULL, typename IP>
+// SPAN: the row's entries end at row_end[row] instead of indptr[row + 1] (kEpiSpan below).
+template <typename T, int VEC, int U, bool FULL, typename IP, bool SPAN = false>
 __device__ __forceinline__ void row_gather(typename Vec<T, VEC>::type& acc,
                                            const IP* __restrict__ indptr,
                                            const int32_t* __restrict__ indices,
                                            const T* __restrict__ vals, int row,
-                                           const T* __restrict__ X, int64_t ldx, int col, bool act)
+                                           const T* __restrict__ X, int64_t ldx, int col, bool act,
+                                           const int64_t* __restrict__ row_end = nullptr)
 {
     typedef typename Vec<T, VEC>::type V;
     const int lane = threadIdx.x & 63;
     const int64_t beg = indptr[row];
-    const int64_t end = indptr[row + 1];
+    int64_t end;
+    if constexpr (SPAN)
+        end = row_end[row];
+    else
+        end = indptr[row + 1];
     if (beg >= end) return;
     // entries past the row end are clamped to its last entry (always a valid id; skipped below)
     int64_t j0 = beg + lane;
@@ -305,13 +311,28 @@ struct Epi {
     int cmode, ns;
     float a1, a2;
     ChebyCoef<float> cf;
+    // row spans (EX == kEpiSpan only): row r's entries are [indptr[r], row_end[r]) instead of
+    // [indptr[r], indptr[r + 1]) -- a column block of a CSR whose rows hold sorted column ids is a
+    // span of each row, so the block needs no copy of the ids and values (srg_spmm_span_f32)
+    const int64_t* row_end;
 };
 
 // Epilogue kinds (template parameter EX of the SpMM kernels).  Every call site sits under
 // `if constexpr`: a runtime branch cost the plain kernels ~20 %, and even an empty inlined call
 // (the reference-bound acc) changed the gather loop's schedule (+10 % per hop on products);
-// guarded, the kEpiPlain kernels are instruction-for-instruction the plain ones.
-constexpr int kEpiPlain = 0, kEpiSend = 1, kEpiCheby = 2;
+// guarded, the kEpiPlain kernels are instruction-for-instruction the plain ones.  kEpiSpan is the
+// plain epilogue (aggregation included) over row spans.
+constexpr int kEpiPlain = 0, kEpiSend = 1, kEpiCheby = 2, kEpiSpan = 3;
+
+// End of row `row`'s entries: the next row's start, or the span's end.
+template <int EX, typename IP>
+__device__ __forceinline__ int64_t row_stop(const IP* __restrict__ indptr, const Epi& e, int row)
+{
+    if constexpr (EX == kEpiSpan)
+        return e.row_end[row];
+    else
+        return (int64_t)indptr[row + 1];
+}
 
 template <int VEC>
 __device__ __forceinline__ void send_row(const Epi& e, int row, int col, const typename Vec<float, VEC>::type& v)
@@ -408,7 +429,7 @@ __device__ __forceinline__ void slice_wave(const IP* __restrict__ indptr,
     if constexpr (EX == kEpiCheby)
         if (cact) cheby_load<1>(epi, row, ccol, X, ldx, cop);
     const int64_t beg = indptr[row];
-    const int64_t end = indptr[row + 1];
+    const int64_t end = row_stop<EX>(indptr, epi, row);
     for (int64_t j = beg; j < end; j += 8 * UH) {
         V4 x[UH];
         float av[UH];
@@ -478,7 +499,7 @@ __device__ __forceinline__ void narrow_rows(const IP* __restrict__ indptr, const
     const int row = rv ? (order ? order[slot] : slot) : 0;
     const bool act = rv && c < d;
     const int64_t beg = rv ? (int64_t)indptr[row] : 0;
-    const int len = rv ? (int)((int64_t)indptr[row + 1] - beg) : 0;
+    const int len = rv ? (int)(row_stop<EX>(indptr, epi, row) - beg) : 0;
     int maxlen = len;
 #pragma unroll
     for (int off = S; off < 64; off <<= 1) {
@@ -545,7 +566,7 @@ __device__ __forceinline__ void packed_rows(const IP* __restrict__ indptr, const
     const bool rv = slot < n_rows;
     const int row = rv ? (order ? order[slot] : slot) : 0;
     const int64_t beg = rv ? (int64_t)indptr[row] : 0;
-    const int len = rv ? (int)((int64_t)indptr[row + 1] - beg) : 0;
+    const int len = rv ? (int)(row_stop<EX>(indptr, epi, row) - beg) : 0;
     int maxlen = len;
 #pragma unroll
     for (int off = S; off < 64; off <<= 1) {
@@ -667,7 +688,8 @@ k_spmm(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
         [[maybe_unused]] ChebyOps<VEC> cop;
         if constexpr (EX == kEpiCheby)
             if (FULL || act) cheby_load<VEC>(epi, row, col, X, ldx, cop);
-        row_gather<float, VEC, U, FULL, IP>(acc, indptr, indices, vals, row, X, ldx, col, act);
+        row_gather<float, VEC, U, FULL, IP, EX == kEpiSpan>(acc, indptr, indices, vals, row, X, ldx, col, act,
+                                                            epi.row_end);
         if (FULL || act) {
             if constexpr (EX == kEpiCheby) cheby_epi<VEC>(epi, row, col, acc, cop);
             vstore<float, VEC>(yrow + col, acc, nt != 0);
@@ -743,7 +765,7 @@ k_spmm_hub(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int lane = threadIdx.x & 63;
     const int64_t beg = indptr[row];
-    const int64_t end = indptr[row + 1];
+    const int64_t end = row_stop<EX>(indptr, epi, row);
     const int n_win = (int)((end - beg + W - 1) / W);
 
     if (wave == 0) {   // ---------------- consumer: 32 column chains ----------------
@@ -1224,6 +1246,31 @@ __global__ void k_validate(const int64_t* __restrict__ indptr, const int32_t* __
     if (b) atomicOr(bad, b);
 }
 
+// Column-block split points: splits[(b-1) * n_rows + r] = the first entry of row r whose column id
+// is >= ceil(b * n_cols / B) (a lower bound over the row's sorted ids), b = 1 .. B-1.  One thread per
+// (row, boundary).  For a row whose ids are not sorted the result is still a position in
+// [indptr[r], indptr[r+1]] and the split points of a row never decrease with b, so the spans still
+// partition the row in CSR order: the hop stays exact, only the blocks' locality is lost.
+__global__ void __launch_bounds__(256)
+k_col_splits(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices, int64_t n_rows,
+             int64_t n_cols, int n_blocks, int64_t* __restrict__ splits)
+{
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n_rows * (n_blocks - 1)) return;
+    const int b = (int)(t / n_rows) + 1;
+    const int64_t r = t % n_rows;
+    const int64_t bound = (b * n_cols + n_blocks - 1) / n_blocks;
+    int64_t lo = indptr[r], hi = indptr[r + 1];
+    while (lo < hi) {
+        const int64_t mid = lo + (hi - lo) / 2;
+        if ((int64_t)indices[mid] < bound)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    splits[t] = lo;
+}
+
 // ------------------------------------------------------------------------------------------------
 // launch helpers
 // ------------------------------------------------------------------------------------------------
@@ -1323,13 +1370,15 @@ int hub_attrs()
     for (const void* fn : {(const void*)k_spmm_hub<true, IP>, (const void*)k_spmm_hub<false, IP>,
                            (const void*)k_spmm_hub<true, IP, 0, kEpiSend>, (const void*)k_spmm_hub<false, IP, 0, kEpiSend>,
                            (const void*)k_spmm_hub<true, IP, 0, kEpiCheby>, (const void*)k_spmm_hub<false, IP, 0, kEpiCheby>,
+                           (const void*)k_spmm_hub<true, IP, 0, kEpiSpan>, (const void*)k_spmm_hub<false, IP, 0, kEpiSpan>,
                            (const void*)k_spmm_hub<true, IP, 1>, (const void*)k_spmm_hub<true, IP, 2>,
                            (const void*)k_spmm_hub<true, IP, 3>, (const void*)k_spmm_hub<true, IP, 4>,
                            (const void*)k_spmm_hub<true, IP, 5>, (const void*)k_spmm_hub<true, IP, 6>})
         SRG_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kHubLdsBytes));
     for (const void* fn : {(const void*)k_spmm_hub<true, IP, 0, false, 256>, (const void*)k_spmm_hub<false, IP, 0, false, 256>,
                            (const void*)k_spmm_hub<true, IP, 0, kEpiSend, 256>, (const void*)k_spmm_hub<false, IP, 0, kEpiSend, 256>,
-                           (const void*)k_spmm_hub<true, IP, 0, kEpiCheby, 256>, (const void*)k_spmm_hub<false, IP, 0, kEpiCheby, 256>})
+                           (const void*)k_spmm_hub<true, IP, 0, kEpiCheby, 256>, (const void*)k_spmm_hub<false, IP, 0, kEpiCheby, 256>,
+                           (const void*)k_spmm_hub<true, IP, 0, kEpiSpan, 256>, (const void*)k_spmm_hub<false, IP, 0, kEpiSpan, 256>})
         SRG_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)HubGeom<256>::LDS_BYTES));
     return SRG_OK;
 }
@@ -1776,6 +1825,28 @@ int srg_spmm_agg_f32(const int64_t* indptr, const int32_t* indices, const float*
     return rc ? rc : ok();
 }
 
+int srg_spmm_span_f32(const int64_t* row_beg, const int64_t* row_end, const int32_t* indices,
+                      const float* values, int64_t n_rows, const int32_t* row_order, int64_t n_hub,
+                      int64_t n_heavy, const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t d,
+                      uint32_t flags, float* agg, int64_t lda, float w, int agg_init, void* stream)
+{
+    SRG_DEVICE_GUARD(stream);
+    int rc = check_spmm_args(row_beg, indices, values, n_rows, X, ldx, Y, ldy, d);
+    if (rc) return rc;
+    if (n_rows > 0 && d > 0 && !row_end) return fail(SRG_ERR_INVALID, "null row_end");
+    if (agg && (lda < d || agg == Y))
+        return fail(SRG_ERR_INVALID, "aggregation panel: lda=%lld < d=%d or agg aliases Y", (long long)lda, d);
+    Epi e{};
+    e.agg = agg;
+    e.lda = lda;
+    e.w = w;
+    e.init = agg_init ? 1 : 0;
+    e.row_end = row_end;
+    rc = launch_spmm<int64_t, kEpiSpan>(row_beg, indices, values, n_rows, row_order, n_hub, n_heavy, X, ldx, Y, ldy,
+                                        d, flags, static_cast<hipStream_t>(stream), e);
+    return rc ? rc : ok();
+}
+
 int srg_spmm_send_f32(const int64_t* indptr, const int32_t* indices, const float* values,
                       int64_t n_rows, const int32_t* row_order, int64_t n_hub, int64_t n_heavy,
                       const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t d, uint32_t flags,
@@ -2082,6 +2153,22 @@ int srg_csr_validate(const int64_t* indptr, const int32_t* indices, int64_t n_ro
     if (bad & 2u) return fail(SRG_ERR_INVALID, "indptr decreases");
     if (bad & 4u) return fail(SRG_ERR_INVALID, "indptr[0] != 0");
     if (bad & 8u) return fail(SRG_ERR_INVALID, "indptr[n_rows] != nnz=%lld", (long long)nnz);
+    return ok();
+}
+
+int srg_csr_col_splits(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t n_cols,
+                       int32_t n_blocks, int64_t* splits, void* stream)
+{
+    SRG_DEVICE_GUARD(stream);
+    if (n_rows < 0 || n_cols < 0) return fail(SRG_ERR_INVALID, "negative size");
+    if (n_blocks < 2 || n_blocks > 64) return fail(SRG_ERR_INVALID, "n_blocks=%d not in [2, 64]", n_blocks);
+    const int64_t work = n_rows * (n_blocks - 1);
+    if (work == 0) return ok();
+    if (!indptr || !splits) return fail(SRG_ERR_INVALID, "null indptr or splits");
+    if ((work + 255) / 256 > INT32_MAX) return fail(SRG_ERR_INVALID, "grid too large");
+    hipLaunchKernelGGL(k_col_splits, dim3((unsigned)((work + 255) / 256)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), indptr, indices, n_rows, n_cols, (int)n_blocks, splits);
+    SRG_HIP_CHECK(hipGetLastError());
     return ok();
 }
 

@@ -48,6 +48,7 @@ EXPORTED_SYMBOLS = (
     "srg_cheby_epilogue_f32",
     "srg_hop_accumulate_f32",
     "srg_spmm_agg_f32",
+    "srg_spmm_span_f32",
     "srg_spmm_send_f32",
     "srg_spmm_cheby_f32",
     "srg_tail_record_f32",
@@ -57,6 +58,7 @@ EXPORTED_SYMBOLS = (
     "srg_spmm_csr_f64",
     "srg_gather_rows_f32",
     "srg_hub_join",
+    "srg_csr_col_splits",
     "srg_csr_validate",
     "srg_comm_unique_id",
     "srg_comm_init_rank",
@@ -103,6 +105,11 @@ def _declare(lib):
     lib.srg_spmm_agg_f32.argtypes = [_p, _p, _p, _i64, _p, _i64, _i64, _p, _i64, _p, _i64, _i32, ctypes.c_uint32,
                                      _p, _i64, _f32, ctypes.c_int, _p]
     lib.srg_spmm_agg_f32.restype = ctypes.c_int
+    lib.srg_spmm_span_f32.argtypes = [_p, _p, _p, _p, _i64, _p, _i64, _i64, _p, _i64, _p, _i64, _i32,
+                                      ctypes.c_uint32, _p, _i64, _f32, ctypes.c_int, _p]
+    lib.srg_spmm_span_f32.restype = ctypes.c_int
+    lib.srg_csr_col_splits.argtypes = [_p, _p, _i64, _i64, _i32, _p, _p]
+    lib.srg_csr_col_splits.restype = ctypes.c_int
     lib.srg_spmm_send_f32.argtypes = [_p, _p, _p, _i64, _p, _i64, _i64, _p, _i64, _p, _i64, _i32, ctypes.c_uint32,
                                       _p, _i64, _p, _p, _p]
     lib.srg_spmm_send_f32.restype = ctypes.c_int

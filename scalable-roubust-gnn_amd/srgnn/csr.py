@@ -89,6 +89,9 @@ class DeviceCSR:
     n_heavy: int
     n_hub: int = 0
     n_heavy_narrow: int | None = None    # slice-wave rows for d <= 32 (None: n_heavy)
+    # row spans (a column block, column_blocks()): row r's entries are [indptr[r], row_end[r]) of
+    # indices / values, and indptr holds n_rows starts instead of n_rows + 1 pointers
+    row_end: torch.Tensor | None = None
     _blocks: dict = field(default_factory=dict, repr=False, compare=False)   # column_blocks() cache
 
     def heavy(self, d: int) -> int:
@@ -98,7 +101,14 @@ class DeviceCSR:
 
     @property
     def nnz(self) -> int:
+        if self.row_end is not None:
+            return int((self.row_end - self.indptr).sum().item()) if self.n_rows else 0
         return int(self.indices.numel())
+
+    @property
+    def is_span(self) -> bool:
+        """A column block: rows are spans of a shared CSR (srg_spmm_span_f32)."""
+        return self.row_end is not None
 
     @property
     def device(self):
@@ -140,51 +150,47 @@ class DeviceCSR:
                                 n_cols=adj.shape[1], heavy_threshold=heavy_threshold, device=device)
 
     def column_blocks(self, B: int):
-        """B operators over the same rows: block b holds each row's entries whose column ids lie in
-        [b * n_cols // B, (b + 1) * n_cols // B), in their stored order (each with its own
-        schedule), or None when some row's entries are not in block order.
+        """B operators over the same rows: block b holds, as a span of each row, the row's entries
+        whose column ids lie in [ceil(b * n_cols / B), ceil((b + 1) * n_cols / B)), each block with
+        its own schedule (or None for an empty operator or B < 2).
 
         A hop is then block 0 from +0.0f and blocks 1..B-1 with ACCUMULATE: each output element is
         the same fma chain over the same entries in the same order, continued from the fp32 value
         the previous block stored, so the result is bitwise the one-launch hop.  Â from
-        construct_adj has sorted column ids (utils.py:81-93 builds a canonical transpose); a CSR
-        with unsorted rows may not be cut (None).  Cached per B."""
+        construct_adj has sorted column ids (utils.py:81-93 builds a canonical transpose), so a
+        block is one span of every row: the blocks share indices / values and hold only their
+        split points (srg_csr_col_splits, one binary search per row and boundary; an n_rows int64
+        array per boundary).  Rows with unsorted ids still split into spans that partition them in
+        CSR order -- exact, only without the locality.  Cached per B."""
         B = int(B)
         if B in self._blocks:
             return self._blocks[B]
+        if self.is_span:
+            raise ValueError("column_blocks of a column block")
         if B < 2 or self.n_rows == 0 or self.nnz == 0:
             self._blocks[B] = None
             return None
-        ip, ix, n = self.indptr, self.indices, self.n_cols
-        row = torch.repeat_interleave(torch.arange(self.n_rows, device=ip.device, dtype=torch.int32),
-                                      ip[1:] - ip[:-1])
-        # block ids in int32 arithmetic where it cannot overflow (billion-entry CSRs: no int64 copy)
-        wide = ix.to(torch.int64) if n * B >= 2 ** 31 else ix
-        blk = torch.div(wide * B, n, rounding_mode="floor").to(torch.int8)
-        del wide
-        same_row = row[1:] == row[:-1]
-        if bool(((blk[1:] < blk[:-1]) & same_row).any()):
-            self._blocks[B] = None
-            return None
-        del same_row
+        ip, n = self.indptr, self.n_cols
+        dev = ip.device
+        splits = torch.empty((B - 1, self.n_rows), dtype=torch.int64, device=dev)
+        _lib.call(dev, "srg_csr_col_splits", ip.data_ptr(), self.indices.data_ptr(), self.n_rows, n, B,
+                  splits.data_ptr(), _lib.stream(dev))
+        bounds = [ip[:-1]] + [splits[b] for b in range(B - 1)] + [ip[1:]]
         out = []
         for b in range(B):
-            m = blk == b
-            cnt = torch.zeros(self.n_rows, dtype=torch.int64, device=ip.device)
-            for c0 in range(0, m.numel(), _CHUNK):
-                cnt += torch.bincount(row[c0:c0 + _CHUNK][m[c0:c0 + _CHUNK]].to(torch.int64), minlength=self.n_rows)
-            bip = torch.zeros(self.n_rows + 1, dtype=torch.int64, device=ip.device)
-            torch.cumsum(cnt, 0, out=bip[1:])
-            del cnt
-            order, n_heavy, n_hub = make_schedule(bip)
-            out.append(DeviceCSR(bip, _masked(ix, m), _masked(self.values, m), self.n_rows, n, order,
-                                 n_heavy, n_hub, narrow_heavy(bip, n_hub)))
-            del m
+            beg, end = bounds[b], bounds[b + 1]
+            deg = end - beg
+            nnz_b = int(deg.sum().item())
+            order, n_heavy, n_hub = schedule_from_degrees(deg, nnz_b)
+            out.append(DeviceCSR(beg, self.indices, self.values, self.n_rows, n, order, n_heavy, n_hub,
+                                 narrow_heavy_degrees(deg, n_hub), row_end=end))
         self._blocks[B] = out
         return out
 
     def rows(self, r0: int, r1: int, heavy_threshold=None, hub_threshold=None) -> "DeviceCSR":
         """Row block [r0, r1) with rebased row pointers (global column ids kept)."""
+        if self.is_span:
+            raise ValueError("rows() of a column block")
         ip = self.indptr[r0:r1 + 1]
         base = int(ip[0].item())
         end = int(ip[-1].item())
@@ -195,17 +201,6 @@ class DeviceCSR:
                          narrow_heavy(ip, n_hub) if _auto_heavy(heavy_threshold) else None)
 
 
-# boolean selections and bincounts go in chunks: past ~2^31 entries torch's nonzero overflows
-_CHUNK = 1 << 28
-
-
-def _masked(t: torch.Tensor, m: torch.Tensor) -> torch.Tensor:
-    """t[m] for 1-D t and mask m of any length (chunked)."""
-    if t.numel() <= _CHUNK:
-        return t[m].contiguous()
-    return torch.cat([t[c0:c0 + _CHUNK][m[c0:c0 + _CHUNK]] for c0 in range(0, t.numel(), _CHUNK)])
-
-
 def _auto_heavy(heavy_threshold) -> bool:
     return heavy_threshold is None and DEFAULT_HEAVY_THRESHOLD is None
 
@@ -213,8 +208,12 @@ def _auto_heavy(heavy_threshold) -> bool:
 def narrow_heavy(indptr: torch.Tensor, n_hub: int, threshold: int | None = None) -> int:
     """Slice-wave rows of the schedule for narrow panels: rows longer than NARROW_HEAVY_THRESHOLD,
     hubs excluded (they lead the same decreasing-length order)."""
+    return narrow_heavy_degrees(indptr[1:] - indptr[:-1], n_hub, threshold)
+
+
+def narrow_heavy_degrees(deg: torch.Tensor, n_hub: int, threshold: int | None = None) -> int:
+    """narrow_heavy from the row lengths."""
     t = NARROW_HEAVY_THRESHOLD if threshold is None else threshold
-    deg = indptr[1:] - indptr[:-1]
     return max(0, int((deg > t).sum().item()) - int(n_hub)) if deg.numel() else 0
 
 
@@ -222,18 +221,23 @@ def make_schedule(indptr: torch.Tensor, heavy_threshold=None, hub_threshold=None
     """(order int32, n_heavy, n_hub) for a CSR with row pointers `indptr`: rows sorted by
     decreasing length; the first n_hub have more than hub_threshold nonzeros, the next n_heavy
     more than heavy_threshold.  A negative threshold disables that group."""
+    return schedule_from_degrees(indptr[1:] - indptr[:-1], int(indptr[-1]) if indptr.numel() else 0,
+                                 heavy_threshold, hub_threshold)
+
+
+def schedule_from_degrees(deg: torch.Tensor, nnz: int, heavy_threshold=None, hub_threshold=None):
+    """make_schedule from the row lengths `deg` (nnz = their sum, for the automatic thresholds)."""
     if heavy_threshold is None:
         heavy_threshold = DEFAULT_HEAVY_THRESHOLD
     if heavy_threshold is None:
-        heavy_threshold = auto_heavy_threshold(int(indptr[-1]) if indptr.numel() else 0)
+        heavy_threshold = auto_heavy_threshold(nnz)
     if hub_threshold is None:
         hub_threshold = DEFAULT_HUB_THRESHOLD
     if hub_threshold is None:
-        hub_threshold = auto_hub_threshold(int(indptr[-1]) if indptr.numel() else 0)
-    deg = indptr[1:] - indptr[:-1]
+        hub_threshold = auto_hub_threshold(nnz)
     n = int(deg.numel())
     if n == 0:
-        return torch.zeros(0, dtype=torch.int32, device=indptr.device), 0, 0
+        return torch.zeros(0, dtype=torch.int32, device=deg.device), 0, 0
     order = torch.sort(deg, descending=True, stable=True).indices.to(torch.int32)
     n_hub = int((deg > hub_threshold).sum().item()) if hub_threshold >= 0 else 0
     n_big = int((deg > heavy_threshold).sum().item()) if heavy_threshold >= 0 else 0

@@ -28,10 +28,11 @@ _COL_BLOCKS_ENV = os.environ.get("SRGNN_COL_BLOCKS", "auto")
 _U2_BLOCKED = os.environ.get("SRGNN_BLOCK_U2", "1") != "0"
 
 
-# Cutting an operator costs about as much as 50 hops gain (products: 21 ms against 0.39 ms per hop,
-# tools/probes/colblock_build_time.py): it is cut for a run of at least this many hops, or when
-# its blocks already exist (a reused operator: bench.py cuts once up front).
-MIN_HOPS_TO_CUT = 48
+# Cutting an operator into column blocks (row spans: one binary search per row and boundary, plus
+# each block's schedule) costs about 3 hops' gain (products: 1.1 ms against 0.42 ms per hop,
+# tools/probes/colblock_build_time.py; 21 ms when the blocks were copies of the ids and values):
+# it is cut for a run of at least this many hops, or when its blocks already exist.
+MIN_HOPS_TO_CUT = 4
 
 
 def auto_col_blocks(A: DeviceCSR, d: int, hops: int | None = None) -> int:
@@ -104,10 +105,26 @@ def spmm(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor | None = None, accumul
     flags = (_lib.SRG_SPMM_ACCUMULATE if accumulate else 0) | (_lib.SRG_SPMM_NT_STORE if nt_store else 0) | \
         (_lib.SRG_SPMM_WIDE_ROWS if wide_rows else 0) | (_lib.SRG_SPMM_HUB_W256 if hub_w256 else 0) | \
         (_lib.SRG_SPMM_HUB_NOJOIN if hub_nojoin else 0) | (_lib.SRG_SPMM_PACKED_U2 if packed_u2 else 0)
+    if A.is_span:
+        _span_call(A, X, out, d, flags, None, 0, 0.0, False)
+        return out
     _lib.call(X.device, "srg_spmm_csr_f32", A.indptr.data_ptr(), A.indices.data_ptr(), A.values.data_ptr(),
               A.n_rows, A.order.data_ptr() if A.n_rows else None, A.n_hub, A.heavy(d), X.data_ptr(),
               X.stride(0), out.data_ptr(), out.stride(0), d, flags, _stream(X.device))
     return out
+
+
+def _span_call(A: DeviceCSR, X, out, d, flags, agg, lda, w, init):
+    """A column block (row spans of a shared CSR): srg_spmm_span_f32, plain or aggregating."""
+    _lib.call(X.device, "srg_spmm_span_f32", A.indptr.data_ptr(), A.row_end.data_ptr(), A.indices.data_ptr(),
+              A.values.data_ptr(), A.n_rows, A.order.data_ptr() if A.n_rows else None, A.n_hub, A.heavy(d),
+              X.data_ptr(), X.stride(0), out.data_ptr(), out.stride(0), d, flags,
+              agg.data_ptr() if agg is not None else None, lda, float(w), 1 if init else 0, _stream(X.device))
+
+
+def _no_spans(A: DeviceCSR, what: str):
+    if A.is_span:
+        raise ValueError(f"{what} takes a whole operator, not a column block")
 
 
 def spmm_agg(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, agg: torch.Tensor, w: float, init: bool,
@@ -123,6 +140,9 @@ def spmm_agg(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, agg: torch.Tensor
         raise ValueError("A, X, out and agg must be on the same device")
     flags = (_lib.SRG_SPMM_NT_STORE if nt_store else 0) | (_lib.SRG_SPMM_ACCUMULATE if accumulate else 0) | \
         (_lib.SRG_SPMM_PACKED_U2 if packed_u2 else 0)
+    if A.is_span:
+        _span_call(A, X, out, d, flags, agg, agg.stride(0), w, init)
+        return out
     _lib.call(X.device, "srg_spmm_agg_f32", A.indptr.data_ptr(), A.indices.data_ptr(), A.values.data_ptr(),
               A.n_rows, A.order.data_ptr() if A.n_rows else None, A.n_hub, A.heavy(d), X.data_ptr(),
               X.stride(0), out.data_ptr(), out.stride(0), d, flags, agg.data_ptr(), agg.stride(0),
@@ -135,6 +155,7 @@ def spmm_send(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, send: torch.Tens
     """out = A @ X and, fused into the same kernels' epilogue, send[send_slot[send_ptr[r]:send_ptr[r+1]]]
     = out[r] for every row r of A (srg_spmm_send_f32: the halo pack of srgnn.dist, bitwise the rows
     of out).  send_ptr is indexed by the row ids A's schedule names (A may be a row-group view)."""
+    _no_spans(A, "spmm_send")
     _check_panel(X, A.n_cols, "X")
     d = X.shape[1]
     _check_panel(out, A.n_rows, "out", d)
@@ -163,6 +184,7 @@ def spmm_cheby(A: DeviceCSR, Tc: torch.Tensor, out: torch.Tensor, mode: int, a1:
     -- srg_spmm_csr_f32 followed by srg_cheby_epilogue_f32, bit for bit.  `out` may be `To` itself
     (each element of To is read by its owner before it is overwritten).  R: [n_scales, rows, d],
     strided views allowed (row-major rows)."""
+    _no_spans(A, "spmm_cheby")
     _check_panel(Tc, A.n_cols, "Tc")
     d = Tc.shape[1]
     _check_panel(out, A.n_rows, "out", d)
@@ -211,6 +233,7 @@ def propagate(A: DeviceCSR, X: torch.Tensor, K: int, panels: list | None = None,
     Device-resident form of GraphOp.propagate's hop loop (SSRG/operators/base_operator.py:32-35):
     the K hops run back to back on the GPU with no host round trips (srg_propagate_khop_f32, or
     hop() per hop when the hops are column-blocked)."""
+    _no_spans(A, "propagate")
     if A.n_rows != A.n_cols:
         raise ValueError("propagate needs a square operator")
     _check_panel(X, A.n_rows, "X")

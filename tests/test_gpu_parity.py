@@ -195,19 +195,51 @@ def test_propagate_column_blocked_bit_exact(name, B):
 
 
 @pytest.mark.parametrize("name", G.names("raw"))
-def test_column_blocks_refused_for_unordered_rows(name):
-    """A CSR whose rows are not in column-block order cannot be cut (the chain order would change):
-    column_blocks returns None and the hop runs as one launch, still bit-exact."""
+def test_column_blocks_exact_for_unordered_rows(name):
+    """Column blocks are spans of each row (srg_csr_col_splits: one binary search per row and
+    boundary), and the split points of any row -- sorted or not -- lie in the row and never
+    decrease, so the spans partition it in CSR order: the blocked hop is the one-launch hop bit
+    for bit even where the ids are unsorted (those rows only lose the blocks' locality)."""
     from srgnn.csr import DeviceCSR
     from srgnn.spmm import hop
     c = G.Case(name)
     a = c.adj()
     ip, ix = np.asarray(a.indptr), np.asarray(a.indices)
     A = DeviceCSR.from_tensors(ip, ix, a.data.astype(np.float32), n_cols=c.n, device="cuda")
-    blk_sorted = all(np.all(np.diff((ix[ip[i]:ip[i + 1]].astype(np.int64) * 2) // c.n) >= 0) for i in range(c.n))
-    assert (A.column_blocks(2) is not None) == blk_sorted
-    Y = hop(A, torch.from_numpy(c.x()).cuda(), torch.empty((c.n, c.x().shape[1]), device="cuda"), col_blocks=2)
-    c.check_hop(1, Y.cpu().numpy())
+    X = torch.from_numpy(c.x()).cuda()
+    want = hop(A, X, torch.empty((c.n, X.shape[1]), device="cuda"), col_blocks=1).cpu().numpy()
+    for B in (2, 3):
+        blocks = A.column_blocks(B)
+        assert blocks is not None and sum(b.nnz for b in blocks) == A.nnz
+        Y = hop(A, X, torch.empty((c.n, X.shape[1]), device="cuda"), col_blocks=B)
+        np.testing.assert_array_equal(Y.cpu().numpy(), want)
+    c.check_hop(1, want)
+
+
+def test_column_block_spans_are_lower_bounds():
+    """srg_csr_col_splits on a host-checkable CSR: for sorted rows each split is the first entry
+    whose id reaches ceil(b n / B); every split lies in its row and is monotone in b (any row)."""
+    from srgnn.csr import DeviceCSR
+    rng = np.random.default_rng(5)
+    n, deg = 997, rng.integers(0, 40, 997)
+    deg[3], deg[10] = 3000, 0
+    ip = np.concatenate([[0], np.cumsum(deg)]).astype(np.int64)
+    ix = np.concatenate([np.sort(rng.integers(0, n, k)) for k in deg]).astype(np.int32)
+    shuffled = ix.copy()
+    shuffled[ip[5]:ip[6]] = shuffled[ip[5]:ip[6]][::-1]
+    for ids, sorted_rows in ((ix, True), (shuffled, False)):
+        A = DeviceCSR.from_tensors(ip, ids, np.ones(ids.size, np.float32), n_cols=n, device="cuda")
+        for B in (2, 3, 7):
+            blocks = A.column_blocks(B)
+            starts = [b.indptr.cpu().numpy() for b in blocks] + [blocks[-1].row_end.cpu().numpy()]
+            assert np.array_equal(starts[0], ip[:-1]) and np.array_equal(starts[-1], ip[1:])
+            for b in range(1, B):
+                assert np.all(starts[b] >= starts[b - 1])
+                assert np.array_equal(blocks[b - 1].row_end.cpu().numpy(), starts[b])
+                if sorted_rows:
+                    bound = -(-b * n // B)
+                    want = np.array([ip[r] + np.searchsorted(ids[ip[r]:ip[r + 1]], bound) for r in range(n)])
+                    assert np.array_equal(starts[b], want)
 
 
 def test_strided_panels_and_row_blocks(oracle_mod):
