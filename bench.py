@@ -390,7 +390,7 @@ def main():
         init_pg()
 
     from srgnn.csr import DeviceCSR
-    from srgnn.spmm import auto_col_blocks, hop, propagate, spmm
+    from srgnn.spmm import auto_col_blocks, column_blocks_for, hop, propagate, spmm
 
     t_build = time.perf_counter()
     ip, ix, vals, n, d, K = graphs.build(a.config, dev, d=a.d)
@@ -411,7 +411,7 @@ def main():
             log(f"mode {mode}: {K} panels need {K * n * d * 4 / 1e9:.1f} GB, {free / 1e9:.1f} GB free")
         # the operator serves every warm-up and timed step: cut it once here when that amortises
         col_blocks = a.col_blocks if a.col_blocks is not None else auto_col_blocks(A, d, hops=K * (a.steps + a.warmup))
-        if col_blocks > 1 and not A.column_blocks(col_blocks):
+        if col_blocks > 1 and not column_blocks_for(A, col_blocks, hops=K * (a.steps + a.warmup)):
             col_blocks = 1
         log(f"schedule: n_hub={A.n_hub} n_heavy={A.n_heavy} column blocks per hop={col_blocks}")
         if a.aggregate:

@@ -33,6 +33,19 @@ _U2_BLOCKED = os.environ.get("SRGNN_BLOCK_U2", "1") != "0"
 # tools/probes/colblock_build_time.py; 21 ms when the blocks were copies of the ids and values):
 # it is cut for a run of at least this many hops, or when its blocks already exist.
 MIN_HOPS_TO_CUT = 4
+# Runs of this many hops copy the blocks' spans into compact arrays (DeviceCSR.compact_column_blocks:
+# 1 % less traffic per hop for one more copy of the ids and values, ~3 ms on products), when the
+# copy fits in a quarter of the free memory.
+MIN_HOPS_TO_COMPACT = 48
+
+
+def column_blocks_for(A: DeviceCSR, B: int, hops: int | None = None):
+    """A's column blocks for a run of `hops` hops: spans, or compact copies for long runs."""
+    if hops is not None and hops >= MIN_HOPS_TO_COMPACT and not A.is_span:
+        free, _ = torch.cuda.mem_get_info(A.device)
+        if A.nnz * (A.indices.element_size() + A.values.element_size()) <= free // 4:
+            return A.compact_column_blocks(B)
+    return A.column_blocks(B)
 
 
 def auto_col_blocks(A: DeviceCSR, d: int, hops: int | None = None) -> int:
@@ -254,7 +267,7 @@ def propagate(A: DeviceCSR, X: torch.Tensor, K: int, panels: list | None = None,
         if p.stride(0) != ld:
             raise ValueError("all panels must share one leading dimension")
     B = auto_col_blocks(A, d, hops=K) if col_blocks is None else int(col_blocks)
-    if K > 0 and B > 1 and A.column_blocks(B):
+    if K > 0 and B > 1 and column_blocks_for(A, B, hops=K):
         for k in range(1, K + 1):
             hop(A, panels[k - 1], panels[k], nt_store=nt_store, col_blocks=B)
     else:

@@ -235,12 +235,12 @@ class HeatWaveletFilter:
     def prepare_column_blocks(self, width: int, hops: int) -> int:
         """Cut L and F into column blocks (spmm.hop) when `hops` SpMMs over panels `width` columns
         wide amortise it (spmm.auto_col_blocks); returns the blocks per SpMM."""
-        from .spmm import auto_col_blocks
+        from .spmm import auto_col_blocks, column_blocks_for
         B = 1
         for vals in (self.lvals, self.fvals):
             A = self._csr(vals)
             B = auto_col_blocks(A, width, hops=hops)
-            if B > 1 and not A.column_blocks(B):
+            if B > 1 and not column_blocks_for(A, B, hops=hops):
                 B = 1
         return B
 

@@ -175,16 +175,19 @@ def test_column_blocked_chain_continuation(name, thr):
         c.check_hop(1, Y.cpu().numpy())
 
 
+@pytest.mark.parametrize("compact", [False, True])
 @pytest.mark.parametrize("B", [2, 3, 5])
 @pytest.mark.parametrize("name", G.names("norm"))
-def test_propagate_column_blocked_bit_exact(name, B):
-    """The product path's column-blocked hops (DeviceCSR.column_blocks + propagate(col_blocks=B):
-    B launches per hop, each block with its own schedule) == the reference's hops, bit for bit."""
+def test_propagate_column_blocked_bit_exact(name, B, compact):
+    """The product path's column-blocked hops (DeviceCSR.column_blocks -- row spans of the shared
+    arrays -- or compact_column_blocks -- the spans copied out -- + propagate(col_blocks=B): B
+    launches per hop, each block with its own schedule) == the reference's hops, bit for bit."""
     from srgnn.spmm import hop, propagate
     c = G.Case(name)
     A = _csr(c, (None, None))
-    blocks = A.column_blocks(B)
+    blocks = A.compact_column_blocks(B) if compact else A.column_blocks(B)
     assert blocks is not None and len(blocks) == B and sum(b.nnz for b in blocks) == A.nnz
+    assert all(b.is_span != compact for b in blocks)
     X = torch.from_numpy(c.x()).cuda()
     hops = propagate(A, X, c.k, col_blocks=B)
     torch.cuda.synchronize()
