@@ -202,3 +202,48 @@ def test_degenerate_inputs():
     assert e[0].tolist() == [0] * 6 and e[1].numel() == 0
     ip, ix, v = C.sym_norm(*(t.cpu().numpy() for t in e), 5, 0.5, device="cuda")
     assert ip.tolist() == list(range(6)) and torch.equal(v.cpu(), torch.ones(5, dtype=torch.float64))
+
+
+@pytest.mark.parametrize("thr", [(-1, -1), (0, -1), (0, 0), (None, None), (4, 64)])
+@pytest.mark.parametrize("d", [1, 7, 64, 128, 130, 256])
+def test_span_blocks_every_path(thr, d):
+    """Column blocks as row spans (srg_spmm_span_f32) through every worker kind the thresholds
+    select -- hub workgroups (0, 0), slice waves, packed / narrow / whole light rows -- plain and
+    with the aggregation epilogue in the last block: bitwise the one-launch srg_spmm_csr_f32 and
+    srg_spmm_agg_f32.  The spans come from srg_csr_col_splits on a CSR with sorted rows."""
+    from srgnn.csr import DeviceCSR, narrow_heavy_degrees, schedule_from_degrees
+    from srgnn.spmm import spmm, spmm_agg
+    n = 3000
+    ip, ix = synth_graph(n)
+    vals = torch.from_numpy(np.random.default_rng(d).random(ix.numel()).astype(np.float32))
+    A = DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, heavy_threshold=thr[0], hub_threshold=thr[1], device="cuda")
+    X = torch.from_numpy(np.random.default_rng(1).standard_normal((n, d)).astype(np.float32)).cuda()
+    prev = torch.from_numpy(np.random.default_rng(2).standard_normal((n, d)).astype(np.float32)).cuda()
+    y_ref = spmm(A, X)
+    agg_ref = prev.clone()
+    spmm_agg(A, X, torch.empty_like(y_ref), agg_ref, 0.37, False)
+    for B in (2, 3):
+        spans = A.column_blocks(B)
+        blocks = []
+        for s in spans:        # the same spans, scheduled with the test's thresholds
+            deg = s.row_end - s.indptr
+            order, n_heavy, n_hub = schedule_from_degrees(deg, int(deg.sum()), thr[0], thr[1])
+            blocks.append(DeviceCSR(s.indptr, s.indices, s.values, n, n, order, n_heavy, n_hub,
+                                    narrow_heavy_degrees(deg, n_hub) if thr == (None, None) else None,
+                                    row_end=s.row_end))
+        if thr == (0, 0):
+            assert any(b.n_hub > 0 for b in blocks)
+        y = torch.empty_like(y_ref)
+        agg = prev.clone()
+        for b, Ab in enumerate(blocks):
+            if b == B - 1:
+                spmm_agg(Ab, X, y, agg, 0.37, False, accumulate=True)
+            else:
+                spmm(Ab, X, out=y, accumulate=b > 0)
+        assert torch.equal(y, y_ref) and torch.equal(agg, agg_ref)
+
+
+def synth_graph(n):
+    from srgnn import synth
+    u, v = synth.rmat_undirected_t(n, 30000, seed=3)
+    return synth.symmetric_csr_t(n, u, v)
