@@ -20,7 +20,7 @@ import torch  # noqa: E402
 
 from srgnn import graphs, roofline, synth  # noqa: E402
 from srgnn.csr import DeviceCSR  # noqa: E402
-from srgnn.spmm import auto_col_blocks, hop  # noqa: E402
+from srgnn.spmm import auto_col_blocks, column_blocks_for, hop  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="products")
@@ -42,7 +42,7 @@ X = synth.uniform_features_t(n, d, device=dev)
 Y = torch.empty_like(X)
 # the probe stands for a long run of hops (bench.py's operator serves every step): the panel rule alone
 B = 1 if a.identity else (a.col_blocks if a.col_blocks is not None else auto_col_blocks(A, d, hops=1 << 30))
-B = B if B > 1 and A.column_blocks(B) else 1
+B = B if B > 1 and column_blocks_for(A, B, hops=1 << 30) else 1   # compact blocks, as bench.py
 torch.cuda.synchronize()
 for _ in range(a.reps):
     hop(A, X, Y, col_blocks=B)      # one hop = B k_spmm launches (column blocks), same bits
