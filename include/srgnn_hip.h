@@ -267,6 +267,14 @@ int srg_hub_join(void* stream);
 int srg_csr_col_splits(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t n_cols,
                        int32_t n_blocks, int64_t* splits, void* stream);
 
+/* Mirror positions (device construct_adj, srgnn/construct.py; SSRG/operators/utils.py:91 transposes
+ * A+I): for a CSR whose rows hold strictly increasing column ids, mirror[e] = the position of entry
+ * (c, r) in row c for entry e = (r, c) (rows[e] = r, int64 [nnz]), or -1 when row c has no column r.
+ * Every entry found <=> the structure is symmetric, and the transpose is then the same structure
+ * with values[mirror].  Asynchronous on `stream`. */
+int srg_csr_mirror(const int64_t* indptr, const int32_t* indices, const int64_t* rows, int64_t n_rows,
+                   int64_t nnz, int64_t* mirror, void* stream);
+
 /* Checks a device CSR: indptr[0] == 0, indptr non-decreasing, indptr[n_rows] == nnz, and every
  * column id in [0, n_cols).  Synchronous on `stream`.  Returns SRG_OK or SRG_ERR_INVALID. */
 int srg_csr_validate(const int64_t* indptr, const int32_t* indices, int64_t n_rows,

@@ -1317,6 +1317,30 @@ k_col_splits(const int64_t* __restrict__ indptr, const int32_t* __restrict__ ind
     splits[t] = lo;
 }
 
+// Mirror positions of a CSR with sorted rows: mirror[e] = the position of entry (c, r) in row c for
+// entry e = (r, c), or -1 when row c holds no column r (one binary search per entry).  All entries
+// found <=> the structure is symmetric, and then the transpose of the matrix is the same structure
+// with values[mirror] -- construct_adj's (A+I)^T without a sort (srgnn/construct.py).
+__global__ void __launch_bounds__(256)
+k_csr_mirror(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
+             const int64_t* __restrict__ rows, int64_t nnz, int64_t* __restrict__ mirror)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nnz; e += stride) {
+        const int64_t r = rows[e];
+        const int32_t c = indices[e];
+        int64_t lo = indptr[c], hi = indptr[c + 1];
+        while (lo < hi) {
+            const int64_t mid = lo + (hi - lo) / 2;
+            if ((int64_t)indices[mid] < r)
+                lo = mid + 1;
+            else
+                hi = mid;
+        }
+        mirror[e] = (lo < indptr[c + 1] && (int64_t)indices[lo] == r) ? lo : -1;
+    }
+}
+
 // ------------------------------------------------------------------------------------------------
 // launch helpers
 // ------------------------------------------------------------------------------------------------
@@ -2214,6 +2238,20 @@ int srg_csr_col_splits(const int64_t* indptr, const int32_t* indices, int64_t n_
     if ((work + 255) / 256 > INT32_MAX) return fail(SRG_ERR_INVALID, "grid too large");
     hipLaunchKernelGGL(k_col_splits, dim3((unsigned)((work + 255) / 256)), dim3(256), 0,
                        static_cast<hipStream_t>(stream), indptr, indices, n_rows, n_cols, (int)n_blocks, splits);
+    SRG_HIP_CHECK(hipGetLastError());
+    return ok();
+}
+
+int srg_csr_mirror(const int64_t* indptr, const int32_t* indices, const int64_t* rows, int64_t n_rows,
+                   int64_t nnz, int64_t* mirror, void* stream)
+{
+    SRG_DEVICE_GUARD(stream);
+    if (n_rows < 0 || nnz < 0) return fail(SRG_ERR_INVALID, "negative size");
+    if (nnz == 0) return ok();
+    if (!indptr || !indices || !rows || !mirror) return fail(SRG_ERR_INVALID, "null pointer");
+    const unsigned blocks = (unsigned)std::min<int64_t>((nnz + 255) / 256, 1 << 20);
+    hipLaunchKernelGGL(k_csr_mirror, dim3(blocks), dim3(256), 0, static_cast<hipStream_t>(stream), indptr, indices,
+                       rows, nnz, mirror);
     SRG_HIP_CHECK(hipGetLastError());
     return ok();
 }

@@ -59,6 +59,7 @@ EXPORTED_SYMBOLS = (
     "srg_gather_rows_f32",
     "srg_hub_join",
     "srg_csr_col_splits",
+    "srg_csr_mirror",
     "srg_csr_validate",
     "srg_comm_unique_id",
     "srg_comm_init_rank",
@@ -110,6 +111,8 @@ def _declare(lib):
     lib.srg_spmm_span_f32.restype = ctypes.c_int
     lib.srg_csr_col_splits.argtypes = [_p, _p, _i64, _i64, _i32, _p, _p]
     lib.srg_csr_col_splits.restype = ctypes.c_int
+    lib.srg_csr_mirror.argtypes = [_p, _p, _p, _i64, _i64, _p, _p]
+    lib.srg_csr_mirror.restype = ctypes.c_int
     lib.srg_spmm_send_f32.argtypes = [_p, _p, _p, _i64, _p, _i64, _i64, _p, _i64, _p, _i64, _i32, ctypes.c_uint32,
                                       _p, _i64, _p, _p, _p]
     lib.srg_spmm_send_f32.restype = ctypes.c_int

@@ -31,6 +31,52 @@ def segment_sum_device(seg_ptr: torch.Tensor, vals: torch.Tensor) -> torch.Tenso
     return out
 
 
+def mirror_device(indptr: torch.Tensor, indices32: torch.Tensor, rows: torch.Tensor) -> torch.Tensor:
+    """srg_csr_mirror: position of entry (c, r) in row c for every entry (r, c), or -1."""
+    out = torch.empty(indices32.numel(), dtype=torch.int64, device=indices32.device)
+    _lib.call(indices32.device, "srg_csr_mirror", indptr.data_ptr(), indices32.data_ptr(), rows.data_ptr(),
+              indptr.numel() - 1, indices32.numel(), out.data_ptr(), _lib.stream(indices32.device))
+    return out
+
+
+def _canonical_plus_identity(ip, ix, v, rows, n):
+    """adj + I without a sort when adj is canonical (strictly increasing column ids within rows,
+    no explicit zeros) and no diagonal entry becomes 0: each row gets its diagonal entry merged at
+    its sorted position (an existing one becomes A[i,i] + 1.0, scipy's csr_plus_csr sum).  Returns
+    (indptr, indices, values, rows) or None when the input needs the general path."""
+    nnz = ix.numel()
+    key = rows * n + ix
+    if nnz and not (bool((key[1:] > key[:-1]).all()) and bool((v != 0).all())):
+        return None
+    dev = ix.device
+    ar = torch.arange(n, device=dev)
+    pos = torch.searchsorted(key, ar * (n + 1))            # first entry >= (r, r) in row r
+    has = (pos < ip[1:]) & (ix[pos.clamp(max=max(nnz - 1, 0))] == ar) if nnz else torch.zeros(n, dtype=torch.bool, device=dev)
+    vv = v.clone()
+    if bool(has.any()):
+        dpos = pos[has]
+        vv[dpos] = v[dpos] + 1.0
+        if not bool((vv[dpos] != 0).all()):
+            return None
+    ins = (~has).to(torch.int64)
+    before = torch.cumsum(ins, 0) - ins                  # inserted diagonals in earlier rows
+    n_new = nnz + int(ins.sum().item())
+    new_ip = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    new_ip[:-1] = ip[:-1] + before
+    new_ip[-1] = n_new
+    new_pos = torch.arange(nnz, device=dev) + before[rows] + (ins[rows] * (ix > rows))
+    new_ix = torch.empty(n_new, dtype=torch.int64, device=dev)
+    new_v = torch.empty(n_new, dtype=torch.float64, device=dev)
+    new_ix[new_pos] = ix
+    new_v[new_pos] = vv
+    r_ins = torch.nonzero(ins).squeeze(1)
+    at = new_ip[r_ins] + (pos[r_ins] - ip[r_ins])
+    new_ix[at] = r_ins
+    new_v[at] = 1.0
+    new_rows = torch.repeat_interleave(ar, new_ip[1:] - new_ip[:-1], output_size=n_new)
+    return new_ip, new_ix, new_v, new_rows
+
+
 def _runs(keys: torch.Tensor):
     """Start offsets (+ end) of the runs of equal values in a sorted 1-D tensor."""
     if keys.numel() == 0:
@@ -66,9 +112,15 @@ def _indptr(rows, n):
     return torch.searchsorted(rows, torch.arange(n + 1, dtype=rows.dtype, device=rows.device))
 
 
-def sym_norm(indptr, indices, data, n: int, r: float, device=None, segsum=None):
+def sym_norm(indptr, indices, data, n: int, r: float, device=None, segsum=None, mirror=None, fast=True):
     """Â = D^(r-1) (A+I)^T D^(-r) of the CSR (indptr, indices, data) (host arrays or tensors).
-    Returns device tensors (indptr int64, indices int32, values fp64), canonical CSR."""
+    Returns device tensors (indptr int64, indices int32, values fp64), canonical CSR.
+
+    fast: a canonical adj (the reference's datasets: csr_matrix((ones, (row, col))) is canonical)
+    gets A+I by merging the diagonals in place instead of a sort, and a structurally symmetric one
+    (undirected graphs) its transpose from one binary search per entry (srg_csr_mirror) instead of
+    a second sort -- the same values from the same fp64 operations, so the same bits; anything else
+    takes the general path."""
     segsum = segsum or segment_sum_device
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
     # copy in the stored dtypes and widen on the device (a host-side int32 -> int64 conversion of
@@ -76,15 +128,32 @@ def sym_norm(indptr, indices, data, n: int, r: float, device=None, segsum=None):
     ip = torch.as_tensor(np.asarray(indptr) if not torch.is_tensor(indptr) else indptr).to(dev).to(torch.int64)
     ix = torch.as_tensor(np.asarray(indices) if not torch.is_tensor(indices) else indices).to(dev).to(torch.int64)
     v = torch.as_tensor(np.asarray(data) if not torch.is_tensor(data) else data).to(dev).to(torch.float64)
-    rows = torch.repeat_interleave(torch.arange(n, device=dev), ip[1:] - ip[:-1])
-    diag = torch.arange(n, device=dev)
-    # adj + I: the identity's entry is added after the row's own (duplicate) entries
-    rows, cols, vals = canonical_sum(torch.cat([rows, diag]), torch.cat([ix, diag]),
-                                     torch.cat([v, torch.ones(n, dtype=torch.float64, device=dev)]), n, segsum)
-    deg = segsum(_indptr(rows, n), vals)
+    rows = torch.repeat_interleave(torch.arange(n, device=dev), ip[1:] - ip[:-1], output_size=ix.numel())
+    api = _canonical_plus_identity(ip, ix, v, rows, n) if fast else None
+    if api is not None:
+        aip, cols, vals, rows = api
+    else:
+        diag = torch.arange(n, device=dev)
+        # adj + I: the identity's entry is added after the row's own (duplicate) entries
+        rows, cols, vals = canonical_sum(torch.cat([rows, diag]), torch.cat([ix, diag]),
+                                         torch.cat([v, torch.ones(n, dtype=torch.float64, device=dev)]), n, segsum)
+        aip = _indptr(rows, n)
+    del ip, ix, v
+    deg = segsum(aip, vals)
     left, right = degree_powers(deg.cpu().numpy(), r)
     left_t = torch.from_numpy(left).to(dev)
     right_t = torch.from_numpy(right).to(dev)
+    if mirror is None and dev.type == "cuda":
+        mirror = mirror_device
+    if fast and mirror is not None and vals.numel():
+        cols32 = cols.to(torch.int32)
+        m = mirror(aip, cols32, rows)
+        if bool((m >= 0).all()):
+            # symmetric structure: Â[i, j] = ((A+I)[j, i] * left[i]) * right[j] at A+I's own positions
+            vhat = (vals[m] * left_t[rows]) * right_t[cols]
+            if bool((vhat != 0).all()):
+                return aip, cols32, vhat
+        del m, cols32
     # stored (rows, cols) of A+I lands at (cols, rows) of Â
     step1 = vals * left_t[cols]
     rows, cols, step1 = _kept(step1 != 0, rows, cols, step1)
@@ -94,10 +163,11 @@ def sym_norm(indptr, indices, data, n: int, r: float, device=None, segsum=None):
     return _indptr(key // n, n), (key % n).to(torch.int32), step2[perm]
 
 
-def ppr_norm(indptr, indices, data, n: int, r: float, alpha: float, device=None, segsum=None):
+def ppr_norm(indptr, indices, data, n: int, r: float, alpha: float, device=None, segsum=None, mirror=None,
+             fast=True):
     """(1 - alpha) Â + alpha I (symmetrical_simgraph_ppr_operator.py:19-21) on the device."""
     segsum = segsum or segment_sum_device
-    ip, ix, v = sym_norm(indptr, indices, data, n, r, device, segsum)
+    ip, ix, v = sym_norm(indptr, indices, data, n, r, device, segsum, mirror, fast)
     dev = ip.device
     rows = torch.repeat_interleave(torch.arange(n, device=dev), ip[1:] - ip[:-1])
     v = (1 - alpha) * v

@@ -20,18 +20,74 @@ def segsum_np(ptr, vals):
     return torch.from_numpy(out)
 
 
+def mirror_np(indptr, indices32, rows):
+    """srg_csr_mirror restated: position of (c, r) in row c for each entry (r, c), or -1."""
+    ip, ix, rw = indptr.numpy(), indices32.numpy(), rows.numpy()
+    out = np.full(ix.size, -1, dtype=np.int64)
+    for e in range(ix.size):
+        c = ix[e]
+        k = ip[c] + np.searchsorted(ix[ip[c]:ip[c + 1]], rw[e])
+        if k < ip[c + 1] and ix[k] == rw[e]:
+            out[e] = k
+    return torch.from_numpy(out)
+
+
+@pytest.mark.parametrize("fast", [False, True])
 @pytest.mark.parametrize("name", [n for n in G.names("norm") if G.manifest()[n]["n"] <= 5000])
-def test_sym_and_ppr_equal_reference(oracle_mod, name):
+def test_sym_and_ppr_equal_reference(oracle_mod, name, fast):
+    """The general path (sorts) and the fast path (diagonal merged in place for canonical input;
+    the transpose from mirror positions for a symmetric structure) both give the reference's Â."""
     c = G.Case(name)
     a = c.adj()
     r = c.meta["r"]
+    kw = dict(device="cpu", segsum=segsum_np, mirror=mirror_np, fast=fast)
     if c.meta["op"] == "ppr":
-        ip, ix, v = C.ppr_norm(a.indptr, a.indices, a.data, c.n, r, c.meta["alpha"], device="cpu", segsum=segsum_np)
+        ip, ix, v = C.ppr_norm(a.indptr, a.indices, a.data, c.n, r, c.meta["alpha"], **kw)
     else:
-        ip, ix, v = C.sym_norm(a.indptr, a.indices, a.data, c.n, r, device="cpu", segsum=segsum_np)
+        ip, ix, v = C.sym_norm(a.indptr, a.indices, a.data, c.n, r, **kw)
     np.testing.assert_array_equal(ip.numpy(), c["ahat_indptr"])
     np.testing.assert_array_equal(ix.numpy(), c["ahat_indices"])
     np.testing.assert_array_equal(v.numpy(), c["ahat_data64"])
+
+
+def test_fast_paths_taken_and_refused():
+    """Which inputs take the in-place A+I merge: canonical ones (with or without stored diagonal
+    entries); not unsorted rows, duplicates, explicit zeros, or a diagonal entry of -1 (A+I drops
+    it to zero)."""
+    import scipy.sparse as sp
+    rng = np.random.default_rng(3)
+    n = 60
+    d = sp.random(n, n, density=0.1, random_state=4, format="csr")
+    d.data[:] = rng.random(d.nnz) + 0.5
+    d = d + d.T
+    d.setdiag(0.0)
+    d.eliminate_zeros()
+    d.sort_indices()
+
+    def api(a):
+        ip = torch.from_numpy(a.indptr.astype(np.int64))
+        ix = torch.from_numpy(a.indices.astype(np.int64))
+        rows = torch.repeat_interleave(torch.arange(n), ip[1:] - ip[:-1])
+        return C._canonical_plus_identity(ip, ix, torch.from_numpy(a.data.astype(np.float64)), rows, n)
+
+    for a in (d, d + sp.identity(n, format="csr") * 0.25):
+        a = sp.csr_matrix(a)
+        a.sort_indices()
+        got = api(a)
+        assert got is not None
+        want = sp.csr_matrix(a + sp.identity(n, format="csr"))
+        np.testing.assert_array_equal(got[0].numpy(), want.indptr)
+        np.testing.assert_array_equal(got[1].numpy(), want.indices)
+        np.testing.assert_array_equal(got[2].numpy(), want.data)
+    neg = sp.csr_matrix(d + sp.identity(n, format="csr") * -1.0)
+    neg.sort_indices()
+    assert api(neg) is None
+    zero = d.copy()
+    zero.data[3] = 0.0
+    assert api(zero) is None
+    unsorted = d.copy()
+    unsorted.indices[unsorted.indptr[5]:unsorted.indptr[6]] = unsorted.indices[unsorted.indptr[5]:unsorted.indptr[6]][::-1]
+    assert d.indptr[6] - d.indptr[5] < 2 or api(unsorted) is None
 
 
 @pytest.mark.parametrize("seed", [0, 1, 2])
