@@ -31,9 +31,13 @@ from srgnn.spmm import propagate as _device_propagate
 def _hops_to_host(A, X, K, ring=3):
     """Hops 1..K of A on the device panel X, each copied to pinned host memory on a copy stream
     while the next hop runs (the D2H of the reference-shaped list overlaps the kernels); device
-    memory holds a ring of `ring` hop panels.  Returns the K host tensors."""
-    from srgnn.spmm import spmm
+    memory holds a ring of `ring` hop panels.  Returns the K host tensors.  The hops are
+    column-blocked where srgnn.spmm.auto_col_blocks says so (bitwise the one-launch hop)."""
+    from srgnn.spmm import auto_col_blocks, column_blocks_for, hop
     dev = A.device
+    B = auto_col_blocks(A, X.shape[1], hops=K)
+    if B > 1 and not column_blocks_for(A, B, hops=K):
+        B = 1
     main = torch.cuda.current_stream(dev)
     copy_s = torch.cuda.Stream(dev)
     R = max(1, min(K, ring))
@@ -45,7 +49,7 @@ def _hops_to_host(A, X, K, ring=3):
         buf = bufs[(k - 1) % R]
         if k > R:
             main.wait_event(copied[k - 1 - R])      # the ring slot's previous hop is on the host
-        spmm(A, prev, out=buf)
+        hop(A, prev, buf, col_blocks=B)
         done = torch.cuda.Event()
         done.record(main)
         copy_s.wait_event(done)
