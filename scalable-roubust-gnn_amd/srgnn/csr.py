@@ -36,6 +36,9 @@ DEFAULT_HEAVY_THRESHOLD = None if _HEAVY_ENV == "auto" else int(_HEAVY_ENV)
 # r02_ab_auto.txt: d = 8 hop 3.34 ms at 32 vs 3.76 at the wide auto threshold; the RMAT-26 wavelet
 # in 32-column blocks 63.8 vs 98.9 ms per block).  Used when the wide threshold is automatic.
 NARROW_HEAVY_THRESHOLD = int(os.environ.get("SRGNN_NARROW_HEAVY_THRESHOLD", "32"))
+# Column blocks: rows of at most this many nonzeros are not cut but computed whole in block 0
+# (DeviceCSR.column_blocks); 0 cuts every row.
+BLOCK_WHOLE_MAX = int(os.environ.get("SRGNN_BLOCK_WHOLE_MAX", "32"))
 # "auto": rows whose slice-wave time (~40 ns per nonzero, measured) would exceed about half of the
 # expected hop time (~nnz / 13.5e9 s at the measured hop rate) go to the hub path:
 # threshold = nnz // 1024, at least 8192.  Products on 1 GPU -> only the top hub; 1/8 of it -> ~15 K.
@@ -92,6 +95,9 @@ class DeviceCSR:
     # row spans (a column block, column_blocks()): row r's entries are [indptr[r], row_end[r]) of
     # indices / values, and indptr holds n_rows starts instead of n_rows + 1 pointers
     row_end: torch.Tensor | None = None
+    # column block 0 only: rows this block computes whole (short rows are not cut: the later blocks
+    # do not schedule them, so their Y is written once instead of written, read and written again)
+    whole_rows: torch.Tensor | None = None
     _blocks: dict = field(default_factory=dict, repr=False, compare=False)   # column_blocks() cache
 
     def heavy(self, d: int) -> int:
@@ -176,17 +182,47 @@ class DeviceCSR:
         splits = torch.empty((B - 1, self.n_rows), dtype=torch.int64, device=dev)
         _lib.call(dev, "srg_csr_col_splits", ip.data_ptr(), self.indices.data_ptr(), self.n_rows, n, B,
                   splits.data_ptr(), _lib.stream(dev))
+        whole = (ip[1:] - ip[:-1]) <= BLOCK_WHOLE_MAX if BLOCK_WHOLE_MAX > 0 else None
+        if whole is not None:
+            # short rows run whole in block 0: their later spans are empty and not scheduled
+            splits = torch.where(whole.unsqueeze(0), ip[1:].unsqueeze(0), splits)
+            later = torch.nonzero(~whole).squeeze(1)
         bounds = [ip[:-1]] + [splits[b] for b in range(B - 1)] + [ip[1:]]
         out = []
         for b in range(B):
             beg, end = bounds[b], bounds[b + 1]
             deg = end - beg
             nnz_b = int(deg.sum().item())
-            order, n_heavy, n_hub = schedule_from_degrees(deg, nnz_b)
-            out.append(DeviceCSR(beg, self.indices, self.values, self.n_rows, n, order, n_heavy, n_hub,
-                                 narrow_heavy_degrees(deg, n_hub), row_end=end))
+            if b > 0 and whole is not None:
+                order, n_heavy, n_hub = schedule_from_degrees(deg[later], nnz_b)
+                order = later[order.to(torch.int64)].to(torch.int32)
+                n_sched, narrow = int(later.numel()), narrow_heavy_degrees(deg[later], n_hub)
+            else:
+                order, n_heavy, n_hub = schedule_from_degrees(deg, nnz_b)
+                n_sched, narrow = self.n_rows, narrow_heavy_degrees(deg, n_hub)
+            out.append(DeviceCSR(beg, self.indices, self.values, n_sched, n, order, n_heavy, n_hub, narrow,
+                                 row_end=end, whole_rows=whole if b == 0 else None))
         self._blocks[B] = out
         return out
+
+    def split_whole(self):
+        """Column block 0 as two schedules over the same arrays: (the cut rows' first spans, the
+        rows it computes whole) -- for a hop whose aggregation epilogue must run in the launch
+        that finishes each row (srgnn.spmm.hop with agg).  Cached."""
+        if self.whole_rows is None:
+            return None
+        if "split" not in self._blocks:
+            parts = []
+            for sel in (~self.whole_rows, self.whole_rows):
+                rows = torch.nonzero(sel).squeeze(1)
+                ip = self.indptr
+                deg = ((self.row_end - ip) if self.is_span else (ip[1:] - ip[:-1]))[rows]
+                order, n_heavy, n_hub = schedule_from_degrees(deg, int(deg.sum().item()))
+                order = rows[order.to(torch.int64)].to(torch.int32)
+                parts.append(DeviceCSR(self.indptr, self.indices, self.values, int(rows.numel()), self.n_cols, order,
+                                       n_heavy, n_hub, narrow_heavy_degrees(deg, n_hub), row_end=self.row_end))
+            self._blocks["split"] = tuple(parts)
+        return self._blocks["split"]
 
     def compact_column_blocks(self, B: int):
         """column_blocks(B) with each block's spans copied into arrays of its own (a plain CSR per
@@ -207,8 +243,8 @@ class DeviceCSR:
             # entry e of row r sits at indptr[r] + (e - bip[r]) of the shared arrays
             idx = torch.repeat_interleave(blk.indptr - bip[:-1], deg, output_size=nnz_b)
             idx += torch.arange(nnz_b, dtype=torch.int64, device=deg.device)
-            out.append(DeviceCSR(bip, self.indices[idx], self.values[idx], self.n_rows, self.n_cols, blk.order,
-                                 blk.n_heavy, blk.n_hub, blk.n_heavy_narrow))
+            out.append(DeviceCSR(bip, self.indices[idx], self.values[idx], blk.n_rows, self.n_cols, blk.order,
+                                 blk.n_heavy, blk.n_hub, blk.n_heavy_narrow, whole_rows=blk.whole_rows))
             del idx
         self._blocks[B] = out
         return out

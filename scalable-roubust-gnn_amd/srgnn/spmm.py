@@ -71,8 +71,13 @@ def hop(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, nt_store: bool = False
     # a block's rows are short: 2 gathers per packed row in flight (d >= 128: 4 or 2 rows per wave;
     # at d = 64, 8 rows per wave, it is 3 % slower)
     u2 = len(blocks) > 1 and d >= 128 and _U2_BLOCKED
+    split = blocks[0].split_whole() if agg is not None and len(blocks) > 1 else None
     for b, Ab in enumerate(blocks):
-        if agg is not None and b == len(blocks) - 1:
+        if split is not None and b == 0:
+            # rows block 0 computes whole finish there: their aggregation runs in that launch
+            spmm(split[0], X, out=out, nt_store=nt_store, packed_u2=u2)
+            spmm_agg(split[1], X, out, agg[0], agg[1], agg[2], nt_store=nt_store, packed_u2=u2)
+        elif agg is not None and b == len(blocks) - 1:
             spmm_agg(Ab, X, out, agg[0], agg[1], agg[2], nt_store=nt_store, accumulate=b > 0, packed_u2=u2)
         else:
             spmm(Ab, X, out=out, accumulate=b > 0, nt_store=nt_store, packed_u2=u2)

@@ -53,20 +53,28 @@ def test_fused_combine_bit_exact(oracle_mod, name, K):
         np.testing.assert_array_equal(got, want, err_msg=f"{name} K={K} {msg.aggr_type} {msg.start}:{msg.end}")
 
 
+@pytest.mark.parametrize("whole", [(0, False), (4, False), (16, True), (1 << 30, False)])
 @pytest.mark.parametrize("B", [2, 3])
 @pytest.mark.parametrize("name", ["cora_sym_k3", "rand_d130_r1", "rand_d36_ppr"])
-def test_propagate_aggregate_column_blocked_bit_exact(oracle_mod, name, B):
+def test_propagate_aggregate_column_blocked_bit_exact(oracle_mod, monkeypatch, name, B, whole):
     """Column-blocked hops in the fused aggregation (spmm.hop: blocks with ACCUMULATE, the
-    aggregation epilogue in the last block's launch) == the reference's combine, bit for bit."""
+    aggregation epilogue in the launch that finishes each row -- the last block's, or block 0's
+    for the short rows it computes whole) == the reference's combine, bit for bit.  whole =
+    (SRGNN_BLOCK_WHOLE_MAX, compact copies)."""
+    from srgnn import csr as csr_mod
     from srgnn.aggregate import combine_plan, combine_steps, propagate_aggregate
     from srgnn.csr import DeviceCSR
+    monkeypatch.setattr(csr_mod, "BLOCK_WHOLE_MAX", whole[0])
     c = G.Case(name)
     ip, ix, v = c.ahat()
     x = c.x()
     K = 5
     hops = oracle_mod.propagate(ip, ix, v, x, K)
     A = DeviceCSR.from_tensors(ip, ix, v, n_cols=c.n, device="cuda")
-    assert A.column_blocks(B) is not None
+    blocks = A.compact_column_blocks(B) if whole[1] else A.column_blocks(B)
+    assert blocks is not None and sum(b.nnz for b in blocks) == A.nnz
+    if whole[0]:
+        assert blocks[0].whole_rows is not None and blocks[0].split_whole() is not None
     X = torch.from_numpy(x).cuda()
     for msg in _ops(K):
         mode, terms, div = combine_plan(msg, K + 1)

@@ -175,14 +175,17 @@ def test_column_blocked_chain_continuation(name, thr):
         c.check_hop(1, Y.cpu().numpy())
 
 
+@pytest.mark.parametrize("whole_max", [0, 8])
 @pytest.mark.parametrize("compact", [False, True])
 @pytest.mark.parametrize("B", [2, 3, 5])
 @pytest.mark.parametrize("name", G.names("norm"))
-def test_propagate_column_blocked_bit_exact(name, B, compact):
+def test_propagate_column_blocked_bit_exact(monkeypatch, name, B, compact, whole_max):
     """The product path's column-blocked hops (DeviceCSR.column_blocks -- row spans of the shared
     arrays -- or compact_column_blocks -- the spans copied out -- + propagate(col_blocks=B): B
     launches per hop, each block with its own schedule) == the reference's hops, bit for bit."""
+    from srgnn import csr as csr_mod
     from srgnn.spmm import hop, propagate
+    monkeypatch.setattr(csr_mod, "BLOCK_WHOLE_MAX", whole_max)   # rows this short run whole in block 0
     c = G.Case(name)
     A = _csr(c, (None, None))
     blocks = A.compact_column_blocks(B) if compact else A.column_blocks(B)
