@@ -17,10 +17,12 @@ from .csr import DeviceCSR
 _stream = _lib.stream
 
 # Column-blocked hops (DeviceCSR.column_blocks): B launches per hop, each gathering from one
-# contiguous slice of X's rows, so the caches hold a larger share of the rows a launch reads.
-# Measured (profiles/r02_colblock_*.json): products (X 1.25 GB) 7.12 vs 7.35 ms per hop at B = 2,
-# 7.28 at 3; arxiv (X 87 MB, already cache-resident) 0.221 vs 0.166 ms.  "auto" takes B = 2 for
-# panels of 512 MiB .. 16 GiB; SRGNN_COL_BLOCKS=<B> forces B.
+# contiguous slice of X's rows, so the caches hold a larger share of the rows a launch reads; rows
+# of <= csr.BLOCK_WHOLE_MAX nonzeros are not cut (block 0 computes them whole).  Measured
+# (profiles/r02t-v_*): products d = 128 7.05 (one launch 7.31) -> 6.67 (B = 2) -> 6.30 ms (B = 4),
+# flat over B = 4..6, 6.47 at 8; d = 256 +9 % and papers100M / RMAT-26 +3 / +2 % for B = 4 over 2 / 1;
+# arxiv (X 87 MB, already cache-resident) 0.224 vs 0.163 ms at B = 2.  "auto" takes B = 4 for panels of
+# >= 512 MiB at d >= 64; SRGNN_COL_BLOCKS=<B> forces B.
 _COL_BLOCKS_ENV = os.environ.get("SRGNN_COL_BLOCKS", "auto")
 # column blocks' launches keep 2 gathers per packed light row in flight (SRG_SPMM_PACKED_U2) for
 # d >= 128: products 7.15 -> 7.03 ms per hop, d = 256 +1.3 %, d = 64 -3 % (so not there);
@@ -49,12 +51,12 @@ def column_blocks_for(A: DeviceCSR, B: int, hops: int | None = None):
 
 
 def auto_col_blocks(A: DeviceCSR, d: int, hops: int | None = None) -> int:
-    """Column blocks per hop for a panel of d columns (1 = the one-launch hop): 2 for panels of
-    512 MiB .. 16 GiB at d >= 64, if A's blocks exist or `hops` hops will amortise cutting it."""
+    """Column blocks per hop for a panel of d columns (1 = the one-launch hop): 4 for panels of
+    >= 512 MiB at d >= 64, if A's blocks exist or `hops` hops will amortise cutting it."""
     if _COL_BLOCKS_ENV != "auto":
         return max(1, int(_COL_BLOCKS_ENV))
     panel = A.n_cols * d * 4
-    B = 2 if d >= 64 and (512 << 20) <= panel <= (16 << 30) else 1
+    B = 4 if d >= 64 and panel >= (512 << 20) else 1
     if B > 1 and B not in A._blocks and (hops is None or hops < MIN_HOPS_TO_CUT):
         return 1
     return B

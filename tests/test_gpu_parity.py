@@ -222,10 +222,14 @@ def test_column_blocks_exact_for_unordered_rows(name):
     c.check_hop(1, want)
 
 
-def test_column_block_spans_are_lower_bounds():
+@pytest.mark.parametrize("whole_max", [0, 16])
+def test_column_block_spans_are_lower_bounds(monkeypatch, whole_max):
     """srg_csr_col_splits on a host-checkable CSR: for sorted rows each split is the first entry
-    whose id reaches ceil(b n / B); every split lies in its row and is monotone in b (any row)."""
+    whose id reaches ceil(b n / B); every split lies in its row and is monotone in b (any row).
+    Rows of <= whole_max entries end in block 0 (every later split at the row's end)."""
+    from srgnn import csr as csr_mod
     from srgnn.csr import DeviceCSR
+    monkeypatch.setattr(csr_mod, "BLOCK_WHOLE_MAX", whole_max)
     rng = np.random.default_rng(5)
     n, deg = 997, rng.integers(0, 40, 997)
     deg[3], deg[10] = 3000, 0
@@ -242,10 +246,12 @@ def test_column_block_spans_are_lower_bounds():
             for b in range(1, B):
                 assert np.all(starts[b] >= starts[b - 1])
                 assert np.array_equal(blocks[b - 1].row_end.cpu().numpy(), starts[b])
+                short = np.diff(ip) <= whole_max
+                assert np.array_equal(starts[b][short], ip[1:][short])
                 if sorted_rows:
                     bound = -(-b * n // B)
                     want = np.array([ip[r] + np.searchsorted(ids[ip[r]:ip[r + 1]], bound) for r in range(n)])
-                    assert np.array_equal(starts[b], want)
+                    assert np.array_equal(starts[b][~short], want[~short])
 
 
 def test_strided_panels_and_row_blocks(oracle_mod):
