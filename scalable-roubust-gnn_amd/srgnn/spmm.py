@@ -39,11 +39,12 @@ MIN_HOPS_TO_CUT = 4
 # 1 % less traffic per hop for one more copy of the ids and values, ~3 ms on products), when the
 # copy fits in a quarter of the free memory.
 MIN_HOPS_TO_COMPACT = 48
+_COMPACT = os.environ.get("SRGNN_COMPACT_BLOCKS", "1") != "0"     # 0: spans only (A/B)
 
 
 def column_blocks_for(A: DeviceCSR, B: int, hops: int | None = None):
     """A's column blocks for a run of `hops` hops: spans, or compact copies for long runs."""
-    if hops is not None and hops >= MIN_HOPS_TO_COMPACT and not A.is_span:
+    if _COMPACT and hops is not None and hops >= MIN_HOPS_TO_COMPACT and not A.is_span:
         free, _ = torch.cuda.mem_get_info(A.device)
         if A.nnz * (A.indices.element_size() + A.values.element_size()) <= free // 4:
             return A.compact_column_blocks(B)
