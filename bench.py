@@ -14,19 +14,34 @@ reference, in nnz-balanced groups exchanged with RCCL all_to_all_single as soon 
 kernel finishes (overlapping the later groups); --exchange allgather: one padded
 all_gather_into_tensor of the whole panel per hop.  Both are bitwise equal to 1 GPU.
 
+--gpus N without torchrun (WORLD_SIZE unset): this process spawns the N ranks itself (one worker
+process per GPU, 127.0.0.1 rendezvous) before touching any GPU, and forwards rank 0's line.
+
 Extra objects on the JSON line:
-  roofline      the SpMM kernel: algorithmic (no-reuse) bytes per launch / its average duration,
-                timed with HIP events on the launch stream; traffic from rocprofv3 PMC counters
-                (profiles/pmc_<config>.json, written by tools/pmc_traffic.py) or null
-  cpu_baseline  rank 0, N = 1 only: the reference's FloatCSRMulDenseOMP compiled from its own
-                matmul.c (oracle/_ref/libmatmul_ref.so), kernel-only hops on pre-converted buffers
-                of the same graph, bounded to ~--cpu-seconds of work
+  roofline         the SpMM hop (one hop = `launches_per_hop` column-block launches): HBM bytes
+                   per hop from rocprofv3 PMC counters (2 * FETCH_SIZE + WRITE_SIZE, the gfx950
+                   correction of MI355X_MICROARCH.md), measured by this run in separate --pmc
+                   passes of tools/spmm_probe.py before the GPU is touched (--pmc), else the
+                   committed profiles/pmc_<config>.json, / the hop's duration (HIP events on the
+                   launch stream) -> achieved, frac.  frac_no_reuse (SURVEY §8(d)'s no-reuse byte
+                   model, > 1 where caches serve re-read rows) and frac_compulsory beside it.
+  cpu_baseline     rank 0, N = 1 only: the reference's FloatCSRMulDenseOMP compiled from its own
+                   matmul.c (oracle/_ref/libmatmul_ref.so), kernel-only hops on pre-converted
+                   buffers of the same graph, bounded to ~--cpu-seconds of work
+  parity_vs_oracle N = 1: after the timed steps, outside the timed region, sampled rows (random +
+                   the longest) of hop 1 and hop K of the timed operator checked bit for bit
+                   against the CPU oracle (test infrastructure, the checker only) fed with the
+                   GPU's previous hop
+  parity_vs_1gpu   N > 1: every rank's rows of hop 1 and hop K against the one-GPU kernels
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import shutil
+import socket
+import subprocess
 import sys
 import time
 
@@ -77,6 +92,11 @@ def parse():
     ap.add_argument("--aggregate", default=None, choices=["sum", "mean", "weighted"],
                     help="one GPU: fused hop aggregation (SGC/SSGC/GBP precompute) instead of the K+1 "
                          "panels: sum / mean over hops 0..K, or GBP weights alpha(1-alpha)^k, alpha 0.15")
+    ap.add_argument("--pmc", default="auto", choices=["auto", "on", "off"],
+                    help="measure the hop's HBM traffic with rocprofv3 --pmc passes of tools/spmm_probe.py "
+                         "before this process touches the GPU (auto: one GPU, K-hop, not under a profiler)")
+    ap.add_argument("--parity-rows", type=int, default=2000,
+                    help="one GPU: random rows (plus the 20 longest) checked against the oracle after timing")
     ap.add_argument("--mode", default="auto", choices=["auto", "panels", "last"],
                     help="panels: all K+1 hop panels kept (GraphOp.propagate); last: two ping-pong "
                          "panels, only A^K X kept (SGC-style, fused aggregation); auto: panels if "
@@ -162,6 +182,8 @@ def cpu_baseline(ip, ix, vals, x_host, n, d, budget_s):
     what = "the reference's FloatCSRMulDenseOMP (oracle/_ref, built from matmul.c)" if use_ref else \
         "the oracle's int64 C restatement (the reference's int32 matmul.c cannot address this graph)"
     return {"value": edges / dt, "unit": "propagated edges/s", "cores": threads,
+            "cores_note": (f"threads used = OMP_NUM_THREADS ({threads}), the CPU share this job is granted; "
+                           f"the host shows {os.cpu_count()} logical CPUs"),
             "kind": "reference" if use_ref else "port",
             "value_1thread": one, "cpu_model": _cpu_model(),
             "sample": f"{what}: {edges} propagated edges ({hops} full hop(s) + row blocks) of the "
@@ -169,18 +191,169 @@ def cpu_baseline(ip, ix, vals, x_host, n, d, budget_s):
                       f"buffers, OMP_NUM_THREADS={threads}, {dt:.1f} s; value_1thread on a row block"}
 
 
-def pmc_traffic(config, kernel_hint="k_spmm", launches_per_hop=1):
+def pmc_traffic(config, launches_per_hop=1, measured=None):
+    """(HBM bytes per hop, source): from this run's PMC passes (`measured`), else from the committed
+    profiles/pmc_<config>.json (tools/pmc_traffic.py) when it was taken with the same hop layout."""
+    if measured is not None and int(measured.get("launches_per_hop", 1)) == int(launches_per_hop):
+        return float(measured["hbm_bytes_per_hop"]), measured["source"]
     path = os.path.join(HERE, "profiles", f"pmc_{config}.json")
     if not os.path.exists(path):
-        return None
+        return None, None
     try:
         with open(path) as f:
             rec = json.load(f)
         if int(rec.get("launches_per_hop", 1)) != int(launches_per_hop):
-            return None       # measured with another hop layout
-        return float(rec["hbm_bytes_per_launch"])
+            return None, None       # measured with another hop layout
+        return float(rec["hbm_bytes_per_launch"]), f"committed profiles/pmc_{config}.json (tools/pmc_traffic.py)"
     except Exception:  # noqa: BLE001
+        return None, None
+
+
+def _under_profiler() -> bool:
+    pre = os.environ.get("LD_PRELOAD", "")
+    return "rocprof" in pre or any(k.startswith(("ROCPROF", "ROCP_")) for k in os.environ)
+
+
+def measure_pmc(a):
+    """HBM traffic of one hop of the bench's operator, from two rocprofv3 --pmc passes (FETCH_SIZE,
+    then WRITE_SIZE: they do not fit one pass) of tools/spmm_probe.py, each in a child process
+    with its own time limit.  Must run before this process initialises the GPU (a process that has
+    must not exec another program).  traffic = 2 * FETCH_SIZE + WRITE_SIZE per hop (gfx950:
+    FETCH_SIZE counts half the bytes of wide reads, MI355X_MICROARCH.md).  None on any failure."""
+    import csv
+    import glob
+    import tempfile
+    prof = shutil.which("rocprofv3")
+    if prof is None:
         return None
+    out = tempfile.mkdtemp(prefix="srg_pmc_", dir="/tmp")
+    env = dict(os.environ, TMPDIR="/tmp")
+    probe = None
+    sums = {}
+    try:
+        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+            d = os.path.join(out, counter)
+            cmd = ["timeout", "-s", "KILL", "120", prof, "--pmc", counter, "-d", d, "-o", "p",
+                   "--output-format", "csv", "--", sys.executable, os.path.join(HERE, "tools", "spmm_probe.py"),
+                   "--config", a.config, "--reps", "3"]
+            k = a.k if a.k is not None else synth.CONFIGS[a.config].get("k", 3)
+            if a.op == "wavelet":       # order 3, every column block of the panel
+                d_cfg = a.d or synth.CONFIGS[a.config]["d"]
+                k = 3 * max(1, d_cfg // (a.col_block or 64))
+            cmd += ["--hops", str(k * (a.steps + a.warmup))]
+            if a.d is not None:
+                cmd += ["--d", str(a.d)]
+            if a.op == "wavelet":
+                cmd += ["--op", "wavelet"] + (["--col-block", str(a.col_block)] if a.col_block else [])
+            elif a.col_blocks is not None:
+                cmd += ["--col-blocks", str(a.col_blocks)]
+            if a.heavy_threshold is not None:
+                cmd += ["--heavy-threshold", str(a.heavy_threshold)]
+            r = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                               timeout=150)
+            if r.returncode != 0:
+                log(f"pmc pass {counter} failed ({r.returncode}): {r.stderr.decode(errors='replace')[-400:]}")
+                return None
+            probe = json.loads(r.stdout.decode().strip().splitlines()[-1])
+            total, launches = 0.0, 0
+            for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+                with open(f) as fh:
+                    for row in csv.DictReader(fh):
+                        name = row.get("Kernel_Name", "")
+                        if "k_spmm<" in name and "k_spmm_hub" not in name and row.get("Counter_Name") == counter:
+                            total += float(row["Counter_Value"])
+                            launches += 1
+            if not launches:
+                log(f"pmc pass {counter}: no k_spmm rows")
+                return None
+            sums[counter] = total / probe["reps"]           # KiB per hop (all of a hop's launches)
+    except Exception as e:  # noqa: BLE001
+        log(f"pmc passes failed: {e!r}")
+        return None
+    finally:
+        shutil.rmtree(out, ignore_errors=True)
+    hop_bytes = 2.0 * sums["FETCH_SIZE"] * 1024 + sums["WRITE_SIZE"] * 1024
+    log(f"pmc: {hop_bytes / 1e9:.2f} GB per hop ({probe['launches_per_hop']} launches)")
+    return {"hbm_bytes_per_hop": hop_bytes, "launches_per_hop": probe["launches_per_hop"],
+            "fetch_kib_per_hop": sums["FETCH_SIZE"], "write_kib_per_hop": sums["WRITE_SIZE"],
+            "source": "measured by this run: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of tools/spmm_probe.py "
+                      "(the same operator and hop layout), 2 * FETCH_SIZE + WRITE_SIZE"}
+
+
+def oracle_sample(ip, ix, vals, n, n_random, n_top=20, seed=11):
+    """Rows checked against the oracle after the timed steps (random rows plus the longest ones) and
+    their sub-problem, extracted on the device: the rows' own entries in CSR order with the column
+    ids renumbered over the X rows they gather (so the oracle needs only those rows)."""
+    deg = ip[1:] - ip[:-1]
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    pick = [torch.randint(0, n, (n_random,), generator=g).to(ip.device)] if n_random else []
+    pick.append(torch.sort(deg, descending=True).indices[:n_top])
+    rows = torch.unique(torch.cat(pick))
+    beg, cnt = ip[rows], deg[rows]
+    tot = int(cnt.sum())
+    pos = torch.repeat_interleave(beg - torch.cumsum(cnt, 0) + cnt, cnt, output_size=tot) + \
+        torch.arange(tot, device=ip.device)
+    ucols, inv = torch.unique(ix[pos].long(), return_inverse=True)
+    return {"rows": rows, "ucols": ucols, "ip": np.r_[0, np.cumsum(cnt.cpu().numpy())].astype(np.int64),
+            "ix": inv.to(torch.int32).cpu().numpy(), "v": vals[pos].cpu().numpy()}
+
+
+def parity_vs_oracle(sample, checks):
+    """Bit-for-bit check of sampled rows of GPU hops against the C oracle (oracle/srg_oracle.c:
+    one fp32 fma chain per element in CSR order, matmul.c:23-40) fed with the GPU's previous hop.
+    checks: [(k, prev_panel, panel)].  Test infrastructure used as the checker, outside the
+    timed region; nothing measured runs through it."""
+    from oracle import oracle as O
+    done, ok = [], True
+    for k, prev, got in checks:
+        want = O.spmm(sample["ip"], sample["ix"], sample["v"], prev[sample["ucols"]].cpu().numpy())
+        have = got[sample["rows"]].cpu().numpy()
+        ok = ok and np.array_equal(have.view(np.uint32), want.view(np.uint32))
+        done.append(k)
+    return {"hops_checked": done, "rows_checked": int(sample["rows"].numel()),
+            "rows": "random rows + the 20 longest", "bit_exact": bool(ok),
+            "checker": "oracle/srg_oracle.c fp32 fma chains fed with the GPU's previous hop (outside the timed region)"}
+
+
+def launch_ranks(n_ranks, args, script=None):
+    """--gpus N without torchrun: spawn the N ranks as worker processes of this script (RANK /
+    LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT as torchrun sets them), before this process
+    touches any GPU, forward rank 0's JSON line and return the first failing exit code."""
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n_ranks):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n_ranks),
+                   LOCAL_WORLD_SIZE=str(n_ranks), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(script or __file__)] + list(args), env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    import threading
+
+    def forward():
+        for line in procs[0].stdout:
+            sys.stdout.write(line.decode())
+            sys.stdout.flush()
+    t = threading.Thread(target=forward, daemon=True)
+    t.start()
+    first_bad = 0
+    while True:           # a rank that fails leaves the others waiting in a collective: end them
+        rcs = [p.poll() for p in procs]
+        failed = [rc for rc in rcs if rc not in (None, 0)]
+        if failed:
+            first_bad = failed[0]
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            break
+        if all(rc is not None for rc in rcs):
+            break
+        time.sleep(0.2)
+    rcs = [p.wait() for p in procs]
+    t.join(timeout=10)
+    if first_bad:
+        log(f"worker exit codes {rcs}")
+    return first_bad
 
 
 def reference_hops(ip, ix, vals, n, X, K, dev):
@@ -207,7 +380,7 @@ def reference_hops(ip, ix, vals, n, X, K, dev):
     return out
 
 
-def run_wavelet(a, dev, world=1, rank=0):
+def run_wavelet(a, dev, world=1, rank=0, pmc=None):
     """SpectralModel's wavelet operator (SSRG/models/base_scalable/base_model.py:180-265) on the
     config's graph: R_s = sum_k c_{s,k} T_k(L~) X for tau = -0.5, +0.5, Chebyshev order 3, fp32.
     value = order * nnz(L) * steps / time: every order is one SpMM pass over the whole panel (in
@@ -273,8 +446,12 @@ def run_wavelet(a, dev, world=1, rank=0):
     kern_s = float(np.mean([ev[2 * r].elapsed_time(ev[2 * r + 1]) * 1e-3 for r in range(a.roofline_reps)]))
     del tb
     # the fused step also reads T_{k-1} and reads + writes every scale's output once
-    b_alg = roofline.bytes_no_reuse(n, nnz, cb) + (n * cb * 4 * (1 + 2 * ns) if fused else 0)
-    achieved = b_alg / kern_s / 1e9
+    extra = n * cb * 4 * (1 + 2 * ns) if fused else 0
+    b_alg = roofline.bytes_no_reuse(n, nnz, cb) + extra
+    b_comp = roofline.bytes_compulsory(n, nnz, cb, n_cols=n) + extra
+    peak = roofline.MI355X_HBM_PEAK_GBS
+    traffic = float(pmc["hbm_bytes_per_hop"]) if pmc is not None and int(pmc["launches_per_hop"]) == B else None
+    achieved = (traffic if traffic else b_comp) / kern_s / 1e9
     res = {
         "metric": "propagated edges/sec (wavelet-basis Chebyshev propagation)",
         "value": a.steps * order * nnz / dt,
@@ -288,12 +465,18 @@ def run_wavelet(a, dev, world=1, rank=0):
                    "mode": ("fp32, one load-balanced launch per order with the Chebyshev epilogue fused"
                             if fused else "fp32, split path (SpMM + epilogue launches)")
                            + " (bit-identical to the fused Chebyshev kernel)"},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": roofline.MI355X_HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / roofline.MI355X_HBM_PEAK_GBS, "traffic": None,
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
+                     "frac": achieved / peak, "traffic": traffic,
+                     "achieved_basis": ("HBM bytes per order's SpMM from PMC counters (traffic) / its time" if traffic
+                                        else "compulsory bytes / the SpMM's time (no counter run: a lower bound)"),
+                     "traffic_source": pmc["source"] if traffic else None,
+                     "unit_of_work": f"one Chebyshev order's SpMM over a {cb}-column block ({B} column-block launches)",
                      "kernel": (f"k_spmm with the Chebyshev epilogue: one order over a {cb}-column block" if fused
                                 else f"k_spmm: one Chebyshev order's SpMM over a {cb}-column block"),
-                     "kernel_ms": kern_s * 1e3, "launches_per_hop": B, "algorithmic_bytes_per_launch": b_alg,
-                     "compulsory_bytes_per_launch": roofline.bytes_compulsory(n, nnz, cb, n_cols=n)},
+                     "kernel_ms": kern_s * 1e3, "launches_per_hop": B, "kernel_ms_per_launch": kern_s * 1e3 / B,
+                     "frac_no_reuse": b_alg / kern_s / 1e9 / peak, "frac_compulsory": b_comp / kern_s / 1e9 / peak,
+                     "algorithmic_bytes_per_hop": b_alg, "compulsory_bytes_per_hop": b_comp,
+                     "traffic_over_compulsory": (traffic / b_comp) if traffic else None},
         "cpu_baseline": None,
     }
     if not a.no_cpu_baseline:
@@ -364,7 +547,14 @@ def run_wavelet_dist(a, dev, world, rank):
 
 def main():
     a = parse()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        return launch_ranks(a.gpus, sys.argv[1:])
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    # the PMC passes are child processes: they must run before this process touches the GPU
+    pmc = None
+    if world == 1 and not a.aggregate and not a.fused_epilogue and \
+            (a.pmc == "on" or (a.pmc == "auto" and not _under_profiler())):
+        pmc = measure_pmc(a)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
@@ -385,7 +575,7 @@ def main():
     if a.op == "wavelet":
         if world > 1:
             init_pg()
-        return run_wavelet(a, dev, world, rank)
+        return run_wavelet(a, dev, world, rank, pmc)
     if world > 1:
         init_pg()
 
@@ -477,6 +667,7 @@ def main():
         # one hop's kernels also compute the ghost rows (the roofline counts that work)
         local_rows, local_nnz = op.rows + op.n_ghost, op.nnz_local + int(op._ghost_pos.numel())
 
+    sample = oracle_sample(ip, ix, vals, n, a.parity_rows) if world == 1 and K > 0 else None
     refs = None
     if ref_full is not None:     # this rank's rows of the 1-GPU hops, checked after the timed steps
         refs = {k: v[op.r0:op.r1].clone() for k, v in ref_full.items()}
@@ -511,6 +702,11 @@ def main():
         dt = float(t.item())
 
     parity = None
+    oracle_checks = None
+    if sample is not None and mode == "panels":
+        # hop 1 from X and hop K from hop K-1, as the timed steps left them
+        oracle_checks = parity_vs_oracle(sample, [(1, panels[0], panels[1])] +
+                                         ([(K, panels[K - 1], panels[K])] if K > 1 else []))
     if world > 1:
         # the N-GPU hops of this rank's rows against the 1-GPU kernels on the whole graph, bit for bit
         ok = refs is not None and all(torch.equal(panels[k][: op.rows], v) for k, v in refs.items())
@@ -543,6 +739,10 @@ def main():
     torch.cuda.synchronize()
     durs = [ev[2 * r].elapsed_time(ev[2 * r + 1]) * 1e-3 for r in range(a.roofline_reps)]
     kern_isolated_s = float(np.mean(durs))
+    if sample is not None and oracle_checks is None:
+        # last-hop / aggregate modes keep no hop K-1: the isolated launches above left hop 1 of X
+        # (the timed operator, the same launches) in panels[1]
+        oracle_checks = parity_vs_oracle(sample, [(1, panels[0], panels[1])])
     # one hop's launch duration: over the timed region itself on one GPU (K hop launches per step,
     # back to back on the launch stream, so the events bracket exactly the kernels plus their
     # few-microsecond gaps); on N GPUs the timed region also waits on the exchange, so the
@@ -550,9 +750,13 @@ def main():
     in_run = world == 1 and not a.aggregate and K > 0
     kern_s = run_s / (a.steps * K) if in_run else kern_isolated_s
     b_alg = roofline.bytes_no_reuse(local_rows, local_nnz, d)
-    achieved = b_alg / kern_s / 1e9
+    b_comp = roofline.bytes_compulsory(local_rows, local_nnz, d, n_cols=n)
     peak = roofline.MI355X_HBM_PEAK_GBS
-    traffic = pmc_traffic(a.config, launches_per_hop=col_blocks) if world == 1 else None
+    traffic, traffic_src = pmc_traffic(a.config, launches_per_hop=col_blocks, measured=pmc) if world == 1 \
+        else (None, None)
+    # achieved: HBM bytes the counters saw per hop / hop time (a lower bound -- the compulsory
+    # bytes -- where no counter run exists for this layout)
+    achieved = (traffic if traffic else b_comp) / kern_s / 1e9
 
     exchange_stats = {}
     if world > 1 and a.exchange == "halo":
@@ -592,6 +796,11 @@ def main():
                    **exchange_stats},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
                      "frac": achieved / peak, "traffic": traffic,
+                     "achieved_basis": ("HBM bytes per hop from PMC counters (traffic) / hop time" if traffic else
+                                        "compulsory bytes per hop / hop time (no counter run for this layout: a lower bound)"),
+                     "traffic_source": traffic_src,
+                     "unit_of_work": "one hop" + (f" = {col_blocks} column-block launches" if col_blocks > 1 else " (one launch)")
+                                     + " + the hub workgroups beside them",
                      "kernel": "k_spmm (+ k_spmm_hub beside it): one hop" + (" of rank 0's rows" if world > 1 else "")
                      + (f" = {col_blocks} column-block launches (bitwise the one-launch hop)" if col_blocks > 1 else ""),
                      "kernel_ms": kern_s * 1e3,
@@ -600,16 +809,21 @@ def main():
                      "kernel_ms_source": ("HIP events over the timed steps / (steps x K)" if in_run
                                           else f"HIP events around {a.roofline_reps} isolated hop launches"),
                      "kernel_ms_isolated": kern_isolated_s * 1e3,
-                     # measured HBM bytes (PMC) per launch / the same launch duration: the share of
-                     # the 8 TB/s peak the kernel actually moves (the no-reuse frac counts cache hits)
-                     "traffic_frac": (traffic / kern_s / 1e9 / peak) if traffic else None,
-                     "algorithmic_bytes_per_launch": b_alg,
-                     "compulsory_bytes_per_launch": roofline.bytes_compulsory(local_rows, local_nnz, d,
-                                                                              n_cols=n)},
+                     # SURVEY §8(d)'s no-reuse model counts every gathered X row as an HBM read, so
+                     # cache hits push it past 1; the compulsory model counts every byte once
+                     "frac_no_reuse": b_alg / kern_s / 1e9 / peak,
+                     "frac_compulsory": b_comp / kern_s / 1e9 / peak,
+                     "algorithmic_bytes_per_hop": b_alg,
+                     "compulsory_bytes_per_hop": b_comp,
+                     "traffic_over_compulsory": (traffic / b_comp) if traffic else None},
         "cpu_baseline": None,
     }
     if parity is not None:
         res["parity_vs_1gpu"] = parity
+    if oracle_checks is not None:
+        res["parity_vs_oracle"] = oracle_checks
+        res["config"]["mode"] = ("exact: sampled rows bit-identical to the oracle (reference arithmetic)"
+                                 if oracle_checks["bit_exact"] else "exact mode, ORACLE MISMATCH")
     if host_copy is not None:
         log("cpu baseline ...")
         ipn, ixn, vn, xn = host_copy
@@ -622,4 +836,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -257,6 +257,9 @@ int srg_gather_rows_f32(const float* src, int64_t lds, int64_t n_src, const int6
 /* `stream` waits (on the device, not the host) for the hub workgroups of the last hub launch
  * forked from `stream` (an SRG_SPMM_HUB_NOJOIN one); no-op if none was forked. */
 int srg_hub_join(void* stream);
+/* Diagnostic: the number of live hub side streams over all devices (at most 8 per device; a caller
+ * stream's entry is evicted, least recently used first, unless it has an unjoined NOJOIN fork). */
+int srg_hub_side_streams(void);
 
 /* Column-block split points of a device CSR for srg_spmm_span_f32 (asynchronous on `stream`):
  * splits[(b-1) * n_rows + r] = the first entry of row r with column id >= ceil(b * n_cols / n_blocks)

@@ -211,6 +211,26 @@ int srg_comm_destroy(srg_comm* comm)
 
 int srg_comm_size(const srg_comm* comm) { return comm ? comm->nranks : 0; }
 
+// The sends and receives of hop k's exchange (inside the caller's GroupStart / GroupEnd bracket).
+static int group_sends(const Rccl* r, srg_comm* comm, const srg_shard_f32* shards, int n_shards,
+                       const int64_t* row_starts, int64_t ld, int k, int P)
+{
+    for (int i = 0; i < n_shards; ++i) {
+        const srg_shard_f32& s = shards[i];
+        const int me = comm->ranks[i];
+        SRG_HIPC(hipSetDevice(s.device));
+        hipStream_t st = static_cast<hipStream_t>(s.stream);
+        for (int q = 0; q < P; ++q) {
+            if (q == me) continue;
+            const size_t nq = (size_t)(row_starts[q + 1] - row_starts[q]) * (size_t)ld;
+            const size_t nme = (size_t)s.n_rows * (size_t)ld;
+            if (nme) SRG_NCCL(r, r->Send(s.panels[k - 1], nme, ncclFloat32, q, comm->comms[i], st));
+            if (nq) SRG_NCCL(r, r->Recv(s.x_full + (size_t)row_starts[q] * ld, nq, ncclFloat32, q, comm->comms[i], st));
+        }
+    }
+    return SRG_OK;
+}
+
 int srg_dist_propagate_khop_f32(srg_comm* comm, const srg_shard_f32* shards, int n_shards,
                                 const int64_t* row_starts, int64_t ld, int32_t d, int32_t K)
 {
@@ -242,20 +262,13 @@ int srg_dist_propagate_khop_f32(srg_comm* comm, const srg_shard_f32* shards, int
     for (int k = 1; k <= K; ++k) {
         // exchange: every rank's block of panel k-1 into every other rank's gathered panel
         SRG_NCCL(r, r->GroupStart());
-        for (int i = 0; i < n_shards; ++i) {
-            const srg_shard_f32& s = shards[i];
-            const int me = comm->ranks[i];
-            SRG_HIPC(hipSetDevice(s.device));
-            hipStream_t st = static_cast<hipStream_t>(s.stream);
-            for (int q = 0; q < P; ++q) {
-                if (q == me) continue;
-                const size_t nq = (size_t)(row_starts[q + 1] - row_starts[q]) * (size_t)ld;
-                const size_t nme = (size_t)s.n_rows * (size_t)ld;
-                if (nme) SRG_NCCL(r, r->Send(s.panels[k - 1], nme, ncclFloat32, q, comm->comms[i], st));
-                if (nq) SRG_NCCL(r, r->Recv(s.x_full + (size_t)row_starts[q] * ld, nq, ncclFloat32, q, comm->comms[i], st));
-            }
-        }
-        SRG_NCCL(r, r->GroupEnd());
+        // every exit from the bracket closes the group: an error inside it must not leave RCCL's
+        // thread-local group open (later RCCL calls of the process, torch's included, would be
+        // folded into it); the first error is the one returned
+        rc = group_sends(r, comm, shards, n_shards, row_starts, ld, k, P);
+        const ncclResult_t ge = r->GroupEnd();
+        if (rc) return rc;
+        if (ge != ncclSuccess) return comm_fail(SRG_ERR_HIP, "ncclGroupEnd failed: %s", r->GetErrorString(ge));
         for (int i = 0; i < n_shards; ++i) {
             const srg_shard_f32& s = shards[i];
             SRG_HIPC(hipSetDevice(s.device));

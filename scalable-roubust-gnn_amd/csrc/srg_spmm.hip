@@ -1419,18 +1419,24 @@ int hub_delay_us()
     return us;
 }
 
-// Hub side streams.  One per (device, caller stream), created on first use and never destroyed,
-// each with its own fork / join events: callers on different streams never share events.  The
-// whole fork sequence of a launch (record fork, side-stream wait, hub launch, record join, main
-// launch, join wait) runs under g_side_mu, so host threads sharing one caller stream cannot
-// interleave their records either.  SRG_SPMM_HUB_NOJOIN leaves the join to srg_hub_join(stream),
-// which waits on the same (device, stream) entry's join event.
+// Hub side streams.  One per (device, caller stream), created on first use, each with its own
+// fork / join events: callers on different streams never share events.  The whole fork sequence
+// of a launch (record fork, side-stream wait, hub launch, record join, main launch, join wait)
+// runs under g_side_mu, so host threads sharing one caller stream cannot interleave their records
+// either.  SRG_SPMM_HUB_NOJOIN leaves the join to srg_hub_join(stream), which waits on the same
+// (device, stream) entry's join event.  At most kMaxSideStreams entries live per device: a caller
+// that makes a new stream per call evicts the least recently used entry without an outstanding
+// NOJOIN fork (its stream is destroyed asynchronously: queued hub work still completes).
 struct SideStream {
     hipStream_t stream = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
+    uint64_t last_use = 0;
+    bool pending = false;      // a NOJOIN fork not yet joined by srg_hub_join
 };
+constexpr int kMaxSideStreams = 8;
 std::mutex g_side_mu;
 std::map<std::pair<int, hipStream_t>, SideStream> g_side;   // guarded by g_side_mu
+uint64_t g_side_tick = 0;                                     // guarded by g_side_mu
 bool g_side_attr[64] = {};                                     // per-device kernel attributes set
 
 // Sets the hub kernels' dynamic-LDS limit on the current device (attributes are per device).
@@ -1465,7 +1471,24 @@ int side_stream_locked(hipStream_t caller, SideStream** out)
         if (rc) return rc;
         g_side_attr[dev] = true;
     }
-    SideStream& ss = g_side[std::make_pair(dev, caller)];
+    const auto key = std::make_pair(dev, caller);
+    if (g_side.find(key) == g_side.end()) {
+        int live = 0;
+        auto lru = g_side.end();
+        for (auto it = g_side.begin(); it != g_side.end(); ++it) {
+            if (it->first.first != dev) continue;
+            ++live;
+            if (!it->second.pending && (lru == g_side.end() || it->second.last_use < lru->second.last_use)) lru = it;
+        }
+        if (live >= kMaxSideStreams && lru != g_side.end()) {
+            (void)hipEventDestroy(lru->second.fork);
+            (void)hipEventDestroy(lru->second.join);
+            (void)hipStreamDestroy(lru->second.stream);
+            g_side.erase(lru);
+        }
+    }
+    SideStream& ss = g_side[key];
+    ss.last_use = ++g_side_tick;
     if (!ss.stream) {
         // highest queue priority: the hub workgroups (9 waves, ~136 KB LDS each) must get CUs
         // before the main launch's many small blocks occupy them all
@@ -1570,6 +1593,7 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
         }
         SRG_HIP_CHECK(hipGetLastError());
         SRG_HIP_CHECK(hipEventRecord(ss->join, ss->stream));
+        ss->pending = (flags & SRG_SPMM_HUB_NOJOIN) != 0;
         if (hub_delay_us() > 0) {
             hipLaunchKernelGGL(k_dispatch_delay, dim3(1), dim3(64), 0, s, hub_delay_us());
             SRG_HIP_CHECK(hipGetLastError());
@@ -2145,13 +2169,21 @@ int srg_gather_rows_f32(const float* src, int64_t lds, int64_t n_src, const int6
     return ok();
 }
 
+int srg_hub_side_streams(void)
+{
+    std::lock_guard<std::mutex> lock(g_side_mu);
+    return (int)g_side.size();
+}
+
 int srg_hub_join(void* stream)
 {
     SRG_DEVICE_GUARD(stream);
     std::lock_guard<std::mutex> lock(g_side_mu);
     auto it = g_side.find(std::make_pair(guard_.dev, static_cast<hipStream_t>(stream)));
-    if (it != g_side.end() && it->second.join)
+    if (it != g_side.end() && it->second.join) {
         SRG_HIP_CHECK(hipStreamWaitEvent(static_cast<hipStream_t>(stream), it->second.join, 0));
+        it->second.pending = false;
+    }
     return ok();
 }
 

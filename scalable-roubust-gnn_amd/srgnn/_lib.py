@@ -58,6 +58,7 @@ EXPORTED_SYMBOLS = (
     "srg_spmm_csr_f64",
     "srg_gather_rows_f32",
     "srg_hub_join",
+    "srg_hub_side_streams",
     "srg_csr_col_splits",
     "srg_csr_mirror",
     "srg_csr_validate",
@@ -135,6 +136,8 @@ def _declare(lib):
     lib.srg_gather_rows_f32.restype = ctypes.c_int
     lib.srg_hub_join.argtypes = [_p]
     lib.srg_hub_join.restype = ctypes.c_int
+    lib.srg_hub_side_streams.argtypes = []
+    lib.srg_hub_side_streams.restype = ctypes.c_int
     lib.srg_csr_validate.argtypes = [_p, _p, _i64, _i64, _i64, _p]
     lib.srg_csr_validate.restype = ctypes.c_int
     lib.srg_comm_unique_id.argtypes = [_p]

@@ -98,7 +98,28 @@ class DeviceCSR:
     # column block 0 only: rows this block computes whole (short rows are not cut: the later blocks
     # do not schedule them, so their Y is written once instead of written, read and written again)
     whole_rows: torch.Tensor | None = None
+    # rows of the output panel a launch may write: the schedule (`order`) names row ids of the whole
+    # operator, so a column block or a row group that schedules a subset of the rows still writes
+    # rows up to row_space - 1 (None: n_rows, a schedule that is a permutation of the rows)
+    row_space: int | None = None
+    # the thresholds the schedule was built with (None = automatic), reused by column blocks
+    thresholds: tuple = (None, None)
     _blocks: dict = field(default_factory=dict, repr=False, compare=False)   # column_blocks() cache
+
+    @property
+    def out_rows(self) -> int:
+        """Rows an output (or aggregation) panel of this operator must have."""
+        return self.n_rows if self.row_space is None else int(self.row_space)
+
+    @property
+    def schedules_subset(self) -> bool:
+        """The schedule covers only some rows of the row space (a column block 1.., a row group)."""
+        return self.out_rows != self.n_rows
+
+    def drop_blocks(self) -> None:
+        """Frees the cached column blocks (compact copies hold one more copy of the ids and
+        values)."""
+        self._blocks.clear()
 
     def heavy(self, d: int) -> int:
         """The slice-wave row count for a panel of d columns (same order, a longer prefix of it
@@ -145,7 +166,8 @@ class DeviceCSR:
                       _lib.stream(device))
         order, n_heavy, n_hub = make_schedule(ip, heavy_threshold, hub_threshold)
         return cls(ip, ix, vv, n_rows, int(n_cols), order, n_heavy, n_hub,
-                   narrow_heavy(ip, n_hub) if _auto_heavy(heavy_threshold) else None)
+                   narrow_heavy(ip, n_hub) if _auto_heavy(heavy_threshold) else None,
+                   thresholds=(heavy_threshold, hub_threshold))
 
     @classmethod
     def from_scipy(cls, adj, heavy_threshold=None, device=None):
@@ -188,20 +210,21 @@ class DeviceCSR:
             splits = torch.where(whole.unsqueeze(0), ip[1:].unsqueeze(0), splits)
             later = torch.nonzero(~whole).squeeze(1)
         bounds = [ip[:-1]] + [splits[b] for b in range(B - 1)] + [ip[1:]]
+        heavy_t, hub_t = self.thresholds
+        auto_narrow = self.n_heavy_narrow is not None      # the parent's narrow split is automatic
         out = []
         for b in range(B):
             beg, end = bounds[b], bounds[b + 1]
             deg = end - beg
             nnz_b = int(deg.sum().item())
+            sel = deg[later] if (b > 0 and whole is not None) else deg
+            order, n_heavy, n_hub = schedule_from_degrees(sel, nnz_b, heavy_t, hub_t)
             if b > 0 and whole is not None:
-                order, n_heavy, n_hub = schedule_from_degrees(deg[later], nnz_b)
                 order = later[order.to(torch.int64)].to(torch.int32)
-                n_sched, narrow = int(later.numel()), narrow_heavy_degrees(deg[later], n_hub)
-            else:
-                order, n_heavy, n_hub = schedule_from_degrees(deg, nnz_b)
-                n_sched, narrow = self.n_rows, narrow_heavy_degrees(deg, n_hub)
-            out.append(DeviceCSR(beg, self.indices, self.values, n_sched, n, order, n_heavy, n_hub, narrow,
-                                 row_end=end, whole_rows=whole if b == 0 else None))
+            narrow = narrow_heavy_degrees(sel, n_hub) if auto_narrow else None
+            out.append(DeviceCSR(beg, self.indices, self.values, int(sel.numel()), n, order, n_heavy, n_hub, narrow,
+                                 row_end=end, whole_rows=whole if b == 0 else None, row_space=self.n_rows,
+                                 thresholds=self.thresholds))
         self._blocks[B] = out
         return out
 
@@ -217,10 +240,13 @@ class DeviceCSR:
                 rows = torch.nonzero(sel).squeeze(1)
                 ip = self.indptr
                 deg = ((self.row_end - ip) if self.is_span else (ip[1:] - ip[:-1]))[rows]
-                order, n_heavy, n_hub = schedule_from_degrees(deg, int(deg.sum().item()))
+                heavy_t, hub_t = self.thresholds
+                order, n_heavy, n_hub = schedule_from_degrees(deg, int(deg.sum().item()), heavy_t, hub_t)
                 order = rows[order.to(torch.int64)].to(torch.int32)
+                narrow = narrow_heavy_degrees(deg, n_hub) if self.n_heavy_narrow is not None else None
                 parts.append(DeviceCSR(self.indptr, self.indices, self.values, int(rows.numel()), self.n_cols, order,
-                                       n_heavy, n_hub, narrow_heavy_degrees(deg, n_hub), row_end=self.row_end))
+                                       n_heavy, n_hub, narrow, row_end=self.row_end, row_space=self.out_rows,
+                                       thresholds=self.thresholds))
             self._blocks["split"] = tuple(parts)
         return self._blocks["split"]
 
@@ -244,7 +270,8 @@ class DeviceCSR:
             idx = torch.repeat_interleave(blk.indptr - bip[:-1], deg, output_size=nnz_b)
             idx += torch.arange(nnz_b, dtype=torch.int64, device=deg.device)
             out.append(DeviceCSR(bip, self.indices[idx], self.values[idx], blk.n_rows, self.n_cols, blk.order,
-                                 blk.n_heavy, blk.n_hub, blk.n_heavy_narrow, whole_rows=blk.whole_rows))
+                                 blk.n_heavy, blk.n_hub, blk.n_heavy_narrow, whole_rows=blk.whole_rows,
+                                 row_space=blk.row_space, thresholds=blk.thresholds))
             del idx
         self._blocks[B] = out
         return out
@@ -260,7 +287,8 @@ class DeviceCSR:
         order, n_heavy, n_hub = make_schedule(ip, heavy_threshold, hub_threshold)
         return DeviceCSR(ip.contiguous(), self.indices[base:end], self.values[base:end],
                          r1 - r0, self.n_cols, order, n_heavy, n_hub,
-                         narrow_heavy(ip, n_hub) if _auto_heavy(heavy_threshold) else None)
+                         narrow_heavy(ip, n_hub) if _auto_heavy(heavy_threshold) else None,
+                         thresholds=(heavy_threshold, hub_threshold))
 
 
 def _auto_heavy(heavy_threshold) -> bool:

@@ -463,8 +463,10 @@ class HaloPartitionedOperator:
                 from . import _lib
                 _lib.call(dev, "srg_csr_validate", lip.data_ptr(), lix.data_ptr(), self.rows + self.halo,
                           lix.numel(), self.ncols_local, _lib.stream(dev))
-            self._A = [DeviceCSR(lip, lix, lvv, n_g, self.ncols_local, order, n_heavy, n_hub, nn)
-                       for (order, n_g, n_heavy, n_hub), nn in zip(self.views + [self.ghost_view], narrow)]
+            # the groups write own rows of the panel, the ghost launch the ghost slots of its halo
+            spaces = [self.rows] * len(self.views) + [self.rows + self.halo]
+            self._A = [DeviceCSR(lip, lix, lvv, n_g, self.ncols_local, order, n_heavy, n_hub, nn, row_space=rs)
+                       for (order, n_g, n_heavy, n_hub), nn, rs in zip(self.views + [self.ghost_view], narrow, spaces)]
             self._spmm = lambda A, X, out: spmm(A, X, out=out)
         else:
             self._A = [(lip, lix, lvv, order) for (order, _, _, _) in self.views + [self.ghost_view]]
@@ -488,7 +490,7 @@ class HaloPartitionedOperator:
         else:
             from .csr import DeviceCSR
             other._A = [DeviceCSR(a.indptr, a.indices, lvv, a.n_rows, a.n_cols, a.order, a.n_heavy, a.n_hub,
-                                  a.n_heavy_narrow)
+                                  a.n_heavy_narrow, row_space=a.row_space)
                         for a in self._A]
         return other
 

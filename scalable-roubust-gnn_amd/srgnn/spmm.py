@@ -46,7 +46,11 @@ def column_blocks_for(A: DeviceCSR, B: int, hops: int | None = None):
     """A's column blocks for a run of `hops` hops: spans, or compact copies for long runs."""
     if _COMPACT and hops is not None and hops >= MIN_HOPS_TO_COMPACT and not A.is_span:
         free, _ = torch.cuda.mem_get_info(A.device)
-        if A.nnz * (A.indices.element_size() + A.values.element_size()) <= free // 4:
+        # the copies (ids + values of every block: nnz entries) stay; while a block is copied its
+        # int64 gather index, the arange added to it and repeat_interleave's output (<= nnz
+        # entries each) are alive too
+        copies = A.nnz * (A.indices.element_size() + A.values.element_size())
+        if copies + 24 * A.nnz <= free // 4:
             return A.compact_column_blocks(B)
     return A.column_blocks(B)
 
@@ -69,6 +73,10 @@ def hop(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, nt_store: bool = False
     and A's rows allow it; bitwise the same either way.  agg = (panel, w, init): the aggregation
     step fused into the (last) launch's epilogue, as spmm_agg."""
     d = X.shape[1]
+    # every launch below writes rows of A's whole row space (the blocks' schedules name them)
+    _check_panel(out, A.out_rows, "out", d)
+    if agg is not None:
+        _check_panel(agg[0], A.out_rows, "agg", d)
     B = auto_col_blocks(A, d) if col_blocks is None else int(col_blocks)
     blocks = (A.column_blocks(B) if B > 1 else None) or [A]
     # a block's rows are short: 2 gathers per packed row in flight (d >= 128: 4 or 2 rows per wave;
@@ -119,8 +127,11 @@ def spmm(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor | None = None, accumul
     if out is None:
         if accumulate:
             raise ValueError("accumulate=True needs an out tensor")
+        if A.schedules_subset:
+            raise ValueError("this operator (a column block or row group) writes only some rows of a "
+                             f"{A.out_rows}-row panel: pass out")
         out = torch.empty((A.n_rows, d), dtype=torch.float32, device=X.device)
-    _check_panel(out, A.n_rows, "out", d)
+    _check_panel(out, A.out_rows, "out", d)
     if out.device != A.device or X.device != A.device:
         raise ValueError("A, X and out must be on the same device")
     flags = (_lib.SRG_SPMM_ACCUMULATE if accumulate else 0) | (_lib.SRG_SPMM_NT_STORE if nt_store else 0) | \
@@ -155,8 +166,8 @@ def spmm_agg(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, agg: torch.Tensor
     accumulate: the chains continue from out's content (the last block of a column-blocked hop)."""
     _check_panel(X, A.n_cols, "X")
     d = X.shape[1]
-    _check_panel(out, A.n_rows, "out", d)
-    _check_panel(agg, A.n_rows, "agg", d)
+    _check_panel(out, A.out_rows, "out", d)
+    _check_panel(agg, A.out_rows, "agg", d)
     if not (out.device == X.device == agg.device == A.device):
         raise ValueError("A, X, out and agg must be on the same device")
     flags = (_lib.SRG_SPMM_NT_STORE if nt_store else 0) | (_lib.SRG_SPMM_ACCUMULATE if accumulate else 0) | \
@@ -179,7 +190,7 @@ def spmm_send(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, send: torch.Tens
     _no_spans(A, "spmm_send")
     _check_panel(X, A.n_cols, "X")
     d = X.shape[1]
-    _check_panel(out, A.n_rows, "out", d)
+    _check_panel(out, A.out_rows, "out", d)
     if not isinstance(send, torch.Tensor) or send.dtype != torch.float32 or send.dim() != 2 or \
             send.shape[1] != d or send.stride(1) != 1 or send.device != A.device:
         raise ValueError("send must be a float32 [m, d] row-major tensor on A's device")
@@ -208,10 +219,10 @@ def spmm_cheby(A: DeviceCSR, Tc: torch.Tensor, out: torch.Tensor, mode: int, a1:
     _no_spans(A, "spmm_cheby")
     _check_panel(Tc, A.n_cols, "Tc")
     d = Tc.shape[1]
-    _check_panel(out, A.n_rows, "out", d)
+    _check_panel(out, A.out_rows, "out", d)
     if To is not None:
-        _check_panel(To, A.n_rows, "To", d)
-    if not isinstance(R, torch.Tensor) or R.dtype != torch.float32 or R.dim() != 3 or R.shape[1] < A.n_rows \
+        _check_panel(To, A.out_rows, "To", d)
+    if not isinstance(R, torch.Tensor) or R.dtype != torch.float32 or R.dim() != 3 or R.shape[1] < A.out_rows \
             or R.shape[2] != d or R.stride(2) != 1 or R.device != A.device:
         raise ValueError("R must be a float32 [n_scales, rows, d] tensor with unit column stride on A's device")
     if not (Tc.device == out.device == A.device) or (To is not None and To.device != A.device):

@@ -1,0 +1,220 @@
+"""The benchmark configurations of BASELINE.json at full size, in the layouts bench.py times.
+
+Each hop is checked against the CPU oracle (oracle/srg_oracle.c: one fp32 fma chain per output
+element in CSR order, matmul.c:23-40) fed with the GPU's previous hop: bit for bit on every row
+where the oracle finishes in seconds (arxiv), on sampled rows plus the longest rows elsewhere --
+the rows' own entries with their columns renumbered over the X rows they gather, so the check
+needs only those rows of the previous panel.  The wavelet filter's fp32 orders are checked the
+same way against the oracle's fp32 chain and within 1e-5 against an fp64 evaluation of the same
+recurrence step (pygsp cheby_op, base_model.py:236-265).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_gb():
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return torch.cuda.mem_get_info()[0] / 1e9
+
+
+def _sample(ip, ix, vals, n, n_random, n_top, seed):
+    """(rows, sub-CSR over renumbered columns, the X rows it gathers) -- device-side extraction."""
+    deg = ip[1:] - ip[:-1]
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    pick = [torch.randint(0, n, (n_random,), generator=g).cuda(), torch.sort(deg, descending=True).indices[:n_top]]
+    rows = torch.unique(torch.cat(pick))
+    beg, cnt = ip[rows], deg[rows]
+    tot = int(cnt.sum())
+    pos = torch.repeat_interleave(beg - torch.cumsum(cnt, 0) + cnt, cnt, output_size=tot) + \
+        torch.arange(tot, device="cuda")
+    ucols, inv = torch.unique(ix[pos].long(), return_inverse=True)
+    sub = (np.r_[0, np.cumsum(cnt.cpu().numpy())].astype(np.int64), inv.to(torch.int32).cpu().numpy(),
+           vals[pos].cpu().numpy())
+    return rows, sub, ucols
+
+
+def _check_rows(oracle_mod, rows, sub, ucols, prev, got, what):
+    want = oracle_mod.spmm(*sub, prev[ucols].cpu().numpy())
+    have = got[rows].cpu().numpy()
+    bad = np.flatnonzero((have.view(np.uint32) != want.view(np.uint32)).any(axis=1))
+    assert bad.size == 0, f"{what}: {bad.size} of {rows.numel()} sampled rows differ (first row {int(rows[bad[0]])})"
+
+
+def test_products_timed_layout_every_hop_bit_exact(oracle_mod):
+    """The operator bench.py times on the headline config: products-shaped graph (126 M nonzeros),
+    K = 10, d = 128, default thresholds, four COMPACT column blocks (>= 48 hops), short rows
+    (<= BLOCK_WHOLE_MAX = 32) whole in block 0, 2 gathers per packed row (PACKED_U2) -- every hop
+    checked on 3000 random rows plus the 50 longest against the oracle fed with the GPU's previous
+    hop."""
+    from srgnn import csr as csr_mod, graphs, spmm as spmm_mod, synth
+    from srgnn.csr import DeviceCSR
+    from srgnn.spmm import auto_col_blocks, column_blocks_for, propagate
+    assert csr_mod.BLOCK_WHOLE_MAX == 32 and spmm_mod._U2_BLOCKED and csr_mod.DEFAULT_HEAVY_THRESHOLD is None
+    ip, ix, vals, n, d, K = graphs.build("products", "cuda")
+    assert K == 10 and d == 128
+    A = DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, device="cuda")
+    hops = K * 25                                   # the driver's 20 steps + 5 warm-up
+    B = auto_col_blocks(A, d, hops=hops)
+    assert B == 4
+    blocks = column_blocks_for(A, B, hops=hops)
+    assert len(blocks) == 4 and not blocks[0].is_span and blocks[0].whole_rows is not None
+    assert sum(b.nnz for b in blocks) == A.nnz and A.n_hub >= 1
+    x = synth.uniform_features_t(n, d, seed=synth.FEATURE_SEED, device="cuda")
+    panels = propagate(A, x, K)                     # col_blocks from auto_col_blocks: the cached 4
+    torch.cuda.synchronize()
+    rows, sub, ucols = _sample(ip, ix, vals, n, 3000, 50, seed=31)
+    for k in range(1, K + 1):
+        _check_rows(oracle_mod, rows, sub, ucols, panels[k - 1], panels[k], f"products hop {k}")
+
+
+def test_arxiv_k5_every_row_bit_exact(oracle_mod):
+    """arxiv-shaped graph (169 K nodes, 2.48 M nonzeros), K = 5, d = 128 (BASELINE configs[1]):
+    every row of every hop equals the oracle's own 5-hop chain from X, bit for bit."""
+    from srgnn import graphs, synth
+    from srgnn.csr import DeviceCSR
+    from srgnn.spmm import auto_col_blocks, propagate
+    ip, ix, vals, n, d, K = graphs.build("arxiv", "cuda")
+    assert K == 5 and d == 128
+    A = DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, device="cuda")
+    assert auto_col_blocks(A, d, hops=K * 25) == 1          # X is cache-resident: one launch per hop
+    x = synth.uniform_features_t(n, d, seed=synth.FEATURE_SEED, device="cuda")
+    panels = propagate(A, x, K)
+    torch.cuda.synchronize()
+    want = oracle_mod.propagate(ip.cpu().numpy(), ix.cpu().numpy(), vals.cpu().numpy(), x.cpu().numpy(), K)
+    for k in range(1, K + 1):
+        got = panels[k].cpu().numpy()
+        assert np.array_equal(got.view(np.uint32), want[k].view(np.uint32)), f"arxiv hop {k}"
+
+
+@pytest.mark.timeout(900)
+def test_rmat26_d256_k8_blocked_sampled_rows_bit_exact(oracle_mod):
+    """RMAT-26 (67 M nodes, 2.2e9 nonzeros: int64 row pointers), d = 256, K = 8 in bench.py's
+    layout for it (two ping-pong panels, four column blocks as row spans): every hop checked on
+    1500 random rows plus the 5 longest against the oracle fed with the GPU's previous hop."""
+    from srgnn import graphs, synth
+    from srgnn.csr import DeviceCSR
+    from srgnn.spmm import auto_col_blocks, column_blocks_for, hop
+    if _free_gb() < 235:
+        pytest.skip("needs a full MI355X (235 GB free)")
+    ip, ix, vals, n, d, K = graphs.build("rmat26", "cuda")
+    assert d == 256 and K == 8 and int(ip[-1]) > 2 ** 31
+    A = DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, device="cuda", validate=False)
+    B = auto_col_blocks(A, d, hops=K * 2)
+    assert B == 4 and column_blocks_for(A, B, hops=K * 2)
+    rows, sub, ucols = _sample(ip, ix, vals, n, 1500, 5, seed=32)
+    del ip, ix, vals
+    cur = synth.uniform_features_t(n, d, seed=synth.FEATURE_SEED, device="cuda")
+    bufs = [torch.empty_like(cur), torch.empty_like(cur)]
+    for k in range(1, K + 1):
+        nxt = bufs[k % 2]
+        hop(A, cur, nxt, col_blocks=B)
+        torch.cuda.synchronize()
+        _check_rows(oracle_mod, rows, sub, ucols, cur, nxt, f"rmat26 hop {k}")
+        cur = nxt
+
+
+@pytest.mark.timeout(900)
+def test_papers100M_blocked_hop_sampled_rows_bit_exact(oracle_mod):
+    """papers100M-shaped graph (111 M nodes, 3.34e9 nonzeros), d = 128, in the four-column-block
+    layout bench.py times it in: two hops, each checked on 1500 random rows plus the 10 longest
+    against the oracle fed with the GPU's previous hop."""
+    from srgnn import graphs, synth
+    from srgnn.csr import DeviceCSR
+    from srgnn.spmm import auto_col_blocks, column_blocks_for, hop
+    if _free_gb() < 180:
+        pytest.skip("needs a full MI355X (180 GB free)")
+    ip, ix, vals, n, d, K = graphs.build("papers100M", "cuda")
+    A = DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, device="cuda", validate=False)
+    B = auto_col_blocks(A, d, hops=K * 2)
+    assert B == 4 and column_blocks_for(A, B, hops=K * 2)
+    rows, sub, ucols = _sample(ip, ix, vals, n, 1500, 10, seed=33)
+    del ip, ix, vals
+    cur = synth.uniform_features_t(n, d, seed=synth.FEATURE_SEED, device="cuda")
+    nxt = torch.empty_like(cur)
+    for k in (1, 2):
+        hop(A, cur, nxt, col_blocks=B)
+        torch.cuda.synchronize()
+        _check_rows(oracle_mod, rows, sub, ucols, cur, nxt, f"papers100M hop {k}")
+        cur, nxt = nxt, cur
+
+
+@pytest.mark.timeout(900)
+def test_rmat26_wavelet_orders_sampled_rows(oracle_mod):
+    """The RMAT-26 heat-wavelet filter bank (bench.py --op wavelet): L and F = (2/a1)(L - a2 I) in
+    four column blocks, a 64-column block of the panel, Chebyshev order 3, two scales.  Per order,
+    on 1500 random rows plus the 5 longest: the SpMM equals the oracle's fp32 chain bit for bit,
+    and T_{k+1} is within 1e-5 (normwise per row) of the fp64 recurrence step evaluated from the
+    GPU's T_k, T_{k-1}; the filter's R (the lean split path, as bench.py runs it) equals the
+    per-order steps' result bit for bit."""
+    from srgnn import _lib, graphs, synth
+    from srgnn import wavelet as W
+    from srgnn.spmm import hop
+    if _free_gb() < 200:
+        pytest.skip("needs a full MI355X (200 GB free)")
+    ip, ix, lv, n, d, lmax = graphs.build_laplacian("rmat26", "cuda")
+    filt = W.HeatWaveletFilter.from_device(ip, ix, lv, n, [-0.5, 0.5], order=3, lmax=lmax, dtype=torch.float32)
+    cb = 64
+    B = filt.prepare_column_blocks(cb, hops=3 * 4 * 2)
+    assert B == 4
+    rows, subL, ucols = _sample(ip, ix, filt.lvals, n, 1500, 5, seed=34)
+    subF = (subL[0], subL[1], filt.fvals[_positions(ip, rows)].cpu().numpy())
+    lv64 = lv.to(torch.float64)[_positions(ip, rows)].cpu().numpy()
+    f64 = ((2.0 / filt.a1) * np.where(ucols.cpu().numpy()[subL[1]] == np.repeat(rows.cpu().numpy(), np.diff(subL[0])),
+                                      lv64 - filt.a2, lv64))
+    del ip, ix, lv
+    S = synth.uniform_features_t(n, cb, seed=synth.FEATURE_SEED, device="cuda")
+    Lm, Fm = filt._csr(filt.lvals), filt._csr(filt.fvals)
+    T = [S]
+    # order 1: y = L S (checked), then the INIT_T epilogue turns it into T1 = (y - a2 S) / a1 in place
+    y = torch.empty_like(S)
+    hop(Lm, S, y, col_blocks=B)
+    torch.cuda.synchronize()
+    _check_rows(oracle_mod, rows, subL, ucols, S, y, "rmat26 wavelet L @ S")
+    _lib.call(S.device, "srg_cheby_epilogue_f32", y.data_ptr(), cb, S.data_ptr(), cb, None, cb, n, cb,
+              _lib.SRG_CHEBY_INIT_T, filt.a1, filt.a2, None, None, 2, None, cb, n * cb, _lib.stream(S.device))
+    torch.cuda.synchronize()
+    ls64 = torch.from_numpy(_spmm64(subL[0], subL[1], lv64, S[ucols].double().cpu().numpy())).cuda()
+    _close(y[rows].double(), (ls64 - filt.a2 * S[rows].double()) / filt.a1, "T1")
+    T.append(y)
+    for k in (2, 3):
+        y = torch.empty_like(S)
+        hop(Fm, T[-1], y, col_blocks=B)
+        torch.cuda.synchronize()
+        _check_rows(oracle_mod, rows, subF, ucols, T[-1], y, f"rmat26 wavelet F @ T{k - 1}")
+        fy64 = torch.from_numpy(_spmm64(subF[0], subF[1], f64, T[-1][ucols].double().cpu().numpy())).cuda()
+        y.sub_(T[-2])                        # the STEP epilogue's T_{k+1} = F T_k - T_{k-1} (fp32)
+        _close(y[rows].double(), fy64 - T[-2][rows].double(), f"T{k}")
+        T.append(y)
+    # R from the lean split path (what the bench times) against the fp64 sums of the GPU's T's
+    R = filt.apply(S, col_block=cb)
+    torch.cuda.synchronize()
+    c = filt.coeffs
+    for s in range(2):
+        want = (c[s, 0] / 2) * T[0][rows].double() + sum(c[s, k] * T[k][rows].double() for k in (1, 2, 3))
+        _close(R[s][rows].double(), want, f"R scale {s}")
+
+
+def _positions(ip, rows):
+    deg = ip[1:] - ip[:-1]
+    beg, cnt = ip[rows], deg[rows]
+    tot = int(cnt.sum())
+    return torch.repeat_interleave(beg - torch.cumsum(cnt, 0) + cnt, cnt, output_size=tot) + \
+        torch.arange(tot, device=ip.device)
+
+
+def _spmm64(ip, ix, v, X):
+    """fp64 product of the sampled sub-CSR (numpy; scipy's order: products added left to right)."""
+    import scipy.sparse as sp
+    A = sp.csr_matrix((v, ix, ip), shape=(ip.size - 1, X.shape[0]))
+    return np.asarray(A @ X)
+
+
+def _close(got, want, what, tol=1e-5):
+    err = (got - want).norm(dim=1)
+    scale = want.norm(dim=1).clamp_min(1e-30)
+    rel = float((err / scale).max())
+    assert rel <= tol, f"{what}: max row-normwise relative error {rel:.3g} > {tol}"

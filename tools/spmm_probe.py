@@ -28,21 +28,57 @@ ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--identity", action="store_true")
 ap.add_argument("--heavy-threshold", type=int, default=None)
 ap.add_argument("--col-blocks", type=int, default=None, help="column blocks per hop (default: auto_col_blocks)")
+ap.add_argument("--d", type=int, default=None, help="panel width (default: the config's)")
+ap.add_argument("--hops", type=int, default=1 << 30,
+                help="hops the operator serves (bench.py: K x (steps + warmup)); picks spans or compact blocks")
+ap.add_argument("--op", default="khop", choices=["khop", "wavelet"],
+                help="wavelet: the Chebyshev STEP operator F = (2/a1)(L - a2 I) of the config's Laplacian "
+                     "on a --col-block wide panel (bench.py --op wavelet's SpMM launches)")
+ap.add_argument("--col-block", type=int, default=None,
+                help="wavelet: column block width (default: bench.py's rule, the widest whose work panels fit)")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
+if a.op == "wavelet":
+    from srgnn import wavelet as W
+    ip, ix, lv, n, d, lmax = graphs.build_laplacian(a.config, dev, d=a.d)
+    filt = W.HeatWaveletFilter.from_device(ip, ix, lv, n, [-0.5, 0.5], order=3, lmax=lmax, dtype=torch.float32,
+                                           heavy_threshold=a.heavy_threshold)
+    S = synth.uniform_features_t(n, d, device=dev)
+    R = torch.empty((2, n, d), dtype=torch.float32, device=dev)     # resident as in bench.py
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    free, _ = torch.cuda.mem_get_info(dev)
+    cb = a.col_block or d
+    while not a.col_block and cb > 8 and filt.work_panels() * n * cb * 4 > free - 2 ** 30:
+        cb //= 2
+    d = cb
+    B = filt.prepare_column_blocks(d, hops=a.hops)
+    A = filt._csr(filt.fvals)
+    X = S[:, :d]
+    Y = torch.empty((n, d), dtype=torch.float32, device=dev)
+    torch.cuda.synchronize()
+    for _ in range(a.reps):
+        hop(A, X, Y, col_blocks=B)
+    torch.cuda.synchronize()
+    nnz = A.nnz
+    print(json.dumps({"config": a.config, "op": "wavelet", "n": n, "nnz": nnz, "d": d, "reps": a.reps,
+                      "launches_per_hop": B, "n_heavy": A.n_heavy, "n_hub": A.n_hub,
+                      "algorithmic_bytes": roofline.bytes_no_reuse(n, nnz, d),
+                      "compulsory_bytes": roofline.bytes_compulsory(n, nnz, d)}))
+    sys.exit(0)
 if a.identity:
     n, d = 4 * 1024 * 1024, 128          # 2 GiB panel (> 256 MiB Infinity Cache)
     ip = torch.arange(n + 1, dtype=torch.int64, device=dev)
     ix = torch.arange(n, dtype=torch.int32, device=dev)
     vals = torch.ones(n, dtype=torch.float32, device=dev)
 else:
-    ip, ix, vals, n, d, _ = graphs.build(a.config, dev)
+    ip, ix, vals, n, d, _ = graphs.build(a.config, dev, d=a.d)
 A = DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, heavy_threshold=a.heavy_threshold, device=dev)
 X = synth.uniform_features_t(n, d, device=dev)
 Y = torch.empty_like(X)
 # the probe stands for a long run of hops (bench.py's operator serves every step): the panel rule alone
-B = 1 if a.identity else (a.col_blocks if a.col_blocks is not None else auto_col_blocks(A, d, hops=1 << 30))
-B = B if B > 1 and column_blocks_for(A, B, hops=1 << 30) else 1   # compact blocks, as bench.py
+B = 1 if a.identity else (a.col_blocks if a.col_blocks is not None else auto_col_blocks(A, d, hops=a.hops))
+B = B if B > 1 and column_blocks_for(A, B, hops=a.hops) else 1   # spans or compact blocks, as bench.py
 torch.cuda.synchronize()
 for _ in range(a.reps):
     hop(A, X, Y, col_blocks=B)      # one hop = B k_spmm launches (column blocks), same bits
