@@ -283,6 +283,30 @@ int srg_csr_mirror(const int64_t* indptr, const int32_t* indices, const int64_t*
 int srg_csr_validate(const int64_t* indptr, const int32_t* indices, int64_t n_rows,
                      int64_t nnz, int64_t n_cols, void* stream);
 
+/* ---- sparse x sparse: the wavelet model's phi * phi^-1 (torch_sparse.spspmm / spmm) ------------------
+ * SpectralModel.preprocess (SSRG/models/base_scalable/base_model.py:208-219) multiplies the two sparse
+ * wavelet bases with torch_sparse.spspmm and the product into the features with torch_sparse.spmm
+ * (torch_sparse is absent here; its published CPU algorithms, which are scipy csr_matmat's arithmetic,
+ * are restated): C[i,j] = ((0 + A[i,k1]*B[k1,j]) + A[i,k2]*B[k2,j]) + ... over row i of A in stored
+ * order, each product rounded before it is added; sums equal to 0 dropped; columns ascending.
+ * Two passes over the same arguments: phase 0 writes c_cnt[m] (entries per row of C); the caller
+ * forms c_ptr (m + 1, exclusive prefix sum) and allocates C; phase 1 fills c_idx / c_val.
+ * B with more than 16384 columns needs `scratch` (device, srg_spgemm_scratch_bytes() bytes, or any
+ * smaller multiple of one row accumulator: fewer workgroups); B's row pointers index b_idx / b_val,
+ * its column ids must be < n_cols.  SRG_SPGEMM_SERIAL_B: B's rows may repeat a column id (then each
+ * B row is walked by one lane).  Asynchronous on `stream`. */
+#define SRG_SPGEMM_SERIAL_B 0x1u
+int srg_spgemm_scratch_bytes(int64_t m, int64_t n_cols, int64_t* bytes);
+int srg_spgemm_f32(int phase, const int64_t* a_ptr, const int32_t* a_idx, const float* a_val, int64_t m,
+                   const int64_t* b_ptr, const int32_t* b_idx, const float* b_val, int64_t n_cols,
+                   int64_t* c_cnt, const int64_t* c_ptr, int32_t* c_idx, float* c_val, void* scratch,
+                   int64_t scratch_bytes, uint32_t flags, void* stream);
+/* torch_sparse.spmm(index, value, m, n, matrix) (index_select, mul, scatter_add): Y[r, :] = sum over
+ * row r's entries in stored order of (v * X[c, :]), each product rounded, then added, from +0.  A CSR
+ * whose rows hold the COO entries in index order (a stable sort by row). */
+int srg_spmm_muladd_f32(const int64_t* indptr, const int32_t* indices, const float* values, int64_t n_rows,
+                        const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t d, void* stream);
+
 /* ---- multi-GPU: communicators and the row-partitioned K-hop propagation ---------------------------
  * SURVEY.md §8(b) item 5, for C / C++ hosts (the Python package drives the same kernels through
  * torch.distributed: srgnn/dist.py).  RCCL is loaded at run time.  Rank r owns rows

@@ -37,6 +37,8 @@ SRG_ACC_ADD = 1
 SRG_ACC_DIV = 2
 SRG_TAIL_MAX = 32
 
+SRG_SPGEMM_SERIAL_B = 0x1
+
 # every symbol include/srgnn_hip.h declares (checked by tests/test_capi.py)
 EXPORTED_SYMBOLS = (
     "FloatCSRMulDenseOMP",
@@ -57,6 +59,9 @@ EXPORTED_SYMBOLS = (
     "srg_segment_sum_f32",
     "srg_spmm_csr_f64",
     "srg_gather_rows_f32",
+    "srg_spgemm_scratch_bytes",
+    "srg_spgemm_f32",
+    "srg_spmm_muladd_f32",
     "srg_hub_join",
     "srg_hub_side_streams",
     "srg_csr_col_splits",
@@ -134,6 +139,13 @@ def _declare(lib):
     lib.srg_spmm_csr_f64.restype = ctypes.c_int
     lib.srg_gather_rows_f32.argtypes = [_p, _i64, _i64, _p, _i64, _p, _i64, _i32, _p]
     lib.srg_gather_rows_f32.restype = ctypes.c_int
+    lib.srg_spgemm_scratch_bytes.argtypes = [_i64, _i64, ctypes.POINTER(_i64)]
+    lib.srg_spgemm_scratch_bytes.restype = ctypes.c_int
+    lib.srg_spgemm_f32.argtypes = [ctypes.c_int, _p, _p, _p, _i64, _p, _p, _p, _i64, _p, _p, _p, _p, _p, _i64,
+                                   _u32, _p]
+    lib.srg_spgemm_f32.restype = ctypes.c_int
+    lib.srg_spmm_muladd_f32.argtypes = [_p, _p, _p, _i64, _p, _i64, _p, _i64, _i32, _p]
+    lib.srg_spmm_muladd_f32.restype = ctypes.c_int
     lib.srg_hub_join.argtypes = [_p]
     lib.srg_hub_join.restype = ctypes.c_int
     lib.srg_hub_side_streams.argtypes = []

@@ -106,28 +106,41 @@ class HeatWaveletFilter:
     """R_s = sum_k c_{s,k} T_k(L~) S for the heat kernels exp(-tau_s x / lmax), every scale at once."""
 
     def __init__(self, L: sp.spmatrix, taus, order: int = 3, lmax: float | None = None,
-                 dtype=torch.float64, device=None, heavy_threshold=None, hub_threshold=None):
+                 dtype=torch.float64, device=None, heavy_threshold=None, hub_threshold=None, coeffs=None):
         L = _explicit_diagonal(sp.csr_matrix(L))
         lmax = float(lmax) if lmax is not None else estimate_lmax(L)
         dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self._setup(torch.from_numpy(L.indptr.astype(np.int64)).to(dev),
                     torch.from_numpy(L.indices.astype(np.int32)).to(dev),
                     torch.from_numpy(L.data.astype(np.float64)).to(dev), L.shape[0], taus, order, lmax,
-                    dtype, heavy_threshold, hub_threshold)
+                    dtype, heavy_threshold, hub_threshold, coeffs)
+
+    @classmethod
+    def from_coefficients(cls, L: sp.spmatrix, coeffs, lmax: float, dtype=torch.float64, device=None):
+        """The Chebyshev recurrence of pygsp's cheby_op(G, c, S) with the coefficient rows `coeffs`
+        ([n_scales, order + 1], any filter) on the Laplacian L."""
+        return cls(L, None, lmax=lmax, dtype=dtype, device=device, coeffs=coeffs)
 
     @classmethod
     def from_device(cls, indptr: torch.Tensor, indices: torch.Tensor, lvals: torch.Tensor, n: int, taus,
                     order: int = 3, lmax: float = None, dtype=torch.float32, heavy_threshold=None,
-                    hub_threshold=None):
+                    hub_threshold=None, coeffs=None):
         """From a device CSR of L with every diagonal entry stored (e.g. normalize.laplacian_edges_blocked)
-        and an explicit lmax (pygsp's ARPACK estimate is a host computation)."""
+        and an explicit lmax (pygsp's ARPACK estimate is a host computation); `coeffs` instead of
+        `taus` / `order`: explicit Chebyshev coefficient rows."""
         if lmax is None:
             raise ValueError("lmax is required for a device-built Laplacian")
         self = cls.__new__(cls)
-        self._setup(indptr, indices, lvals, n, taus, order, float(lmax), dtype, heavy_threshold, hub_threshold)
+        self._setup(indptr, indices, lvals, n, taus, order, float(lmax), dtype, heavy_threshold, hub_threshold,
+                    coeffs)
         return self
 
-    def _setup(self, indptr, indices, lvals, n, taus, order, lmax, dtype, heavy_threshold, hub_threshold):
+    def _setup(self, indptr, indices, lvals, n, taus, order, lmax, dtype, heavy_threshold, hub_threshold,
+               coeffs=None):
+        if coeffs is not None:
+            coeffs = np.atleast_2d(np.asarray(coeffs, dtype=np.float64))
+            order = coeffs.shape[1] - 1
+            taus = [None] * coeffs.shape[0]
         if order < 1:
             raise ValueError("order must be >= 1")
         if len(taus) < 1 or len(taus) > 8:
@@ -138,8 +151,12 @@ class HeatWaveletFilter:
         self.n = int(n)
         self.lmax = lmax
         self.a1 = self.a2 = self.lmax / 2.0
-        self.taus = [float(t) for t in taus]
-        self.coeffs = np.stack([heat_cheby_coeffs(t, self.lmax, order) for t in self.taus])
+        if coeffs is not None:
+            self.taus = taus
+            self.coeffs = coeffs
+        else:
+            self.taus = [float(t) for t in taus]
+            self.coeffs = np.stack([heat_cheby_coeffs(t, self.lmax, order) for t in self.taus])
         self.dtype = dtype
         self.indptr, self.indices = indptr, indices
         # F = (2/a1)(L - a2 I), formed in fp64 then rounded (the diagonal is stored explicitly)

@@ -145,11 +145,15 @@ def test_papers100M_blocked_hop_sampled_rows_bit_exact(oracle_mod):
 @pytest.mark.timeout(900)
 def test_rmat26_wavelet_orders_sampled_rows(oracle_mod):
     """The RMAT-26 heat-wavelet filter bank (bench.py --op wavelet): L and F = (2/a1)(L - a2 I) in
-    four column blocks, a 64-column block of the panel, Chebyshev order 3, two scales.  Per order,
-    on 1500 random rows plus the 5 longest: the SpMM equals the oracle's fp32 chain bit for bit,
-    and T_{k+1} is within 1e-5 (normwise per row) of the fp64 recurrence step evaluated from the
-    GPU's T_k, T_{k-1}; the filter's R (the lean split path, as bench.py runs it) equals the
-    per-order steps' result bit for bit."""
+    four column blocks, a 64-column block of the panel, Chebyshev order 3, two scales, fp32.  Per
+    order, on 1500 random rows plus the 5 longest:
+      * the SpMM equals the oracle's fp32 chain bit for bit (fed with the GPU's previous T);
+      * T_{k+1} and every scale's output R agree with the fp64 evaluation of the same step (pygsp's
+        arithmetic, base_model.py:236-265) within the fp32 forward-error bound of the step,
+        gamma_{deg+c} * (sum of |terms|), gamma_n = n u / (1 - n u), u = 2^-24, element by element;
+      * rows of degree <= 64 (the bulk of the graph) within 1e-5 normwise.
+    Rows with ~10^5-10^6 nonzeros accumulate fp32 rounding over their chains (the fp64 entry,
+    srg_cheby_step_f64, is the reference's precision at twice the bytes)."""
     from srgnn import _lib, graphs, synth
     from srgnn import wavelet as W
     from srgnn.spmm import hop
@@ -161,6 +165,7 @@ def test_rmat26_wavelet_orders_sampled_rows(oracle_mod):
     B = filt.prepare_column_blocks(cb, hops=3 * 4 * 2)
     assert B == 4
     rows, subL, ucols = _sample(ip, ix, filt.lvals, n, 1500, 5, seed=34)
+    deg = torch.from_numpy(np.diff(subL[0])).cuda().double().unsqueeze(1)
     subF = (subL[0], subL[1], filt.fvals[_positions(ip, rows)].cpu().numpy())
     lv64 = lv.to(torch.float64)[_positions(ip, rows)].cpu().numpy()
     f64 = ((2.0 / filt.a1) * np.where(ucols.cpu().numpy()[subL[1]] == np.repeat(rows.cpu().numpy(), np.diff(subL[0])),
@@ -169,6 +174,11 @@ def test_rmat26_wavelet_orders_sampled_rows(oracle_mod):
     S = synth.uniform_features_t(n, cb, seed=synth.FEATURE_SEED, device="cuda")
     Lm, Fm = filt._csr(filt.lvals), filt._csr(filt.fvals)
     T = [S]
+
+    def prod64(vals, P, absolute=False):
+        x = P[ucols].double().cpu().numpy()
+        out = _spmm64(subL[0], subL[1], np.abs(vals) if absolute else vals, np.abs(x) if absolute else x)
+        return torch.from_numpy(out).cuda()
     # order 1: y = L S (checked), then the INIT_T epilogue turns it into T1 = (y - a2 S) / a1 in place
     y = torch.empty_like(S)
     hop(Lm, S, y, col_blocks=B)
@@ -177,25 +187,43 @@ def test_rmat26_wavelet_orders_sampled_rows(oracle_mod):
     _lib.call(S.device, "srg_cheby_epilogue_f32", y.data_ptr(), cb, S.data_ptr(), cb, None, cb, n, cb,
               _lib.SRG_CHEBY_INIT_T, filt.a1, filt.a2, None, None, 2, None, cb, n * cb, _lib.stream(S.device))
     torch.cuda.synchronize()
-    ls64 = torch.from_numpy(_spmm64(subL[0], subL[1], lv64, S[ucols].double().cpu().numpy())).cuda()
-    _close(y[rows].double(), (ls64 - filt.a2 * S[rows].double()) / filt.a1, "T1")
+    s_abs = filt.a2 * S[rows].double().abs()
+    _within_fp32(y[rows].double(), (prod64(lv64, S) - filt.a2 * S[rows].double()) / filt.a1,
+                 (prod64(lv64, S, True) + s_abs) / filt.a1, deg + 3, deg, "T1")
     T.append(y)
     for k in (2, 3):
         y = torch.empty_like(S)
         hop(Fm, T[-1], y, col_blocks=B)
         torch.cuda.synchronize()
         _check_rows(oracle_mod, rows, subF, ucols, T[-1], y, f"rmat26 wavelet F @ T{k - 1}")
-        fy64 = torch.from_numpy(_spmm64(subF[0], subF[1], f64, T[-1][ucols].double().cpu().numpy())).cuda()
         y.sub_(T[-2])                        # the STEP epilogue's T_{k+1} = F T_k - T_{k-1} (fp32)
-        _close(y[rows].double(), fy64 - T[-2][rows].double(), f"T{k}")
+        _within_fp32(y[rows].double(), prod64(f64, T[-1]) - T[-2][rows].double(),
+                     prod64(f64, T[-1], True) + T[-2][rows].double().abs(), deg + 2, deg, f"T{k}")
         T.append(y)
     # R from the lean split path (what the bench times) against the fp64 sums of the GPU's T's
     R = filt.apply(S, col_block=cb)
     torch.cuda.synchronize()
     c = filt.coeffs
     for s in range(2):
-        want = (c[s, 0] / 2) * T[0][rows].double() + sum(c[s, k] * T[k][rows].double() for k in (1, 2, 3))
-        _close(R[s][rows].double(), want, f"R scale {s}")
+        terms = [(c[s, 0] / 2) * T[0][rows].double()] + [c[s, k] * T[k][rows].double() for k in (1, 2, 3)]
+        _within_fp32(R[s][rows].double(), sum(terms), sum(t.abs() for t in terms), torch.full_like(deg, 8.0), deg,
+                     f"R scale {s}")
+
+
+def _within_fp32(got, want, abs_terms, n_ops, deg, what, tol=1e-5, bulk_degree=64):
+    """Element-wise |got - want| <= gamma_{n_ops} * abs_terms (the fp32 forward-error bound of a
+    chain of n_ops roundings over terms whose magnitudes sum to abs_terms), and rows of degree <=
+    bulk_degree within `tol` normwise."""
+    u = 2.0 ** -24
+    gamma = n_ops * u / (1 - n_ops * u)
+    err = (got - want).abs()
+    over = err > gamma * abs_terms
+    assert not bool(over.any()), f"{what}: {int(over.any(dim=1).sum())} rows beyond the fp32 error bound, " \
+                                 f"worst ratio {float((err / (gamma * abs_terms).clamp_min(1e-300)).max()):.3g}"
+    bulk = deg.squeeze(1) <= bulk_degree
+    rel = (got - want).norm(dim=1) / want.norm(dim=1).clamp_min(1e-30)
+    worst = float(rel[bulk].max()) if bool(bulk.any()) else 0.0
+    assert worst <= tol, f"{what}: rows of degree <= {bulk_degree}: max normwise relative error {worst:.3g} > {tol}"
 
 
 def _positions(ip, rows):
@@ -213,8 +241,3 @@ def _spmm64(ip, ix, v, X):
     return np.asarray(A @ X)
 
 
-def _close(got, want, what, tol=1e-5):
-    err = (got - want).norm(dim=1)
-    scale = want.norm(dim=1).clamp_min(1e-30)
-    rel = float((err / scale).max())
-    assert rel <= tol, f"{what}: max row-normwise relative error {rel:.3g} > {tol}"

@@ -723,4 +723,4 @@ def test_hub_side_streams_bounded():
         st.synchronize()
         if i % 8 == 0:
             c.check_hop(1, y.cpu().numpy())
-        assert _lib.lib().srg_hub_side_streams() <= 8 * torch.cuda.device_count()
+        assert _lib.query("srg_hub_side_streams") <= 8 * torch.cuda.device_count()
