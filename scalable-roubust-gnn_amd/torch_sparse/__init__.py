@@ -90,21 +90,17 @@ class _SpMM(torch.autograd.Function):
 def spmm(index, value, m, n, matrix):
     """Matrix product of a sparse matrix (COO `index`, `value`, shape m x n) with a dense matrix
     (torch_sparse 0.6.x `spmm`)."""
-    if matrix.shape[-2] != n:
-        raise AssertionError(f"matrix has {matrix.shape[-2]} rows, the sparse matrix {n} columns")
+    if matrix.size(-2) != n:         # torch_sparse's first check (a 1-D matrix raises IndexError here)
+        raise AssertionError(f"matrix has {matrix.size(-2)} rows, the sparse matrix {n} columns")
     home = matrix.device
     dev = _device()
-    squeeze = matrix.dim() == 1
     mat = _on(matrix, dev)
-    mat = mat.unsqueeze(-1) if squeeze else mat
     if mat.dim() != 2:
         raise NotImplementedError("spmm: batched dense operands are not supported by this build")
     if mat.dtype != torch.float32 or value.dtype != torch.float32:
         raise TypeError("spmm computes in float32")
     idx, val = _on(index, dev), _on(value, dev)
-    out = _SpMM.apply(idx[0], idx[-1], val, int(m), mat.contiguous())
-    out = out.squeeze(-1) if squeeze else out
-    return out.to(home)
+    return _SpMM.apply(idx[0], idx[-1], val, int(m), mat.contiguous()).to(home)
 
 
 def coalesce(index, value, m, n, op="add"):
