@@ -195,7 +195,8 @@ def test_spmm_equals_scipy_and_scatter_add(d):
     Xr, vr = X.clone().requires_grad_(True), val.clone().requires_grad_(True)
     torch.zeros(m, d).index_add(0, idx[0], Xr.index_select(0, idx[1]) * vr.unsqueeze(-1)).backward(g)
     np.testing.assert_array_equal(Xg.grad.numpy(), Xr.grad.numpy())
-    torch.testing.assert_close(vg.grad, vr.grad, rtol=1e-6, atol=1e-6)
+    # d-term dot products: the reduction order of the sum over columns is the device's
+    torch.testing.assert_close(vg.grad, vr.grad, rtol=1e-5, atol=1e-5 * float(vr.grad.abs().max()))
     with pytest.raises(IndexError):            # torch_sparse asserts n == matrix.size(-2) first
         torch_sparse.spmm(idx, val, m, n, X[:, 0])
 
