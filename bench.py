@@ -92,6 +92,9 @@ def parse():
     ap.add_argument("--aggregate", default=None, choices=["sum", "mean", "weighted"],
                     help="one GPU: fused hop aggregation (SGC/SSGC/GBP precompute) instead of the K+1 "
                          "panels: sum / mean over hops 0..K, or GBP weights alpha(1-alpha)^k, alpha 0.15")
+    ap.add_argument("--fast", action="store_true",
+                    help="tolerance mode (SRG_SPMM_FAST): hub rows as 64 exact segment chains plus their "
+                         "ordered sum; other rows bit-exact; parity then checked within tolerance")
     ap.add_argument("--pmc", default="auto", choices=["auto", "on", "off"],
                     help="measure the hop's HBM traffic with rocprofv3 --pmc passes of tools/spmm_probe.py "
                          "before this process touches the GPU (auto: one GPU, K-hop, not under a profiler)")
@@ -298,21 +301,34 @@ def oracle_sample(ip, ix, vals, n, n_random, n_top=20, seed=11):
             "ix": inv.to(torch.int32).cpu().numpy(), "v": vals[pos].cpu().numpy()}
 
 
-def parity_vs_oracle(sample, checks):
+def parity_vs_oracle(sample, checks, tolerance=False):
     """Bit-for-bit check of sampled rows of GPU hops against the C oracle (oracle/srg_oracle.c:
     one fp32 fma chain per element in CSR order, matmul.c:23-40) fed with the GPU's previous hop.
-    checks: [(k, prev_panel, panel)].  Test infrastructure used as the checker, outside the
-    timed region; nothing measured runs through it."""
+    checks: [(k, prev_panel, panel)].  tolerance (FAST mode): also whether every element is within
+    the fp32 forward-error bound gamma_{len+65} * sum |a| |x| of the exact value (the oracle's fp64
+    product).  Test infrastructure used as the checker, outside the timed region; nothing measured
+    runs through it."""
     from oracle import oracle as O
-    done, ok = [], True
+    done, ok, within = [], True, True
+    lens = np.diff(sample["ip"]).astype(np.float64)[:, None]
     for k, prev, got in checks:
-        want = O.spmm(sample["ip"], sample["ix"], sample["v"], prev[sample["ucols"]].cpu().numpy())
+        x = prev[sample["ucols"]].cpu().numpy()
+        want = O.spmm(sample["ip"], sample["ix"], sample["v"], x)
         have = got[sample["rows"]].cpu().numpy()
         ok = ok and np.array_equal(have.view(np.uint32), want.view(np.uint32))
+        if tolerance:
+            exact = O.spmm64(sample["ip"], sample["ix"], sample["v"].astype(np.float64), x.astype(np.float64))
+            mag = O.spmm64(sample["ip"], sample["ix"], np.abs(sample["v"]).astype(np.float64), np.abs(x).astype(np.float64))
+            n_ops = lens + 65
+            gamma = n_ops * 2.0 ** -24 / (1 - n_ops * 2.0 ** -24)
+            within = within and bool((np.abs(have.astype(np.float64) - exact) <= gamma * mag).all())
         done.append(k)
-    return {"hops_checked": done, "rows_checked": int(sample["rows"].numel()),
-            "rows": "random rows + the 20 longest", "bit_exact": bool(ok),
-            "checker": "oracle/srg_oracle.c fp32 fma chains fed with the GPU's previous hop (outside the timed region)"}
+    res = {"hops_checked": done, "rows_checked": int(sample["rows"].numel()),
+           "rows": "random rows + the 20 longest", "bit_exact": bool(ok),
+           "checker": "oracle/srg_oracle.c fp32 fma chains fed with the GPU's previous hop (outside the timed region)"}
+    if tolerance:
+        res["within_fp32_bound_of_exact"] = within
+    return res
 
 
 def launch_ranks(n_ranks, args, script=None):
@@ -623,7 +639,7 @@ def main():
             panels = [X] + [buf[k] for k in range(K)]
 
             def step():
-                propagate(A, X, K, panels=panels, nt_store=a.nt_store, col_blocks=col_blocks)
+                propagate(A, X, K, panels=panels, nt_store=a.nt_store, col_blocks=col_blocks, fast=a.fast)
         else:
             from srgnn.aggregate import propagate_aggregate
             panels = [X, None]
@@ -649,7 +665,7 @@ def main():
     elif world > 1:
         from srgnn.dist import HaloPartitionedOperator
         op = HaloPartitionedOperator(ip, ix, vals, n, chunks=(a.chunks or (4 if world <= 2 else 6)), heavy_threshold=a.heavy_threshold,
-                                     device=dev, ghost_max_degree=a.ghost_max_degree)
+                                     device=dev, ghost_max_degree=a.ghost_max_degree, fast=a.fast)
         log(f"rank {rank}: rows={op.rows} nnz={op.nnz_local} halo={op.halo} (received {op.n_recv}, "
             f"ghosts {op.n_ghost} <= degree {op.ghost_max_degree}, {op._ghost_pos.numel()} ghost nnz; "
             f"link {op.link_bps / 1e9:.1f} GB/s) "
@@ -706,13 +722,19 @@ def main():
     if sample is not None and mode == "panels":
         # hop 1 from X and hop K from hop K-1, as the timed steps left them
         oracle_checks = parity_vs_oracle(sample, [(1, panels[0], panels[1])] +
-                                         ([(K, panels[K - 1], panels[K])] if K > 1 else []))
+                                         ([(K, panels[K - 1], panels[K])] if K > 1 else []), tolerance=a.fast)
     if world > 1:
         # the N-GPU hops of this rank's rows against the 1-GPU kernels on the whole graph, bit for bit
-        ok = refs is not None and all(torch.equal(panels[k][: op.rows], v) for k, v in refs.items())
+        if a.fast:      # hub rows re-associated: normwise relative difference per row vs the exact hops
+            ok = refs is not None and all(
+                bool(((panels[k][: op.rows] - v).norm(dim=1) <= 1e-5 * v.norm(dim=1) + 1e-30).all())
+                for k, v in refs.items())
+        else:
+            ok = refs is not None and all(torch.equal(panels[k][: op.rows], v) for k, v in refs.items())
         flags = torch.tensor([int(refs is not None), int(ok)], dtype=torch.int32, device=dev)
         dist.all_reduce(flags, op=dist.ReduceOp.MIN)
-        parity = ({"hops_checked": sorted(refs), "bitwise_equal_to_1gpu": bool(flags[1].item()), "ranks": world}
+        parity = ({"hops_checked": sorted(refs), ("within_1e-5_of_1gpu" if a.fast else "bitwise_equal_to_1gpu"):
+                   bool(flags[1].item()), "ranks": world}
                   if flags[0].item() else {"skipped": "the whole graph's panels do not fit beside a rank's share"})
         del refs
 
@@ -721,7 +743,7 @@ def main():
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * a.roofline_reps)]
     if world == 1:
         def one_hop():
-            hop(A, panels[0], panels[1], nt_store=a.nt_store, col_blocks=col_blocks)
+            hop(A, panels[0], panels[1], nt_store=a.nt_store, col_blocks=col_blocks, fast=a.fast)
         if panels[1] is None:
             panels[1] = torch.empty_like(X)
     elif a.exchange == "allgather":
@@ -742,7 +764,7 @@ def main():
     if sample is not None and oracle_checks is None:
         # last-hop / aggregate modes keep no hop K-1: the isolated launches above left hop 1 of X
         # (the timed operator, the same launches) in panels[1]
-        oracle_checks = parity_vs_oracle(sample, [(1, panels[0], panels[1])])
+        oracle_checks = parity_vs_oracle(sample, [(1, panels[0], panels[1])], tolerance=a.fast)
     # one hop's launch duration: over the timed region itself on one GPU (K hop launches per step,
     # back to back on the launch stream, so the events bracket exactly the kernels plus their
     # few-microsecond gaps); on N GPUs the timed region also waits on the exchange, so the
@@ -822,8 +844,13 @@ def main():
         res["parity_vs_1gpu"] = parity
     if oracle_checks is not None:
         res["parity_vs_oracle"] = oracle_checks
-        res["config"]["mode"] = ("exact: sampled rows bit-identical to the oracle (reference arithmetic)"
-                                 if oracle_checks["bit_exact"] else "exact mode, ORACLE MISMATCH")
+        if a.fast:
+            res["config"]["mode"] = ("fast (SRG_SPMM_FAST: hub rows re-associated in 64 segments; sampled rows within "
+                                     "the fp32 error bound of the exact product)"
+                                     if oracle_checks["within_fp32_bound_of_exact"] else "fast mode, OUT OF TOLERANCE")
+        else:
+            res["config"]["mode"] = ("exact: sampled rows bit-identical to the oracle (reference arithmetic)"
+                                     if oracle_checks["bit_exact"] else "exact mode, ORACLE MISMATCH")
     if host_copy is not None:
         log("cpu baseline ...")
         ipn, ixn, vn, xn = host_copy

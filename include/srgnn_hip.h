@@ -65,6 +65,16 @@ extern "C" {
  * column block (srgnn.spmm.hop passes it for column-blocked hops; products 7.15 -> 7.01 ms per hop),
  * worse for whole rows.  Results are identical either way. */
 #define SRG_SPMM_PACKED_U2 0x20u
+/* Tolerance mode (EXACT, FAST, ACCUMULATE).  The hub rows (the first n_hub of
+ * row_order) are not one chain each: a hub row's entries are cut into 64 consecutive segments,
+ * each an exact fp32 fma chain in CSR order (slice waves of the span kernel, into a scratch panel
+ * taken from the stream-ordered pool with hipMallocAsync / hipFreeAsync on the hub side stream),
+ * and the 64 partial sums are added in segment order (from Y's content with ACCUMULATE).  Results
+ * are deterministic and within fp32 re-association error of the reference chain (the tests hold
+ * them to the forward-error bound and 1e-5 relative); every other row is bit-exact.  The longest
+ * row's latency drops ~64-fold: the straggler of a row-partitioned hop.  Plain and span entries
+ * only (the aggregation / send / Chebyshev epilogues run exact). */
+#define SRG_SPMM_FAST 0x40u
 
 /* =============================================================================================
  * (A) drop-in entry points

@@ -1535,6 +1535,48 @@ struct DeviceGuard {
     DeviceGuard guard_(static_cast<hipStream_t>(stream));          \
     if (guard_.rc) return guard_.rc
 
+// ------------------------------------------------------------------------------------------------
+// SRG_SPMM_FAST: the hub rows as kFastSegs segments each.  Segment s of hub row h (row order[h]) is
+// entries [b + len*s/S, b + len*(s+1)/S) of the row -- a row span -- computed as an exact fma
+// chain by the slice waves of the span kernel into a scratch panel; the S partial sums of a row are
+// then added in segment order.  Tolerance mode (the reference's single chain is re-associated into
+// S pieces, deterministically); the longest row's latency drops ~S-fold.
+// ------------------------------------------------------------------------------------------------
+constexpr int kFastSegs = 64;
+
+template <typename IP, bool SPAN>
+__global__ __launch_bounds__(256) void k_fast_segments(const IP* __restrict__ indptr, const int64_t* __restrict__ row_end,
+                                                       const int32_t* __restrict__ order, int64_t n_hub,
+                                                       int64_t* __restrict__ seg_beg, int64_t* __restrict__ seg_end,
+                                                       int32_t* __restrict__ seg_order)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_hub * kFastSegs) return;
+    const int64_t h = i / kFastSegs, sg = i % kFastSegs;
+    const int r = order[h];
+    const int64_t b = (int64_t)indptr[r];
+    const int64_t e = SPAN ? row_end[r] : (int64_t)indptr[r + 1];
+    const int64_t len = e - b;
+    seg_beg[i] = b + len * sg / kFastSegs;
+    seg_end[i] = b + len * (sg + 1) / kFastSegs;
+    seg_order[i] = (int32_t)i;
+}
+
+__global__ __launch_bounds__(256) void k_fast_reduce(const int32_t* __restrict__ order, int64_t n_hub,
+                                                     const float* __restrict__ part, int64_t ldp,
+                                                     float* __restrict__ Y, int64_t ldy, int d, int acc)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t h = i / d;
+    const int c = (int)(i % d);
+    if (h >= n_hub) return;
+    float* y = Y + (int64_t)order[h] * ldy + c;
+    float v = acc ? *y : 0.0f;
+    const float* p = part + h * kFastSegs * ldp + c;
+    for (int sg = 0; sg < kFastSegs; ++sg) v = __fadd_rn(v, p[sg * ldp]);
+    *y = v;
+}
+
 template <typename IP, int EX = kEpiPlain>
 int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int64_t n_rows,
                 const int32_t* order, int64_t n_hub, int64_t n_heavy, const float* X, int64_t ldx,
@@ -1561,7 +1603,43 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
 
     SideStream* ss = nullptr;
     std::unique_lock<std::mutex> side_lock(g_side_mu, std::defer_lock);
-    if (n_hub > 0) {   // fork: hub blocks run beside the main launch
+    const bool fast = (flags & SRG_SPMM_FAST) && (EX == kEpiPlain || EX == kEpiSpan) && !epi.agg;
+    if (n_hub > 0 && fast) {   // fork: the hub rows' segments, then their sums, beside the main launch
+        side_lock.lock();
+        int rc = side_stream_locked(s, &ss);
+        if (rc) return rc;
+        SRG_HIP_CHECK(hipEventRecord(ss->fork, s));
+        SRG_HIP_CHECK(hipStreamWaitEvent(ss->stream, ss->fork, 0));
+        const int64_t T = n_hub * kFastSegs;
+        const int64_t ldp = (d + 3) & ~3;
+        const size_t idx_bytes = ((size_t)T * (2 * sizeof(int64_t) + sizeof(int32_t)) + 255) & ~(size_t)255;
+        void* buf = nullptr;
+        SRG_HIP_CHECK(hipMallocAsync(&buf, idx_bytes + (size_t)T * ldp * sizeof(float), ss->stream));
+        int64_t* seg_beg = static_cast<int64_t*>(buf);
+        int64_t* seg_end = seg_beg + T;
+        int32_t* seg_order = reinterpret_cast<int32_t*>(seg_end + T);
+        float* part = reinterpret_cast<float*>(static_cast<char*>(buf) + idx_bytes);
+        const unsigned gs = (unsigned)((T + 255) / 256);
+        if (EX == kEpiSpan)
+            hipLaunchKernelGGL((k_fast_segments<IP, true>), dim3(gs), dim3(256), 0, ss->stream, indptr, epi.row_end,
+                               order, n_hub, seg_beg, seg_end, seg_order);
+        else
+            hipLaunchKernelGGL((k_fast_segments<IP, false>), dim3(gs), dim3(256), 0, ss->stream, indptr, nullptr,
+                               order, n_hub, seg_beg, seg_end, seg_order);
+        SRG_HIP_CHECK(hipGetLastError());
+        Epi se{};
+        se.row_end = seg_end;
+        // every segment a slice-wave row (exact chain over its span), no hubs, no accumulation
+        rc = launch_spmm<int64_t, kEpiSpan>(seg_beg, indices, vals, T, seg_order, 0, T, X, ldx, part, ldp, d,
+                                            flags & SRG_SPMM_PACKED_U2, ss->stream, se);
+        if (rc) return rc;
+        const unsigned gr = (unsigned)((n_hub * d + 255) / 256);
+        hipLaunchKernelGGL(k_fast_reduce, dim3(gr), dim3(256), 0, ss->stream, order, n_hub, part, ldp, Y, ldy, d, acc);
+        SRG_HIP_CHECK(hipGetLastError());
+        SRG_HIP_CHECK(hipFreeAsync(buf, ss->stream));
+        SRG_HIP_CHECK(hipEventRecord(ss->join, ss->stream));
+        ss->pending = (flags & SRG_SPMM_HUB_NOJOIN) != 0;
+    } else if (n_hub > 0) {   // fork: hub blocks run beside the main launch
         side_lock.lock();
         int rc = side_stream_locked(s, &ss);
         if (rc) return rc;

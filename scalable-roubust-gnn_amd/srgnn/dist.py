@@ -278,10 +278,13 @@ class HaloPartitionedOperator:
     def __init__(self, indptr, indices, values, n: int, group=None, chunks: int = 4,
                  heavy_threshold=None, hub_threshold=None, device=None, rank=None, world=None,
                  local_spmm=None, ghost_max_degree=None, hub_launches=None, giant_weight=None,
-                 calibrate_link: bool = True):
+                 calibrate_link: bool = True, fast: bool = False):
         from .csr import (DEFAULT_HEAVY_THRESHOLD, DEFAULT_HUB_THRESHOLD, NARROW_HEAVY_THRESHOLD,
                           auto_heavy_threshold, auto_hub_threshold)
         self.group = group
+        # tolerance mode for the hub group (SRG_SPMM_FAST: each hub row as 64 exact segment chains
+        # plus their ordered sum; the other rows stay bit-exact)
+        self.fast = bool(fast)
         self.virtual = rank is not None
         self.rank = rank if rank is not None else (dist.get_rank(group) if dist.is_initialized() else 0)
         self.world = world if world is not None else (dist.get_world_size(group) if dist.is_initialized() else 1)
@@ -595,7 +598,7 @@ class HaloPartitionedOperator:
             if packed is not None:
                 spmm_send(self._A[C], src, out, packed, self._send_ptr, self._send_slot)
             elif fork:
-                spmm(self._A[C], src, out=out, hub_nojoin=True)
+                spmm(self._A[C], src, out=out, hub_nojoin=True, fast=self.fast)
             else:
                 self._spmm(self._A[C], src, out)
         for c in range(C):
@@ -665,7 +668,7 @@ class HaloPartitionedOperator:
         fork = bool(self.views[C][1] and self.views[C][3])
         if self.views[C][1]:
             if fork:
-                spmm(self._A[C], src, out=out, hub_nojoin=True)
+                spmm(self._A[C], src, out=out, hub_nojoin=True, fast=self.fast)
             else:
                 self._spmm(self._A[C], src, out)
         pending = []

@@ -68,10 +68,11 @@ def auto_col_blocks(A: DeviceCSR, d: int, hops: int | None = None) -> int:
 
 
 def hop(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, nt_store: bool = False, col_blocks=None,
-        agg=None) -> torch.Tensor:
+        agg=None, fast: bool = False) -> torch.Tensor:
     """out = A @ X (one hop, exact), column-blocked when auto_col_blocks (or `col_blocks`) says so
     and A's rows allow it; bitwise the same either way.  agg = (panel, w, init): the aggregation
-    step fused into the (last) launch's epilogue, as spmm_agg."""
+    step fused into the (last) launch's epilogue, as spmm_agg.  fast: SRG_SPMM_FAST for the hub
+    rows of every launch (tolerance mode, see spmm)."""
     d = X.shape[1]
     # every launch below writes rows of A's whole row space (the blocks' schedules name them)
     _check_panel(out, A.out_rows, "out", d)
@@ -86,12 +87,12 @@ def hop(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, nt_store: bool = False
     for b, Ab in enumerate(blocks):
         if split is not None and b == 0:
             # rows block 0 computes whole finish there: their aggregation runs in that launch
-            spmm(split[0], X, out=out, nt_store=nt_store, packed_u2=u2)
+            spmm(split[0], X, out=out, nt_store=nt_store, packed_u2=u2, fast=fast)
             spmm_agg(split[1], X, out, agg[0], agg[1], agg[2], nt_store=nt_store, packed_u2=u2)
         elif agg is not None and b == len(blocks) - 1:
             spmm_agg(Ab, X, out, agg[0], agg[1], agg[2], nt_store=nt_store, accumulate=b > 0, packed_u2=u2)
         else:
-            spmm(Ab, X, out=out, accumulate=b > 0, nt_store=nt_store, packed_u2=u2)
+            spmm(Ab, X, out=out, accumulate=b > 0, nt_store=nt_store, packed_u2=u2, fast=fast)
     return out
 
 
@@ -115,8 +116,11 @@ def _check_panel(X: torch.Tensor, rows: int, name: str, d=None):
 
 def spmm(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor | None = None, accumulate: bool = False,
          nt_store: bool = False, wide_rows: bool = False, hub_w256: bool = False,
-         hub_nojoin: bool = False, packed_u2: bool = False) -> torch.Tensor:
+         hub_nojoin: bool = False, packed_u2: bool = False, fast: bool = False) -> torch.Tensor:
     """out[r, :] (+)= A[r, :] @ X  for the rows of A (one hop; exact fma chains in CSR order).
+    fast: tolerance mode (SRG_SPMM_FAST): A's hub rows are summed as 64 exact segment chains whose
+    partial sums are then added in order -- deterministic, within fp32 re-association error of the
+    exact chain, ~64x shorter latency for the longest rows; every other row stays bit-exact.
     wide_rows: diagnostic, one row per wave for every light row (no narrow or packed rows);
     hub_w256: diagnostic, 256-nonzero
     hub windows for any hub launch (same results either way).  hub_nojoin: A's hub rows are left
@@ -136,7 +140,8 @@ def spmm(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor | None = None, accumul
         raise ValueError("A, X and out must be on the same device")
     flags = (_lib.SRG_SPMM_ACCUMULATE if accumulate else 0) | (_lib.SRG_SPMM_NT_STORE if nt_store else 0) | \
         (_lib.SRG_SPMM_WIDE_ROWS if wide_rows else 0) | (_lib.SRG_SPMM_HUB_W256 if hub_w256 else 0) | \
-        (_lib.SRG_SPMM_HUB_NOJOIN if hub_nojoin else 0) | (_lib.SRG_SPMM_PACKED_U2 if packed_u2 else 0)
+        (_lib.SRG_SPMM_HUB_NOJOIN if hub_nojoin else 0) | (_lib.SRG_SPMM_PACKED_U2 if packed_u2 else 0) | \
+        (_lib.SRG_SPMM_FAST if fast else 0)
     if A.is_span:
         _span_call(A, X, out, d, flags, None, 0, 0.0, False)
         return out
@@ -259,12 +264,12 @@ def gather_rows(src: torch.Tensor, idx: torch.Tensor, out: torch.Tensor | None =
 
 
 def propagate(A: DeviceCSR, X: torch.Tensor, K: int, panels: list | None = None,
-              nt_store: bool = False, col_blocks=None) -> list:
+              nt_store: bool = False, col_blocks=None, fast: bool = False) -> list:
     """[X, ÂX, …, Â^K X] as device tensors (panels[0] is X itself, like the reference's list).
 
     Device-resident form of GraphOp.propagate's hop loop (SSRG/operators/base_operator.py:32-35):
     the K hops run back to back on the GPU with no host round trips (srg_propagate_khop_f32, or
-    hop() per hop when the hops are column-blocked)."""
+    hop() per hop when the hops are column-blocked).  fast: tolerance mode for the hub rows (spmm)."""
     _no_spans(A, "propagate")
     if A.n_rows != A.n_cols:
         raise ValueError("propagate needs a square operator")
@@ -288,10 +293,10 @@ def propagate(A: DeviceCSR, X: torch.Tensor, K: int, panels: list | None = None,
     B = auto_col_blocks(A, d, hops=K) if col_blocks is None else int(col_blocks)
     if K > 0 and B > 1 and column_blocks_for(A, B, hops=K):
         for k in range(1, K + 1):
-            hop(A, panels[k - 1], panels[k], nt_store=nt_store, col_blocks=B)
+            hop(A, panels[k - 1], panels[k], nt_store=nt_store, col_blocks=B, fast=fast)
     else:
         arr = (ctypes.c_void_p * (K + 1))(*[p.data_ptr() for p in panels])
-        flags = _lib.SRG_SPMM_NT_STORE if nt_store else 0
+        flags = (_lib.SRG_SPMM_NT_STORE if nt_store else 0) | (_lib.SRG_SPMM_FAST if fast else 0)
         _lib.call(X.device, "srg_propagate_khop_f32", A.indptr.data_ptr(), A.indices.data_ptr(),
                   A.values.data_ptr(), n, A.order.data_ptr() if n else None, A.n_hub, A.heavy(d), arr, ld, d,
                   K, flags, _stream(X.device))
