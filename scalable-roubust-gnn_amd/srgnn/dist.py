@@ -20,6 +20,8 @@ GPU: the multi-GPU results are bitwise equal to the single-GPU ones.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -250,6 +252,11 @@ def ghost_plan(halos, elig, deg, owner, gip, starts, caps=GHOST_CAPS, link_bps=N
     return best, model
 
 
+# column blocks per row-chunk launch of the halo path for large local panels (1 = off);
+# SRGNN_HALO_COL_BLOCKS overrides.  Bitwise the same hops either way.
+AUTO_HALO_COL_BLOCKS = int(os.environ.get("SRGNN_HALO_COL_BLOCKS", "1"))
+
+
 class HaloPartitionedOperator:
     """Rank p's share of Â for the halo-exchange multi-GPU propagation.
 
@@ -278,13 +285,16 @@ class HaloPartitionedOperator:
     def __init__(self, indptr, indices, values, n: int, group=None, chunks: int = 4,
                  heavy_threshold=None, hub_threshold=None, device=None, rank=None, world=None,
                  local_spmm=None, ghost_max_degree=None, hub_launches=None, giant_weight=None,
-                 calibrate_link: bool = True, fast: bool = False):
+                 calibrate_link: bool = True, fast: bool = False, col_blocks=None):
         from .csr import (DEFAULT_HEAVY_THRESHOLD, DEFAULT_HUB_THRESHOLD, NARROW_HEAVY_THRESHOLD,
                           auto_heavy_threshold, auto_hub_threshold)
         self.group = group
         # tolerance mode for the hub group (SRG_SPMM_FAST: each hub row as 64 exact segment chains
         # plus their ordered sum; the other rows stay bit-exact)
         self.fast = bool(fast)
+        # column blocks of the row chunks' launches (None: the automatic rule of _col_blocks_for)
+        self.col_blocks = col_blocks
+        self._cb = {}
         self.virtual = rank is not None
         self.rank = rank if rank is not None else (dist.get_rank(group) if dist.is_initialized() else 0)
         self.world = world if world is not None else (dist.get_world_size(group) if dist.is_initialized() else 1)
@@ -422,7 +432,12 @@ class HaloPartitionedOperator:
         g2l[gh] = self.rows + self.n_recv + torch.arange(self.n_ghost, device=dev)
         gdeg = deg[gh]
         self._ghost_pos = _row_positions(gip, gh, gdeg)              # global nnz ids of the ghost rows
-        lix = g2l[torch.cat([gix[b0:b1].to(torch.int64), gix[self._ghost_pos].to(torch.int64)])]
+        glob = torch.cat([gix[b0:b1].to(torch.int64), gix[self._ghost_pos].to(torch.int64)])
+        lix = g2l[glob]
+        # the entries' GLOBAL column ids (sorted within each row, as Â's are): the column blocks
+        # of the chunks' launches split every row where these cross the global block bounds
+        self._lix_glob = glob.to(torch.int32).contiguous() if dev.type == "cuda" else None
+        del glob
         if bool((lix < 0).any()):
             raise RuntimeError("halo layout misses a referenced column")
         lens = torch.cat([deg[r0:r1], torch.zeros(self.n_recv, dtype=torch.int64, device=dev), gdeg])
@@ -439,6 +454,8 @@ class HaloPartitionedOperator:
         # per launch: the rank's nonzeros split over its row chunks, as for the hub threshold
         auto_heavy = heavy_threshold is None
         heavy_t = auto_heavy_threshold(int(lip[self.rows]), launches=C) if auto_heavy else heavy_threshold
+        self._auto_heavy = auto_heavy
+        self._heavy_explicit = heavy_threshold
         self.views = []
         narrow = []           # slice-wave rows of each view for narrow panels (d <= 32), automatic only
         for g in range(G):
@@ -488,6 +505,7 @@ class HaloPartitionedOperator:
         other = copy.copy(self)
         lvv = self._local_values(values)
         other._lvv = lvv
+        other._cb = {}                 # column blocks hold the values: rebuilt for `other` on use
         if isinstance(self._A[0], tuple):
             other._A = [(a[0], a[1], lvv, a[3]) for a in self._A]
         else:
@@ -496,6 +514,78 @@ class HaloPartitionedOperator:
                                   a.n_heavy_narrow, row_space=a.row_space)
                         for a in self._A]
         return other
+
+    def _col_blocks_for(self, d: int) -> int:
+        """Column blocks per row-chunk launch for a panel of d columns: `col_blocks` if given, else
+        AUTO_HALO_COL_BLOCKS for local panels ([own | halo] rows) of >= 256 MiB at d >= 64 (HIP
+        ranks only)."""
+        if not self._hip:
+            return 1
+        if self.col_blocks is not None:
+            return max(1, int(self.col_blocks))
+        panel = (self.rows + self.halo) * d * 4
+        return AUTO_HALO_COL_BLOCKS if d >= 64 and panel >= (256 << 20) else 1
+
+    def chunk_blocks(self, d: int):
+        """The row chunks' column blocks for a panel of d columns: per chunk, B DeviceCSRs over row
+        spans of the local operator (block b of a row: its entries whose GLOBAL column ids lie in
+        [ceil(b n / B), ceil((b+1) n / B)), each block with its own schedule), or None for one
+        launch per chunk.  Block 0 runs from +0.0f and blocks 1.. continue every chain with
+        ACCUMULATE, so each row is the same fma chain in the same order: bitwise the unblocked
+        chunk.  Rows of <= csr.BLOCK_WHOLE_MAX entries are computed whole in block 0.  Each launch
+        gathers from 1 / B of the global columns, so the caches hold B times as many of the rows
+        it reads (one GPU: csr.DeviceCSR.column_blocks).  Cached per B."""
+        B = self._col_blocks_for(d)
+        if B < 2:
+            return None
+        if B in self._cb:
+            return self._cb[B]
+        from . import _lib
+        from .csr import (BLOCK_WHOLE_MAX, DeviceCSR, auto_heavy_threshold, narrow_heavy_degrees,
+                          schedule_from_degrees)
+        dev = self.device
+        nloc = self.rows + self.halo
+        lip = self._lip
+        splits = torch.empty((B - 1, nloc), dtype=torch.int64, device=dev)
+        if nloc:
+            _lib.call(dev, "srg_csr_col_splits", lip.data_ptr(), self._lix_glob.data_ptr() if self._lix_glob.numel() else None,
+                      nloc, self.n, B, splits.data_ptr(), _lib.stream(dev))
+        deg = lip[1:] - lip[:-1]
+        whole = (deg <= BLOCK_WHOLE_MAX) if BLOCK_WHOLE_MAX > 0 else torch.zeros_like(deg, dtype=torch.bool)
+        splits = torch.where(whole.unsqueeze(0), lip[1:].unsqueeze(0), splits)
+        bounds = [lip[:-1]] + [splits[b] for b in range(B - 1)] + [lip[1:]]
+        heavy_t = auto_heavy_threshold(self.nnz_local, launches=self.C * B) if self._auto_heavy \
+            else self._heavy_explicit
+        per_chunk = []
+        for c in range(self.C):
+            rows_c = self.views[c][0].to(torch.int64)
+            if rows_c.numel() == 0:
+                per_chunk.append(None)
+                continue
+            cut = rows_c[~whole[rows_c]]
+            blocks = []
+            for b in range(B):
+                beg, end = bounds[b], bounds[b + 1]
+                sel = rows_c if b == 0 else cut
+                dsel = (end - beg)[sel]
+                order, n_heavy, _ = schedule_from_degrees(dsel, int(dsel.sum()) if dsel.numel() else 0, heavy_t, -1)
+                order = sel[order.to(torch.int64)].to(torch.int32).contiguous()
+                narrow = narrow_heavy_degrees(dsel, 0) if self._auto_heavy else None
+                blocks.append(DeviceCSR(beg, self._lix, self._lvv, int(sel.numel()), self.ncols_local, order,
+                                        n_heavy, 0, narrow, row_end=end, row_space=self.rows))
+            per_chunk.append(blocks)
+        self._cb[B] = per_chunk
+        return per_chunk
+
+    def _chunk_spmm(self, c: int, src: torch.Tensor, out: torch.Tensor, blocks=None):
+        """Row chunk c's launch(es): one, or its column blocks in order (bitwise the same)."""
+        if blocks is not None and blocks[c] is not None:
+            from .spmm import spmm
+            u2 = src.shape[1] >= 128
+            for b, Ab in enumerate(blocks[c]):
+                spmm(Ab, src, out=out, accumulate=b > 0, packed_u2=u2)
+        else:
+            self._spmm(self._A[c], src, out)
 
     def _local_values(self, values: torch.Tensor) -> torch.Tensor:
         """The local operator's values: the own rows' slice, then the ghost rows' entries."""
@@ -601,12 +691,13 @@ class HaloPartitionedOperator:
                 spmm(self._A[C], src, out=out, hub_nojoin=True, fast=self.fast)
             else:
                 self._spmm(self._A[C], src, out)
+        blocks = self.chunk_blocks(src.shape[1]) if packed is None else None
         for c in range(C):
             if self.views[c][1]:
                 if packed is not None:
                     spmm_send(self._A[c], src, out, packed, self._send_ptr, self._send_slot)
                 else:
-                    self._spmm(self._A[c], src, out)
+                    self._chunk_spmm(c, src, out, blocks)
             if after_group is not None:
                 after_group(c)
         if ghosts and self.n_ghost:
@@ -672,9 +763,10 @@ class HaloPartitionedOperator:
             else:
                 self._spmm(self._A[C], src, out)
         pending = []
+        blocks = self.chunk_blocks(src.shape[1])
         for c in range(C):
             if self.views[c][1]:
-                self._spmm(self._A[c], src, out)
+                self._chunk_spmm(c, src, out, blocks)
             if c == 0 and fork:
                 _lib.call(self.device, "srg_hub_join", _lib.stream(self.device))
             a, b = self.chunk_ranges[c]
@@ -740,14 +832,14 @@ def _virtual_exchange(shares, panels, ghosts: bool = False):
 
 def simulate_halo_propagate(indptr, indices, values, n: int, x: torch.Tensor, K: int, world: int,
                             chunks: int = 3, heavy_threshold=None, hub_threshold=None, device=None,
-                            ghost_max_degree=None, shares=None):
+                            ghost_max_degree=None, shares=None, col_blocks=None):
     """P virtual halo-exchange ranks in ONE process (all_to_all emulated by copies); returns the
     K+1 full [n, d] panels.  Exercises the group split, ghost rows, halo layout and column remap
     on a device."""
     if shares is None:
         shares = [HaloPartitionedOperator(indptr, indices, values, n, chunks=chunks, heavy_threshold=heavy_threshold,
                                           hub_threshold=hub_threshold, device=device, rank=q, world=world,
-                                          ghost_max_degree=ghost_max_degree)
+                                          ghost_max_degree=ghost_max_degree, col_blocks=col_blocks)
                   for q in range(world)]
     d = x.shape[1]
     panels = [[s.new_panel(d) for _ in range(K + 1)] for s in shares]

@@ -37,6 +37,9 @@ def main():
                     help="launch count the hub threshold assumes (default: the chunk count)")
     ap.add_argument("--giant-weight", type=float, default=None,
                     help="partition weight of giant rows (default: srgnn.dist.GIANT_WEIGHT)")
+    ap.add_argument("--fast", action="store_true", help="the hub group in tolerance mode (SRG_SPMM_FAST)")
+    ap.add_argument("--col-blocks", default=None,
+                    help="column blocks of the row chunks' launches: one value or a comma list (default: auto)")
     ap.add_argument("--ghost", default="auto",
                     help="ghost row degree cap(s): 'auto' (the operator's cost model) or a comma list")
     a = ap.parse_args()
@@ -46,12 +49,13 @@ def main():
     print(f"{a.config}: n={n} nnz={int(ix.numel())} d={d} built", file=sys.stderr, flush=True)
     out = {"config": a.config, "n": n, "nnz": int(ix.numel()), "d": d, "worlds": {}}
     ghosts = [None] if a.ghost == "auto" else [int(c) for c in a.ghost.split(",")]
-    for P, ghost in [(int(w), gc) for w in a.worlds.split(",") for gc in ghosts]:
+    cbs = [None] if a.col_blocks is None else [int(c) for c in a.col_blocks.split(",")]
+    for P, ghost, cb in [(int(w), gc, cb) for w in a.worlds.split(",") for gc in ghosts for cb in cbs]:
         ranks = []
         for q in range(P):
             op = HaloPartitionedOperator(ip, ix, vals, n, chunks=a.chunks, device=dev, rank=q, world=P,
                                          ghost_max_degree=ghost, hub_launches=a.hub_launches,
-                                         giant_weight=a.giant_weight)
+                                         giant_weight=a.giant_weight, fast=a.fast, col_blocks=cb)
             src = op.new_panel(d)
             src[: op.rows].copy_(x[op.r0:op.r1])
             src[op.rows:].uniform_(-1, 1)
@@ -147,14 +151,15 @@ def main():
             del op, src, dst
             torch.cuda.empty_cache()
         worst = max(ranks, key=lambda r: max(r["ms_hub"], r["ms_chunks"]))
-        out["worlds"][f"{P}" if a.ghost == "auto" else f"{P}/ghost{ghost}"] = {"ranks": ranks,
+        key = (f"{P}" if a.ghost == "auto" else f"{P}/ghost{ghost}") + ("" if cb is None else f"/cb{cb}")
+        out["worlds"][key] = {"ranks": ranks, "col_blocks": cb,
                             "max_hop_compute_ms": max(r["ms_compute"] for r in ranks),
                             "max_compute_ms": max(max(r["ms_hub"], r["ms_chunks"]) for r in ranks),
                             "mean_chunks_ms": sum(r["ms_chunks"] for r in ranks) / P,
                             "worst_rank": worst["rank"],
                             "max_halo_GB": max(r["halo_bytes"] for r in ranks) / 1e9}
-        W = out["worlds"][f"{P}" if a.ghost == "auto" else f"{P}/ghost{ghost}"]
-        print(f"P={P} ghost cap {ranks[0]['ghost_max_degree']}: hop compute {W['max_hop_compute_ms']:.3f} ms, "
+        W = out["worlds"][key]
+        print(f"P={P} col blocks {cb} ghost cap {ranks[0]['ghost_max_degree']}: hop compute {W['max_hop_compute_ms']:.3f} ms, "
               f"max compute {W['max_compute_ms']:.3f} ms "
               f"(rank {worst['rank']}: chunks {worst['ms_chunks']:.3f}, hub {worst['ms_hub']:.3f}), "
               f"mean chunks {W['mean_chunks_ms']:.3f} ms, max received halo "
