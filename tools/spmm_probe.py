@@ -67,7 +67,8 @@ if a.op == "wavelet":
                       "compulsory_bytes": roofline.bytes_compulsory(n, nnz, d)}))
     sys.exit(0)
 if a.identity:
-    n, d = 4 * 1024 * 1024, 128          # 2 GiB panel (> 256 MiB Infinity Cache)
+    d = a.d or 128
+    n = (1 << 31) // (4 * d)              # 2 GiB panel (> 256 MiB Infinity Cache)
     ip = torch.arange(n + 1, dtype=torch.int64, device=dev)
     ix = torch.arange(n, dtype=torch.int32, device=dev)
     vals = torch.ones(n, dtype=torch.float32, device=dev)
