@@ -6,7 +6,7 @@ O=$R/gpurun_out/$1; ROUNDS=$2; C=$3; shift 3
 mkdir -p "$O"
 for r in $(seq 1 "$ROUNDS"); do
   for E in "$@"; do
-    env $(echo "$E" | tr ',' ' ') timeout -k 10 300 python "$R/bench.py" --config "$C" --steps 5 --warmup 1 --no-cpu-baseline > "$O/tmp.json" 2> "$O/tmp.err" || { cat "$O/tmp.err"; exit 1; }
+    env $(echo "$E" | tr ',' ' ') timeout -k 10 300 python "$R/bench.py" --config "$C" --steps 5 --warmup 1 --no-cpu-baseline --pmc off > "$O/tmp.json" 2> "$O/tmp.err" || { cat "$O/tmp.err"; exit 1; }
     python3 -c "import json,sys; r=json.load(open('$O/tmp.json')); print('$C', '$E', round(r['ms_per_step'],3), round(r['roofline']['kernel_ms'],4), round(r['value']/1e9,2))" | tee -a "$O/ab_$C.txt"
   done
 done
