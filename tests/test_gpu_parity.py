@@ -726,3 +726,25 @@ def test_hub_side_streams_bounded():
         if i % 8 == 0:
             c.check_hop(1, y.cpu().numpy())
         assert _lib.query("srg_hub_side_streams") <= 8 * torch.cuda.device_count()
+
+
+def test_column_blocks_keep_explicit_thresholds():
+    """An operator built with explicit thresholds schedules its column blocks (and block 0's split
+    parts) with the same thresholds and no automatic narrow split; the automatic operator's blocks
+    keep the narrow split.  Same bits either way."""
+    from srgnn.spmm import hop
+    c = G.Case("rand_d128_r05")
+    A = _csr(c, (5, 60))
+    assert A.n_heavy_narrow is None and A.thresholds == (5, 60)
+    X = torch.from_numpy(c.x()).cuda()
+    for blk in A.column_blocks(3):
+        assert blk.thresholds == (5, 60) and blk.n_heavy_narrow is None
+        deg = (blk.row_end - blk.indptr)[blk.order.long()]
+        assert blk.n_hub == int((deg > 60).sum()) and blk.n_hub + blk.n_heavy == int((deg > 5).sum())
+    for part in A.column_blocks(3)[0].split_whole() or ():
+        assert part.n_heavy_narrow is None
+    auto = _csr(c, (None, None))
+    assert all(b.n_heavy_narrow is not None for b in auto.column_blocks(3))
+    y = hop(A, X, torch.empty_like(X), col_blocks=3, agg=(torch.zeros_like(X), 1.0, True))
+    torch.cuda.synchronize()
+    c.check_hop(1, y.cpu().numpy())
