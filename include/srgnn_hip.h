@@ -65,6 +65,13 @@ extern "C" {
  * column block (srgnn.spmm.hop passes it for column-blocked hops; products 7.15 -> 7.01 ms per hop),
  * worse for whole rows.  Results are identical either way. */
 #define SRG_SPMM_PACKED_U2 0x20u
+/* With SRG_SPMM_HUB_NOJOIN, after an unjoined NOJOIN fork from the same stream: the hub rows'
+ * workgroups are appended to the hub side stream without a new fork from `stream` (and without
+ * the dispatch delay).  For the column blocks of one hop: X is unchanged during the hop and only
+ * the side stream touches the hub rows, so block b's hub span needs no order against block b-1's
+ * main launch -- only against block b-1's hub span, which the side stream gives.  One join at the
+ * end of the hop.  Without a pending fork it is an ordinary fork.  Results are identical. */
+#define SRG_SPMM_HUB_CONTINUE 0x80u
 /* Tolerance mode (EXACT, FAST, ACCUMULATE).  The hub rows (the first n_hub of
  * row_order) are not one chain each: a hub row's entries are cut into 64 consecutive segments,
  * each an exact fp32 fma chain in CSR order (slice waves of the span kernel, into a scratch panel

@@ -1643,8 +1643,14 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
         side_lock.lock();
         int rc = side_stream_locked(s, &ss);
         if (rc) return rc;
-        SRG_HIP_CHECK(hipEventRecord(ss->fork, s));
-        SRG_HIP_CHECK(hipStreamWaitEvent(ss->stream, ss->fork, 0));
+        // CONTINUE after an unjoined fork: the hub rows are appended to the side stream, which is
+        // already ordered after everything they read (the caller's guarantee), with no new fork
+        // and no dispatch delay on the caller's stream
+        const bool cont = (flags & SRG_SPMM_HUB_CONTINUE) && ss->pending;
+        if (!cont) {
+            SRG_HIP_CHECK(hipEventRecord(ss->fork, s));
+            SRG_HIP_CHECK(hipStreamWaitEvent(ss->stream, ss->fork, 0));
+        }
         const dim3 hgrid((unsigned)(n_hub * n_slices));
         static const int abl = [] { const char* e = getenv("SRGNN_HUB_ABLATION"); return e ? atoi(e) : 0; }();
         if (EX == kEpiPlain && sfull && abl >= 1 && abl <= 6) {
@@ -1672,7 +1678,7 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
         SRG_HIP_CHECK(hipGetLastError());
         SRG_HIP_CHECK(hipEventRecord(ss->join, ss->stream));
         ss->pending = (flags & SRG_SPMM_HUB_NOJOIN) != 0;
-        if (hub_delay_us() > 0) {
+        if (!cont && hub_delay_us() > 0) {
             hipLaunchKernelGGL(k_dispatch_delay, dim3(1), dim3(64), 0, s, hub_delay_us());
             SRG_HIP_CHECK(hipGetLastError());
         }

@@ -28,6 +28,9 @@ _COL_BLOCKS_ENV = os.environ.get("SRGNN_COL_BLOCKS", "auto")
 # d >= 128: products 7.15 -> 7.03 ms per hop, d = 256 +1.3 %, d = 64 -3 % (so not there);
 # SRGNN_BLOCK_U2=0 turns it off (A/B, profiles/r02_ab_col_blocks.txt)
 _U2_BLOCKED = os.environ.get("SRGNN_BLOCK_U2", "1") != "0"
+# column-blocked hops: block b's hub rows continue block b-1's side-stream fork (SRG_SPMM_HUB_CONTINUE)
+# instead of a fork, dispatch delay and join per block; SRGNN_HUB_CHAIN=0 for the A/B
+_HUB_CHAIN = os.environ.get("SRGNN_HUB_CHAIN", "1") != "0"
 
 
 # Cutting an operator into column blocks (row spans: one binary search per row and boundary, plus
@@ -84,6 +87,11 @@ def hop(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, nt_store: bool = False
     # at d = 64, 8 rows per wave, it is 3 % slower)
     u2 = len(blocks) > 1 and d >= 128 and _U2_BLOCKED
     split = blocks[0].split_whole() if agg is not None and len(blocks) > 1 else None
+    # the blocks' hub spans chained on the side stream: one fork (the first block with hub rows),
+    # one join at the end of the hop; X is not written during the hop and only the side stream
+    # touches the hub rows, so nothing else orders them
+    chain = len(blocks) > 1 and agg is None and not fast and _HUB_CHAIN
+    forked = False
     for b, Ab in enumerate(blocks):
         if split is not None and b == 0:
             # rows block 0 computes whole finish there: their aggregation runs in that launch
@@ -91,8 +99,14 @@ def hop(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, nt_store: bool = False
             spmm_agg(split[1], X, out, agg[0], agg[1], agg[2], nt_store=nt_store, packed_u2=u2)
         elif agg is not None and b == len(blocks) - 1:
             spmm_agg(Ab, X, out, agg[0], agg[1], agg[2], nt_store=nt_store, accumulate=b > 0, packed_u2=u2)
+        elif chain and Ab.n_hub > 0:
+            spmm(Ab, X, out=out, accumulate=b > 0, nt_store=nt_store, packed_u2=u2, hub_nojoin=True,
+                 hub_continue=forked)
+            forked = True
         else:
             spmm(Ab, X, out=out, accumulate=b > 0, nt_store=nt_store, packed_u2=u2, fast=fast)
+    if forked:
+        _lib.call(X.device, "srg_hub_join", _stream(X.device))
     return out
 
 
@@ -116,7 +130,8 @@ def _check_panel(X: torch.Tensor, rows: int, name: str, d=None):
 
 def spmm(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor | None = None, accumulate: bool = False,
          nt_store: bool = False, wide_rows: bool = False, hub_w256: bool = False,
-         hub_nojoin: bool = False, packed_u2: bool = False, fast: bool = False) -> torch.Tensor:
+         hub_nojoin: bool = False, packed_u2: bool = False, fast: bool = False,
+         hub_continue: bool = False) -> torch.Tensor:
     """out[r, :] (+)= A[r, :] @ X  for the rows of A (one hop; exact fma chains in CSR order).
     fast: tolerance mode (SRG_SPMM_FAST): A's hub rows are summed as 64 exact segment chains whose
     partial sums are then added in order -- deterministic, within fp32 re-association error of the
@@ -125,7 +140,8 @@ def spmm(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor | None = None, accumul
     hub_w256: diagnostic, 256-nonzero
     hub windows for any hub launch (same results either way).  hub_nojoin: A's hub rows are left
     running on the library's side stream; the caller must make a stream wait for them
-    (srg_hub_join) before reading them."""
+    (srg_hub_join) before reading them.  hub_continue (with hub_nojoin, after an unjoined fork):
+    the hub rows are appended to the side stream without a new fork (SRG_SPMM_HUB_CONTINUE)."""
     _check_panel(X, A.n_cols, "X")
     d = X.shape[1]
     if out is None:
@@ -141,7 +157,7 @@ def spmm(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor | None = None, accumul
     flags = (_lib.SRG_SPMM_ACCUMULATE if accumulate else 0) | (_lib.SRG_SPMM_NT_STORE if nt_store else 0) | \
         (_lib.SRG_SPMM_WIDE_ROWS if wide_rows else 0) | (_lib.SRG_SPMM_HUB_W256 if hub_w256 else 0) | \
         (_lib.SRG_SPMM_HUB_NOJOIN if hub_nojoin else 0) | (_lib.SRG_SPMM_PACKED_U2 if packed_u2 else 0) | \
-        (_lib.SRG_SPMM_FAST if fast else 0)
+        (_lib.SRG_SPMM_FAST if fast else 0) | (_lib.SRG_SPMM_HUB_CONTINUE if hub_continue else 0)
     if A.is_span:
         _span_call(A, X, out, d, flags, None, 0, 0.0, False)
         return out
