@@ -69,6 +69,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--nt-store", action="store_true")
+    ap.add_argument("--graph", action="store_true",
+                    help="one GPU, K-hop panels mode: capture one step (its K hops, hub forks and joins) in a "
+                         "HIP graph after the warm-up and replay it for the timed steps")
     ap.add_argument("--col-blocks", type=int, default=None,
                     help="column blocks per hop on one GPU (default: srgnn.spmm.auto_col_blocks; 1 = one launch)")
     ap.add_argument("--exchange", default="halo", choices=["halo", "allgather"])
@@ -697,6 +700,24 @@ def main():
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
+    graphed = False
+    if a.graph and world == 1 and mode == "panels" and not a.fast:
+        # the step's launches (hub forks / joins included: the side stream joins the capture through
+        # the library's events) as one HIP graph on a capture stream warmed up first (the library's
+        # side stream for it is created outside the capture); replayed on the launch stream
+        cap = torch.cuda.Stream(dev)
+        cap.wait_stream(stream)
+        with torch.cuda.stream(cap):
+            step()
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=cap):
+            step()
+        torch.cuda.synchronize()
+        plain_step, step = step, g.replay
+        g.replay()
+        torch.cuda.synchronize()
+        graphed = True
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -811,6 +832,7 @@ def main():
                    + (", X whole on every rank (hop 0's halo gathered locally)" if world > 1 and a.exchange == "halo"
                       and not a.exchange_x else ""),
                    "mode": "exact (bit-identical to reference)",
+                   **({"launch": "HIP graph of one step, replayed"} if graphed else {}),
                    "outputs": ("all K+1 hop panels" if mode in ("panels", "auto") else
                                f"fused {a.aggregate} of hops 0..K (srgnn.aggregate, bit-exact vs the reference combine)"
                                if a.aggregate else "last hop only (2 ping-pong panels)")
