@@ -88,9 +88,10 @@ def hop(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, nt_store: bool = False
     u2 = len(blocks) > 1 and d >= 128 and _U2_BLOCKED
     split = blocks[0].split_whole() if agg is not None and len(blocks) > 1 else None
     # the blocks' hub spans chained on the side stream: one fork (the first block with hub rows),
-    # one join at the end of the hop; X is not written during the hop and only the side stream
-    # touches the hub rows, so nothing else orders them
-    chain = len(blocks) > 1 and agg is None and not fast and _HUB_CHAIN
+    # one join at the end of the hop.  X is not written during the hop, and when every block has
+    # the same hub rows only the side stream touches them, so nothing else orders them (a row that
+    # is a hub in one block only would have spans on both streams: then every block forks and joins)
+    chain = len(blocks) > 1 and agg is None and not fast and _HUB_CHAIN and _same_hub_rows(A, B, blocks)
     forked = False
     for b, Ab in enumerate(blocks):
         if split is not None and b == 0:
@@ -108,6 +109,15 @@ def hop(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, nt_store: bool = False
     if forked:
         _lib.call(X.device, "srg_hub_join", _stream(X.device))
     return out
+
+
+def _same_hub_rows(A: DeviceCSR, B: int, blocks) -> bool:
+    """Whether every column block schedules the same set of hub rows (cached per B on A)."""
+    key = ("same_hubs", B)
+    if key not in A._blocks:
+        sets = [torch.sort(b.order[: b.n_hub].to(torch.int64)).values for b in blocks]
+        A._blocks[key] = all(s.numel() == sets[0].numel() and bool(torch.equal(s, sets[0])) for s in sets)
+    return A._blocks[key]
 
 
 def _check_panel(X: torch.Tensor, rows: int, name: str, d=None):

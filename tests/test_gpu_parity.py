@@ -748,3 +748,30 @@ def test_column_blocks_keep_explicit_thresholds():
     y = hop(A, X, torch.empty_like(X), col_blocks=3, agg=(torch.zeros_like(X), 1.0, True))
     torch.cuda.synchronize()
     c.check_hop(1, y.cpu().numpy())
+
+
+@pytest.mark.parametrize("hub_threshold", [300, 2000])
+def test_blocked_hop_hub_rows_chained_or_forked_bit_exact(oracle_mod, hub_threshold):
+    """Column-blocked hops chain the blocks' hub spans on the side stream only when every block has
+    the same hub rows (then no other launch touches them); when a row is a hub in some blocks only,
+    every block forks and joins.  Both are bitwise the one-launch hop, repeated hops included."""
+    from srgnn import synth
+    from srgnn.csr import DeviceCSR
+    from srgnn.normalize import sym_norm_binary
+    from srgnn.spmm import _same_hub_rows, hop, spmm
+    n = 30000
+    u, v = synth.rmat_undirected_t(n, 400000, seed=51, device="cuda")
+    ip, ix = synth.symmetric_csr_t(n, u, v)
+    ip, ix, vals = sym_norm_binary(ip, ix, n, 0.5)
+    x = synth.uniform_features_t(n, 128, device="cuda")
+    A = DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, hub_threshold=hub_threshold, device="cuda")
+    want = spmm(A, x)
+    blocks = A.column_blocks(3)
+    assert any(b.n_hub for b in blocks)
+    same = _same_hub_rows(A, 3, blocks)
+    assert same == (hub_threshold == 2000) or hub_threshold == 2000
+    y = torch.empty_like(x)
+    for _ in range(3):
+        hop(A, x, y, col_blocks=3)
+        torch.cuda.synchronize()
+        assert torch.equal(y, want), f"hub_threshold={hub_threshold} chained={same}"
