@@ -285,7 +285,7 @@ class HaloPartitionedOperator:
     def __init__(self, indptr, indices, values, n: int, group=None, chunks: int = 4,
                  heavy_threshold=None, hub_threshold=None, device=None, rank=None, world=None,
                  local_spmm=None, ghost_max_degree=None, hub_launches=None, giant_weight=None,
-                 calibrate_link: bool = True, fast: bool = False, col_blocks=None):
+                 calibrate_link: bool = True, fast: bool = False, col_blocks=None, early_degree=None):
         from .csr import (DEFAULT_HEAVY_THRESHOLD, DEFAULT_HUB_THRESHOLD, NARROW_HEAVY_THRESHOLD,
                           auto_heavy_threshold, auto_hub_threshold)
         self.group = group
@@ -333,6 +333,12 @@ class HaloPartitionedOperator:
                 # local row range of each chunk (its hub rows included: they belong to group C)
                 self.chunk_ranges = [(cb[c], cb[c + 1]) for c in range(C)]
         grp[is_hub] = C
+        # early_degree: non-hub rows longer than this join the first chunk, whose launch starts the
+        # hop, so their slice-wave chains (~38 ns per nonzero) run beside the rest of the hop's work
+        # instead of outlasting a later chunk (probe of a raised hub threshold, tools/halo_ranks.py)
+        self._early = early_degree is not None
+        if early_degree is not None:
+            grp[(deg > int(early_degree)) & ~is_hub] = 0
         self.n_groups = C + 1
         G = self.n_groups
         r0, r1 = self.starts[p], self.starts[p + 1]
@@ -752,6 +758,8 @@ class HaloPartitionedOperator:
         kernels (no ghost rows: the epilogue covers own rows only)."""
         if not (self._hip and self.world > 1 and not self.virtual) or self.n_ghost:
             raise RuntimeError("hop_with_epilogue needs real GPU ranks with the HIP kernels and no ghost rows")
+        if self._early:
+            raise RuntimeError("hop_with_epilogue needs every chunk's rows in its own row range (no early_degree)")
         from . import _lib
         from .spmm import spmm
         out = dst[: self.rows]

@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--giant-weight", type=float, default=None,
                     help="partition weight of giant rows (default: srgnn.dist.GIANT_WEIGHT)")
     ap.add_argument("--fast", action="store_true", help="the hub group in tolerance mode (SRG_SPMM_FAST)")
+    ap.add_argument("--early-degree", type=int, default=None,
+                    help="non-hub rows longer than this run in the first chunk (srgnn.dist early_degree)")
     ap.add_argument("--col-blocks", default=None,
                     help="column blocks of the row chunks' launches: one value or a comma list (default: auto)")
     ap.add_argument("--ghost", default="auto",
@@ -55,7 +57,8 @@ def main():
         for q in range(P):
             op = HaloPartitionedOperator(ip, ix, vals, n, chunks=a.chunks, device=dev, rank=q, world=P,
                                          ghost_max_degree=ghost, hub_launches=a.hub_launches,
-                                         giant_weight=a.giant_weight, fast=a.fast, col_blocks=cb)
+                                         giant_weight=a.giant_weight, fast=a.fast, col_blocks=cb,
+                                         early_degree=a.early_degree)
             src = op.new_panel(d)
             src[: op.rows].copy_(x[op.r0:op.r1])
             src[op.rows:].uniform_(-1, 1)
