@@ -91,15 +91,27 @@ def hop(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, nt_store: bool = False
     # one join at the end of the hop.  X is not written during the hop, and when every block has
     # the same hub rows only the side stream touches them, so nothing else orders them (a row that
     # is a hub in one block only would have spans on both streams: then every block forks and joins)
-    chain = len(blocks) > 1 and agg is None and not fast and _HUB_CHAIN and _same_hub_rows(A, B, blocks)
+    # (with the aggregation split, the launches over cut rows are split[0] and blocks 1..; split[1]'s
+    # rows -- whole rows -- are in no other launch, so its hub rows never matter)
+    chain = len(blocks) > 1 and not fast and _HUB_CHAIN and \
+        _same_hub_rows(A, B, ([split[0]] + blocks[1:]) if split is not None else blocks, agg=split is not None)
     forked = False
+
+    def hubs(Ab):       # hub flags of one launch: chained when it has hub rows
+        nonlocal forked
+        if not (chain and Ab.n_hub > 0):
+            return {}
+        f = {"hub_nojoin": True, "hub_continue": forked}
+        forked = True
+        return f
     for b, Ab in enumerate(blocks):
         if split is not None and b == 0:
             # rows block 0 computes whole finish there: their aggregation runs in that launch
-            spmm(split[0], X, out=out, nt_store=nt_store, packed_u2=u2, fast=fast)
-            spmm_agg(split[1], X, out, agg[0], agg[1], agg[2], nt_store=nt_store, packed_u2=u2)
+            spmm(split[0], X, out=out, nt_store=nt_store, packed_u2=u2, fast=fast, **hubs(split[0]))
+            spmm_agg(split[1], X, out, agg[0], agg[1], agg[2], nt_store=nt_store, packed_u2=u2, **hubs(split[1]))
         elif agg is not None and b == len(blocks) - 1:
-            spmm_agg(Ab, X, out, agg[0], agg[1], agg[2], nt_store=nt_store, accumulate=b > 0, packed_u2=u2)
+            spmm_agg(Ab, X, out, agg[0], agg[1], agg[2], nt_store=nt_store, accumulate=b > 0, packed_u2=u2,
+                     **hubs(Ab))
         elif chain and Ab.n_hub > 0:
             spmm(Ab, X, out=out, accumulate=b > 0, nt_store=nt_store, packed_u2=u2, hub_nojoin=True,
                  hub_continue=forked)
@@ -111,9 +123,9 @@ def hop(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, nt_store: bool = False
     return out
 
 
-def _same_hub_rows(A: DeviceCSR, B: int, blocks) -> bool:
+def _same_hub_rows(A: DeviceCSR, B: int, blocks, agg: bool = False) -> bool:
     """Whether every column block schedules the same set of hub rows (cached per B on A)."""
-    key = ("same_hubs", B)
+    key = ("same_hubs", B, agg)
     if key not in A._blocks:
         sets = [torch.sort(b.order[: b.n_hub].to(torch.int64)).values for b in blocks]
         A._blocks[key] = all(s.numel() == sets[0].numel() and bool(torch.equal(s, sets[0])) for s in sets)
@@ -191,7 +203,8 @@ def _no_spans(A: DeviceCSR, what: str):
 
 
 def spmm_agg(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, agg: torch.Tensor, w: float, init: bool,
-             nt_store: bool = False, accumulate: bool = False, packed_u2: bool = False) -> torch.Tensor:
+             nt_store: bool = False, accumulate: bool = False, packed_u2: bool = False,
+             hub_nojoin: bool = False, hub_continue: bool = False) -> torch.Tensor:
     """out = A @ X and, fused into the same kernels' epilogue, agg = (0 if init else agg) + w * out
     (srg_spmm_agg_f32; the arithmetic of spmm followed by one srg_hop_accumulate_f32 step).
     accumulate: the chains continue from out's content (the last block of a column-blocked hop)."""
@@ -202,7 +215,8 @@ def spmm_agg(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, agg: torch.Tensor
     if not (out.device == X.device == agg.device == A.device):
         raise ValueError("A, X, out and agg must be on the same device")
     flags = (_lib.SRG_SPMM_NT_STORE if nt_store else 0) | (_lib.SRG_SPMM_ACCUMULATE if accumulate else 0) | \
-        (_lib.SRG_SPMM_PACKED_U2 if packed_u2 else 0)
+        (_lib.SRG_SPMM_PACKED_U2 if packed_u2 else 0) | (_lib.SRG_SPMM_HUB_NOJOIN if hub_nojoin else 0) | \
+        (_lib.SRG_SPMM_HUB_CONTINUE if hub_continue else 0)
     if A.is_span:
         _span_call(A, X, out, d, flags, agg, agg.stride(0), w, init)
         return out

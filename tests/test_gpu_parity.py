@@ -777,3 +777,10 @@ def test_blocked_hop_hub_rows_chained_or_forked_bit_exact(oracle_mod, mode):
         hop(A, x, y, col_blocks=3)
         torch.cuda.synchronize()
         assert torch.equal(y, want), mode
+    # with the aggregation step fused (the split block 0 and the aggregating last block in the chain)
+    assert _same_hub_rows(A, 3, [blocks[0].split_whole()[0]] + blocks[1:], agg=True) == (mode == "same")
+    agg = torch.empty_like(x)
+    for _ in range(2):
+        hop(A, x, y, col_blocks=3, agg=(agg, 0.5, True))
+        torch.cuda.synchronize()
+        assert torch.equal(y, want) and torch.equal(agg, 0.0 + 0.5 * want), mode
