@@ -185,6 +185,7 @@ def cpu_baseline(ip, ix, vals, x_host, n, d, budget_s):
         rows(0, r1, cur, nxt)
         one = int(ip[r1] - ip[0]) / (time.perf_counter() - t1)
         _omp_set_threads(threads)
+    scipy_rate = _scipy_rate(ip, ix32, v32, cur, n, budget_s / 8)
     what = "the reference's FloatCSRMulDenseOMP (oracle/_ref, built from matmul.c)" if use_ref else \
         "the oracle's int64 C restatement (the reference's int32 matmul.c cannot address this graph)"
     return {"value": edges / dt, "unit": "propagated edges/s", "cores": threads,
@@ -192,9 +193,35 @@ def cpu_baseline(ip, ix, vals, x_host, n, d, budget_s):
                            f"the host shows {os.cpu_count()} logical CPUs"),
             "kind": "reference" if use_ref else "port",
             "value_1thread": one, "cpu_model": _cpu_model(),
+            "scipy_value_1thread": scipy_rate,
+            "scipy_sample": ("the reference's non-Linux branch (base_operator.py:309-314: adj.dot(x), an fp64 csr "
+                             "times the fp32 panel, fp64 result), scipy single-threaded on a row block"),
             "sample": f"{what}: {edges} propagated edges ({hops} full hop(s) + row blocks) of the "
                       f"{n}-node graph (nnz {nnz}, d {d}), kernel-only on pre-converted int32/fp32 "
                       f"buffers, OMP_NUM_THREADS={threads}, {dt:.1f} s; value_1thread on a row block"}
+
+
+def _scipy_rate(ip, ix32, v32, x, n, budget_s):
+    """Propagated edges/s of scipy's csr @ dense (fp64 Â values, fp32 X: scipy upcasts, as the
+    reference's adj.dot(x) does) on a row block sized to ~budget_s; None if scipy is unusable."""
+    try:
+        import scipy.sparse as sps
+        nnz = int(ip[-1])
+        r1 = max(1, int(n * min(1.0, 2e7 / max(nnz, 1))))
+        e1 = int(ip[r1])
+        A = sps.csr_matrix((v32[:e1].astype(np.float64), ix32[:e1], np.asarray(ip[:r1 + 1], dtype=np.int64)),
+                           shape=(r1, n))
+        t0 = time.perf_counter()
+        reps = 0
+        while True:
+            A.dot(x)
+            reps += 1
+            if time.perf_counter() - t0 >= budget_s:
+                break
+        return e1 * reps / (time.perf_counter() - t0)
+    except Exception as e:  # noqa: BLE001
+        log(f"scipy baseline skipped: {e!r}")
+        return None
 
 
 def pmc_traffic(config, launches_per_hop=1, measured=None):
