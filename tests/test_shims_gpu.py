@@ -209,3 +209,25 @@ def test_coalesce_sorts_and_sums_in_order():
     assert i.tolist() == [[0, 1, 2], [3, 0, 1]] and v.tolist() == [7.0, 4.0, 4.0]
     i2, v2 = torch_sparse.coalesce(idx, torch.stack([val, -val], 1), 3, 4)
     assert torch.equal(i2, i) and v2[:, 1].tolist() == [-7.0, -4.0, -4.0]
+
+
+def test_sparse_products_edge_cases():
+    """Empty operands, rows without entries, products that cancel to zero (dropped, as scipy and
+    torch_sparse drop them), a single entry, and an empty sparse operand in spmm."""
+    import torch_sparse
+    e = torch.zeros((2, 0), dtype=torch.int64)
+    ev = torch.zeros(0)
+    idx, val = torch_sparse.spspmm(e, ev, e, ev, 5, 4, 3)
+    assert idx.shape == (2, 0) and val.numel() == 0
+    # a @ b where two products cancel exactly: (1 * 2) + (-1 * 2) = 0 -> dropped
+    ia = torch.tensor([[0, 0, 2], [0, 1, 1]])
+    va = torch.tensor([1.0, -1.0, 3.0])
+    ib = torch.tensor([[0, 1, 1], [2, 2, 0]])
+    vb = torch.tensor([2.0, 2.0, 5.0])
+    idx, val = torch_sparse.spspmm(ia, va, ib, vb, 3, 2, 3)
+    assert idx.tolist() == [[0, 2, 2], [0, 0, 2]] and val.tolist() == [-5.0, 15.0, 6.0]
+    one_i, one_v = torch_sparse.spspmm(torch.tensor([[0], [0]]), torch.tensor([3.0]), torch.tensor([[0], [0]]),
+                                       torch.tensor([0.5]), 1, 1, 1)
+    assert one_i.tolist() == [[0], [0]] and one_v.tolist() == [1.5]
+    y = torch_sparse.spmm(e, ev, 4, 3, torch.ones(3, 2))
+    assert y.shape == (4, 2) and bool((y == 0).all())
