@@ -255,6 +255,9 @@ def ghost_plan(halos, elig, deg, owner, gip, starts, caps=GHOST_CAPS, link_bps=N
 # column blocks per row-chunk launch of the halo path for large local panels (1 = off);
 # SRGNN_HALO_COL_BLOCKS overrides.  Bitwise the same hops either way.
 AUTO_HALO_COL_BLOCKS = int(os.environ.get("SRGNN_HALO_COL_BLOCKS", "1"))
+# column blocks of the hub group's launch (chained on the hub side stream; 1 = one launch);
+# SRGNN_HALO_HUB_BLOCKS overrides.  Bitwise the same hops either way.
+AUTO_HALO_HUB_BLOCKS = int(os.environ.get("SRGNN_HALO_HUB_BLOCKS", "1"))
 
 
 class HaloPartitionedOperator:
@@ -285,7 +288,8 @@ class HaloPartitionedOperator:
     def __init__(self, indptr, indices, values, n: int, group=None, chunks: int = 4,
                  heavy_threshold=None, hub_threshold=None, device=None, rank=None, world=None,
                  local_spmm=None, ghost_max_degree=None, hub_launches=None, giant_weight=None,
-                 calibrate_link: bool = True, fast: bool = False, col_blocks=None, early_degree=None):
+                 calibrate_link: bool = True, fast: bool = False, col_blocks=None, early_degree=None,
+                 hub_col_blocks=None):
         from .csr import (DEFAULT_HEAVY_THRESHOLD, DEFAULT_HUB_THRESHOLD, NARROW_HEAVY_THRESHOLD,
                           auto_heavy_threshold, auto_hub_threshold)
         self.group = group
@@ -294,6 +298,8 @@ class HaloPartitionedOperator:
         self.fast = bool(fast)
         # column blocks of the row chunks' launches (None: the automatic rule of _col_blocks_for)
         self.col_blocks = col_blocks
+        # column blocks of the hub group's launch (None: the automatic rule of _hub_blocks_for)
+        self.hub_col_blocks = hub_col_blocks
         self._cb = {}
         self.virtual = rank is not None
         self.rank = rank if rank is not None else (dist.get_rank(group) if dist.is_initialized() else 0)
@@ -546,20 +552,8 @@ class HaloPartitionedOperator:
             return None
         if B in self._cb:
             return self._cb[B]
-        from . import _lib
-        from .csr import (BLOCK_WHOLE_MAX, DeviceCSR, auto_heavy_threshold, narrow_heavy_degrees,
-                          schedule_from_degrees)
-        dev = self.device
-        nloc = self.rows + self.halo
-        lip = self._lip
-        splits = torch.empty((B - 1, nloc), dtype=torch.int64, device=dev)
-        if nloc:
-            _lib.call(dev, "srg_csr_col_splits", lip.data_ptr(), self._lix_glob.data_ptr() if self._lix_glob.numel() else None,
-                      nloc, self.n, B, splits.data_ptr(), _lib.stream(dev))
-        deg = lip[1:] - lip[:-1]
-        whole = (deg <= BLOCK_WHOLE_MAX) if BLOCK_WHOLE_MAX > 0 else torch.zeros_like(deg, dtype=torch.bool)
-        splits = torch.where(whole.unsqueeze(0), lip[1:].unsqueeze(0), splits)
-        bounds = [lip[:-1]] + [splits[b] for b in range(B - 1)] + [lip[1:]]
+        from .csr import DeviceCSR, auto_heavy_threshold, narrow_heavy_degrees, schedule_from_degrees
+        bounds, whole = self._block_bounds(B)
         heavy_t = auto_heavy_threshold(self.nnz_local, launches=self.C * B) if self._auto_heavy \
             else self._heavy_explicit
         per_chunk = []
@@ -582,6 +576,68 @@ class HaloPartitionedOperator:
             per_chunk.append(blocks)
         self._cb[B] = per_chunk
         return per_chunk
+
+    def _block_bounds(self, B: int):
+        """Per local row, the CSR positions where its entries' GLOBAL column ids cross the bounds
+        ceil(b n / B) (srg_csr_col_splits): B + 1 position vectors, and the mask of the rows of
+        <= csr.BLOCK_WHOLE_MAX entries, which stay whole in block 0 (their later spans empty).
+        Cached per B."""
+        key = ("bounds", B)
+        if key in self._cb:
+            return self._cb[key]
+        from . import _lib
+        from .csr import BLOCK_WHOLE_MAX
+        dev = self.device
+        nloc = self.rows + self.halo
+        lip = self._lip
+        splits = torch.empty((B - 1, nloc), dtype=torch.int64, device=dev)
+        if nloc:
+            _lib.call(dev, "srg_csr_col_splits", lip.data_ptr(), self._lix_glob.data_ptr() if self._lix_glob.numel() else None,
+                      nloc, self.n, B, splits.data_ptr(), _lib.stream(dev))
+        deg = lip[1:] - lip[:-1]
+        whole = (deg <= BLOCK_WHOLE_MAX) if BLOCK_WHOLE_MAX > 0 else torch.zeros_like(deg, dtype=torch.bool)
+        splits = torch.where(whole.unsqueeze(0), lip[1:].unsqueeze(0), splits)
+        self._cb[key] = ([lip[:-1]] + [splits[b] for b in range(B - 1)] + [lip[1:]], whole)
+        return self._cb[key]
+
+    def _hub_blocks_for(self, d: int) -> int:
+        """Column blocks of the hub group's launches: `hub_col_blocks` if given, else
+        AUTO_HALO_HUB_BLOCKS (HIP ranks, exact mode, d >= 64; FAST hub rows are one launch)."""
+        if not self._hip or self.fast or not (self.views[self.C][1] and self.views[self.C][3]):
+            return 1
+        if self.hub_col_blocks is not None:
+            return max(1, int(self.hub_col_blocks))
+        return AUTO_HALO_HUB_BLOCKS if d >= 64 else 1
+
+    def hub_blocks(self, d: int):
+        """The hub group's column blocks for a panel of d columns: B DeviceCSRs over the row spans
+        of _block_bounds(B), every hub row in every block (so the launches chain on the hub side
+        stream with SRG_SPMM_HUB_CONTINUE: each hub row's workgroups of block b run after its block
+        b-1 workgroups), or None for one launch.  Bitwise the one launch, as for the chunks."""
+        B = self._hub_blocks_for(d)
+        if B < 2:
+            return None
+        key = ("hub", B)
+        if key in self._cb:
+            return self._cb[key]
+        from .csr import DeviceCSR
+        bounds, _ = self._block_bounds(B)
+        order, n_g, _, n_hub = self.views[self.C]
+        blocks = [DeviceCSR(bounds[b], self._lix, self._lvv, n_g, self.ncols_local, order, 0, n_hub, None,
+                            row_end=bounds[b + 1], row_space=self.rows) for b in range(B)]
+        self._cb[key] = blocks
+        return blocks
+
+    def _hub_launch(self, src: torch.Tensor, out: torch.Tensor):
+        """The hub group forked onto the library's hub side stream (joined by the caller): one
+        launch, or its column blocks chained on the side stream."""
+        from .spmm import spmm
+        blocks = self.hub_blocks(src.shape[1])
+        if blocks is None:
+            spmm(self._A[self.C], src, out=out, hub_nojoin=True, fast=self.fast)
+            return
+        for b, Ab in enumerate(blocks):
+            spmm(Ab, src, out=out, accumulate=b > 0, hub_nojoin=True, hub_continue=b > 0)
 
     def _chunk_spmm(self, c: int, src: torch.Tensor, out: torch.Tensor, blocks=None):
         """Row chunk c's launch(es): one, or its column blocks in order (bitwise the same)."""
@@ -694,7 +750,7 @@ class HaloPartitionedOperator:
             if packed is not None:
                 spmm_send(self._A[C], src, out, packed, self._send_ptr, self._send_slot)
             elif fork:
-                spmm(self._A[C], src, out=out, hub_nojoin=True, fast=self.fast)
+                self._hub_launch(src, out)
             else:
                 self._spmm(self._A[C], src, out)
         blocks = self.chunk_blocks(src.shape[1]) if packed is None else None
@@ -767,7 +823,7 @@ class HaloPartitionedOperator:
         fork = bool(self.views[C][1] and self.views[C][3])
         if self.views[C][1]:
             if fork:
-                spmm(self._A[C], src, out=out, hub_nojoin=True, fast=self.fast)
+                self._hub_launch(src, out)
             else:
                 self._spmm(self._A[C], src, out)
         pending = []
@@ -840,14 +896,15 @@ def _virtual_exchange(shares, panels, ghosts: bool = False):
 
 def simulate_halo_propagate(indptr, indices, values, n: int, x: torch.Tensor, K: int, world: int,
                             chunks: int = 3, heavy_threshold=None, hub_threshold=None, device=None,
-                            ghost_max_degree=None, shares=None, col_blocks=None):
+                            ghost_max_degree=None, shares=None, col_blocks=None, hub_col_blocks=None):
     """P virtual halo-exchange ranks in ONE process (all_to_all emulated by copies); returns the
     K+1 full [n, d] panels.  Exercises the group split, ghost rows, halo layout and column remap
     on a device."""
     if shares is None:
         shares = [HaloPartitionedOperator(indptr, indices, values, n, chunks=chunks, heavy_threshold=heavy_threshold,
                                           hub_threshold=hub_threshold, device=device, rank=q, world=world,
-                                          ghost_max_degree=ghost_max_degree, col_blocks=col_blocks)
+                                          ghost_max_degree=ghost_max_degree, col_blocks=col_blocks,
+                                          hub_col_blocks=hub_col_blocks)
                   for q in range(world)]
     d = x.shape[1]
     panels = [[s.new_panel(d) for _ in range(K + 1)] for s in shares]

@@ -382,13 +382,16 @@ def test_products_scale_sampled_rows_bit_exact(oracle_mod):
     assert bool((y[:, 1:] == y[:, :1]).all())
 
 
-@pytest.mark.parametrize("world,chunks,ghost,cb", [(2, 3, None, None), (8, 4, None, None), (2, 3, 0, None),
-                                                   (4, 2, 64, None), (8, 3, 8, None), (2, 3, None, 2),
-                                                   (8, 4, None, 3), (4, 2, 64, 4)])
-def test_halo_virtual_ranks_bitwise(world, chunks, ghost, cb):
+@pytest.mark.parametrize("world,chunks,ghost,cb,hcb", [(2, 3, None, None, None), (8, 4, None, None, None),
+                                                       (2, 3, 0, None, None), (4, 2, 64, None, None),
+                                                       (8, 3, 8, None, None), (2, 3, None, 2, None),
+                                                       (8, 4, None, 3, None), (4, 2, 64, 4, None),
+                                                       (2, 3, None, None, 3), (8, 4, None, 2, 4)])
+def test_halo_virtual_ranks_bitwise(world, chunks, ghost, cb, hcb):
     """The halo-exchange multi-GPU layout (groups, remapped columns, hub group, ghost rows
-    computed into the halo, the row chunks' column blocks split by GLOBAL column ids) on one
-    device with the real kernels: bitwise equal to the single-device propagation."""
+    computed into the halo, the row chunks' column blocks split by GLOBAL column ids, the hub
+    group's column blocks chained on the hub side stream) on one device with the real kernels:
+    bitwise equal to the single-device propagation."""
     from srgnn import synth
     from srgnn.csr import DeviceCSR
     from srgnn.dist import simulate_halo_propagate
@@ -401,7 +404,7 @@ def test_halo_virtual_ranks_bitwise(world, chunks, ghost, cb):
     x = synth.uniform_features_t(n, 128, device="cuda")
     want = propagate(DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, device="cuda"), x, 3)
     got = simulate_halo_propagate(ip, ix, vals, n, x, 3, world, chunks=chunks, hub_threshold=300,
-                                  device="cuda", ghost_max_degree=ghost, col_blocks=cb)
+                                  device="cuda", ghost_max_degree=ghost, col_blocks=cb, hub_col_blocks=hcb)
     for k in range(1, 4):
         assert torch.equal(got[k], want[k]), f"hop {k} differs with {world} virtual halo ranks"
 

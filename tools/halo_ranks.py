@@ -42,6 +42,8 @@ def main():
                     help="non-hub rows longer than this run in the first chunk (srgnn.dist early_degree)")
     ap.add_argument("--col-blocks", default=None,
                     help="column blocks of the row chunks' launches: one value or a comma list (default: auto)")
+    ap.add_argument("--hub-col-blocks", default=None,
+                    help="column blocks of the hub group's launch: one value or a comma list (default: auto)")
     ap.add_argument("--ghost", default="auto",
                     help="ghost row degree cap(s): 'auto' (the operator's cost model) or a comma list")
     a = ap.parse_args()
@@ -52,13 +54,15 @@ def main():
     out = {"config": a.config, "n": n, "nnz": int(ix.numel()), "d": d, "worlds": {}}
     ghosts = [None] if a.ghost == "auto" else [int(c) for c in a.ghost.split(",")]
     cbs = [None] if a.col_blocks is None else [int(c) for c in a.col_blocks.split(",")]
-    for P, ghost, cb in [(int(w), gc, cb) for w in a.worlds.split(",") for gc in ghosts for cb in cbs]:
+    hcbs = [None] if a.hub_col_blocks is None else [int(c) for c in a.hub_col_blocks.split(",")]
+    for P, ghost, cb, hcb in [(int(w), gc, cb, h) for w in a.worlds.split(",") for gc in ghosts for cb in cbs
+                              for h in hcbs]:
         ranks = []
         for q in range(P):
             op = HaloPartitionedOperator(ip, ix, vals, n, chunks=a.chunks, device=dev, rank=q, world=P,
                                          ghost_max_degree=ghost, hub_launches=a.hub_launches,
                                          giant_weight=a.giant_weight, fast=a.fast, col_blocks=cb,
-                                         early_degree=a.early_degree)
+                                         early_degree=a.early_degree, hub_col_blocks=hcb)
             src = op.new_panel(d)
             src[: op.rows].copy_(x[op.r0:op.r1])
             src[op.rows:].uniform_(-1, 1)
@@ -90,6 +94,18 @@ def main():
             torch.cuda.synchronize()
             ms = sorted(ev[2 * r].elapsed_time(ev[2 * r + 1]) for r in range(a.reps))
             times["compute"] = ms[len(ms) // 2]
+            # the hub group as the hop issues it (its column blocks chained on the side stream)
+            if op.views[op.C][1] and op.views[op.C][3]:
+                from srgnn import _lib
+                ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * a.reps)]
+                for r in range(a.reps):
+                    ev[2 * r].record()
+                    op._hub_launch(src, dst[: op.rows])
+                    _lib.call(dev, "srg_hub_join", _lib.stream(dev))
+                    ev[2 * r + 1].record()
+                torch.cuda.synchronize()
+                ms = sorted(ev[2 * r].elapsed_time(ev[2 * r + 1]) for r in range(a.reps))
+                times["hub_launch"] = ms[len(ms) // 2]
             # the send-side pack (index_select of the rows peers need, per group) alone, and the
             # chunks with each group's pack on a second stream as the real hop issues it
             for name, fn in (("pack_index_select", lambda t, i: t.index_select(0, i)), ("pack", gather_rows)):
@@ -132,7 +148,7 @@ def main():
                    "halo_bytes": op.n_recv * d * 4, "send_rows": int(sum(t.numel() for t in op.send_cat)),
                    "hub_rows": op.views[op.C][1],
                    "ms_all_serial": times["all"], "ms_hub": times["hub"], "ms_chunks": times["chunks"],
-                   "ms_compute": times["compute"]}
+                   "ms_compute": times["compute"], "ms_hub_launch": times.get("hub_launch")}
             if a.fused:
                 # the fused pack (srg_spmm_send_f32): the chunks' kernels store the send rows themselves
                 from srgnn.spmm import spmm_send
@@ -150,19 +166,21 @@ def main():
             ranks.append(rec)
             print(f"  P={P} rank {q}: rows={op.rows} halo={op.halo} (received {op.n_recv}, ghosts {op.n_ghost} "
                   f"<= degree {op.ghost_max_degree}) chunks {times['chunks']:.3f} ms (ghosts {times['ghosts']:.3f}), "
-                  f"hub {times['hub']:.3f} ms", file=sys.stderr, flush=True)
+                  f"hub {times['hub']:.3f} ms (as launched {times.get('hub_launch', 0.0):.3f}), "
+                  f"compute {times['compute']:.3f} ms", file=sys.stderr, flush=True)
             del op, src, dst
             torch.cuda.empty_cache()
         worst = max(ranks, key=lambda r: max(r["ms_hub"], r["ms_chunks"]))
-        key = (f"{P}" if a.ghost == "auto" else f"{P}/ghost{ghost}") + ("" if cb is None else f"/cb{cb}")
-        out["worlds"][key] = {"ranks": ranks, "col_blocks": cb,
+        key = (f"{P}" if a.ghost == "auto" else f"{P}/ghost{ghost}") + ("" if cb is None else f"/cb{cb}") + \
+            ("" if hcb is None else f"/hcb{hcb}")
+        out["worlds"][key] = {"ranks": ranks, "col_blocks": cb, "hub_col_blocks": hcb,
                             "max_hop_compute_ms": max(r["ms_compute"] for r in ranks),
                             "max_compute_ms": max(max(r["ms_hub"], r["ms_chunks"]) for r in ranks),
                             "mean_chunks_ms": sum(r["ms_chunks"] for r in ranks) / P,
                             "worst_rank": worst["rank"],
                             "max_halo_GB": max(r["halo_bytes"] for r in ranks) / 1e9}
         W = out["worlds"][key]
-        print(f"P={P} col blocks {cb} ghost cap {ranks[0]['ghost_max_degree']}: hop compute {W['max_hop_compute_ms']:.3f} ms, "
+        print(f"P={P} col blocks {cb} hub blocks {hcb} ghost cap {ranks[0]['ghost_max_degree']}: hop compute {W['max_hop_compute_ms']:.3f} ms, "
               f"max compute {W['max_compute_ms']:.3f} ms "
               f"(rank {worst['rank']}: chunks {worst['ms_chunks']:.3f}, hub {worst['ms_hub']:.3f}), "
               f"mean chunks {W['mean_chunks_ms']:.3f} ms, max received halo "
