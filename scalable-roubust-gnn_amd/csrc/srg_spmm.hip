@@ -743,6 +743,38 @@ struct HubGeom {
 constexpr int kHubWideLaunch = 256;   // more hub workgroups than this (the CU count) -> W = 256
 __device__ __forceinline__ int hub_swz(int c) { return (c >> 2) & 7; }
 constexpr int kHubL = 7;   // consumer: (tile, value) LDS read pairs in flight in a full window
+// Full windows take their link values by DPP quad broadcast (hub_links16); SRG_HUB_DPP=0 builds the
+// value-read-per-4-links loop instead (A/B)
+#ifndef SRG_HUB_DPP
+#define SRG_HUB_DPP 1
+#endif
+constexpr bool kHubDpp = SRG_HUB_DPP != 0;
+constexpr int kHubDppL = 3;   // 16-link sets in flight (4 tile reads + 1 value read each)
+
+// 16 links of one column chain: link 4i + j multiplies x = t[i][j] by the value that quad lane i
+// holds in a[j] (quad_perm broadcast), acc = fma(value, x, acc) -- v_fmac_f32 with a DPP first
+// operand, one instruction per link.  One asm block: the compiler's hazard pass would otherwise pad
+// every link with an s_nop (it treats the chained accumulator like a DPP source; 0.95 vs 0.86 ms on
+// the products hub row).  The DPP'd operands a[] come straight from LDS reads, which no VALU writes.
+__device__ __forceinline__ void hub_links16(float& acc, const typename Vec<float, 4>::type& a,
+                                            const typename Vec<float, 4>::type (&t)[4])
+{
+#define SRG_QP(I) " quad_perm:[" #I "," #I "," #I "," #I "] row_mask:0xf bank_mask:0xf\n"
+    asm volatile(
+        "v_fmac_f32_dpp %0, %1, %5" SRG_QP(0) "v_fmac_f32_dpp %0, %2, %6" SRG_QP(0)
+        "v_fmac_f32_dpp %0, %3, %7" SRG_QP(0) "v_fmac_f32_dpp %0, %4, %8" SRG_QP(0)
+        "v_fmac_f32_dpp %0, %1, %9" SRG_QP(1) "v_fmac_f32_dpp %0, %2, %10" SRG_QP(1)
+        "v_fmac_f32_dpp %0, %3, %11" SRG_QP(1) "v_fmac_f32_dpp %0, %4, %12" SRG_QP(1)
+        "v_fmac_f32_dpp %0, %1, %13" SRG_QP(2) "v_fmac_f32_dpp %0, %2, %14" SRG_QP(2)
+        "v_fmac_f32_dpp %0, %3, %15" SRG_QP(2) "v_fmac_f32_dpp %0, %4, %16" SRG_QP(2)
+        "v_fmac_f32_dpp %0, %1, %17" SRG_QP(3) "v_fmac_f32_dpp %0, %2, %18" SRG_QP(3)
+        "v_fmac_f32_dpp %0, %3, %19" SRG_QP(3) "v_fmac_f32_dpp %0, %4, %20" SRG_QP(3)
+        : "+v"(acc)
+        : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]),
+          "v"(t[0][0]), "v"(t[0][1]), "v"(t[0][2]), "v"(t[0][3]), "v"(t[1][0]), "v"(t[1][1]), "v"(t[1][2]), "v"(t[1][3]),
+          "v"(t[2][0]), "v"(t[2][1]), "v"(t[2][2]), "v"(t[2][3]), "v"(t[3][0]), "v"(t[3][1]), "v"(t[3][2]), "v"(t[3][3]));
+#undef SRG_QP
+}
 
 // ABL (diagnostic ablations, SRGNN_HUB_ABLATION): 0 = the kernel; 1 = the consumer skips its
 // chains; 2 = the producers skip gathers and LDS writes; 3 = the consumer's fmas read registers
@@ -808,6 +840,47 @@ k_spmm_hub(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
                     }
                 };
                 if (ABL == 1) continue;
+                if (kHubDpp && (ABL == 0 || ABL == 2 || ABL == 4) && nb == W) {
+                    // full window, values by DPP: per 16 links one ds_read_b128 of values (lane l
+                    // reads values 16k + 4 (l & 3) .. +3, so register j of quad lane i holds value
+                    // 16k + 4i + j) and four tile reads (4 links each); link 4i + j is
+                    //   v_fmac_f32_dpp acc, a[j], t_i[j] quad_perm:[i,i,i,i]
+                    // (the quad broadcast of lane i's a[j] as the fma's first operand: the same
+                    // fused multiply-add as v_fma_f32, so the chain keeps its bits).  The value
+                    // reads drop from one per 4 links to one per 16.  Ring: kHubDppL 16-link sets
+                    // in flight (5 LDS reads each, 5 * kHubDppL <= 15 = lgkmcnt's range).
+                    constexpr int NK = W / 16;
+                    const float* tb[8];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) tb[k] = hub_lds + (h & 1) * HubGeom<W>::TILE + c * HubGeom<W>::LD + ((k ^ sw) << 2);
+                    const float* avl = av + 4 * (lane & 3);
+                    auto rt = [&](int grp) { return *reinterpret_cast<const V4*>(tb[grp & 7] + (grp >> 3) * 32); };
+                    auto rv = [&](int k) { return *reinterpret_cast<const V4*>(avl + 16 * k); };
+                    V4 t[kHubDppL][4], a[kHubDppL];
+#pragma unroll
+                    for (int r = 0; r < kHubDppL; ++r) {
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) t[r][i] = rt(4 * r + i);
+                        a[r] = rv(r);
+                    }
+#pragma unroll
+                    for (int k0 = 0; k0 < NK; k0 += kHubDppL) {
+#pragma unroll
+                        for (int r = 0; r < kHubDppL; ++r) {
+                            const int k = k0 + r;
+                            if (k < NK) {
+                                hub_links16(acc, a[r], t[r]);
+                                if (k + kHubDppL < NK) {
+#pragma unroll
+                                    for (int i = 0; i < 4; ++i) t[r][i] = rt(4 * (k + kHubDppL) + i);
+                                    a[r] = rv(k + kHubDppL);
+                                }
+                                __builtin_amdgcn_sched_barrier(0);
+                            }
+                        }
+                    }
+                    continue;
+                }
                 if ((ABL == 0 || ABL == 2 || ABL == 4) && nb == W) {
                     // full window, fully unrolled: every LDS read is a per-lane base (the XOR swizzle
                     // of group k & 7 folded in, hoisted per window) or the value base, plus an
