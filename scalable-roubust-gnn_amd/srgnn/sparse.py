@@ -53,6 +53,16 @@ def _rows_have_unique_cols(ip: torch.Tensor, ix: torch.Tensor, n_rows: int) -> b
     return not bool((ks[1:] == ks[:-1]).any())
 
 
+def _check_csr(ip: torch.Tensor, ix: torch.Tensor, v: torch.Tensor) -> None:
+    """The kernels trust the row pointers: int64, from 0 to nnz, non-decreasing."""
+    if ip.dtype != torch.int64 or ip.dim() != 1 or ip.numel() < 1:
+        raise ValueError("indptr must be a 1-D int64 tensor of n_rows + 1 entries")
+    if ix.numel() != v.numel():
+        raise ValueError(f"indices ({ix.numel()}) and values ({v.numel()}) differ in length")
+    if int(ip[0]) != 0 or int(ip[-1]) != ix.numel() or (ip.numel() > 1 and bool((ip[1:] < ip[:-1]).any())):
+        raise ValueError("indptr must run from 0 to nnz without decreasing")
+
+
 def spgemm(a_ip, a_ix, a_v, b_ip, b_ix, b_v, n_cols: int, scratch_limit: int | None = None):
     """C = A @ B for device CSRs (A: m x k with column ids < k = rows of B; B: k x n_cols), fp32,
     in torch_sparse / scipy's arithmetic (module docstring).  Returns (indptr, indices, values)."""
@@ -64,6 +74,8 @@ def spgemm(a_ip, a_ix, a_v, b_ip, b_ix, b_v, n_cols: int, scratch_limit: int | N
     for t in (a_v, b_v):
         if t.dtype != torch.float32:
             raise TypeError(f"spgemm computes in fp32, got {t.dtype}")
+    _check_csr(a_ip, a_ix, a_v)
+    _check_csr(b_ip, b_ix, b_v)
     if a_ix.numel() and (int(a_ix.min()) < 0 or int(a_ix.max()) >= k):
         raise ValueError("A's column ids must index B's rows")
     if b_ix.numel() and (int(b_ix.min()) < 0 or int(b_ix.max()) >= n_cols):
@@ -111,10 +123,14 @@ def spmm_scatter(ip, ix, v, X: torch.Tensor, out: torch.Tensor | None = None) ->
     if X.dim() != 2 or X.stride(1) != 1:
         X = X.reshape(X.shape[0], -1).contiguous()
     n_rows, d = ip.numel() - 1, X.shape[1]
+    _check_csr(ip, ix, v)
     if ix.numel() and (int(ix.min()) < 0 or int(ix.max()) >= X.shape[0]):
         raise ValueError("column ids must index X's rows")
     if out is None:
         out = torch.empty((n_rows, d), dtype=torch.float32, device=dev)
+    elif (out.dtype != torch.float32 or out.device != dev or out.dim() != 2 or tuple(out.shape) != (n_rows, d)
+          or (d > 1 and out.stride(1) != 1)):
+        raise ValueError(f"out must be a float32 [{n_rows}, {d}] tensor with unit column stride on {dev}")
     _lib.call(dev, "srg_spmm_muladd_f32", ip.data_ptr(), ix.data_ptr() if ix.numel() else None,
               v.data_ptr() if v.numel() else None, n_rows, X.data_ptr(), X.stride(0) if X.shape[0] > 1 else d,
               out.data_ptr(), out.stride(0) if n_rows > 1 else d, d, _lib.stream(dev))

@@ -231,3 +231,27 @@ def test_sparse_products_edge_cases():
     assert one_i.tolist() == [[0], [0]] and one_v.tolist() == [1.5]
     y = torch_sparse.spmm(e, ev, 4, 3, torch.ones(3, 2))
     assert y.shape == (4, 2) and bool((y == 0).all())
+
+
+def test_sparse_products_reject_bad_csr_and_out():
+    """srgnn.sparse validates what its kernels trust: row pointers from 0 to nnz without decreasing,
+    ids and values of one length, and an `out` of the product's shape (ValueError, nothing launched)."""
+    from srgnn import sparse as S
+    ip = torch.tensor([0, 2, 3], dtype=torch.int64, device="cuda")
+    ix = torch.tensor([0, 1, 1], dtype=torch.int32, device="cuda")
+    v = torch.tensor([1.0, 2.0, 3.0], device="cuda")
+    X = torch.ones((2, 4), device="cuda")
+    assert torch.equal(S.spmm_scatter(ip, ix, v, X), torch.tensor([[3.0] * 4, [3.0] * 4], device="cuda"))
+    for bad in (torch.tensor([0, 2, 4], dtype=torch.int64, device="cuda"),     # ends past nnz
+                torch.tensor([0, 3, 2], dtype=torch.int64, device="cuda"),     # decreasing
+                torch.tensor([1, 2, 3], dtype=torch.int64, device="cuda")):    # does not start at 0
+        with pytest.raises(ValueError):
+            S.spmm_scatter(bad, ix, v, X)
+        with pytest.raises(ValueError):
+            S.spgemm(bad, ix, v, ip, ix, v, 2)
+    with pytest.raises(ValueError):
+        S.spmm_scatter(ip, ix, v[:2], X)
+    for out in (torch.empty((1, 4), device="cuda"), torch.empty((2, 3), device="cuda"),
+                torch.empty((4, 2), device="cuda").t(), torch.empty((2, 4), dtype=torch.float64, device="cuda")):
+        with pytest.raises(ValueError):
+            S.spmm_scatter(ip, ix, v, X, out=out)
