@@ -437,7 +437,7 @@ def run_wavelet(a, dev, world=1, rank=0, pmc=None):
     from srgnn import wavelet as W
     from srgnn.csr import DeviceCSR
     from srgnn import _lib
-    from srgnn.spmm import auto_col_blocks, hop, spmm_cheby
+    from srgnn.spmm import auto_col_blocks, hop, launches_per_hop, spmm_cheby
     t_build = time.perf_counter()
     ip, ix, lv, n, d, lmax = graphs.build_laplacian(a.config, dev, d=a.d)
     nnz = int(ix.numel())
@@ -477,6 +477,7 @@ def run_wavelet(a, dev, world=1, rank=0, pmc=None):
     Fm = filt._csr(filt.fvals)
     B = auto_col_blocks(Fm, cb)
     B = 1 if fused or B < 2 or not Fm.column_blocks(B) else B
+    LB = launches_per_hop(Fm, B)
     tb = torch.zeros((n, cb), dtype=torch.float32, device=dev)
     ns = len(filt.taus)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * a.roofline_reps)]
@@ -496,7 +497,7 @@ def run_wavelet(a, dev, world=1, rank=0, pmc=None):
     b_alg = roofline.bytes_no_reuse(n, nnz, cb) + extra
     b_comp = roofline.bytes_compulsory(n, nnz, cb, n_cols=n) + extra
     peak = roofline.MI355X_HBM_PEAK_GBS
-    traffic = float(pmc["hbm_bytes_per_hop"]) if pmc is not None and int(pmc["launches_per_hop"]) == B else None
+    traffic = float(pmc["hbm_bytes_per_hop"]) if pmc is not None and int(pmc["launches_per_hop"]) == LB else None
     achieved = (traffic if traffic else b_comp) / kern_s / 1e9
     res = {
         "metric": "propagated edges/sec (wavelet-basis Chebyshev propagation)",
@@ -516,10 +517,10 @@ def run_wavelet(a, dev, world=1, rank=0, pmc=None):
                      "achieved_basis": ("HBM bytes per order's SpMM from PMC counters (traffic) / its time" if traffic
                                         else "compulsory bytes / the SpMM's time (no counter run: a lower bound)"),
                      "traffic_source": pmc["source"] if traffic else None,
-                     "unit_of_work": f"one Chebyshev order's SpMM over a {cb}-column block ({B} column-block launches)",
+                     "unit_of_work": f"one Chebyshev order's SpMM over a {cb}-column block ({B} column blocks, {LB} launches)",
                      "kernel": (f"k_spmm with the Chebyshev epilogue: one order over a {cb}-column block" if fused
                                 else f"k_spmm: one Chebyshev order's SpMM over a {cb}-column block"),
-                     "kernel_ms": kern_s * 1e3, "launches_per_hop": B, "kernel_ms_per_launch": kern_s * 1e3 / B,
+                     "kernel_ms": kern_s * 1e3, "launches_per_hop": LB, "kernel_ms_per_launch": kern_s * 1e3 / LB,
                      "frac_no_reuse": b_alg / kern_s / 1e9 / peak, "frac_compulsory": b_comp / kern_s / 1e9 / peak,
                      "algorithmic_bytes_per_hop": b_alg, "compulsory_bytes_per_hop": b_comp,
                      "traffic_over_compulsory": (traffic / b_comp) if traffic else None},
@@ -626,7 +627,7 @@ def main():
         init_pg()
 
     from srgnn.csr import DeviceCSR
-    from srgnn.spmm import auto_col_blocks, column_blocks_for, hop, propagate, spmm
+    from srgnn.spmm import auto_col_blocks, column_blocks_for, hop, launches_per_hop, propagate, spmm
 
     t_build = time.perf_counter()
     ip, ix, vals, n, d, K = graphs.build(a.config, dev, d=a.d)
@@ -649,7 +650,8 @@ def main():
         col_blocks = a.col_blocks if a.col_blocks is not None else auto_col_blocks(A, d, hops=K * (a.steps + a.warmup))
         if col_blocks > 1 and not column_blocks_for(A, col_blocks, hops=K * (a.steps + a.warmup)):
             col_blocks = 1
-        log(f"schedule: n_hub={A.n_hub} n_heavy={A.n_heavy} column blocks per hop={col_blocks}")
+        launches = launches_per_hop(A, col_blocks, agg=bool(a.aggregate))
+        log(f"schedule: n_hub={A.n_hub} n_heavy={A.n_heavy} column blocks per hop={col_blocks} ({launches} launches)")
         if a.aggregate:
             from srgnn.aggregate import combine_plan, combine_steps, propagate_aggregate
 
@@ -679,7 +681,7 @@ def main():
                 panels[1] = propagate_aggregate(A, X, K, last_only=True, col_blocks=col_blocks)
         local_rows, local_nnz = n, nnz
     else:
-        col_blocks = 1
+        col_blocks = launches = 1
     if world > 1 and a.exchange == "allgather":
         from srgnn.dist import RowPartitionedOperator
         op = RowPartitionedOperator(ip, ix, vals, n, heavy_threshold=a.heavy_threshold, device=dev)
@@ -822,7 +824,7 @@ def main():
     b_alg = roofline.bytes_no_reuse(local_rows, local_nnz, d)
     b_comp = roofline.bytes_compulsory(local_rows, local_nnz, d, n_cols=n)
     peak = roofline.MI355X_HBM_PEAK_GBS
-    traffic, traffic_src = pmc_traffic(a.config, launches_per_hop=col_blocks, measured=pmc) if world == 1 \
+    traffic, traffic_src = pmc_traffic(a.config, launches_per_hop=launches, measured=pmc) if world == 1 \
         else (None, None)
     # achieved: HBM bytes the counters saw per hop / hop time (a lower bound -- the compulsory
     # bytes -- where no counter run exists for this layout)
@@ -870,13 +872,15 @@ def main():
                      "achieved_basis": ("HBM bytes per hop from PMC counters (traffic) / hop time" if traffic else
                                         "compulsory bytes per hop / hop time (no counter run for this layout: a lower bound)"),
                      "traffic_source": traffic_src,
-                     "unit_of_work": "one hop" + (f" = {col_blocks} column-block launches" if col_blocks > 1 else " (one launch)")
+                     "unit_of_work": "one hop" + (f" = {col_blocks} column blocks in {launches} launches" if col_blocks > 1
+                                                  else " (one launch)")
                                      + " + the hub workgroups beside them",
                      "kernel": "k_spmm (+ k_spmm_hub beside it): one hop" + (" of rank 0's rows" if world > 1 else "")
-                     + (f" = {col_blocks} column-block launches (bitwise the one-launch hop)" if col_blocks > 1 else ""),
+                     + (f" = {col_blocks} column blocks in {launches} launches (bitwise the one-launch hop)"
+                        if col_blocks > 1 else ""),
                      "kernel_ms": kern_s * 1e3,
-                     "launches_per_hop": col_blocks,
-                     "kernel_ms_per_launch": kern_s * 1e3 / col_blocks,
+                     "launches_per_hop": launches,
+                     "kernel_ms_per_launch": kern_s * 1e3 / launches,
                      "kernel_ms_source": ("HIP events over the timed steps / (steps x K)" if in_run
                                           else f"HIP events around {a.roofline_reps} isolated hop launches"),
                      "kernel_ms_isolated": kern_isolated_s * 1e3,

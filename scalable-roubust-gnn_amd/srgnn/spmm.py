@@ -31,6 +31,11 @@ _U2_BLOCKED = os.environ.get("SRGNN_BLOCK_U2", "1") != "0"
 # column-blocked hops: block b's hub rows continue block b-1's side-stream fork (SRG_SPMM_HUB_CONTINUE)
 # instead of a fork, dispatch delay and join per block; SRGNN_HUB_CHAIN=0 for the A/B
 _HUB_CHAIN = os.environ.get("SRGNN_HUB_CHAIN", "1") != "0"
+# block 0 of a column-blocked hop as two launches over the same arrays (DeviceCSR.split_whole): the
+# cut rows' first spans, then the rows it computes whole.  Products: 6.21 vs 6.24 ms per hop, six
+# alternations; the whole rows first, last or after the cut spans measure the same, and beside the
+# blocks on a second stream 6.80 ms (profiles/r03_ab_split_block0.txt).  SRGNN_SPLIT_BLOCK0=0: one launch
+_SPLIT_BLOCK0 = os.environ.get("SRGNN_SPLIT_BLOCK0", "1") != "0"
 
 
 # Cutting an operator into column blocks (row spans: one binary search per row and boundary, plus
@@ -70,6 +75,15 @@ def auto_col_blocks(A: DeviceCSR, d: int, hops: int | None = None) -> int:
     return B
 
 
+def launches_per_hop(A: DeviceCSR, B: int, agg: bool = False) -> int:
+    """k_spmm launches of one hop of A in B column blocks (hop()): B, plus one when block 0 runs
+    as its cut spans and its whole rows (_SPLIT_BLOCK0, or the aggregation epilogue)."""
+    blocks = A.column_blocks(B) if B > 1 else None
+    if not blocks:
+        return 1
+    return len(blocks) + (1 if (agg or _SPLIT_BLOCK0) and blocks[0].whole_rows is not None else 0)
+
+
 def hop(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, nt_store: bool = False, col_blocks=None,
         agg=None, fast: bool = False) -> torch.Tensor:
     """out = A @ X (one hop, exact), column-blocked when auto_col_blocks (or `col_blocks`) says so
@@ -86,7 +100,7 @@ def hop(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, nt_store: bool = False
     # a block's rows are short: 2 gathers per packed row in flight (d >= 128: 4 or 2 rows per wave;
     # at d = 64, 8 rows per wave, it is 3 % slower)
     u2 = len(blocks) > 1 and d >= 128 and _U2_BLOCKED
-    split = blocks[0].split_whole() if agg is not None and len(blocks) > 1 else None
+    split = blocks[0].split_whole() if (agg is not None or _SPLIT_BLOCK0) and len(blocks) > 1 else None
     # the blocks' hub spans chained on the side stream: one fork (the first block with hub rows),
     # one join at the end of the hop.  X is not written during the hop, and when every block has
     # the same hub rows only the side stream touches them, so nothing else orders them (a row that
@@ -108,7 +122,10 @@ def hop(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, nt_store: bool = False
         if split is not None and b == 0:
             # rows block 0 computes whole finish there: their aggregation runs in that launch
             spmm(split[0], X, out=out, nt_store=nt_store, packed_u2=u2, fast=fast, **hubs(split[0]))
-            spmm_agg(split[1], X, out, agg[0], agg[1], agg[2], nt_store=nt_store, packed_u2=u2, **hubs(split[1]))
+            if agg is None:
+                spmm(split[1], X, out=out, nt_store=nt_store, packed_u2=u2, fast=fast, **hubs(split[1]))
+            else:
+                spmm_agg(split[1], X, out, agg[0], agg[1], agg[2], nt_store=nt_store, packed_u2=u2, **hubs(split[1]))
         elif agg is not None and b == len(blocks) - 1:
             spmm_agg(Ab, X, out, agg[0], agg[1], agg[2], nt_store=nt_store, accumulate=b > 0, packed_u2=u2,
                      **hubs(Ab))

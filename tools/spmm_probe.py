@@ -20,7 +20,7 @@ import torch  # noqa: E402
 
 from srgnn import graphs, roofline, synth  # noqa: E402
 from srgnn.csr import DeviceCSR  # noqa: E402
-from srgnn.spmm import auto_col_blocks, column_blocks_for, hop  # noqa: E402
+from srgnn.spmm import auto_col_blocks, column_blocks_for, hop, launches_per_hop  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="products")
@@ -62,7 +62,7 @@ if a.op == "wavelet":
     torch.cuda.synchronize()
     nnz = A.nnz
     print(json.dumps({"config": a.config, "op": "wavelet", "n": n, "nnz": nnz, "d": d, "reps": a.reps,
-                      "launches_per_hop": B, "n_heavy": A.n_heavy, "n_hub": A.n_hub,
+                      "launches_per_hop": launches_per_hop(A, B), "column_blocks": B, "n_heavy": A.n_heavy, "n_hub": A.n_hub,
                       "algorithmic_bytes": roofline.bytes_no_reuse(n, nnz, d),
                       "compulsory_bytes": roofline.bytes_compulsory(n, nnz, d)}))
     sys.exit(0)
@@ -86,7 +86,8 @@ for _ in range(a.reps):
 torch.cuda.synchronize()
 nnz = A.nnz
 print(json.dumps({"config": "identity" if a.identity else a.config, "n": n, "nnz": nnz, "d": d,
-                  "reps": a.reps, "launches_per_hop": B, "n_heavy": A.n_heavy, "n_hub": A.n_hub,
+                  "reps": a.reps, "launches_per_hop": launches_per_hop(A, B), "column_blocks": B,
+                  "n_heavy": A.n_heavy, "n_hub": A.n_hub,
                   "algorithmic_bytes": roofline.bytes_no_reuse(n, nnz, d),
                   "compulsory_bytes": roofline.bytes_compulsory(n, nnz, d),
                   "x_read_bytes": n * 4 * d, "y_write_bytes": n * 4 * d,
