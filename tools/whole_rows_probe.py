@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Probe: the launch of block 0's whole rows (the short rows a column-blocked hop computes in one
+piece, DeviceCSR.split_whole()[1]) timed alone, next to one cut-span launch of the same hop, under
+the process's packed-row settings (SRGNN_PACKED_ROWS / SRGNN_PACKED_U are read once per process:
+run it once per setting).  Prints one JSON line.
+
+    SRGNN_PACKED_U=4 python tools/whole_rows_probe.py [--config products] [--reps 20]
+"""
+import argparse
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(HERE, "scalable-roubust-gnn_amd"))
+
+import torch  # noqa: E402
+
+from srgnn import graphs, synth  # noqa: E402
+from srgnn.csr import DeviceCSR  # noqa: E402
+from srgnn.spmm import spmm  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--config", default="products")
+ap.add_argument("--reps", type=int, default=20)
+ap.add_argument("--u2", type=int, default=0, help="pass SRG_SPMM_PACKED_U2 to the whole-row launch")
+ap.add_argument("--natural", action="store_true", help="whole rows in row order (no length sort)")
+a = ap.parse_args()
+dev = torch.device("cuda", 0)
+ip, ix, vals, n, d, _ = graphs.build(a.config, dev)
+A = DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, device=dev)
+X = synth.uniform_features_t(n, d, device=dev)
+Y = torch.empty_like(X)
+blocks = A.compact_column_blocks(4)
+cut, whole = blocks[0].split_whole()
+if a.natural:
+    whole.order = torch.sort(whole.order).values.contiguous()
+    whole.n_heavy = 0
+
+
+def timed(fn):
+    fn()
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record()
+    for _ in range(a.reps):
+        fn()
+    ev[1].record()
+    torch.cuda.synchronize()
+    return ev[0].elapsed_time(ev[1]) / a.reps
+
+
+deg = whole.indptr[1:] - whole.indptr[:-1]
+w_rows = whole.order.to(torch.int64)
+res = {"config": a.config, "env": {k: v for k, v in os.environ.items() if k.startswith("SRGNN_")},
+       "u2": a.u2, "natural": a.natural,
+       "whole_rows": whole.n_rows, "whole_nnz": int(deg[w_rows].sum()),
+       "ms_whole": timed(lambda: spmm(whole, X, out=Y, packed_u2=bool(a.u2))),
+       "ms_block1": timed(lambda: spmm(blocks[1], X, out=Y, accumulate=True, packed_u2=True))}
+print(json.dumps(res))
