@@ -199,6 +199,31 @@ def test_propagate_column_blocked_bit_exact(monkeypatch, name, B, compact, whole
     c.check_hop(1, one.cpu().numpy())
 
 
+@pytest.mark.parametrize("name", ["rand_d128_r05", "rand_d36_ppr", "cora_sym_k3"])
+@pytest.mark.parametrize("compact", [False, True])
+def test_block0_split_launches_bit_exact(monkeypatch, name, compact):
+    """Block 0 of a column-blocked hop as two launches (its cut spans, then its whole rows; the
+    default) or one (SRGNN_SPLIT_BLOCK0=0): the same bits as the reference either way, and
+    launches_per_hop counts B + 1 or B launches."""
+    from srgnn import csr as csr_mod
+    from srgnn import spmm as spmm_mod
+    monkeypatch.setattr(csr_mod, "BLOCK_WHOLE_MAX", 8)
+    c = G.Case(name)
+    A = _csr(c, (None, None))
+    blocks = A.compact_column_blocks(4) if compact else A.column_blocks(4)
+    assert blocks[0].whole_rows is not None and bool(blocks[0].whole_rows.any())
+    X = torch.from_numpy(c.x()).cuda()
+    for split in (True, False):
+        monkeypatch.setattr(spmm_mod, "_SPLIT_BLOCK0", split)
+        assert spmm_mod.launches_per_hop(A, 4) == (5 if split else 4)
+        assert spmm_mod.launches_per_hop(A, 4, agg=True) == 5
+        hops = spmm_mod.propagate(A, X, c.k, col_blocks=4)
+        torch.cuda.synchronize()
+        for k in range(1, c.k + 1):
+            c.check_hop(k, hops[k].cpu().numpy())
+    assert spmm_mod.launches_per_hop(A, 1) == 1
+
+
 @pytest.mark.parametrize("name", G.names("raw"))
 def test_column_blocks_exact_for_unordered_rows(name):
     """Column blocks are spans of each row (srg_csr_col_splits: one binary search per row and
