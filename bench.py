@@ -477,7 +477,7 @@ def run_wavelet(a, dev, world=1, rank=0, pmc=None):
     Fm = filt._csr(filt.fvals)
     B = auto_col_blocks(Fm, cb)
     B = 1 if fused or B < 2 or not Fm.column_blocks(B) else B
-    LB = launches_per_hop(Fm, B)
+    LB = launches_per_hop(Fm, B, cb)
     tb = torch.zeros((n, cb), dtype=torch.float32, device=dev)
     ns = len(filt.taus)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * a.roofline_reps)]
@@ -650,7 +650,7 @@ def main():
         col_blocks = a.col_blocks if a.col_blocks is not None else auto_col_blocks(A, d, hops=K * (a.steps + a.warmup))
         if col_blocks > 1 and not column_blocks_for(A, col_blocks, hops=K * (a.steps + a.warmup)):
             col_blocks = 1
-        launches = launches_per_hop(A, col_blocks, agg=bool(a.aggregate))
+        launches = launches_per_hop(A, col_blocks, d, agg=bool(a.aggregate))
         log(f"schedule: n_hub={A.n_hub} n_heavy={A.n_heavy} column blocks per hop={col_blocks} ({launches} launches)")
         if a.aggregate:
             from srgnn.aggregate import combine_plan, combine_steps, propagate_aggregate

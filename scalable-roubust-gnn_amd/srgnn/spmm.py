@@ -32,10 +32,20 @@ _U2_BLOCKED = os.environ.get("SRGNN_BLOCK_U2", "1") != "0"
 # instead of a fork, dispatch delay and join per block; SRGNN_HUB_CHAIN=0 for the A/B
 _HUB_CHAIN = os.environ.get("SRGNN_HUB_CHAIN", "1") != "0"
 # block 0 of a column-blocked hop as two launches over the same arrays (DeviceCSR.split_whole): the
-# cut rows' first spans, then the rows it computes whole.  Products: 6.21 vs 6.24 ms per hop, six
-# alternations; the whole rows first, last or after the cut spans measure the same, and beside the
-# blocks on a second stream 6.80 ms (profiles/r03_ab_split_block0.txt).  SRGNN_SPLIT_BLOCK0=0: one launch
-_SPLIT_BLOCK0 = os.environ.get("SRGNN_SPLIT_BLOCK0", "1") != "0"
+# cut rows' first spans, then the rows it computes whole.  Products (1.25 GB panel): 6.21 vs 6.24 ms
+# per hop, six alternations; the whole rows first, last or after the cut spans measure the same, and
+# beside the blocks on a second stream 6.80 ms.  The HBM-bound giants lose: papers100M (57 GB panel)
+# 245.6-246.1 vs 244.1-244.2 ms, RMAT-26 (68 GB) 314.3-315.8 vs 311.5-313.1 ms
+# (profiles/r03_ab_split_block0*.txt).  "auto": split for panels below SPLIT_BLOCK0_MAX_PANEL;
+# SRGNN_SPLIT_BLOCK0=1 / 0 forces it on / off
+_SPLIT_BLOCK0_ENV = os.environ.get("SRGNN_SPLIT_BLOCK0", "auto")
+SPLIT_BLOCK0_MAX_PANEL = 16 << 30
+
+
+def _split_block0(A: DeviceCSR, d: int) -> bool:
+    if _SPLIT_BLOCK0_ENV != "auto":
+        return _SPLIT_BLOCK0_ENV != "0"
+    return A.n_cols * d * 4 < SPLIT_BLOCK0_MAX_PANEL
 
 
 # Cutting an operator into column blocks (row spans: one binary search per row and boundary, plus
@@ -75,13 +85,14 @@ def auto_col_blocks(A: DeviceCSR, d: int, hops: int | None = None) -> int:
     return B
 
 
-def launches_per_hop(A: DeviceCSR, B: int, agg: bool = False) -> int:
-    """k_spmm launches of one hop of A in B column blocks (hop()): B, plus one when block 0 runs
-    as its cut spans and its whole rows (_SPLIT_BLOCK0, or the aggregation epilogue)."""
+def launches_per_hop(A: DeviceCSR, B: int, d: int, agg: bool = False) -> int:
+    """k_spmm launches of one hop of A over a d-column panel in B column blocks (hop()): B, plus
+    one when block 0 runs as its cut spans and its whole rows (_split_block0, or the aggregation
+    epilogue)."""
     blocks = A.column_blocks(B) if B > 1 else None
     if not blocks:
         return 1
-    return len(blocks) + (1 if (agg or _SPLIT_BLOCK0) and blocks[0].whole_rows is not None else 0)
+    return len(blocks) + (1 if (agg or _split_block0(A, d)) and blocks[0].whole_rows is not None else 0)
 
 
 def hop(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, nt_store: bool = False, col_blocks=None,
@@ -100,7 +111,7 @@ def hop(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, nt_store: bool = False
     # a block's rows are short: 2 gathers per packed row in flight (d >= 128: 4 or 2 rows per wave;
     # at d = 64, 8 rows per wave, it is 3 % slower)
     u2 = len(blocks) > 1 and d >= 128 and _U2_BLOCKED
-    split = blocks[0].split_whole() if (agg is not None or _SPLIT_BLOCK0) and len(blocks) > 1 else None
+    split = blocks[0].split_whole() if (agg is not None or _split_block0(A, d)) and len(blocks) > 1 else None
     # the blocks' hub spans chained on the side stream: one fork (the first block with hub rows),
     # one join at the end of the hop.  X is not written during the hop, and when every block has
     # the same hub rows only the side stream touches them, so nothing else orders them (a row that

@@ -213,15 +213,20 @@ def test_block0_split_launches_bit_exact(monkeypatch, name, compact):
     blocks = A.compact_column_blocks(4) if compact else A.column_blocks(4)
     assert blocks[0].whole_rows is not None and bool(blocks[0].whole_rows.any())
     X = torch.from_numpy(c.x()).cuda()
+    d = X.shape[1]
+    assert spmm_mod._split_block0(A, d)            # "auto": a small panel is split
     for split in (True, False):
-        monkeypatch.setattr(spmm_mod, "_SPLIT_BLOCK0", split)
-        assert spmm_mod.launches_per_hop(A, 4) == (5 if split else 4)
-        assert spmm_mod.launches_per_hop(A, 4, agg=True) == 5
+        monkeypatch.setattr(spmm_mod, "_SPLIT_BLOCK0_ENV", "1" if split else "0")
+        assert spmm_mod.launches_per_hop(A, 4, d) == (5 if split else 4)
+        assert spmm_mod.launches_per_hop(A, 4, d, agg=True) == 5
         hops = spmm_mod.propagate(A, X, c.k, col_blocks=4)
         torch.cuda.synchronize()
         for k in range(1, c.k + 1):
             c.check_hop(k, hops[k].cpu().numpy())
-    assert spmm_mod.launches_per_hop(A, 1) == 1
+    assert spmm_mod.launches_per_hop(A, 1, d) == 1
+    monkeypatch.setattr(spmm_mod, "_SPLIT_BLOCK0_ENV", "auto")
+    monkeypatch.setattr(spmm_mod, "SPLIT_BLOCK0_MAX_PANEL", 1)   # a "giant" panel: one launch
+    assert spmm_mod.launches_per_hop(A, 4, d) == 4
 
 
 @pytest.mark.parametrize("name", G.names("raw"))

@@ -62,7 +62,7 @@ if a.op == "wavelet":
     torch.cuda.synchronize()
     nnz = A.nnz
     print(json.dumps({"config": a.config, "op": "wavelet", "n": n, "nnz": nnz, "d": d, "reps": a.reps,
-                      "launches_per_hop": launches_per_hop(A, B), "column_blocks": B, "n_heavy": A.n_heavy, "n_hub": A.n_hub,
+                      "launches_per_hop": launches_per_hop(A, B, d), "column_blocks": B, "n_heavy": A.n_heavy, "n_hub": A.n_hub,
                       "algorithmic_bytes": roofline.bytes_no_reuse(n, nnz, d),
                       "compulsory_bytes": roofline.bytes_compulsory(n, nnz, d)}))
     sys.exit(0)
@@ -86,7 +86,7 @@ for _ in range(a.reps):
 torch.cuda.synchronize()
 nnz = A.nnz
 print(json.dumps({"config": "identity" if a.identity else a.config, "n": n, "nnz": nnz, "d": d,
-                  "reps": a.reps, "launches_per_hop": launches_per_hop(A, B), "column_blocks": B,
+                  "reps": a.reps, "launches_per_hop": launches_per_hop(A, B, d), "column_blocks": B,
                   "n_heavy": A.n_heavy, "n_hub": A.n_hub,
                   "algorithmic_bytes": roofline.bytes_no_reuse(n, nnz, d),
                   "compulsory_bytes": roofline.bytes_compulsory(n, nnz, d),
