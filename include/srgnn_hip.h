@@ -133,6 +133,33 @@ int srg_propagate_khop_f32(const int64_t* indptr, const int32_t* indices, const 
                            int64_t n_heavy, float* const* panels,
                            int64_t ld, int32_t d, int32_t K, uint32_t flags, void* stream);
 
+/* One launch of a column-blocked hop, as srgnn.csr.DeviceCSR holds a column block (or block 0's two
+ * parts): a CSR over the row space (row_end == NULL: row_beg has row_space + 1 entries) or row spans of
+ * a shared CSR (row_end != NULL: row r's entries are [row_beg[r], row_end[r])), the schedule
+ * (row_order: n_rows row ids, the first n_hub hub rows, then n_heavy slice-wave rows) and the launch's
+ * SRG_SPMM_* flags (ACCUMULATE for blocks 1.., PACKED_U2, HUB_NOJOIN / HUB_CONTINUE for chained hub
+ * spans, NT_STORE, FAST). */
+typedef struct srg_hop_launch {
+    const int64_t* row_beg;
+    const int64_t* row_end;
+    const int32_t* indices;
+    const float* values;
+    const int32_t* row_order;
+    int64_t n_rows;
+    int64_t n_hub;
+    int64_t n_heavy;
+    uint32_t flags;
+} srg_hop_launch;
+
+/* K column-blocked hops: for k = 1..K, the n_launch launches of `launches` (a HOST array) run in
+ * order with X = panels[k-1], Y = panels[k]; with join_hub, the hub side stream (forked by the
+ * first HUB_NOJOIN launch of the hop) is joined back into `stream` at the end of every hop.  The
+ * device-resident form of srgnn.spmm.propagate's blocked hop loop: bitwise the one-launch hops
+ * (the same fma chains, continued across the blocks).  panels: HOST array of K+1 device pointers
+ * of leading dimension ld. */
+int srg_propagate_plan_f32(const srg_hop_launch* launches, int32_t n_launch, int32_t join_hub,
+                           float* const* panels, int64_t ld, int32_t d, int32_t K, void* stream);
+
 /* Chebyshev heat-kernel filter bank (wavelet basis), SSRG/models/base_scalable/base_model.py:
  * 184-191, 236-265 via pygsp cheby_op.  One fused launch per Chebyshev order:
  *   mode SRG_CHEBY_INIT (order 1):  Tn = (A*Tc - a2*Tc) / a1;   R_s  = (c0_s/2)*Tc + c1_s*Tn

@@ -2182,6 +2182,50 @@ int srg_propagate_khop_f32(const int64_t* indptr, const int32_t* indices, const 
     return ok();
 }
 
+int srg_propagate_plan_f32(const srg_hop_launch* launches, int32_t n_launch, int32_t join_hub,
+                           float* const* panels, int64_t ld, int32_t d, int32_t K, void* stream)
+{
+    SRG_DEVICE_GUARD(stream);
+    if (K < 0 || n_launch < 0) return fail(SRG_ERR_INVALID, "K=%d / n_launch=%d < 0", K, n_launch);
+    if (K == 0 || n_launch == 0) return ok();
+    if (!launches || !panels) return fail(SRG_ERR_INVALID, "null launches or panels");
+    for (int k = 0; k <= K; ++k)
+        if (!panels[k] && d > 0) return fail(SRG_ERR_INVALID, "panels[%d] is null", k);
+    for (int i = 0; i < n_launch; ++i) {
+        const srg_hop_launch& L = launches[i];
+        int rc = check_spmm_args(L.row_beg, L.indices, L.values, L.n_rows, panels[0], ld, panels[0], ld, d);
+        if (rc) return rc;
+        if (L.n_rows > 0 && L.n_hub + L.n_heavy > 0 && !L.row_order)
+            return fail(SRG_ERR_INVALID, "launch %d: hub / heavy rows need a row_order", i);
+    }
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    for (int k = 1; k <= K; ++k) {
+        for (int i = 0; i < n_launch; ++i) {
+            const srg_hop_launch& L = launches[i];
+            int rc;
+            if (L.row_end) {
+                Epi e{};
+                e.row_end = L.row_end;
+                rc = launch_spmm<int64_t, kEpiSpan>(L.row_beg, L.indices, L.values, L.n_rows, L.row_order, L.n_hub,
+                                                    L.n_heavy, panels[k - 1], ld, panels[k], ld, d, L.flags, s, e);
+            } else {
+                rc = launch_spmm<int64_t>(L.row_beg, L.indices, L.values, L.n_rows, L.row_order, L.n_hub, L.n_heavy,
+                                          panels[k - 1], ld, panels[k], ld, d, L.flags, s);
+            }
+            if (rc) return rc;
+        }
+        if (join_hub) {
+            std::lock_guard<std::mutex> lock(g_side_mu);
+            auto it = g_side.find(std::make_pair(guard_.dev, s));
+            if (it != g_side.end() && it->second.pending) {
+                SRG_HIP_CHECK(hipStreamWaitEvent(s, it->second.join, 0));
+                it->second.pending = false;
+            }
+        }
+    }
+    return ok();
+}
+
 int srg_cheby_step_f64(const int64_t* indptr, const int32_t* indices, const double* values,
                        int64_t n_rows, const int32_t* row_order, const double* Tc,
                        const double* To, double* Tn, int64_t ld, int32_t d, int mode, double a1,

@@ -47,6 +47,7 @@ EXPORTED_SYMBOLS = (
     "FloatCSRMulDense",
     "srg_spmm_csr_f32",
     "srg_propagate_khop_f32",
+    "srg_propagate_plan_f32",
     "srg_cheby_step_f64",
     "srg_cheby_step_f32",
     "srg_cheby_epilogue_f32",
@@ -102,6 +103,8 @@ def _declare(lib):
     lib.srg_spmm_csr_f32.restype = ctypes.c_int
     lib.srg_propagate_khop_f32.argtypes = [_p, _p, _p, _i64, _p, _i64, _i64, _p, _i64, _i32, _i32, _u32, _p]
     lib.srg_propagate_khop_f32.restype = ctypes.c_int
+    lib.srg_propagate_plan_f32.argtypes = [_p, _i32, _i32, _p, _i64, _i32, _i32, _p]
+    lib.srg_propagate_plan_f32.restype = ctypes.c_int
     lib.srg_cheby_step_f64.argtypes = [_p, _p, _p, _i64, _p, _p, _p, _p, _i64, _i32, ctypes.c_int,
                                        _f64, _f64, _p, _p, _i32, _p, _i64, _p]
     lib.srg_cheby_step_f64.restype = ctypes.c_int

@@ -95,6 +95,43 @@ def launches_per_hop(A: DeviceCSR, B: int, d: int, agg: bool = False) -> int:
     return len(blocks) + (1 if (agg or _split_block0(A, d)) and blocks[0].whole_rows is not None else 0)
 
 
+def _hop_plan(A: DeviceCSR, d: int, B: int, nt_store: bool = False, fast: bool = False, agg: bool = False):
+    """The launches of one hop of A over a d-column panel in B column blocks: ([(operator, flags,
+    kind)], join) with kind "plain" or "agg" (the launch that carries the aggregation epilogue), and
+    join = whether the hub side stream must be joined at the end of the hop."""
+    blocks = (A.column_blocks(B) if B > 1 else None) or [A]
+    # a block's rows are short: 2 gathers per packed row in flight (d >= 128: 4 or 2 rows per wave;
+    # at d = 64, 8 rows per wave, it is 3 % slower)
+    u2 = len(blocks) > 1 and d >= 128 and _U2_BLOCKED
+    split = blocks[0].split_whole() if (agg or _split_block0(A, d)) and len(blocks) > 1 else None
+    # the blocks' hub spans chained on the side stream: one fork (the first block with hub rows),
+    # one join at the end of the hop.  X is not written during the hop, and when every block has
+    # the same hub rows only the side stream touches them, so nothing else orders them (a row that
+    # is a hub in one block only would have spans on both streams: then every block forks and joins)
+    # (with block 0 split, the launches over cut rows are split[0] and blocks 1..; split[1]'s rows --
+    # whole rows -- are in no other launch, so its hub rows never matter)
+    chain = len(blocks) > 1 and not fast and _HUB_CHAIN and \
+        _same_hub_rows(A, B, ([split[0]] + blocks[1:]) if split is not None else blocks, agg=split is not None)
+    base = (_lib.SRG_SPMM_NT_STORE if nt_store else 0) | (_lib.SRG_SPMM_PACKED_U2 if u2 else 0)
+    seq = []     # (operator, accumulate, kind)
+    for b, Ab in enumerate(blocks):
+        if split is not None and b == 0:
+            # rows block 0 computes whole finish there: their aggregation runs in that launch
+            seq += [(split[0], False, "plain"), (split[1], False, "agg" if agg else "plain")]
+        else:
+            seq.append((Ab, b > 0, "agg" if agg and b == len(blocks) - 1 else "plain"))
+    plan, forked = [], False
+    for Ab, acc, kind in seq:
+        f = base | (_lib.SRG_SPMM_ACCUMULATE if acc else 0)
+        if chain and Ab.n_hub > 0:
+            f |= _lib.SRG_SPMM_HUB_NOJOIN | (_lib.SRG_SPMM_HUB_CONTINUE if forked else 0)
+            forked = True
+        elif fast and kind == "plain":
+            f |= _lib.SRG_SPMM_FAST
+        plan.append((Ab, f, kind))
+    return plan, forked
+
+
 def hop(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, nt_store: bool = False, col_blocks=None,
         agg=None, fast: bool = False) -> torch.Tensor:
     """out = A @ X (one hop, exact), column-blocked when auto_col_blocks (or `col_blocks`) says so
@@ -103,52 +140,53 @@ def hop(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, nt_store: bool = False
     rows of every launch (tolerance mode, see spmm)."""
     d = X.shape[1]
     # every launch below writes rows of A's whole row space (the blocks' schedules name them)
+    _check_panel(X, A.n_cols, "X")
     _check_panel(out, A.out_rows, "out", d)
     if agg is not None:
         _check_panel(agg[0], A.out_rows, "agg", d)
+    if out.device != A.device or X.device != A.device:
+        raise ValueError("A, X and out must be on the same device")
     B = auto_col_blocks(A, d) if col_blocks is None else int(col_blocks)
-    blocks = (A.column_blocks(B) if B > 1 else None) or [A]
-    # a block's rows are short: 2 gathers per packed row in flight (d >= 128: 4 or 2 rows per wave;
-    # at d = 64, 8 rows per wave, it is 3 % slower)
-    u2 = len(blocks) > 1 and d >= 128 and _U2_BLOCKED
-    split = blocks[0].split_whole() if (agg is not None or _split_block0(A, d)) and len(blocks) > 1 else None
-    # the blocks' hub spans chained on the side stream: one fork (the first block with hub rows),
-    # one join at the end of the hop.  X is not written during the hop, and when every block has
-    # the same hub rows only the side stream touches them, so nothing else orders them (a row that
-    # is a hub in one block only would have spans on both streams: then every block forks and joins)
-    # (with the aggregation split, the launches over cut rows are split[0] and blocks 1..; split[1]'s
-    # rows -- whole rows -- are in no other launch, so its hub rows never matter)
-    chain = len(blocks) > 1 and not fast and _HUB_CHAIN and \
-        _same_hub_rows(A, B, ([split[0]] + blocks[1:]) if split is not None else blocks, agg=split is not None)
-    forked = False
-
-    def hubs(Ab):       # hub flags of one launch: chained when it has hub rows
-        nonlocal forked
-        if not (chain and Ab.n_hub > 0):
-            return {}
-        f = {"hub_nojoin": True, "hub_continue": forked}
-        forked = True
-        return f
-    for b, Ab in enumerate(blocks):
-        if split is not None and b == 0:
-            # rows block 0 computes whole finish there: their aggregation runs in that launch
-            spmm(split[0], X, out=out, nt_store=nt_store, packed_u2=u2, fast=fast, **hubs(split[0]))
-            if agg is None:
-                spmm(split[1], X, out=out, nt_store=nt_store, packed_u2=u2, fast=fast, **hubs(split[1]))
-            else:
-                spmm_agg(split[1], X, out, agg[0], agg[1], agg[2], nt_store=nt_store, packed_u2=u2, **hubs(split[1]))
-        elif agg is not None and b == len(blocks) - 1:
-            spmm_agg(Ab, X, out, agg[0], agg[1], agg[2], nt_store=nt_store, accumulate=b > 0, packed_u2=u2,
-                     **hubs(Ab))
-        elif chain and Ab.n_hub > 0:
-            spmm(Ab, X, out=out, accumulate=b > 0, nt_store=nt_store, packed_u2=u2, hub_nojoin=True,
-                 hub_continue=forked)
-            forked = True
+    plan, join = _hop_plan(A, d, B, nt_store, fast, agg is not None)
+    for Ab, f, kind in plan:
+        if kind == "agg":
+            _launch(Ab, X, out, d, f, agg[0], agg[1], agg[2])
         else:
-            spmm(Ab, X, out=out, accumulate=b > 0, nt_store=nt_store, packed_u2=u2, fast=fast)
-    if forked:
+            _launch(Ab, X, out, d, f)
+    if join:
         _lib.call(X.device, "srg_hub_join", _stream(X.device))
     return out
+
+
+def _launch(A: DeviceCSR, X, out, d, flags, agg=None, w=0.0, init=False):
+    """One k_spmm launch of a planned hop (operands checked by the caller)."""
+    if A.is_span:
+        _span_call(A, X, out, d, flags, agg, agg.stride(0) if agg is not None else 0, w, init)
+    elif agg is not None:
+        _lib.call(X.device, "srg_spmm_agg_f32", A.indptr.data_ptr(), A.indices.data_ptr(), A.values.data_ptr(),
+                  A.n_rows, A.order.data_ptr() if A.n_rows else None, A.n_hub, A.heavy(d), X.data_ptr(),
+                  X.stride(0), out.data_ptr(), out.stride(0), d, flags, agg.data_ptr(), agg.stride(0), float(w),
+                  1 if init else 0, _stream(X.device))
+    else:
+        _lib.call(X.device, "srg_spmm_csr_f32", A.indptr.data_ptr(), A.indices.data_ptr(), A.values.data_ptr(),
+                  A.n_rows, A.order.data_ptr() if A.n_rows else None, A.n_hub, A.heavy(d), X.data_ptr(),
+                  X.stride(0), out.data_ptr(), out.stride(0), d, flags, _stream(X.device))
+
+
+class _HopLaunch(ctypes.Structure):
+    """srg_hop_launch (include/srgnn_hip.h)."""
+    _fields_ = [("row_beg", ctypes.c_void_p), ("row_end", ctypes.c_void_p), ("indices", ctypes.c_void_p),
+                ("values", ctypes.c_void_p), ("row_order", ctypes.c_void_p), ("n_rows", ctypes.c_int64),
+                ("n_hub", ctypes.c_int64), ("n_heavy", ctypes.c_int64), ("flags", ctypes.c_uint32)]
+
+
+def _plan_array(plan, d):
+    arr = (_HopLaunch * len(plan))()
+    for i, (Ab, f, _) in enumerate(plan):
+        arr[i] = _HopLaunch(Ab.indptr.data_ptr(), Ab.row_end.data_ptr() if Ab.is_span else None,
+                            Ab.indices.data_ptr(), Ab.values.data_ptr(), Ab.order.data_ptr() if Ab.n_rows else None,
+                            Ab.n_rows, Ab.n_hub, Ab.heavy(d), f)
+    return arr
 
 
 def _same_hub_rows(A: DeviceCSR, B: int, blocks, agg: bool = False) -> bool:
@@ -360,8 +398,11 @@ def propagate(A: DeviceCSR, X: torch.Tensor, K: int, panels: list | None = None,
             raise ValueError("all panels must share one leading dimension")
     B = auto_col_blocks(A, d, hops=K) if col_blocks is None else int(col_blocks)
     if K > 0 and B > 1 and column_blocks_for(A, B, hops=K):
-        for k in range(1, K + 1):
-            hop(A, panels[k - 1], panels[k], nt_store=nt_store, col_blocks=B, fast=fast)
+        # the blocked hop loop runs natively: one call for the K hops (srg_propagate_plan_f32)
+        plan, join = _hop_plan(A, d, B, nt_store, fast)
+        arr = (ctypes.c_void_p * (K + 1))(*[p.data_ptr() for p in panels])
+        _lib.call(X.device, "srg_propagate_plan_f32", _plan_array(plan, d), len(plan), 1 if join else 0, arr,
+                  ld, d, K, _stream(X.device))
     else:
         arr = (ctypes.c_void_p * (K + 1))(*[p.data_ptr() for p in panels])
         flags = (_lib.SRG_SPMM_NT_STORE if nt_store else 0) | (_lib.SRG_SPMM_FAST if fast else 0)

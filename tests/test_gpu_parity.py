@@ -817,3 +817,31 @@ def test_blocked_hop_hub_rows_chained_or_forked_bit_exact(oracle_mod, mode):
         hop(A, x, y, col_blocks=3, agg=(agg, 0.5, True))
         torch.cuda.synchronize()
         assert torch.equal(y, want) and torch.equal(agg, 0.0 + 0.5 * want), mode
+
+
+def test_propagate_plan_entry_rejects_bad_launches():
+    """srg_propagate_plan_f32 (the native blocked hop loop) validates every launch before the first
+    kernel: a schedule with hub / heavy rows but no row_order, a null panel, negative K."""
+    import ctypes
+    from srgnn import _lib
+    from srgnn import spmm as spmm_mod
+    c = G.Case("rand_d128_r05")
+    A = _csr(c, (None, None))
+    X = torch.from_numpy(c.x()).cuda()
+    Y = torch.empty_like(X)
+    d = X.shape[1]
+    plan, join = spmm_mod._hop_plan(A, d, 2)
+    arr = spmm_mod._plan_array(plan, d)
+    panels = (ctypes.c_void_p * 2)(X.data_ptr(), Y.data_ptr())
+    _lib.call(X.device, "srg_propagate_plan_f32", arr, len(plan), int(join), panels, d, d, 1, _lib.stream(X.device))
+    torch.cuda.synchronize()
+    c.check_hop(1, Y.cpu().numpy())
+    bad = spmm_mod._plan_array(plan, d)
+    bad[0].n_heavy, bad[0].row_order = max(1, bad[0].n_heavy), None
+    with pytest.raises(RuntimeError):
+        _lib.call(X.device, "srg_propagate_plan_f32", bad, len(plan), int(join), panels, d, d, 1, _lib.stream(X.device))
+    nulls = (ctypes.c_void_p * 2)(X.data_ptr(), None)
+    with pytest.raises(RuntimeError):
+        _lib.call(X.device, "srg_propagate_plan_f32", arr, len(plan), int(join), nulls, d, d, 1, _lib.stream(X.device))
+    with pytest.raises(RuntimeError):
+        _lib.call(X.device, "srg_propagate_plan_f32", arr, len(plan), int(join), panels, d, d, -1, _lib.stream(X.device))
