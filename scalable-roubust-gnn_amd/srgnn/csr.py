@@ -218,7 +218,7 @@ class DeviceCSR:
             deg = end - beg
             nnz_b = int(deg.sum().item())
             sel = deg[later] if (b > 0 and whole is not None) else deg
-            order, n_heavy, n_hub = schedule_from_degrees(sel, nnz_b, heavy_t, hub_t)
+            order, n_heavy, n_hub = schedule_from_degrees(sel, nnz_b, heavy_t, hub_t, block=True)
             if b > 0 and whole is not None:
                 order = later[order.to(torch.int64)].to(torch.int32)
             narrow = narrow_heavy_degrees(sel, n_hub) if auto_narrow else None
@@ -241,7 +241,8 @@ class DeviceCSR:
                 ip = self.indptr
                 deg = ((self.row_end - ip) if self.is_span else (ip[1:] - ip[:-1]))[rows]
                 heavy_t, hub_t = self.thresholds
-                order, n_heavy, n_hub = schedule_from_degrees(deg, int(deg.sum().item()), heavy_t, hub_t)
+                order, n_heavy, n_hub = schedule_from_degrees(deg, int(deg.sum().item()), heavy_t, hub_t,
+                                                              block=True)
                 order = rows[order.to(torch.int64)].to(torch.int32)
                 narrow = narrow_heavy_degrees(deg, n_hub) if self.n_heavy_narrow is not None else None
                 parts.append(DeviceCSR(self.indptr, self.indices, self.values, int(rows.numel()), self.n_cols, order,
@@ -315,12 +316,20 @@ def make_schedule(indptr: torch.Tensor, heavy_threshold=None, hub_threshold=None
                                  heavy_threshold, hub_threshold)
 
 
-def schedule_from_degrees(deg: torch.Tensor, nnz: int, heavy_threshold=None, hub_threshold=None):
-    """make_schedule from the row lengths `deg` (nnz = their sum, for the automatic thresholds)."""
+# Column blocks' spans take the slice waves from a lower length per nonzero of the launch: nnz_b /
+# BLOCK_HEAVY_PER (products, five blocks: 300-500 best, 6.13 ms per hop; 160: 6.43, 600: 6.19, the
+# whole-operator rule nnz_b / 100000 ~ 230: 6.18; profiles/r03_ab_heavy_threshold_B5.txt)
+BLOCK_HEAVY_PER = 60000
+
+
+def schedule_from_degrees(deg: torch.Tensor, nnz: int, heavy_threshold=None, hub_threshold=None,
+                          block: bool = False):
+    """make_schedule from the row lengths `deg` (nnz = their sum, for the automatic thresholds);
+    block: the lengths are a column block's spans (BLOCK_HEAVY_PER for the automatic heavy split)."""
     if heavy_threshold is None:
         heavy_threshold = DEFAULT_HEAVY_THRESHOLD
     if heavy_threshold is None:
-        heavy_threshold = auto_heavy_threshold(nnz)
+        heavy_threshold = max(96, int(nnz) // BLOCK_HEAVY_PER) if block else auto_heavy_threshold(nnz)
     if hub_threshold is None:
         hub_threshold = DEFAULT_HUB_THRESHOLD
     if hub_threshold is None:

@@ -4,7 +4,7 @@ The exchange / partition / column-remap logic of srgnn.dist runs exactly as on G
 local product is the oracle (injected), so the test checks that the partitioned result is
 BITWISE equal to the single-process propagation."""
 import os
-import socket
+import tempfile
 
 import numpy as np
 import pytest
@@ -14,9 +14,12 @@ import torch.multiprocessing as mp
 
 
 def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    """A fresh file:// rendezvous for the ranks' process group: no TCP port to pick and then race
+    for (a port probed free here was once taken before rank 0 listened on it: EADDRINUSE)."""
+    fd, path = tempfile.mkstemp(prefix="srgnn_pg_")
+    os.close(fd)
+    os.unlink(path)
+    return path
 
 
 def _graph():
@@ -35,8 +38,7 @@ def _worker(rank, world, port, out_path):
     here = os.path.dirname(os.path.abspath(__file__))
     repo = os.path.dirname(here)
     sys.path[:0] = [os.path.join(repo, "scalable-roubust-gnn_amd"), repo]
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method="file://" + port, rank=rank, world_size=world)
     from oracle import oracle as O
     from srgnn.dist import RowPartitionedOperator
 
@@ -100,8 +102,7 @@ def _halo_worker(rank, world, port, out_path, chunks, ghost=None, full_x=False):
     here = os.path.dirname(os.path.abspath(__file__))
     repo = os.path.dirname(here)
     sys.path[:0] = [os.path.join(repo, "scalable-roubust-gnn_amd"), repo]
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method="file://" + port, rank=rank, world_size=world)
     from oracle import oracle as O
     from srgnn.dist import HaloPartitionedOperator
 
@@ -260,8 +261,7 @@ def _wavelet_worker(rank, world, port, out_path):
     here = os.path.dirname(os.path.abspath(__file__))
     repo = os.path.dirname(here)
     sys.path[:0] = [os.path.join(repo, "scalable-roubust-gnn_amd"), repo]
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method="file://" + port, rank=rank, world_size=world)
     from oracle import oracle as O
     from srgnn.dist import HaloWaveletFilter
 

@@ -4,7 +4,7 @@ rank runs HaloPartitionedOperator.propagate exactly as on a multi-GPU node -- th
 join, the packs and the asynchronous all_to_all per group, ghost rows, hop 0 exchanged or gathered
 from the whole X -- and its rows of every hop must be bitwise the single-GPU propagation."""
 import os
-import socket
+import tempfile
 
 import numpy as np
 import pytest
@@ -16,17 +16,19 @@ pytestmark = pytest.mark.gpu
 
 
 def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    """A fresh file:// rendezvous for the ranks' process group: no TCP port to pick and then race
+    for (a port probed free here was once taken before rank 0 listened on it: EADDRINUSE)."""
+    fd, path = tempfile.mkstemp(prefix="srgnn_pg_")
+    os.close(fd)
+    os.unlink(path)
+    return path
 
 
 def _worker(rank, world, port, out_path, ghost, whole_x, chunks, cb=None, fast=False):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path[:0] = [os.path.join(os.path.dirname(here), "scalable-roubust-gnn_amd")]
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method="file://" + port, rank=rank, world_size=world)
     from srgnn import synth
     from srgnn.csr import DeviceCSR
     from srgnn.dist import HaloPartitionedOperator
@@ -78,8 +80,7 @@ def _wavelet_worker(rank, world, port, out_path, chunks):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path[:0] = [os.path.join(os.path.dirname(here), "scalable-roubust-gnn_amd")]
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method="file://" + port, rank=rank, world_size=world)
     from srgnn import graphs, synth
     from srgnn.dist import HaloWaveletFilter, simulate_halo_wavelet
     dev = torch.device("cuda", 0)
