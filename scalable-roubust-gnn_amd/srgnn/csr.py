@@ -251,30 +251,57 @@ class DeviceCSR:
             self._blocks["split"] = tuple(parts)
         return self._blocks["split"]
 
+    def _copy_in_order(self, rows: torch.Tensor):
+        """(beg, end, indices, values): the entries of `rows` (int64 row ids) copied out one row after
+        the other in that order, row r's at [beg[r], end[r]) of the copies (rows not listed: empty)."""
+        ip = self.indptr
+        b0 = ip[rows]
+        deg = (self.row_end[rows] if self.is_span else ip[rows + 1]) - b0
+        pos = torch.zeros(rows.numel() + 1, dtype=torch.int64, device=ip.device)
+        torch.cumsum(deg, 0, out=pos[1:])
+        nnz = int(pos[-1].item())
+        # entry e of the copy is entry b0[i] + (e - pos[i]) of row i of the list
+        idx = torch.repeat_interleave(b0 - pos[:-1], deg, output_size=nnz)
+        idx += torch.arange(nnz, dtype=torch.int64, device=ip.device)
+        beg = torch.zeros(self.out_rows, dtype=torch.int64, device=ip.device)
+        end = torch.zeros(self.out_rows, dtype=torch.int64, device=ip.device)
+        beg[rows] = pos[:-1]
+        end[rows] = pos[1:]
+        ix, v = self.indices[idx], self.values[idx]
+        del idx
+        return beg, end, ix, v
+
     def compact_column_blocks(self, B: int):
-        """column_blocks(B) with each block's spans copied into arrays of its own (a plain CSR per
-        block, run by the whole-row kernels): one more copy of the ids and values (1 GB on
-        products), but no cache line of the id / value streams is read by two launches -- 1 %
-        less traffic per hop (45.4 -> 44.9 GB on products).  For operators that serve many hops
-        (spmm.MIN_HOPS_TO_COMPACT); same bits as the spans."""
+        """column_blocks(B) with each block's entries copied into arrays of its own, laid out in the
+        order its launches take the rows: block b's schedule, and for block 0 the schedule of its
+        cut rows' spans followed by that of its whole rows (its two launches, split_whole()).  One
+        more copy of the ids and values (1 GB on products), for operators that serve many hops
+        (spmm.MIN_HOPS_TO_COMPACT): no cache line of the id / value streams is read by two launches
+        (45.4 -> 44.9 GB per hop on products, round 2), and the consecutive rows a wave takes read
+        consecutive entries (round 3, tools/whole_rows_probe.py --sched: the whole-row launch 0.898
+        -> 0.862 ms, block 0's cut spans 1.339 -> 1.301, a later block 1.399 -> 1.384).  Each block
+        is a span operator over its copy; the same entries in the same order per row, so the same
+        bits as the spans."""
         B = int(B)
+        key = ("compact", B)
         blocks = self.column_blocks(B)
-        if not blocks or not blocks[0].is_span:
+        if not blocks or self._blocks.get(key):
             return blocks
         out = []
         for blk in blocks:
-            deg = blk.row_end - blk.indptr
-            bip = torch.zeros(self.n_rows + 1, dtype=torch.int64, device=deg.device)
-            torch.cumsum(deg, 0, out=bip[1:])
-            nnz_b = int(bip[-1].item())
-            # entry e of row r sits at indptr[r] + (e - bip[r]) of the shared arrays
-            idx = torch.repeat_interleave(blk.indptr - bip[:-1], deg, output_size=nnz_b)
-            idx += torch.arange(nnz_b, dtype=torch.int64, device=deg.device)
-            out.append(DeviceCSR(bip, self.indices[idx], self.values[idx], blk.n_rows, self.n_cols, blk.order,
-                                 blk.n_heavy, blk.n_hub, blk.n_heavy_narrow, whole_rows=blk.whole_rows,
-                                 row_space=blk.row_space, thresholds=blk.thresholds))
-            del idx
+            parts = blk.split_whole() if blk.whole_rows is not None else None
+            rows = torch.cat([parts[0].order, parts[1].order]) if parts else blk.order
+            beg, end, ix, v = blk._copy_in_order(rows.to(torch.int64))
+            nb = DeviceCSR(beg, ix, v, blk.n_rows, self.n_cols, blk.order, blk.n_heavy, blk.n_hub, blk.n_heavy_narrow,
+                           row_end=end, whole_rows=blk.whole_rows, row_space=blk.row_space, thresholds=blk.thresholds)
+            if parts:
+                nb._blocks["split"] = tuple(
+                    DeviceCSR(beg, ix, v, p.n_rows, self.n_cols, p.order, p.n_heavy, p.n_hub, p.n_heavy_narrow,
+                              row_end=end, row_space=p.row_space, thresholds=p.thresholds) for p in parts)
+            out.append(nb)
+            del beg, end, ix, v
         self._blocks[B] = out
+        self._blocks[key] = True
         return out
 
     def rows(self, r0: int, r1: int, heavy_threshold=None, hub_threshold=None) -> "DeviceCSR":

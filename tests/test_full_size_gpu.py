@@ -62,7 +62,7 @@ def test_products_timed_layout_every_hop_bit_exact(oracle_mod):
     B = auto_col_blocks(A, d, hops=hops)
     assert B == 5
     blocks = column_blocks_for(A, B, hops=hops)
-    assert len(blocks) == 5 and not blocks[0].is_span and blocks[0].whole_rows is not None
+    assert len(blocks) == 5 and A._blocks.get(("compact", 5)) and blocks[0].whole_rows is not None
     assert sum(b.nnz for b in blocks) == A.nnz and A.n_hub >= 1
     assert spmm_mod.launches_per_hop(A, B, d) == 6
     x = synth.uniform_features_t(n, d, seed=synth.FEATURE_SEED, device="cuda")

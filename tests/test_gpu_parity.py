@@ -189,7 +189,9 @@ def test_propagate_column_blocked_bit_exact(monkeypatch, name, B, compact, whole
     A = _csr(c, (None, None))
     blocks = A.compact_column_blocks(B) if compact else A.column_blocks(B)
     assert blocks is not None and len(blocks) == B and sum(b.nnz for b in blocks) == A.nnz
-    assert all(b.is_span != compact for b in blocks)
+    assert all(b.is_span for b in blocks)
+    # compact blocks hold copies of their entries (laid out in launch order), spans share A's arrays
+    assert all((b.indices.data_ptr() != A.indices.data_ptr()) == compact for b in blocks)
     X = torch.from_numpy(c.x()).cuda()
     hops = propagate(A, X, c.k, col_blocks=B)
     torch.cuda.synchronize()

@@ -25,17 +25,23 @@ ap.add_argument("--config", default="products")
 ap.add_argument("--reps", type=int, default=20)
 ap.add_argument("--u2", type=int, default=0, help="pass SRG_SPMM_PACKED_U2 to the whole-row launch")
 ap.add_argument("--natural", action="store_true", help="whole rows in row order (no length sort)")
+ap.add_argument("--check", action="store_true", help="the launches together == hop(), bitwise")
+ap.add_argument("--sched", action="store_true", help="entries copied out in schedule order (DeviceCSR.schedule_ordered)")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 ip, ix, vals, n, d, _ = graphs.build(a.config, dev)
 A = DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, device=dev)
 X = synth.uniform_features_t(n, d, device=dev)
 Y = torch.empty_like(X)
-blocks = A.compact_column_blocks(4)
+blocks = A.compact_column_blocks(4)   # the probe's fixed layout: four blocks
 cut, whole = blocks[0].split_whole()
 if a.natural:
     whole.order = torch.sort(whole.order).values.contiguous()
     whole.n_heavy = 0
+if a.sched:
+    whole = whole.schedule_ordered()
+    cut = cut.schedule_ordered()
+    blocks = [blocks[0]] + [b.schedule_ordered() for b in blocks[1:]]
 
 
 def timed(fn):
@@ -50,11 +56,21 @@ def timed(fn):
     return ev[0].elapsed_time(ev[1]) / a.reps
 
 
-deg = whole.indptr[1:] - whole.indptr[:-1]
-w_rows = whole.order.to(torch.int64)
 res = {"config": a.config, "env": {k: v for k, v in os.environ.items() if k.startswith("SRGNN_")},
-       "u2": a.u2, "natural": a.natural,
-       "whole_rows": whole.n_rows, "whole_nnz": int(deg[w_rows].sum()),
+       "u2": a.u2, "natural": a.natural, "sched": a.sched,
+       "whole_rows": whole.n_rows, "whole_nnz": int(((whole.row_end if whole.is_span else whole.indptr[1:])
+                                                      - whole.indptr[: whole.out_rows])[whole.order.long()].sum()),
        "ms_whole": timed(lambda: spmm(whole, X, out=Y, packed_u2=bool(a.u2))),
-       "ms_block1": timed(lambda: spmm(blocks[1], X, out=Y, accumulate=True, packed_u2=True))}
+       "ms_block1": timed(lambda: spmm(blocks[1], X, out=Y, accumulate=True, packed_u2=True)),
+       "ms_cut0": timed(lambda: spmm(cut, X, out=Y, packed_u2=True))}
+if a.check:
+    from srgnn.spmm import hop
+    ref = hop(A, X, torch.empty_like(X), col_blocks=4)
+    Y2 = torch.empty_like(X)
+    spmm(cut, X, out=Y2, packed_u2=True)
+    spmm(whole, X, out=Y2, packed_u2=True)
+    for b in blocks[1:]:
+        spmm(b, X, out=Y2, accumulate=True, packed_u2=True)
+    torch.cuda.synchronize()
+    res["bitwise_equal_to_hop"] = bool(torch.equal(ref, Y2))
 print(json.dumps(res))
