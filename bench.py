@@ -627,7 +627,7 @@ def main():
         init_pg()
 
     from srgnn.csr import DeviceCSR
-    from srgnn.spmm import auto_col_blocks, column_blocks_for, hop, launches_per_hop, propagate, spmm
+    from srgnn.spmm import column_blocks_for, hop, launches_per_hop, prepare, propagate, spmm
 
     t_build = time.perf_counter()
     ip, ix, vals, n, d, K = graphs.build(a.config, dev, d=a.d)
@@ -647,9 +647,12 @@ def main():
             mode = "panels" if K * n * d * 4 < 0.9 * free else "last"
             log(f"mode {mode}: {K} panels need {K * n * d * 4 / 1e9:.1f} GB, {free / 1e9:.1f} GB free")
         # the operator serves every warm-up and timed step: cut it once here when that amortises
-        col_blocks = a.col_blocks if a.col_blocks is not None else auto_col_blocks(A, d, hops=K * (a.steps + a.warmup))
-        if col_blocks > 1 and not column_blocks_for(A, col_blocks, hops=K * (a.steps + a.warmup)):
-            col_blocks = 1
+        if a.col_blocks is None:
+            col_blocks = prepare(A, d, hops=K * (a.steps + a.warmup))
+        else:
+            col_blocks = a.col_blocks
+            if col_blocks > 1 and not column_blocks_for(A, col_blocks, hops=K * (a.steps + a.warmup)):
+                col_blocks = 1
         launches = launches_per_hop(A, col_blocks, d, agg=bool(a.aggregate))
         log(f"schedule: n_hub={A.n_hub} n_heavy={A.n_heavy} column blocks per hop={col_blocks} ({launches} launches)")
         if a.aggregate:

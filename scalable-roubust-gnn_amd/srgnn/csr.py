@@ -271,6 +271,18 @@ class DeviceCSR:
         del idx
         return beg, end, ix, v
 
+    def schedule_ordered(self) -> "DeviceCSR":
+        """This operator with its entries copied out in the order its launch takes the rows (its
+        schedule): a span operator over the copy, the same entries in the same order per row, so the
+        same bits.  For a long-lived one-launch operator (spmm.propagate), as compact_column_blocks
+        is for blocked ones.  Cached."""
+        if "sched" not in self._blocks:
+            beg, end, ix, v = self._copy_in_order(self.order.to(torch.int64))
+            self._blocks["sched"] = DeviceCSR(beg, ix, v, self.n_rows, self.n_cols, self.order, self.n_heavy, self.n_hub,
+                                              self.n_heavy_narrow, row_end=end, row_space=self.out_rows,
+                                              thresholds=self.thresholds)
+        return self._blocks["sched"]
+
     def compact_column_blocks(self, B: int):
         """column_blocks(B) with each block's entries copied into arrays of its own, laid out in the
         order its launches take the rows: block b's schedule, and for block 0 the schedule of its

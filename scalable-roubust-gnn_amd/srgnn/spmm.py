@@ -60,6 +60,20 @@ MIN_HOPS_TO_COMPACT = 48
 _COMPACT = os.environ.get("SRGNN_COMPACT_BLOCKS", "1") != "0"     # 0: spans only (A/B)
 
 
+def prepare(A: DeviceCSR, d: int, hops: int) -> int:
+    """Lays A out for a run of `hops` hops over d-column panels: column blocks (spans, or compact
+    copies in launch order for long runs) or, for one launch per hop and a long run, a launch-ordered
+    copy of the whole operator (DeviceCSR.schedule_ordered).  Returns the column blocks per hop."""
+    B = auto_col_blocks(A, d, hops=hops)
+    if B > 1 and column_blocks_for(A, B, hops=hops):
+        return B
+    if _COMPACT and hops >= MIN_HOPS_TO_COMPACT and not A.is_span and A.n_rows == A.n_cols:
+        free, _ = torch.cuda.mem_get_info(A.device)
+        if A.nnz * (A.indices.element_size() + A.values.element_size()) + 24 * A.nnz <= free // 4:
+            A.schedule_ordered()
+    return 1
+
+
 def column_blocks_for(A: DeviceCSR, B: int, hops: int | None = None):
     """A's column blocks for a run of `hops` hops: spans, or compact copies for long runs."""
     if _COMPACT and hops is not None and hops >= MIN_HOPS_TO_COMPACT and not A.is_span:
@@ -109,7 +123,8 @@ def _hop_plan(A: DeviceCSR, d: int, B: int, nt_store: bool = False, fast: bool =
     """The launches of one hop of A over a d-column panel in B column blocks: ([(operator, flags,
     kind)], join) with kind "plain" or "agg" (the launch that carries the aggregation epilogue), and
     join = whether the hub side stream must be joined at the end of the hop."""
-    blocks = (A.column_blocks(B) if B > 1 else None) or [A]
+    # one launch: a long-lived operator's launch-ordered copy when prepare() made one
+    blocks = (A.column_blocks(B) if B > 1 else None) or [A._blocks.get("sched", A) if _COMPACT else A]
     # a block's rows are short: 2 gathers per packed row in flight (d >= 128: 4 or 2 rows per wave;
     # at d = 64, 8 rows per wave, it is 3 % slower)
     u2 = len(blocks) > 1 and d >= 128 and _U2_BLOCKED
@@ -413,6 +428,14 @@ def propagate(A: DeviceCSR, X: torch.Tensor, K: int, panels: list | None = None,
         arr = (ctypes.c_void_p * (K + 1))(*[p.data_ptr() for p in panels])
         _lib.call(X.device, "srg_propagate_plan_f32", _plan_array(plan, d), len(plan), 1 if join else 0, arr,
                   ld, d, K, _stream(X.device))
+    elif K > 0 and _COMPACT and "sched" in A._blocks:
+        # a long-lived operator's launch-ordered copy (DeviceCSR.schedule_ordered): the one launch
+        # per hop as a span operator, through the native plan loop
+        S = A._blocks["sched"]
+        flags = (_lib.SRG_SPMM_NT_STORE if nt_store else 0) | (_lib.SRG_SPMM_FAST if fast else 0)
+        arr = (ctypes.c_void_p * (K + 1))(*[p.data_ptr() for p in panels])
+        _lib.call(X.device, "srg_propagate_plan_f32", _plan_array([(S, flags, "plain")], d), 1, 0, arr, ld, d, K,
+                  _stream(X.device))
     else:
         arr = (ctypes.c_void_p * (K + 1))(*[p.data_ptr() for p in panels])
         flags = (_lib.SRG_SPMM_NT_STORE if nt_store else 0) | (_lib.SRG_SPMM_FAST if fast else 0)

@@ -847,3 +847,22 @@ def test_propagate_plan_entry_rejects_bad_launches():
         _lib.call(X.device, "srg_propagate_plan_f32", arr, len(plan), int(join), nulls, d, d, 1, _lib.stream(X.device))
     with pytest.raises(RuntimeError):
         _lib.call(X.device, "srg_propagate_plan_f32", arr, len(plan), int(join), panels, d, d, -1, _lib.stream(X.device))
+
+
+@pytest.mark.parametrize("name", ["rand_d128_r05", "rand_d36_ppr", "cora_sym_k3"])
+def test_schedule_ordered_one_launch_bit_exact(name):
+    """A long-lived one-launch operator's launch-ordered copy (DeviceCSR.schedule_ordered, made by
+    spmm.prepare for runs of >= MIN_HOPS_TO_COMPACT hops): propagate and hop through it == the
+    reference, bit for bit."""
+    from srgnn import spmm as spmm_mod
+    c = G.Case(name)
+    A = _csr(c, (None, None))
+    X = torch.from_numpy(c.x()).cuda()
+    assert spmm_mod.prepare(A, X.shape[1], hops=1000) == 1
+    S = A._blocks["sched"]
+    assert S.is_span and S.nnz == A.nnz and S.indices.data_ptr() != A.indices.data_ptr()
+    hops = spmm_mod.propagate(A, X, c.k)
+    torch.cuda.synchronize()
+    for k in range(1, c.k + 1):
+        c.check_hop(k, hops[k].cpu().numpy())
+    c.check_hop(1, spmm_mod.hop(A, X, torch.empty_like(X), col_blocks=1).cpu().numpy())

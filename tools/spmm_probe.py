@@ -20,7 +20,7 @@ import torch  # noqa: E402
 
 from srgnn import graphs, roofline, synth  # noqa: E402
 from srgnn.csr import DeviceCSR  # noqa: E402
-from srgnn.spmm import auto_col_blocks, column_blocks_for, hop, launches_per_hop  # noqa: E402
+from srgnn.spmm import column_blocks_for, hop, launches_per_hop, prepare  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="products")
@@ -78,8 +78,12 @@ A = DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, heavy_threshold=a.heavy_thres
 X = synth.uniform_features_t(n, d, device=dev)
 Y = torch.empty_like(X)
 # the probe stands for a long run of hops (bench.py's operator serves every step): the panel rule alone
-B = 1 if a.identity else (a.col_blocks if a.col_blocks is not None else auto_col_blocks(A, d, hops=a.hops))
-B = B if B > 1 and column_blocks_for(A, B, hops=a.hops) else 1   # spans or compact blocks, as bench.py
+if a.identity:
+    B = 1
+elif a.col_blocks is None:
+    B = prepare(A, d, hops=a.hops)          # as bench.py: blocks, or a launch-ordered copy for long runs
+else:
+    B = a.col_blocks if a.col_blocks > 1 and column_blocks_for(A, a.col_blocks, hops=a.hops) else 1
 torch.cuda.synchronize()
 for _ in range(a.reps):
     hop(A, X, Y, col_blocks=B)      # one hop = B k_spmm launches (column blocks), same bits
