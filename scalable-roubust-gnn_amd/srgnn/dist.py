@@ -260,6 +260,14 @@ AUTO_HALO_COL_BLOCKS = int(os.environ.get("SRGNN_HALO_COL_BLOCKS", "1"))
 AUTO_HALO_HUB_BLOCKS = int(os.environ.get("SRGNN_HALO_HUB_BLOCKS", "1"))
 
 
+# GPU ranks may launch their groups from copies of the entries laid out in schedule order
+# (_launch_op, SRGNN_HALO_LAUNCH_ORDER=1).  Off: unlike one GPU's column blocks (+2 %), the halo
+# groups gain nothing -- products per-rank hop 3.74 / 2.01 / 1.07 ms at P = 2 / 4 / 8 against
+# 3.74 / 1.91 / 1.03 (profiles/r03_halo_launch_order_negative.txt): a row chunk is a contiguous range
+# of rows, so its entries are already read in nearly the order its launch takes them
+LAUNCH_ORDER = os.environ.get("SRGNN_HALO_LAUNCH_ORDER", "0") != "0"
+
+
 class HaloPartitionedOperator:
     """Rank p's share of Â for the halo-exchange multi-GPU propagation.
 
@@ -301,6 +309,7 @@ class HaloPartitionedOperator:
         # column blocks of the hub group's launch (None: the automatic rule of _hub_blocks_for)
         self.hub_col_blocks = hub_col_blocks
         self._cb = {}
+        self._lo_ok = None             # launch-ordered copies fit (_launch_op), decided on first use
         self.virtual = rank is not None
         self.rank = rank if rank is not None else (dist.get_rank(group) if dist.is_initialized() else 0)
         self.world = world if world is not None else (dist.get_world_size(group) if dist.is_initialized() else 1)
@@ -518,6 +527,7 @@ class HaloPartitionedOperator:
         lvv = self._local_values(values)
         other._lvv = lvv
         other._cb = {}                 # column blocks hold the values: rebuilt for `other` on use
+        other._lo_ok = None
         if isinstance(self._A[0], tuple):
             other._A = [(a[0], a[1], lvv, a[3]) for a in self._A]
         else:
@@ -628,13 +638,30 @@ class HaloPartitionedOperator:
         self._cb[key] = blocks
         return blocks
 
+    def _launch_op(self, g: int):
+        """Group g's operator as its launch takes it: on GPU ranks a copy of its entries laid out in
+        its schedule's order (DeviceCSR.schedule_ordered, cached on the operator; the same chains),
+        which reads the id / value streams in order; else the operator itself.  Memory permitting
+        (a quarter of the free memory for the copies); opt-in, SRGNN_HALO_LAUNCH_ORDER=1."""
+        A = self._A[g]
+        if not (self._hip and LAUNCH_ORDER):
+            return A
+        if "sched" not in A._blocks:
+            if self._lo_ok is None:
+                free, _ = torch.cuda.mem_get_info(self.device)
+                need = self._lix.numel() * 8 + 16 * (self.rows + self.halo) * len(self._A)
+                self._lo_ok = need <= free // 4
+            if not self._lo_ok:
+                return A
+        return A.schedule_ordered()
+
     def _hub_launch(self, src: torch.Tensor, out: torch.Tensor):
         """The hub group forked onto the library's hub side stream (joined by the caller): one
         launch, or its column blocks chained on the side stream."""
         from .spmm import spmm
         blocks = self.hub_blocks(src.shape[1])
         if blocks is None:
-            spmm(self._A[self.C], src, out=out, hub_nojoin=True, fast=self.fast)
+            spmm(self._launch_op(self.C), src, out=out, hub_nojoin=True, fast=self.fast)
             return
         for b, Ab in enumerate(blocks):
             spmm(Ab, src, out=out, accumulate=b > 0, hub_nojoin=True, hub_continue=b > 0)
@@ -647,7 +674,7 @@ class HaloPartitionedOperator:
             for b, Ab in enumerate(blocks[c]):
                 spmm(Ab, src, out=out, accumulate=b > 0, packed_u2=u2)
         else:
-            self._spmm(self._A[c], src, out)
+            self._spmm(self._launch_op(c), src, out)
 
     def _local_values(self, values: torch.Tensor) -> torch.Tensor:
         """The local operator's values: the own rows' slice, then the ghost rows' entries."""
@@ -752,7 +779,7 @@ class HaloPartitionedOperator:
             elif fork:
                 self._hub_launch(src, out)
             else:
-                self._spmm(self._A[C], src, out)
+                self._spmm(self._launch_op(C), src, out)
         blocks = self.chunk_blocks(src.shape[1]) if packed is None else None
         for c in range(C):
             if self.views[c][1]:
@@ -763,7 +790,7 @@ class HaloPartitionedOperator:
             if after_group is not None:
                 after_group(c)
         if ghosts and self.n_ghost:
-            self._spmm(gA, src, dst)
+            self._spmm(self._launch_op(self.n_groups) if packed is None else gA, src, dst)
         if fork:
             _lib.call(self.device, "srg_hub_join", _lib.stream(self.device))
         if after_group is not None:
