@@ -441,6 +441,27 @@ def test_halo_virtual_ranks_bitwise(world, chunks, ghost, cb, hcb):
         assert torch.equal(got[k], want[k]), f"hop {k} differs with {world} virtual halo ranks"
 
 
+@pytest.mark.parametrize("world,chunks,ghost", [(2, 3, None), (8, 4, 8), (4, 2, 64)])
+def test_halo_virtual_ranks_launch_order_bitwise(monkeypatch, world, chunks, ghost):
+    """The halo groups launched from launch-ordered copies of their entries (opt-in,
+    SRGNN_HALO_LAUNCH_ORDER=1): bitwise equal to the single-device propagation."""
+    from srgnn import dist as dist_mod, synth
+    from srgnn.csr import DeviceCSR
+    from srgnn.normalize import sym_norm_binary
+    from srgnn.spmm import propagate
+    monkeypatch.setattr(dist_mod, "LAUNCH_ORDER", True)
+    n = 20000
+    u, v = synth.rmat_undirected_t(n, 150000, seed=22, device="cuda")
+    ip, ix = synth.symmetric_csr_t(n, u, v)
+    ip, ix, vals = sym_norm_binary(ip, ix, n, 0.5)
+    x = synth.uniform_features_t(n, 128, device="cuda")
+    want = propagate(DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, device="cuda"), x, 3)
+    got = dist_mod.simulate_halo_propagate(ip, ix, vals, n, x, 3, world, chunks=chunks, hub_threshold=300,
+                                           device="cuda", ghost_max_degree=ghost)
+    for k in range(1, 4):
+        assert torch.equal(got[k], want[k]), f"hop {k} differs with {world} virtual halo ranks"
+
+
 @pytest.mark.parametrize("world,chunks,d", [(3, 2, 128), (8, 4, 128), (4, 3, 36), (2, 2, 7), (4, 2, 256)])
 def test_halo_fused_pack_equals_gathered_rows(world, chunks, d):
     """srg_spmm_send_f32 (the halo pack fused into the SpMM epilogue, every path: row waves incl.
