@@ -21,7 +21,7 @@ _stream = _lib.stream
 # of <= csr.BLOCK_WHOLE_MAX nonzeros are not cut (block 0 computes them whole).  Measured
 # (profiles/r02t-v_*): products d = 128 7.05 (one launch 7.31) -> 6.67 (B = 2) -> 6.30 ms (B = 4),
 # flat over B = 4..6, 6.47 at 8; d = 256 +9 % and papers100M / RMAT-26 +3 / +2 % for B = 4 over 2 / 1;
-# arxiv (X 87 MB, already cache-resident) 0.224 vs 0.163 ms at B = 2.  "auto": auto_col_blocks (4 to 6
+# arxiv (X 87 MB, already cache-resident) 0.224 vs 0.163 ms at B = 2.  "auto": auto_col_blocks (4 to 8
 # blocks for panels of >= 512 MiB at d >= 64); SRGNN_COL_BLOCKS=<B> forces B.
 _COL_BLOCKS_ENV = os.environ.get("SRGNN_COL_BLOCKS", "auto")
 # column blocks' launches keep 2 gathers per packed light row in flight (SRG_SPMM_PACKED_U2) for
@@ -90,11 +90,12 @@ def column_blocks_for(A: DeviceCSR, B: int, hops: int | None = None):
 def auto_col_blocks(A: DeviceCSR, d: int, hops: int | None = None) -> int:
     """Column blocks per hop for a panel of d columns (1 = the one-launch hop), if A's blocks exist
     or `hops` hops will amortise cutting it: for panels of >= 512 MiB at d >= 64, one block per
-    ~256 MiB of panel (the Infinity Cache's size), 4 to 6; 4 for panels of >= 16 GiB.  Round 3,
-    with block 0 in two launches (profiles/r03_ab_col_blocks_round3.txt): products d = 128 (1.25 GB)
-    6.19 ms at B = 5 against 6.23 at 4 and 6; d = 256 (2.5 GB) 12.55 at 6, 12.59 at 8, 12.67 at 5,
-    12.70 at 10, 12.91 at 4; d = 64 (0.63 GB) flat over 4-5; RMAT-26 (68 GB) 312.8 at 4 against
-    315.6 at 5, papers100M (57 GB) 242.9 against 242.0."""
+    ~200 MiB of panel (a slice well inside the 256 MiB Infinity Cache), 4 to 8; 4 for panels of
+    >= 16 GiB.  Round 3, block 0 in two launches, compact blocks in launch order
+    (profiles/r03_ab_col_blocks_round3.txt): products d = 128 (1.25 GB) 5.98 ms at B = 6 against
+    6.00-6.01 at 5 and 7, 6.03 at 8, 6.10 at 4; d = 256 (2.5 GB) 12.35 ms at 7-8 against 12.40 at 6
+    (before the launch order: 12.55 at 6, 12.67 at 5, 12.70 at 10, 12.91 at 4); d = 64 (0.63 GB) flat
+    over 4-5; RMAT-26 (68 GB) 312.8 at 4 against 315.6 at 5, papers100M (57 GB) 242.9 against 242.0."""
     if _COL_BLOCKS_ENV != "auto":
         return max(1, int(_COL_BLOCKS_ENV))
     panel = A.n_cols * d * 4
@@ -103,7 +104,7 @@ def auto_col_blocks(A: DeviceCSR, d: int, hops: int | None = None) -> int:
     elif panel >= SPLIT_BLOCK0_MAX_PANEL:
         B = 4
     else:
-        B = min(6, max(4, int(round(panel / (256 << 20)))))
+        B = min(8, max(4, int(round(panel / (200 << 20)))))
     if B > 1 and B not in A._blocks and (hops is None or hops < MIN_HOPS_TO_CUT):
         return 1
     return B

@@ -46,7 +46,7 @@ def _check_rows(oracle_mod, rows, sub, ucols, prev, got, what):
 
 def test_products_timed_layout_every_hop_bit_exact(oracle_mod):
     """The operator bench.py times on the headline config: products-shaped graph (126 M nonzeros),
-    K = 10, d = 128, default thresholds, five COMPACT column blocks (>= 48 hops; block 0 in two
+    K = 10, d = 128, default thresholds, six COMPACT column blocks (>= 48 hops; block 0 in two
     launches, its cut spans then its whole rows), short rows
     (<= BLOCK_WHOLE_MAX = 32) whole in block 0, 2 gathers per packed row (PACKED_U2) -- every hop
     checked on 3000 random rows plus the 50 longest against the oracle fed with the GPU's previous
@@ -60,13 +60,13 @@ def test_products_timed_layout_every_hop_bit_exact(oracle_mod):
     A = DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, device="cuda")
     hops = K * 25                                   # the driver's 20 steps + 5 warm-up
     B = auto_col_blocks(A, d, hops=hops)
-    assert B == 5
+    assert B == 6
     blocks = column_blocks_for(A, B, hops=hops)
-    assert len(blocks) == 5 and A._blocks.get(("compact", 5)) and blocks[0].whole_rows is not None
+    assert len(blocks) == 6 and A._blocks.get(("compact", 6)) and blocks[0].whole_rows is not None
     assert sum(b.nnz for b in blocks) == A.nnz and A.n_hub >= 1
-    assert spmm_mod.launches_per_hop(A, B, d) == 6
+    assert spmm_mod.launches_per_hop(A, B, d) == 7
     x = synth.uniform_features_t(n, d, seed=synth.FEATURE_SEED, device="cuda")
-    panels = propagate(A, x, K)                     # col_blocks from auto_col_blocks: the cached 5
+    panels = propagate(A, x, K)                     # col_blocks from auto_col_blocks: the cached 6
     torch.cuda.synchronize()
     rows, sub, ucols = _sample(ip, ix, vals, n, 3000, 50, seed=31)
     for k in range(1, K + 1):
