@@ -149,6 +149,11 @@ typedef struct srg_hop_launch {
     int64_t n_hub;
     int64_t n_heavy;
     uint32_t flags;
+    /* optional (row_end != NULL only): the spans by schedule slot, slot_beg[i] / slot_end[i] = the span
+     * of row row_order[i] (n_rows entries each, or both NULL): the packed light rows read these,
+     * so consecutive slots read consecutive addresses */
+    const int64_t* slot_beg;
+    const int64_t* slot_end;
 } srg_hop_launch;
 
 /* K column-blocked hops: for k = 1..K, the n_launch launches of `launches` (a HOST array) run in

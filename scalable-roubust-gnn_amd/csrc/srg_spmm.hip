@@ -315,6 +315,11 @@ struct Epi {
     // [indptr[r], indptr[r + 1]) -- a column block of a CSR whose rows hold sorted column ids is a
     // span of each row, so the block needs no copy of the ids and values (srg_spmm_span_f32)
     const int64_t* row_end;
+    // kEpiSpan, optional: the spans by schedule slot (slot_beg[s] / slot_end[s] = the span of the row
+    // in slot s of this launch's light-row schedule), read by the packed light rows instead of the
+    // row-indexed arrays: consecutive slots, consecutive addresses (srg_propagate_plan_f32)
+    const int64_t* slot_beg;
+    const int64_t* slot_end;
 };
 
 // Epilogue kinds (template parameter EX of the SpMM kernels).  Every call site sits under
@@ -565,8 +570,22 @@ __device__ __forceinline__ void packed_rows(const IP* __restrict__ indptr, const
     const int slot = first + g;
     const bool rv = slot < n_rows;
     const int row = rv ? (order ? order[slot] : slot) : 0;
-    const int64_t beg = rv ? (int64_t)indptr[row] : 0;
-    const int len = rv ? (int)(row_stop<EX>(indptr, epi, row) - beg) : 0;
+    int64_t beg = 0;
+    int len = 0;
+    if (rv) {
+        if constexpr (EX == kEpiSpan) {
+            if (epi.slot_beg) {
+                beg = epi.slot_beg[slot];
+                len = (int)(epi.slot_end[slot] - beg);
+            } else {
+                beg = indptr[row];
+                len = (int)(epi.row_end[row] - beg);
+            }
+        } else {
+            beg = indptr[row];
+            len = (int)(row_stop<EX>(indptr, epi, row) - beg);
+        }
+    }
     int maxlen = len;
 #pragma unroll
     for (int off = S; off < 64; off <<= 1) {
@@ -2197,6 +2216,8 @@ int srg_propagate_plan_f32(const srg_hop_launch* launches, int32_t n_launch, int
         if (rc) return rc;
         if (L.n_rows > 0 && L.n_hub + L.n_heavy > 0 && !L.row_order)
             return fail(SRG_ERR_INVALID, "launch %d: hub / heavy rows need a row_order", i);
+        if ((L.slot_beg != nullptr) != (L.slot_end != nullptr) || (L.slot_beg && !L.row_end))
+            return fail(SRG_ERR_INVALID, "launch %d: slot_beg / slot_end come together, with row_end", i);
     }
     const hipStream_t s = static_cast<hipStream_t>(stream);
     for (int k = 1; k <= K; ++k) {
@@ -2206,6 +2227,9 @@ int srg_propagate_plan_f32(const srg_hop_launch* launches, int32_t n_launch, int
             if (L.row_end) {
                 Epi e{};
                 e.row_end = L.row_end;
+                // the light rows' slots count from the first non-hub row of the schedule
+                e.slot_beg = L.slot_beg ? L.slot_beg + L.n_hub : nullptr;
+                e.slot_end = L.slot_beg ? L.slot_end + L.n_hub : nullptr;
                 rc = launch_spmm<int64_t, kEpiSpan>(L.row_beg, L.indices, L.values, L.n_rows, L.row_order, L.n_hub,
                                                     L.n_heavy, panels[k - 1], ld, panels[k], ld, d, L.flags, s, e);
             } else {

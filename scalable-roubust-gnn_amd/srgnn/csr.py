@@ -251,6 +251,14 @@ class DeviceCSR:
             self._blocks["split"] = tuple(parts)
         return self._blocks["split"]
 
+    def slot_spans(self):
+        """(beg, end) int64 [n_rows]: the span of the row in each schedule slot (span operators).
+        Cached."""
+        if "slots" not in self._blocks:
+            o = self.order.to(torch.int64)
+            self._blocks["slots"] = (self.indptr[o].contiguous(), self.row_end[o].contiguous())
+        return self._blocks["slots"]
+
     def _copy_in_order(self, rows: torch.Tensor):
         """(beg, end, indices, values): the entries of `rows` (int64 row ids) copied out one row after
         the other in that order, row r's at [beg[r], end[r]) of the copies (rows not listed: empty)."""

@@ -31,6 +31,9 @@ _U2_BLOCKED = os.environ.get("SRGNN_BLOCK_U2", "1") != "0"
 # column-blocked hops: block b's hub rows continue block b-1's side-stream fork (SRG_SPMM_HUB_CONTINUE)
 # instead of a fork, dispatch delay and join per block; SRGNN_HUB_CHAIN=0 for the A/B
 _HUB_CHAIN = os.environ.get("SRGNN_HUB_CHAIN", "1") != "0"
+# span launches of the native plan loop hand the packed light rows their spans by schedule slot
+# (DeviceCSR.slot_spans); SRGNN_SLOT_SPANS=0 for the A/B
+_SLOT_SPANS = os.environ.get("SRGNN_SLOT_SPANS", "1") != "0"
 # block 0 of a column-blocked hop as two launches over the same arrays (DeviceCSR.split_whole): the
 # cut rows' first spans, then the rows it computes whole.  Products (1.25 GB panel): 6.21 vs 6.24 ms
 # per hop, six alternations; the whole rows first, last or after the cut spans measure the same, and
@@ -203,15 +206,18 @@ class _HopLaunch(ctypes.Structure):
     """srg_hop_launch (include/srgnn_hip.h)."""
     _fields_ = [("row_beg", ctypes.c_void_p), ("row_end", ctypes.c_void_p), ("indices", ctypes.c_void_p),
                 ("values", ctypes.c_void_p), ("row_order", ctypes.c_void_p), ("n_rows", ctypes.c_int64),
-                ("n_hub", ctypes.c_int64), ("n_heavy", ctypes.c_int64), ("flags", ctypes.c_uint32)]
+                ("n_hub", ctypes.c_int64), ("n_heavy", ctypes.c_int64), ("flags", ctypes.c_uint32),
+                ("slot_beg", ctypes.c_void_p), ("slot_end", ctypes.c_void_p)]
 
 
 def _plan_array(plan, d):
     arr = (_HopLaunch * len(plan))()
     for i, (Ab, f, _) in enumerate(plan):
+        sb, se = Ab.slot_spans() if (Ab.is_span and Ab.n_rows and _SLOT_SPANS) else (None, None)
         arr[i] = _HopLaunch(Ab.indptr.data_ptr(), Ab.row_end.data_ptr() if Ab.is_span else None,
                             Ab.indices.data_ptr(), Ab.values.data_ptr(), Ab.order.data_ptr() if Ab.n_rows else None,
-                            Ab.n_rows, Ab.n_hub, Ab.heavy(d), f)
+                            Ab.n_rows, Ab.n_hub, Ab.heavy(d), f, sb.data_ptr() if sb is not None else None,
+                            se.data_ptr() if se is not None else None)
     return arr
 
 
