@@ -863,6 +863,13 @@ def test_propagate_plan_entry_rejects_bad_launches():
     bad[0].n_heavy, bad[0].row_order = max(1, bad[0].n_heavy), None
     with pytest.raises(RuntimeError):
         _lib.call(X.device, "srg_propagate_plan_f32", bad, len(plan), int(join), panels, d, d, 1, _lib.stream(X.device))
+    if any(Ab.is_span for Ab, _, _ in plan):
+        half = spmm_mod._plan_array(plan, d)
+        i = next(j for j, (Ab, _, _) in enumerate(plan) if Ab.is_span)
+        half[i].slot_end = None                   # slot spans come in pairs
+        with pytest.raises(RuntimeError):
+            _lib.call(X.device, "srg_propagate_plan_f32", half, len(plan), int(join), panels, d, d, 1,
+                      _lib.stream(X.device))
     nulls = (ctypes.c_void_p * 2)(X.data_ptr(), None)
     with pytest.raises(RuntimeError):
         _lib.call(X.device, "srg_propagate_plan_f32", arr, len(plan), int(join), nulls, d, d, 1, _lib.stream(X.device))
