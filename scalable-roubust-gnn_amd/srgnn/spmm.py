@@ -177,6 +177,12 @@ def hop(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, nt_store: bool = False
         raise ValueError("A, X and out must be on the same device")
     B = auto_col_blocks(A, d) if col_blocks is None else int(col_blocks)
     plan, join = _hop_plan(A, d, B, nt_store, fast, agg is not None)
+    if agg is None and X.stride(0) == out.stride(0) and X.data_ptr() != out.data_ptr():
+        # one hop through the native plan loop (the packed rows get their spans by slot there)
+        arr = (ctypes.c_void_p * 2)(X.data_ptr(), out.data_ptr())
+        _lib.call(X.device, "srg_propagate_plan_f32", _plan_array(plan, d), len(plan), 1 if join else 0, arr,
+                  X.stride(0), d, 1, _stream(X.device))
+        return out
     for Ab, f, kind in plan:
         if kind == "agg":
             _launch(Ab, X, out, d, f, agg[0], agg[1], agg[2])
