@@ -70,7 +70,10 @@ extern "C" {
  * the dispatch delay).  For the column blocks of one hop: X is unchanged during the hop and only
  * the side stream touches the hub rows, so block b's hub span needs no order against block b-1's
  * main launch -- only against block b-1's hub span, which the side stream gives.  One join at the
- * end of the hop.  Without a pending fork it is an ordinary fork.  Results are identical. */
+ * end of the hop.  Without a pending fork it is an ordinary fork.  Results are identical.
+ * The pending state belongs to the (device, stream handle) pair: join (srg_hub_join) a stream with
+ * an unjoined NOJOIN fork before destroying it, or a new stream that reuses the handle value would
+ * inherit the pending fork and its first CONTINUE launch would skip its own fork. */
 #define SRG_SPMM_HUB_CONTINUE 0x80u
 /* Tolerance mode (EXACT, FAST, ACCUMULATE).  The hub rows (the first n_hub of
  * row_order) are not one chain each: a hub row's entries are cut into 64 consecutive segments,
@@ -161,7 +164,9 @@ typedef struct srg_hop_launch {
  * first HUB_NOJOIN launch of the hop) is joined back into `stream` at the end of every hop.  The
  * device-resident form of srgnn.spmm.propagate's blocked hop loop: bitwise the one-launch hops
  * (the same fma chains, continued across the blocks).  panels: HOST array of K+1 device pointers
- * of leading dimension ld. */
+ * of leading dimension ld.  A plan with HUB_NOJOIN launches over K > 1 hops needs join_hub (else
+ * SRG_ERR_INVALID: hop k+1 would read hub rows still being written); with join_hub = 0 (K = 1) the
+ * caller must srg_hub_join(stream) after the call, before anything reads the hub rows. */
 int srg_propagate_plan_f32(const srg_hop_launch* launches, int32_t n_launch, int32_t join_hub,
                            float* const* panels, int64_t ld, int32_t d, int32_t K, void* stream);
 

@@ -72,7 +72,15 @@ struct DeviceOf {          // the device of `s` current for the call (the null s
     ~DeviceOf() { if (prev >= 0) (void)hipSetDevice(prev); }
 };
 
-constexpr int kLdsCols = 16384;          // dense accumulator in LDS up to this many columns (64 KiB)
+// dense accumulator in LDS up to this many columns: 64 KiB of sums + 2 KiB of bitmap = 66 KiB, which
+// fits only because gfx950 gives a workgroup up to 160 KiB of LDS (the 64 KiB of earlier CDNA parts
+// would not hold it).  Cost model of the output scan below: it walks every bitmap word between the
+// row's smallest and largest touched column, 64 words (2048 columns) per iteration, so a row costs
+// O((hi - lo) / 2048) iterations however few entries it has -- on the scratch path (n_cols > 16384) a
+// row touching columns 0 and n - 1 of an n = 2.4 M basis takes ~1.2 K iterations.  The wavelet bases
+// the reference builds are dense-ish rows over N of a few thousand to ~10^5 columns (it is O(N^2) in
+// memory), where the scan is a small part of the row; DESIGN.md §5.7.
+constexpr int kLdsCols = 16384;
 constexpr int kMaxGlobalSlots = 2048;    // workgroups of the scratch-accumulator path
 constexpr int kWave = 64;
 

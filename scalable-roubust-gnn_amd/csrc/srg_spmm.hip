@@ -774,12 +774,17 @@ constexpr int kHubDppL = 3;   // 16-link sets in flight (4 tile reads + 1 value 
 // holds in a[j] (quad_perm broadcast), acc = fma(value, x, acc) -- v_fmac_f32 with a DPP first
 // operand, one instruction per link.  One asm block: the compiler's hazard pass would otherwise pad
 // every link with an s_nop (it treats the chained accumulator like a DPP source; 0.95 vs 0.86 ms on
-// the products hub row).  The DPP'd operands a[] come straight from LDS reads, which no VALU writes.
+// the products hub row).  The DPP'd operands a[] normally come straight from LDS reads, but nothing
+// stops the register allocator from producing one with a VALU copy (v_mov / v_accvgpr_read) right
+// before the block, and gfx9 needs 2 wait states between a VALU write of a VGPR and a DPP read of
+// it: the hazard pass cannot see inside the asm, so the block opens with its own `s_nop 1`.  This
+// guard must stay (2 cycles per 16 links).
 __device__ __forceinline__ void hub_links16(float& acc, const typename Vec<float, 4>::type& a,
                                             const typename Vec<float, 4>::type (&t)[4])
 {
 #define SRG_QP(I) " quad_perm:[" #I "," #I "," #I "," #I "] row_mask:0xf bank_mask:0xf\n"
     asm volatile(
+        "s_nop 1\n"
         "v_fmac_f32_dpp %0, %1, %5" SRG_QP(0) "v_fmac_f32_dpp %0, %2, %6" SRG_QP(0)
         "v_fmac_f32_dpp %0, %3, %7" SRG_QP(0) "v_fmac_f32_dpp %0, %4, %8" SRG_QP(0)
         "v_fmac_f32_dpp %0, %1, %9" SRG_QP(1) "v_fmac_f32_dpp %0, %2, %10" SRG_QP(1)
@@ -2218,6 +2223,10 @@ int srg_propagate_plan_f32(const srg_hop_launch* launches, int32_t n_launch, int
             return fail(SRG_ERR_INVALID, "launch %d: hub / heavy rows need a row_order", i);
         if ((L.slot_beg != nullptr) != (L.slot_end != nullptr) || (L.slot_beg && !L.row_end))
             return fail(SRG_ERR_INVALID, "launch %d: slot_beg / slot_end come together, with row_end", i);
+        // without the per-hop join, hop k's hub rows would still run on the side stream while hop
+        // k+1's launches on `stream` read panels[k]: a data race
+        if (!join_hub && K > 1 && L.n_hub > 0 && (L.flags & SRG_SPMM_HUB_NOJOIN))
+            return fail(SRG_ERR_INVALID, "launch %d: HUB_NOJOIN hub rows over K=%d hops need join_hub", i, K);
     }
     const hipStream_t s = static_cast<hipStream_t>(stream);
     for (int k = 1; k <= K; ++k) {

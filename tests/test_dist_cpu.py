@@ -303,3 +303,63 @@ def test_halo_wavelet_bitwise_equals_single_rank(tmp_path, oracle_mod, world):
                                device="cpu", rank=0, world=1, local_spmm=local_spmm, epilogue=_cpu_epilogue)
     R = single.apply(S)
     np.testing.assert_array_equal(np.load(out), R.numpy())
+
+
+def _sampled_parity_worker(rank, world, port, out_path, corrupt):
+    import importlib.util
+    import json
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    repo = os.path.dirname(here)
+    sys.path[:0] = [os.path.join(repo, "scalable-roubust-gnn_amd"), repo]
+    dist.init_process_group("gloo", init_method="file://" + port, rank=rank, world_size=world)
+    from oracle import oracle as O
+    from srgnn.dist import HaloPartitionedOperator
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(repo, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+
+    def local_spmm(A, X, out):
+        ip, ix, vv, order = A
+        full = torch.from_numpy(O.spmm(ip.numpy(), ix.numpy(), vv.numpy(), X.numpy()))
+        o = order.long()
+        out[o] = full[o]
+
+    ip, ix, vals, x, n = _graph()
+    K = 3
+    op = HaloPartitionedOperator(ip, ix, vals, n, chunks=2, hub_threshold=60, local_spmm=local_spmm,
+                                 device="cpu", ghost_max_degree=4)
+    panels = op.propagate(x[op.r0:op.r1], K, x_full=x)
+    if corrupt == "own" and rank == world - 1:         # one bit of one own row of hop K
+        panels[K][0, 1] = torch.nextafter(panels[K][0, 1], torch.tensor(float("inf")))
+    if corrupt == "halo" and rank == 0:                # one bit of every halo row of panel K-1
+        panels[K - 1][op.rows:op.rows + op.halo, 0] = torch.nextafter(
+            panels[K - 1][op.rows:op.rows + op.halo, 0], torch.tensor(float("inf")))
+    res = bench.dist_sampled_parity(op, panels, K, n_random=op.rows, n_top=5, n_halo=op.halo)
+    dev = bench.rank_devices(torch.device("cpu"), "gloo", world)
+    if rank == 0:
+        with open(out_path, "w") as f:
+            json.dump({"parity": res, "devices": dev}, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("corrupt", ["none", "own", "halo"])
+def test_bench_sampled_dist_parity_on_gloo_ranks(tmp_path, oracle_mod, corrupt):
+    """bench.py's N-GPU check for the configurations whose whole-graph reference does not fit a
+    rank (papers100M, RMAT-26): sampled own rows of hop 1 and hop K against the oracle fed with the
+    rank's previous panel, and sampled halo rows against their owners -- green on a correct run,
+    and a flipped bit in an own row or in the halo is caught; the device record lists every rank."""
+    import json
+    out = str(tmp_path / "par.json")
+    world = 2
+    mp.spawn(_sampled_parity_worker, args=(world, _free_port(), out, corrupt), nprocs=world, join=True)
+    with open(out) as f:
+        rec = json.load(f)
+    par = rec["parity"]
+    assert par["hops_checked"] == [1, 3] and par["rows_checked_rank0"] > 0
+    # (a corrupted halo row also feeds the oracle a value the hop did not read: both checks see it)
+    assert par["bit_exact"] == (corrupt == "none")
+    assert par["halo_equal_to_owners"] == (corrupt != "halo")
+    assert rec["devices"]["world_size"] == 2 and rec["devices"]["backend"] == "gloo"
+    assert [r["rank"] for r in rec["devices"]["ranks"]] == [0, 1]

@@ -44,13 +44,14 @@ def _check_rows(oracle_mod, rows, sub, ucols, prev, got, what):
     assert bad.size == 0, f"{what}: {bad.size} of {rows.numel()} sampled rows differ (first row {int(rows[bad[0]])})"
 
 
+@pytest.mark.timeout(600)
 def test_products_timed_layout_every_hop_bit_exact(oracle_mod):
     """The operator bench.py times on the headline config: products-shaped graph (126 M nonzeros),
     K = 10, d = 128, default thresholds, six COMPACT column blocks (>= 48 hops; block 0 in two
-    launches, its cut spans then its whole rows), short rows
-    (<= BLOCK_WHOLE_MAX = 32) whole in block 0, 2 gathers per packed row (PACKED_U2) -- every hop
-    checked on 3000 random rows plus the 50 longest against the oracle fed with the GPU's previous
-    hop."""
+    launches, its cut spans then its whole rows; compact copies in launch order, packed rows reading
+    their spans by schedule slot), short rows (<= BLOCK_WHOLE_MAX = 32) whole in block 0, 2 gathers
+    per packed row (PACKED_U2) -- EVERY row of every hop (2,449,029 x 128 per hop) checked bit for
+    bit against the oracle fed with the GPU's previous hop (~1-3 s of host time per hop)."""
     from srgnn import csr as csr_mod, graphs, spmm as spmm_mod, synth
     from srgnn.csr import DeviceCSR
     from srgnn.spmm import auto_col_blocks, column_blocks_for, propagate
@@ -68,9 +69,16 @@ def test_products_timed_layout_every_hop_bit_exact(oracle_mod):
     x = synth.uniform_features_t(n, d, seed=synth.FEATURE_SEED, device="cuda")
     panels = propagate(A, x, K)                     # col_blocks from auto_col_blocks: the cached 6
     torch.cuda.synchronize()
-    rows, sub, ucols = _sample(ip, ix, vals, n, 3000, 50, seed=31)
+    ipn, ixn, vn = ip.cpu().numpy(), ix.cpu().numpy(), vals.cpu().numpy()
+    del ip, ix, vals
+    prev = panels[0].cpu().numpy()
+    want = np.empty_like(prev)
     for k in range(1, K + 1):
-        _check_rows(oracle_mod, rows, sub, ucols, panels[k - 1], panels[k], f"products hop {k}")
+        oracle_mod.spmm(ipn, ixn, vn, prev, out=want)
+        got = panels[k].cpu().numpy()
+        bad = np.flatnonzero((got.view(np.uint32) != want.view(np.uint32)).any(axis=1))
+        assert bad.size == 0, f"products hop {k}: {bad.size} of {n} rows differ (first row {int(bad[0])})"
+        prev = got
 
 
 def test_arxiv_k5_every_row_bit_exact(oracle_mod):
@@ -122,8 +130,8 @@ def test_rmat26_d256_k8_blocked_sampled_rows_bit_exact(oracle_mod):
 @pytest.mark.timeout(900)
 def test_papers100M_blocked_hop_sampled_rows_bit_exact(oracle_mod):
     """papers100M-shaped graph (111 M nodes, 3.34e9 nonzeros), d = 128, in the four-column-block
-    layout bench.py times it in: two hops, each checked on 1500 random rows plus the 10 longest
-    against the oracle fed with the GPU's previous hop."""
+    layout bench.py times it in: all K = 5 hops, each checked on 1500 random rows plus the 10
+    longest against the oracle fed with the GPU's previous hop."""
     from srgnn import graphs, synth
     from srgnn.csr import DeviceCSR
     from srgnn.spmm import auto_col_blocks, column_blocks_for, hop
@@ -137,7 +145,8 @@ def test_papers100M_blocked_hop_sampled_rows_bit_exact(oracle_mod):
     del ip, ix, vals
     cur = synth.uniform_features_t(n, d, seed=synth.FEATURE_SEED, device="cuda")
     nxt = torch.empty_like(cur)
-    for k in (1, 2):
+    assert K == 5
+    for k in range(1, K + 1):
         hop(A, cur, nxt, col_blocks=B)
         torch.cuda.synchronize()
         _check_rows(oracle_mod, rows, sub, ucols, cur, nxt, f"papers100M hop {k}")

@@ -875,6 +875,19 @@ def test_propagate_plan_entry_rejects_bad_launches():
         _lib.call(X.device, "srg_propagate_plan_f32", arr, len(plan), int(join), nulls, d, d, 1, _lib.stream(X.device))
     with pytest.raises(RuntimeError):
         _lib.call(X.device, "srg_propagate_plan_f32", arr, len(plan), int(join), panels, d, d, -1, _lib.stream(X.device))
+    # unjoined hub forks over several hops would race the next hop's reads: rejected
+    Ah = _csr(c, (16, 64))
+    hplan = [(Ah, _lib.SRG_SPMM_HUB_NOJOIN, "plain")]
+    assert Ah.n_hub > 0
+    nj = spmm_mod._plan_array(hplan, d)
+    Z = torch.empty_like(X)
+    three = (ctypes.c_void_p * 3)(X.data_ptr(), Y.data_ptr(), Z.data_ptr())
+    with pytest.raises(RuntimeError, match="join_hub"):
+        _lib.call(X.device, "srg_propagate_plan_f32", nj, 1, 0, three, d, d, 2, _lib.stream(X.device))
+    _lib.call(X.device, "srg_propagate_plan_f32", nj, 1, 1, three, d, d, 2, _lib.stream(X.device))
+    torch.cuda.synchronize()
+    c.check_hop(1, Y.cpu().numpy())
+    c.check_hop(2, Z.cpu().numpy())
 
 
 @pytest.mark.parametrize("name", ["rand_d128_r05", "rand_d36_ppr", "cora_sym_k3"])

@@ -167,9 +167,30 @@ def test_spspmm_unsorted_duplicates_and_coalesced():
     keys = sorted(kk for kk, v in want.items() if v != 0)
     np.testing.assert_array_equal(idx.numpy().T, np.array(keys).reshape(-1, 2))
     np.testing.assert_array_equal(val.numpy(), np.array([want[kk] for kk in keys], np.float32))
+    # coalesced=True coalesces both inputs first (torch_sparse's docstring): B's duplicate (row, col)
+    # entries are summed in their stored order, then every product uses the summed value; A's
+    # shuffled entries are sorted by (row, col)
     perm = rng.permutation(ia.shape[1])
     idx2, val2 = torch_sparse.spspmm(ia[:, perm], va[perm], ib, torch.from_numpy(vb), m, k, n, coalesced=True)
-    assert idx2.shape[1] > 0
+    bsum = {}
+    for q in range(rows.size):                  # rows are sorted, duplicates in stored order
+        key = (int(rows[q]), int(cols[q]))
+        bsum[key] = np.float32(bsum.get(key, np.float32(0)) + vb[q])
+    brow = {}
+    for (r, cc), v in sorted(bsum.items()):
+        brow.setdefault(r, []).append((cc, v))
+    want2 = {}
+    As = Ad.sorted_indices()                    # coalesced: A's entries by (row, col)
+    for i in range(m):
+        for e in range(As.indptr[i], As.indptr[i + 1]):
+            kk, a = As.indices[e], As.data[e]
+            for cc, v in brow.get(int(kk), []):
+                key = (i, cc)
+                want2[key] = np.float32(want2.get(key, np.float32(0)) + np.float32(a * v))
+    keys2 = sorted(kk for kk, v in want2.items() if v != 0)
+    assert len(bsum) < rows.size                # the fixture has duplicates to sum
+    np.testing.assert_array_equal(idx2.numpy().T, np.array(keys2).reshape(-1, 2))
+    np.testing.assert_array_equal(val2.numpy(), np.array([want2[kk] for kk in keys2], np.float32))
 
 
 @pytest.mark.parametrize("d", [1, 16, 64, 130])

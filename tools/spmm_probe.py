@@ -6,6 +6,10 @@
                with the SAME kernel and access widths as the real hop -> FETCH_SIZE / WRITE_SIZE
                scale factors for this access pattern (MI355X_MICROARCH.md: FETCH_SIZE under-counts
                wide reads on gfx950; calibrate on a known byte count).
+  --permutation  calibration on gathers: Â = a random permutation matrix with the config's N (one
+               nonzero per row, a random column, every column once), so every launch gathers each
+               X row exactly once as a random whole-row read -- the hop kernel's access pattern with
+               no reuse and known bytes (N*4d read, N*4d written, plus ids, values, pointers).
 Prints one JSON line with the launch geometry and algorithmic bytes.
 """
 import argparse
@@ -26,6 +30,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="products")
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--identity", action="store_true")
+ap.add_argument("--permutation", action="store_true")
 ap.add_argument("--heavy-threshold", type=int, default=None)
 ap.add_argument("--col-blocks", type=int, default=None, help="column blocks per hop (default: auto_col_blocks)")
 ap.add_argument("--d", type=int, default=None, help="panel width (default: the config's)")
@@ -72,13 +77,20 @@ if a.identity:
     ip = torch.arange(n + 1, dtype=torch.int64, device=dev)
     ix = torch.arange(n, dtype=torch.int32, device=dev)
     vals = torch.ones(n, dtype=torch.float32, device=dev)
+elif a.permutation:
+    n = synth.CONFIGS[a.config]["n"]
+    d = a.d or synth.CONFIGS[a.config]["d"]
+    ip = torch.arange(n + 1, dtype=torch.int64, device=dev)
+    g = torch.Generator(device="cpu").manual_seed(5)
+    ix = torch.randperm(n, generator=g).to(dev, torch.int32)
+    vals = torch.ones(n, dtype=torch.float32, device=dev)
 else:
     ip, ix, vals, n, d, _ = graphs.build(a.config, dev, d=a.d)
 A = DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, heavy_threshold=a.heavy_threshold, device=dev)
 X = synth.uniform_features_t(n, d, device=dev)
 Y = torch.empty_like(X)
 # the probe stands for a long run of hops (bench.py's operator serves every step): the panel rule alone
-if a.identity:
+if a.identity or a.permutation:
     B = 1
 elif a.col_blocks is None:
     B = prepare(A, d, hops=a.hops)          # as bench.py: blocks, or a launch-ordered copy for long runs
@@ -89,7 +101,7 @@ for _ in range(a.reps):
     hop(A, X, Y, col_blocks=B)      # one hop = B k_spmm launches (column blocks), same bits
 torch.cuda.synchronize()
 nnz = A.nnz
-print(json.dumps({"config": "identity" if a.identity else a.config, "n": n, "nnz": nnz, "d": d,
+print(json.dumps({"config": "identity" if a.identity else (f"permutation-{a.config}" if a.permutation else a.config), "n": n, "nnz": nnz, "d": d,
                   "reps": a.reps, "launches_per_hop": launches_per_hop(A, B, d), "column_blocks": B,
                   "n_heavy": A.n_heavy, "n_hub": A.n_hub,
                   "algorithmic_bytes": roofline.bytes_no_reuse(n, nnz, d),
