@@ -400,6 +400,85 @@ typedef struct {
 int srg_dist_propagate_khop_f32(srg_comm* comm, const srg_shard_f32* shards, int n_shards,
                                 const int64_t* row_starts, int64_t ld, int32_t d, int32_t K);
 
+/* ---- multi-GPU: the halo-exchange partition (the default multi-GPU path) -----------------------
+ * The row-partitioned K-hop of srg_dist_propagate_khop_f32 moves every rank's whole block each hop
+ * (an all-gather, 2.6x the bytes on the products graph at 8 ranks) and computes after the exchange.
+ * The halo path moves only the remote rows each rank's rows reference, and overlaps that exchange
+ * with the hop: a rank's rows are cut into C nnz-balanced row chunks plus one group of hub rows;
+ * per hop the hub group is forked beside the chunks, and after each chunk's launch its rows that
+ * peers need are packed and sent (grouped ncclSend / ncclRecv on a comm stream that waits only for
+ * that pack), while the next chunks compute; the hub group's rows go last.  Low-degree halo rows
+ * whose own columns are all local ("ghost rows") are computed locally instead of received.  Every
+ * row keeps its entries in CSR order, so the hops are bitwise the one-GPU hops.  The same plan as
+ * the Python package's srgnn/dist.py HaloPartitionedOperator (its automatic ghost cap, a link-rate
+ * cost model, stays in Python: C hosts pass the cap).  Replaces the reference's single-process hop
+ * loop, SSRG/operators/base_operator.py:32-35; SURVEY.md §8(b) item 5, §8(e). */
+#define SRG_HALO_AUTO (-1)     /* threshold chosen as the Python plan does (csr.auto_*_threshold) */
+#define SRG_HALO_NONE (-2)     /* hub_threshold: no hub rows */
+typedef struct srg_halo_plan srg_halo_plan;
+typedef struct srg_halo_share srg_halo_share;
+typedef struct {
+    int64_t row0, n_rows;          /* own rows [row0, row0 + n_rows) of the global operator */
+    int64_t n_recv, n_ghost, halo; /* panel rows after the own ones: received, then ghosts */
+    int64_t nnz_local;             /* entries of the local CSR (own rows + ghost rows) */
+    int64_t n_groups, hub_rows, send_rows;
+    int32_t ghost_max_degree, chunks, nranks, rank;
+} srg_halo_info;
+/* Rank `rank`'s share, from the GLOBAL CSR on the host (int64 indptr[n+1] from 0, int32 column ids;
+ * the same arrays on every rank).  chunks in [1, 250]; hub_threshold / heavy_threshold a row length,
+ * SRG_HALO_AUTO, or (hub) SRG_HALO_NONE; ghost_max_degree >= 0 (0: no ghost rows).  Host-only: needs
+ * no device.  Validates the CSR (SRG_ERR_INVALID). */
+int srg_halo_plan_build(const int64_t* indptr, const int32_t* indices, int64_t n, int32_t nranks, int32_t rank,
+                        int32_t chunks, int64_t hub_threshold, int64_t heavy_threshold, int32_t ghost_max_degree,
+                        srg_halo_plan** plan);
+int srg_halo_plan_destroy(srg_halo_plan* plan);
+int srg_halo_plan_info(const srg_halo_plan* plan, srg_halo_info* info);
+/* Read-only view of one of the plan's host arrays (diagnostics and tests): *data points into the plan
+ * (valid until it is destroyed), *count elements of the type given beside each selector. */
+#define SRG_HALO_STARTS 0             /* int64 [nranks + 1] row blocks */
+#define SRG_HALO_LOCAL_INDPTR 1       /* int64 [n_rows + halo + 1] */
+#define SRG_HALO_LOCAL_INDICES 2      /* int32 [nnz_local] panel row ids */
+#define SRG_HALO_GHOST_POSITIONS 3    /* int64: global entry positions of the ghost rows' entries */
+#define SRG_HALO_HALO_IDS 4           /* int64 [halo] global ids of the halo rows, panel order */
+#define SRG_HALO_GROUP_OFFSETS 5      /* int64 [n_groups] */
+#define SRG_HALO_GHOST_SEND 6         /* int64 own local rows sent as peers' ghosts (X only) */
+#define SRG_HALO_GHOST_SEND_COUNTS 7  /* int64 [nranks] */
+#define SRG_HALO_GHOST_RECV_COUNTS 8  /* int64 [nranks] */
+#define SRG_HALO_CHUNK_RANGES 9       /* int64 [chunks + 1] local row bounds of the chunks */
+#define SRG_HALO_HUB_THRESHOLDS 10    /* int64 [nranks] */
+#define SRG_HALO_VIEW_ORDER 11        /* int32 schedule of view `index` (chunks, hub group, ghosts) */
+#define SRG_HALO_VIEW_META 12         /* int64 [4]: rows, hub rows, slice rows (d > 32), slice rows (d <= 32) */
+#define SRG_HALO_SEND_ROWS 13         /* int64 own local rows sent in group `index`, peers ascending */
+#define SRG_HALO_SEND_COUNTS 14       /* int64 [nranks] of group `index` */
+#define SRG_HALO_RECV_COUNTS 15       /* int64 [nranks] of group `index` */
+int srg_halo_plan_array(const srg_halo_plan* plan, int32_t what, int32_t index, const void** data, int64_t* count);
+/* The share on `device`: local CSR (values gathered from the GLOBAL fp32 host array `values`),
+ * schedules, send lists, a send buffer for panels up to d_max columns, a comm stream and events.
+ * The plan must outlive the share. */
+int srg_halo_share_create(const srg_halo_plan* plan, const float* values, int device, int32_t d_max,
+                          srg_halo_share** share);
+int srg_halo_share_destroy(srg_halo_share* share);
+/* Panel 0 from the WHOLE feature matrix X [n, ldx] on the share's device (as GraphOp.propagate is
+ * handed the whole feature): own rows, then the halo rows gathered by global id.  Then pass
+ * SRG_HALO_X_HALO_FILLED to srg_halo_propagate_f32 (no exchange of X). */
+int srg_halo_fill_x_halo(const srg_halo_share* share, const float* X, int64_t ldx, float* panel0, int64_t ld,
+                         int32_t d, void* stream);
+/* K hops for the local shares of `comm` (shares[i] is the communicator's i-th local rank; for a
+ * loopback communicator, ranks 0 .. nranks-1 in order).  panels: per share, a HOST array of K + 1
+ * device pointers, each a [n_rows + halo, d] panel (ld == d: the halo rows are RCCL buffers) on the
+ * share's device; panel 0's own rows hold X's rows of the rank, its halo is exchanged first unless
+ * flags has SRG_HALO_X_HALO_FILLED.  streams: per share (NULL array or entries: the null stream).
+ * Asynchronous on those streams; every panel k's own rows (and halo, k < K) are bitwise the one-GPU
+ * hop k.  d <= the shares' d_max. */
+#define SRG_HALO_X_HALO_FILLED 0x1u
+int srg_halo_propagate_f32(srg_comm* comm, srg_halo_share* const* shares, int n_shards, float* const* const* panels,
+                           int64_t ld, int32_t d, int32_t K, uint32_t flags, void* const* streams);
+/* A communicator of nranks virtual ranks in ONE process on one device whose exchange is device-to-
+ * device copies on a library stream: srg_halo_propagate_f32 then runs every rank's share (its
+ * kernels, packs, groups and offsets) on one GPU -- the tests' and a single-GPU host's rehearsal of
+ * the RCCL path.  Serves srg_halo_propagate_f32 only. */
+int srg_comm_init_loopback(int nranks, int device, srg_comm** comm);
+
 /* ---- diagnostics ----------------------------------------------------------------------------- */
 const char* srg_last_error(void);   /* thread-local message of the last failure ("" if none) */
 int srg_last_error_code(void);      /* thread-local status of the last call (SRG_OK if fine)  */

@@ -25,6 +25,7 @@
 #include <new>
 #include <vector>
 
+#include "srg_halo_internal.h"
 #include "srgnn_hip.h"
 
 extern "C" void srg_set_error(int code, const char* msg);   // srg_spmm.hip: thread-local srg_last_error
@@ -124,6 +125,10 @@ struct srg_comm {
     std::vector<ncclComm_t> comms;   // one per local device
     std::vector<int> ranks;          // their global ranks
     std::vector<int> devices;
+    // loopback: every rank in this process on one device, exchanges by device copies (no RCCL)
+    bool loopback = false;
+    hipStream_t lb_stream = nullptr;
+    hipEvent_t lb_done = nullptr;
 };
 
 extern "C" {
@@ -193,9 +198,44 @@ int srg_comm_init_all(int ndev, const int* devices, srg_comm** out)
     return SRG_OK;
 }
 
+int srg_comm_init_loopback(int nranks, int device, srg_comm** out)
+{
+    if (!out) return comm_fail(SRG_ERR_INVALID, "null argument");
+    *out = nullptr;
+    if (nranks < 1) return comm_fail(SRG_ERR_INVALID, "nranks=%d < 1", nranks);
+    DeviceScope scope;
+    SRG_HIPC(hipSetDevice(device));
+    srg_comm* comm = new (std::nothrow) srg_comm();
+    if (!comm) return comm_fail(SRG_ERR_ALLOC, "out of host memory");
+    comm->nranks = nranks;
+    comm->loopback = true;
+    for (int i = 0; i < nranks; ++i) {
+        comm->ranks.push_back(i);
+        comm->devices.push_back(device);
+    }
+    if (hipStreamCreateWithFlags(&comm->lb_stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&comm->lb_done, hipEventDisableTiming) != hipSuccess) {
+        srg_comm_destroy(comm);
+        return comm_fail(SRG_ERR_HIP, "loopback stream / event creation failed");
+    }
+    *out = comm;
+    return SRG_OK;
+}
+
 int srg_comm_destroy(srg_comm* comm)
 {
     if (!comm) return SRG_OK;
+    if (comm->loopback) {
+        DeviceScope scope;
+        (void)hipSetDevice(comm->devices.empty() ? 0 : comm->devices[0]);
+        if (comm->lb_stream) {
+            (void)hipStreamSynchronize(comm->lb_stream);
+            (void)hipStreamDestroy(comm->lb_stream);
+        }
+        if (comm->lb_done) (void)hipEventDestroy(comm->lb_done);
+        delete comm;
+        return SRG_OK;
+    }
     const Rccl* r = nullptr;
     int rc = load_rccl(&r);
     if (rc) return rc;
@@ -235,6 +275,7 @@ int srg_dist_propagate_khop_f32(srg_comm* comm, const srg_shard_f32* shards, int
                                 const int64_t* row_starts, int64_t ld, int32_t d, int32_t K)
 {
     if (!comm || !shards || !row_starts) return comm_fail(SRG_ERR_INVALID, "null argument");
+    if (comm->loopback) return comm_fail(SRG_ERR_INVALID, "a loopback communicator serves srg_halo_propagate_f32 only");
     if (n_shards != (int)comm->comms.size())
         return comm_fail(SRG_ERR_INVALID, "%d shards for %d local ranks", n_shards, (int)comm->comms.size());
     if (K < 0 || d < 0 || ld < d) return comm_fail(SRG_ERR_INVALID, "K=%d d=%d ld=%lld", K, d, (long long)ld);
@@ -279,6 +320,217 @@ int srg_dist_propagate_khop_f32(srg_comm* comm, const srg_shard_f32* shards, int
             int e = srg_spmm_csr_f32(s.indptr, s.indices, s.values, s.n_rows, s.row_order, s.n_hub, s.n_heavy,
                                      s.x_full, ld, s.panels[k], ld, d, 0, s.stream);
             if (e) return e;
+        }
+    }
+    return SRG_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------------------------------------
+// the halo-exchange hop loop (srg_halo.hip builds the plan and the shares)
+// ------------------------------------------------------------------------------------------------
+namespace {
+
+int64_t view_heavy(const SrgHaloView& V, int d) { return d <= 32 ? V.n_heavy_narrow : V.n_heavy; }
+
+// rows of group g (g == C + 1: the ghost rows of X) that `pl`'s rank sends to / receives from rank q
+int64_t send_count(const srg_halo_plan& pl, int g, int q)
+{
+    return g <= pl.C ? pl.send_counts[g][q] : pl.ghost_send_counts[q];
+}
+int64_t recv_count(const srg_halo_plan& pl, int g, int q)
+{
+    return g <= pl.C ? pl.recv_counts[g][q] : pl.ghost_recv_counts[q];
+}
+int64_t recv_base(const srg_halo_plan& pl, int g)
+{
+    return pl.rows + (g <= pl.C ? pl.group_offsets[g] : pl.n_recv);
+}
+
+// group g's send rows of `panel` (own rows) into the share's send buffer, on `s`; the event marks it
+int halo_pack(srg_halo_share* S, int g, const float* panel, int32_t d, hipStream_t s)
+{
+    const int64_t cnt = S->send_off[g + 1] - S->send_off[g];
+    if (cnt > 0) {
+        int rc = srg_gather_rows_f32(panel, d, S->plan->rows, S->send_idx[g], cnt, S->sendbuf + S->send_off[g] * d,
+                                     d, d, s);
+        if (rc) return rc;
+    }
+    SRG_HIPC(hipEventRecord(S->packed[g], s));
+    return SRG_OK;
+}
+
+// group g's exchange into the panels `dst` (one per shard): RCCL grouped sends / receives on each
+// shard's comm stream, which waits only for that group's pack; or, loopback, device copies
+int halo_transport(const Rccl* r, srg_comm* comm, srg_halo_share* const* shares, int n, int g,
+                   float* const* dst, int32_t d)
+{
+    const int P = comm->nranks;
+    if (comm->loopback) {
+        hipStream_t L = comm->lb_stream;
+        for (int i = 0; i < n; ++i) SRG_HIPC(hipStreamWaitEvent(L, shares[i]->packed[g], 0));
+        for (int q = 0; q < n; ++q) {
+            const srg_halo_plan& pq = *shares[q]->plan;
+            int64_t roff = recv_base(pq, g);
+            for (int s = 0; s < P; ++s) {
+                if (s == q) continue;
+                const int64_t cnt = recv_count(pq, g, s);
+                if (cnt > 0) {
+                    const srg_halo_plan& ps = *shares[s]->plan;
+                    int64_t soff = shares[s]->send_off[g];
+                    for (int t = 0; t < q; ++t)
+                        if (t != s) soff += send_count(ps, g, t);
+                    SRG_HIPC(hipMemcpyAsync(dst[q] + roff * d, shares[s]->sendbuf + soff * d,
+                                            (size_t)cnt * d * sizeof(float), hipMemcpyDeviceToDevice, L));
+                }
+                roff += cnt;
+            }
+        }
+        return SRG_OK;
+    }
+    for (int i = 0; i < n; ++i) {
+        SRG_HIPC(hipSetDevice(shares[i]->device));
+        SRG_HIPC(hipStreamWaitEvent(shares[i]->comm_stream, shares[i]->packed[g], 0));
+    }
+    SRG_NCCL(r, r->GroupStart());
+    int rc = SRG_OK;
+    for (int i = 0; i < n && !rc; ++i) {
+        srg_halo_share* S = shares[i];
+        const srg_halo_plan& pl = *S->plan;
+        const int me = comm->ranks[i];
+        int64_t soff = S->send_off[g], roff = recv_base(pl, g);
+        for (int q = 0; q < P && !rc; ++q) {
+            if (q == me) continue;
+            const int64_t sc = send_count(pl, g, q), rcn = recv_count(pl, g, q);
+            ncclResult_t e = ncclSuccess;
+            if (sc > 0) e = r->Send(S->sendbuf + soff * d, (size_t)sc * d, ncclFloat32, q, comm->comms[i], S->comm_stream);
+            if (e == ncclSuccess && rcn > 0)
+                e = r->Recv(dst[i] + roff * d, (size_t)rcn * d, ncclFloat32, q, comm->comms[i], S->comm_stream);
+            if (e != ncclSuccess) rc = comm_fail(SRG_ERR_HIP, "ncclSend / ncclRecv failed: %s", r->GetErrorString(e));
+            soff += sc;
+            roff += rcn;
+        }
+    }
+    // every exit closes the group (RCCL's group state is thread-local and shared with torch)
+    const ncclResult_t ge = r->GroupEnd();
+    if (rc) return rc;
+    if (ge != ncclSuccess) return comm_fail(SRG_ERR_HIP, "ncclGroupEnd failed: %s", r->GetErrorString(ge));
+    return SRG_OK;
+}
+
+// every shard's stream waits for the exchanges issued so far (on the device, not the host)
+int halo_finish(srg_comm* comm, srg_halo_share* const* shares, int n, void* const* streams)
+{
+    if (comm->loopback) {
+        SRG_HIPC(hipEventRecord(comm->lb_done, comm->lb_stream));
+        for (int i = 0; i < n; ++i)
+            SRG_HIPC(hipStreamWaitEvent(streams ? static_cast<hipStream_t>(streams[i]) : nullptr, comm->lb_done, 0));
+        return SRG_OK;
+    }
+    for (int i = 0; i < n; ++i) {
+        SRG_HIPC(hipSetDevice(shares[i]->device));
+        SRG_HIPC(hipEventRecord(shares[i]->comm_done, shares[i]->comm_stream));
+        SRG_HIPC(hipStreamWaitEvent(streams ? static_cast<hipStream_t>(streams[i]) : nullptr, shares[i]->comm_done, 0));
+    }
+    return SRG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int srg_halo_propagate_f32(srg_comm* comm, srg_halo_share* const* shares, int n_shards, float* const* const* panels,
+                           int64_t ld, int32_t d, int32_t K, uint32_t flags, void* const* streams)
+{
+    if (!comm || !shares || !panels) return comm_fail(SRG_ERR_INVALID, "null argument");
+    const int P = comm->nranks;
+    const int local = comm->loopback ? P : (int)comm->comms.size();
+    if (n_shards != local) return comm_fail(SRG_ERR_INVALID, "%d shares for %d local ranks", n_shards, local);
+    if (K < 0 || d < 0) return comm_fail(SRG_ERR_INVALID, "K=%d d=%d", K, d);
+    if (ld != d) return comm_fail(SRG_ERR_INVALID, "ld=%lld != d=%d: the halo rows are contiguous exchange buffers",
+                                  (long long)ld, d);
+    int C = -1;
+    for (int i = 0; i < n_shards; ++i) {
+        const srg_halo_share* S = shares[i];
+        if (!S || !S->plan || !panels[i]) return comm_fail(SRG_ERR_INVALID, "share %d: null share or panels", i);
+        const srg_halo_plan& pl = *S->plan;
+        if (pl.P != P || pl.p != comm->ranks[i])
+            return comm_fail(SRG_ERR_INVALID, "share %d is rank %d of %d, its communicator rank %d of %d", i, pl.p, pl.P,
+                             comm->ranks[i], P);
+        if (S->device != comm->devices[i])
+            return comm_fail(SRG_ERR_INVALID, "share %d on device %d, its communicator on %d", i, S->device, comm->devices[i]);
+        if (d > S->d_cap) return comm_fail(SRG_ERR_INVALID, "d=%d > the share's d_max=%lld", d, (long long)S->d_cap);
+        if (C >= 0 && pl.C != C) return comm_fail(SRG_ERR_INVALID, "shares with different chunk counts");
+        C = pl.C;
+        for (int k = 0; k <= K; ++k)
+            if (!panels[i][k] && d > 0) return comm_fail(SRG_ERR_INVALID, "share %d: panels[%d] is null", i, k);
+    }
+    if (comm->loopback)    // the plans of the in-process ranks must agree on every count
+        for (int g = 0; g <= C + 1; ++g)
+            for (int q = 0; q < P; ++q)
+                for (int s = 0; s < P; ++s)
+                    if (s != q && recv_count(*shares[q]->plan, g, s) != send_count(*shares[s]->plan, g, q))
+                        return comm_fail(SRG_ERR_INVALID, "group %d: rank %d receives %lld rows from %d, which sends %lld",
+                                         g, q, (long long)recv_count(*shares[q]->plan, g, s), s,
+                                         (long long)send_count(*shares[s]->plan, g, q));
+    if (K == 0 || d == 0) return SRG_OK;
+    const Rccl* r = nullptr;
+    if (!comm->loopback) {
+        int rc = load_rccl(&r);
+        if (rc) return rc;
+    }
+    DeviceScope scope;
+    const int G = C + 1;
+    auto st = [&](int i) { return streams ? static_cast<hipStream_t>(streams[i]) : nullptr; };
+    std::vector<float*> dst(n_shards);
+    auto panel_k = [&](int k) {
+        for (int i = 0; i < n_shards; ++i) dst[i] = panels[i][k];
+        return dst.data();
+    };
+    int rc = SRG_OK;
+    // hop 0's halo (received rows by group, then the ghost rows), unless the caller filled it
+    if (!(flags & SRG_HALO_X_HALO_FILLED)) {
+        for (int g = 0; g <= G; ++g) {
+            for (int i = 0; i < n_shards; ++i) {
+                SRG_HIPC(hipSetDevice(shares[i]->device));
+                if ((rc = halo_pack(shares[i], g, panels[i][0], d, st(i)))) return rc;
+            }
+            if ((rc = halo_transport(r, comm, shares, n_shards, g, panel_k(0), d))) return rc;
+        }
+        if ((rc = halo_finish(comm, shares, n_shards, streams))) return rc;
+    }
+    for (int k = 1; k <= K; ++k) {
+        const bool ex = k < K;       // the last hop's halo is never read
+        auto launch = [&](int i, int v, uint32_t f) -> int {
+            const srg_halo_share* S = shares[i];
+            const SrgHaloView& V = S->plan->views[v];
+            if (V.n == 0) return SRG_OK;
+            return srg_spmm_csr_f32(S->lip, S->lix, S->lvv, V.n, S->orders[v], V.n_hub, view_heavy(V, d),
+                                    panels[i][k - 1], ld, panels[i][k], ld, d, f, st(i));
+        };
+        // the hub group forked onto the library's side stream, beside the chunks
+        for (int i = 0; i < n_shards; ++i) {
+            SRG_HIPC(hipSetDevice(shares[i]->device));
+            if ((rc = launch(i, C, SRG_SPMM_HUB_NOJOIN))) return rc;
+        }
+        for (int c = 0; c < C; ++c) {
+            for (int i = 0; i < n_shards; ++i) {
+                SRG_HIPC(hipSetDevice(shares[i]->device));
+                if ((rc = launch(i, c, 0))) return rc;
+                if (ex && (rc = halo_pack(shares[i], c, panels[i][k], d, st(i)))) return rc;
+            }
+            if (ex && (rc = halo_transport(r, comm, shares, n_shards, c, panel_k(k), d))) return rc;
+        }
+        for (int i = 0; i < n_shards; ++i) {
+            SRG_HIPC(hipSetDevice(shares[i]->device));
+            if (ex && (rc = launch(i, G, 0))) return rc;            // the ghost rows into their halo slots
+            if (shares[i]->plan->views[C].n && (rc = srg_hub_join(st(i)))) return rc;
+            if (ex && (rc = halo_pack(shares[i], C, panels[i][k], d, st(i)))) return rc;
+        }
+        if (ex) {
+            if ((rc = halo_transport(r, comm, shares, n_shards, C, panel_k(k), d))) return rc;
+            if ((rc = halo_finish(comm, shares, n_shards, streams))) return rc;
         }
     }
     return SRG_OK;

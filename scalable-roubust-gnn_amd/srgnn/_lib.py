@@ -41,6 +41,21 @@ SRG_TAIL_MAX = 32
 
 SRG_SPGEMM_SERIAL_B = 0x1
 
+SRG_HALO_AUTO = -1
+SRG_HALO_NONE = -2
+SRG_HALO_X_HALO_FILLED = 0x1
+(SRG_HALO_STARTS, SRG_HALO_LOCAL_INDPTR, SRG_HALO_LOCAL_INDICES, SRG_HALO_GHOST_POSITIONS, SRG_HALO_HALO_IDS,
+ SRG_HALO_GROUP_OFFSETS, SRG_HALO_GHOST_SEND, SRG_HALO_GHOST_SEND_COUNTS, SRG_HALO_GHOST_RECV_COUNTS,
+ SRG_HALO_CHUNK_RANGES, SRG_HALO_HUB_THRESHOLDS, SRG_HALO_VIEW_ORDER, SRG_HALO_VIEW_META, SRG_HALO_SEND_ROWS,
+ SRG_HALO_SEND_COUNTS, SRG_HALO_RECV_COUNTS) = range(16)
+
+
+class HaloInfo(ctypes.Structure):
+    """srg_halo_info (include/srgnn_hip.h)."""
+    _fields_ = [(k, ctypes.c_int64) for k in ("row0", "n_rows", "n_recv", "n_ghost", "halo", "nnz_local",
+                                               "n_groups", "hub_rows", "send_rows")] + \
+               [(k, ctypes.c_int32) for k in ("ghost_max_degree", "chunks", "nranks", "rank")]
+
 # every symbol include/srgnn_hip.h declares (checked by tests/test_capi.py)
 EXPORTED_SYMBOLS = (
     "FloatCSRMulDenseOMP",
@@ -76,6 +91,15 @@ EXPORTED_SYMBOLS = (
     "srg_comm_destroy",
     "srg_comm_size",
     "srg_dist_propagate_khop_f32",
+    "srg_halo_plan_build",
+    "srg_halo_plan_destroy",
+    "srg_halo_plan_info",
+    "srg_halo_plan_array",
+    "srg_halo_share_create",
+    "srg_halo_share_destroy",
+    "srg_halo_fill_x_halo",
+    "srg_halo_propagate_f32",
+    "srg_comm_init_loopback",
     "srg_last_error",
     "srg_last_error_code",
     "srg_clear_error",
@@ -169,6 +193,19 @@ def _declare(lib):
     lib.srg_comm_size.restype = ctypes.c_int
     lib.srg_dist_propagate_khop_f32.argtypes = [_p, _p, ctypes.c_int, _p, _i64, _i32, _i32]
     lib.srg_dist_propagate_khop_f32.restype = ctypes.c_int
+    lib.srg_halo_plan_build.argtypes = [_p, _p, _i64, _i32, _i32, _i32, _i64, _i64, _i32, ctypes.POINTER(_p)]
+    lib.srg_halo_plan_destroy.argtypes = [_p]
+    lib.srg_halo_plan_info.argtypes = [_p, ctypes.POINTER(HaloInfo)]
+    lib.srg_halo_plan_array.argtypes = [_p, _i32, _i32, ctypes.POINTER(_p), ctypes.POINTER(_i64)]
+    lib.srg_halo_share_create.argtypes = [_p, _p, ctypes.c_int, _i32, ctypes.POINTER(_p)]
+    lib.srg_halo_share_destroy.argtypes = [_p]
+    lib.srg_halo_fill_x_halo.argtypes = [_p, _p, _i64, _p, _i64, _i32, _p]
+    lib.srg_halo_propagate_f32.argtypes = [_p, _p, ctypes.c_int, _p, _i64, _i32, _i32, _u32, _p]
+    lib.srg_comm_init_loopback.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(_p)]
+    for name in ("srg_halo_plan_build", "srg_halo_plan_destroy", "srg_halo_plan_info", "srg_halo_plan_array",
+                 "srg_halo_share_create", "srg_halo_share_destroy", "srg_halo_fill_x_halo", "srg_halo_propagate_f32",
+                 "srg_comm_init_loopback"):
+        getattr(lib, name).restype = ctypes.c_int
     lib.srg_last_error.argtypes = []
     lib.srg_last_error.restype = ctypes.c_char_p
     lib.srg_last_error_code.argtypes = []

@@ -89,3 +89,113 @@ class Comm:
 
     def _rank_of(self, i: int) -> int:
         return self._first_rank + i
+
+
+# ------------------------------------------------------------------------------------------------
+# the halo-exchange partition through the C-ABI (srg_halo_*): the plan a C / C++ host builds, its
+# device shares, and the hop loop over RCCL or the loopback transport
+# ------------------------------------------------------------------------------------------------
+_HALO_DTYPES = {_lib.SRG_HALO_STARTS: ctypes.c_int64, _lib.SRG_HALO_LOCAL_INDPTR: ctypes.c_int64,
+                _lib.SRG_HALO_LOCAL_INDICES: ctypes.c_int32, _lib.SRG_HALO_GHOST_POSITIONS: ctypes.c_int64,
+                _lib.SRG_HALO_HALO_IDS: ctypes.c_int64, _lib.SRG_HALO_GROUP_OFFSETS: ctypes.c_int64,
+                _lib.SRG_HALO_GHOST_SEND: ctypes.c_int64, _lib.SRG_HALO_GHOST_SEND_COUNTS: ctypes.c_int64,
+                _lib.SRG_HALO_GHOST_RECV_COUNTS: ctypes.c_int64, _lib.SRG_HALO_CHUNK_RANGES: ctypes.c_int64,
+                _lib.SRG_HALO_HUB_THRESHOLDS: ctypes.c_int64, _lib.SRG_HALO_VIEW_ORDER: ctypes.c_int32,
+                _lib.SRG_HALO_VIEW_META: ctypes.c_int64, _lib.SRG_HALO_SEND_ROWS: ctypes.c_int64,
+                _lib.SRG_HALO_SEND_COUNTS: ctypes.c_int64, _lib.SRG_HALO_RECV_COUNTS: ctypes.c_int64}
+
+
+class HaloPlan:
+    """srg_halo_plan: rank `rank`'s share of the halo partition, built by the library's host planner
+    from the global CSR (numpy / CPU arrays).  Needs no device."""
+
+    def __init__(self, indptr, indices, n: int, nranks: int, rank: int, chunks: int = 4,
+                 hub_threshold: int = _lib.SRG_HALO_AUTO, heavy_threshold: int = _lib.SRG_HALO_AUTO,
+                 ghost_max_degree: int = 0):
+        import numpy as np
+        self._ip = np.ascontiguousarray(np.asarray(indptr), dtype=np.int64)
+        self._ix = np.ascontiguousarray(np.asarray(indices), dtype=np.int32)
+        h = ctypes.c_void_p()
+        _lib.call_host("srg_halo_plan_build", self._ip.ctypes.data, self._ix.ctypes.data if self._ix.size else None,
+                       int(n), int(nranks), int(rank), int(chunks), int(hub_threshold), int(heavy_threshold),
+                       int(ghost_max_degree), ctypes.byref(h))
+        self._h = h
+        info = _lib.HaloInfo()
+        _lib.call_host("srg_halo_plan_info", self._h, ctypes.byref(info))
+        self.info = {k: getattr(info, k) for k, _ in _lib.HaloInfo._fields_}
+
+    def array(self, what: int, index: int = 0):
+        """A copy of one of the plan's arrays (numpy)."""
+        import numpy as np
+        data, count = ctypes.c_void_p(), ctypes.c_int64()
+        _lib.call_host("srg_halo_plan_array", self._h, int(what), int(index), ctypes.byref(data), ctypes.byref(count))
+        ct = _HALO_DTYPES[what]
+        if count.value == 0:
+            return np.zeros(0, dtype=np.int64 if ct is ctypes.c_int64 else np.int32)
+        return np.ctypeslib.as_array(ctypes.cast(data, ctypes.POINTER(ct)), shape=(count.value,)).copy()
+
+    def destroy(self):
+        if self._h:
+            _lib.call_host("srg_halo_plan_destroy", self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:  # noqa: BLE001
+            pass
+
+
+class HaloShare:
+    """srg_halo_share: a plan's device arrays on `device` (values: the GLOBAL fp32 values, host)."""
+
+    def __init__(self, plan: HaloPlan, values, device: int, d_max: int):
+        import numpy as np
+        v = np.ascontiguousarray(np.asarray(values), dtype=np.float32)
+        h = ctypes.c_void_p()
+        _lib.call_host("srg_halo_share_create", plan._h, v.ctypes.data if v.size else None, int(device), int(d_max),
+                       ctypes.byref(h))
+        self._h, self.plan, self.device = h, plan, torch.device("cuda", int(device))
+        self.rows, self.halo = plan.info["n_rows"], plan.info["halo"]
+
+    def new_panel(self, d: int) -> torch.Tensor:
+        return torch.zeros((self.rows + self.halo, d), dtype=torch.float32, device=self.device)
+
+    def fill_x_halo(self, X: torch.Tensor, panel0: torch.Tensor):
+        """Panel 0 from the whole X: own rows, then the halo rows gathered by global id."""
+        _lib.call(self.device, "srg_halo_fill_x_halo", self._h, X.data_ptr(), X.stride(0), panel0.data_ptr(),
+                  panel0.stride(0), X.shape[1], _lib.stream(self.device))
+
+    def destroy(self):
+        if self._h:
+            _lib.call_host("srg_halo_share_destroy", self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:  # noqa: BLE001
+            pass
+
+
+def loopback(nranks: int, device: int = 0) -> Comm:
+    """srg_comm_init_loopback: nranks virtual ranks in this process on one device."""
+    h = ctypes.c_void_p()
+    _lib.call_host("srg_comm_init_loopback", int(nranks), int(device), ctypes.byref(h))
+    return Comm(h, [device] * nranks)
+
+
+def halo_propagate(comm: Comm, shares: list[HaloShare], panels: list[list[torch.Tensor]], K: int,
+                   x_halo_filled: bool = False, streams=None):
+    """srg_halo_propagate_f32 over the local shares (loopback: every rank, in order); panels[i][k]
+    [rows + halo, d] of share i; asynchronous on each share's stream (torch's current one by
+    default)."""
+    d = int(panels[0][0].shape[1])
+    n = len(shares)
+    arrs = [(ctypes.c_void_p * (K + 1))(*[p.data_ptr() for p in ps]) for ps in panels]
+    parr = (ctypes.c_void_p * n)(*[ctypes.cast(a, ctypes.c_void_p) for a in arrs])
+    sh = (ctypes.c_void_p * n)(*[s._h for s in shares])
+    strm = (ctypes.c_void_p * n)(*[(streams[i] if streams else torch.cuda.current_stream(s.device).cuda_stream)
+                                   for i, s in enumerate(shares)])
+    _lib.call_host("srg_halo_propagate_f32", comm._h, sh, n, parr, d, d, int(K),
+                   _lib.SRG_HALO_X_HALO_FILLED if x_halo_filled else 0, strm)

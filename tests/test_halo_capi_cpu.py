@@ -1,0 +1,80 @@
+"""The C-ABI halo planner (srg_halo_plan_build, include/srgnn_hip.h) on the CPU: for a C / C++ host it
+builds rank p's share of the halo-exchange partition from the global CSR -- the same plan as the
+Python package's srgnn.dist.HaloPartitionedOperator.  Every array of the two plans is compared: row
+blocks, local CSR (remapped columns), schedules and their slice / hub counts, receive and send
+lists per group, ghost rows and their sends, halo ids.  Host-only entry: no device needed."""
+import numpy as np
+import pytest
+import torch
+
+
+def _graph(n=1500, e=9000, seed=12):
+    from srgnn import synth
+    from srgnn.normalize import sym_norm_binary
+    u, v = synth.rmat_undirected_t(n, e, seed=seed)
+    ip, ix = synth.symmetric_csr_t(n, u, v)
+    ip, ix, vals = sym_norm_binary(ip, ix, n, 0.5)
+    return ip, ix, vals, n
+
+
+def _python_share(ip, ix, vals, n, world, rank, chunks, hub, ghost):
+    from srgnn.dist import HaloPartitionedOperator
+    return HaloPartitionedOperator(ip, ix, vals, n, chunks=chunks, hub_threshold=hub, device="cpu", rank=rank,
+                                   world=world, local_spmm=lambda *a: None, ghost_max_degree=ghost)
+
+
+@pytest.mark.parametrize("world,chunks,hub,ghost", [(2, 3, 60, 0), (3, 2, 60, 8), (8, 6, None, 2), (4, 4, 40, 16),
+                                                   (1, 2, None, 0)])
+def test_c_planner_equals_python_plan(world, chunks, hub, ghost):
+    from srgnn import _lib
+    from srgnn.comm import HaloPlan
+    ip, ix, vals, n = _graph()
+    for rank in range(world):
+        op = _python_share(ip, ix, vals, n, world, rank, chunks, hub, ghost)
+        pl = HaloPlan(ip.numpy(), ix.numpy(), n, world, rank, chunks=chunks,
+                      hub_threshold=_lib.SRG_HALO_AUTO if hub is None else hub, ghost_max_degree=ghost)
+        info = pl.info
+        assert (info["row0"], info["n_rows"], info["n_recv"], info["n_ghost"], info["halo"]) == \
+            (op.r0, op.rows, op.n_recv, op.n_ghost, op.halo)
+        assert info["n_groups"] == op.n_groups and info["hub_rows"] == op.views[op.C][1]
+        np.testing.assert_array_equal(pl.array(_lib.SRG_HALO_STARTS), op.starts)
+        np.testing.assert_array_equal(pl.array(_lib.SRG_HALO_LOCAL_INDPTR), op._lip.numpy())
+        np.testing.assert_array_equal(pl.array(_lib.SRG_HALO_LOCAL_INDICES), op._lix.numpy())
+        np.testing.assert_array_equal(pl.array(_lib.SRG_HALO_GHOST_POSITIONS), op._ghost_pos.numpy())
+        np.testing.assert_array_equal(pl.array(_lib.SRG_HALO_HALO_IDS), op.halo_ids().numpy())
+        np.testing.assert_array_equal(pl.array(_lib.SRG_HALO_GROUP_OFFSETS), op.group_offsets)
+        np.testing.assert_array_equal(pl.array(_lib.SRG_HALO_CHUNK_RANGES)[1:],
+                                      [b for _, b in op.chunk_ranges])
+        for g in range(op.n_groups):
+            np.testing.assert_array_equal(pl.array(_lib.SRG_HALO_RECV_COUNTS, g), op.recv_counts[g])
+            np.testing.assert_array_equal(pl.array(_lib.SRG_HALO_SEND_COUNTS, g), op.send_counts[g])
+            np.testing.assert_array_equal(pl.array(_lib.SRG_HALO_SEND_ROWS, g), op.send_cat[g].numpy())
+        np.testing.assert_array_equal(pl.array(_lib.SRG_HALO_GHOST_SEND), op.ghost_send_cat.numpy())
+        np.testing.assert_array_equal(pl.array(_lib.SRG_HALO_GHOST_SEND_COUNTS), op.ghost_send_counts)
+        np.testing.assert_array_equal(pl.array(_lib.SRG_HALO_GHOST_RECV_COUNTS), op.ghost_recv_counts)
+        for v, (order, n_g, n_heavy, n_hub) in enumerate(op.views + [op.ghost_view]):
+            np.testing.assert_array_equal(pl.array(_lib.SRG_HALO_VIEW_ORDER, v), order.numpy(), err_msg=f"view {v}")
+            meta = pl.array(_lib.SRG_HALO_VIEW_META, v)
+            assert (meta[0], meta[1], meta[2]) == (n_g, n_hub, n_heavy), f"view {v}"
+        pl.destroy()
+
+
+def test_c_planner_argument_checks():
+    from srgnn import _lib
+    from srgnn.comm import HaloPlan
+    ip, ix, vals, n = _graph(n=300, e=1500)
+    with pytest.raises(_lib.SrgError, match="rank"):
+        HaloPlan(ip.numpy(), ix.numpy(), n, 2, 2)
+    with pytest.raises(_lib.SrgError, match="chunks"):
+        HaloPlan(ip.numpy(), ix.numpy(), n, 2, 0, chunks=0)
+    bad = ix.numpy().copy()
+    bad[7] = n
+    with pytest.raises(_lib.SrgError, match="outside"):
+        HaloPlan(ip.numpy(), bad, n, 2, 0)
+    ipb = ip.numpy().copy()
+    ipb[5] = ipb[6] + 1
+    with pytest.raises(_lib.SrgError, match="decreases"):
+        HaloPlan(ipb, ix.numpy(), n, 2, 0)
+    # no hub rows at all
+    pl = HaloPlan(ip.numpy(), ix.numpy(), n, 3, 1, chunks=2, hub_threshold=_lib.SRG_HALO_NONE)
+    assert pl.info["hub_rows"] == 0
