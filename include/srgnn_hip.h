@@ -261,6 +261,19 @@ int srg_spmm_span_f32(const int64_t* row_beg, const int64_t* row_end, const int3
                       int64_t n_heavy, const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t d,
                       uint32_t flags, float* agg, int64_t lda, float w, int agg_init, void* stream);
 
+/* A span launch in which each row decides for itself whether its chain starts from +0.0f or
+ * continues from Y: row r accumulates iff row_beg[r] != row_first[r] (its span does not start at
+ * the row's first entry; row_first: the full CSR's row pointers).  One launch can then finish some
+ * rows whole and carry on others from an earlier launch's partial chain -- the halo path's row
+ * chunks each compute their own rows plus one column span of every medium hub row (spans in
+ * ascending column order over the chunks, so the chains stay exact; srgnn/dist.py).  No hub rows,
+ * no ACCUMULATE / FAST / HUB_* flags; otherwise as srg_spmm_span_f32 (n_heavy slice-wave rows
+ * first in row_order).  No reference counterpart: the reference is single process. */
+int srg_spmm_span_rowacc_f32(const int64_t* row_beg, const int64_t* row_end, const int64_t* row_first,
+                             const int32_t* indices, const float* values, int64_t n_rows, const int32_t* row_order,
+                             int64_t n_heavy, const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t d,
+                             uint32_t flags, void* stream);
+
 /* srg_spmm_csr_f32 with the halo pack of the multi-GPU exchange fused into its epilogue
  * (srgnn/dist.py HaloPartitionedOperator; no reference counterpart -- the reference is single
  * process): every row r it computes is also stored, unchanged, into the send-buffer rows

@@ -320,6 +320,10 @@ struct Epi {
     // row-indexed arrays: consecutive slots, consecutive addresses (srg_propagate_plan_f32)
     const int64_t* slot_beg;
     const int64_t* slot_end;
+    // kEpiSpanRA only: row r's chain continues from Y (accumulate) iff its span does not start at
+    // the row's first entry, row_first[r] -- one launch then starts some rows from +0.0f and continues
+    // others (the halo path's row chunks, which also carry one column span of each medium hub row)
+    const int64_t* row_first;
 };
 
 // Epilogue kinds (template parameter EX of the SpMM kernels).  Every call site sits under
@@ -327,13 +331,15 @@ struct Epi {
 // (the reference-bound acc) changed the gather loop's schedule (+10 % per hop on products);
 // guarded, the kEpiPlain kernels are instruction-for-instruction the plain ones.  kEpiSpan is the
 // plain epilogue (aggregation included) over row spans.
-constexpr int kEpiPlain = 0, kEpiSend = 1, kEpiCheby = 2, kEpiSpan = 3;
+constexpr int kEpiPlain = 0, kEpiSend = 1, kEpiCheby = 2, kEpiSpan = 3, kEpiSpanRA = 4;
+// row spans (kEpiSpan, and kEpiSpanRA: spans with the accumulate decision per row)
+template <int EX> constexpr bool kIsSpan = EX == kEpiSpan || EX == kEpiSpanRA;
 
 // End of row `row`'s entries: the next row's start, or the span's end.
 template <int EX, typename IP>
 __device__ __forceinline__ int64_t row_stop(const IP* __restrict__ indptr, const Epi& e, int row)
 {
-    if constexpr (EX == kEpiSpan)
+    if constexpr (kIsSpan<EX>)
         return e.row_end[row];
     else
         return (int64_t)indptr[row + 1];
@@ -428,12 +434,13 @@ __device__ __forceinline__ void slice_wave(const IP* __restrict__ indptr,
     const bool cact = lane < kSliceCols && (SFULL || ccol < d);
     float* __restrict__ yrow = Y + (int64_t)row * ldy;
     float acc = 0.0f;
+    const int64_t beg = indptr[row];
+    if constexpr (EX == kEpiSpanRA) accumulate = beg != epi.row_first[row];
     if (accumulate && cact) acc = yrow[ccol];
     const float aprev = (epi.agg && !epi.init && cact) ? epi.agg[(int64_t)row * epi.lda + ccol] : 0.0f;
     [[maybe_unused]] ChebyOps<1> cop;
     if constexpr (EX == kEpiCheby)
         if (cact) cheby_load<1>(epi, row, ccol, X, ldx, cop);
-    const int64_t beg = indptr[row];
     const int64_t end = row_stop<EX>(indptr, epi, row);
     for (int64_t j = beg; j < end; j += 8 * UH) {
         V4 x[UH];
@@ -513,6 +520,7 @@ __device__ __forceinline__ void narrow_rows(const IP* __restrict__ indptr, const
     }
     maxlen = __builtin_amdgcn_readfirstlane(maxlen);
     float* __restrict__ yrow = Y + (int64_t)row * ldy;
+    if constexpr (EX == kEpiSpanRA) accumulate = rv && beg != epi.row_first[row];
     float acc = (accumulate && act) ? yrow[c] : 0.0f;
     const float aprev = (epi.agg && !epi.init && act) ? epi.agg[(int64_t)row * epi.lda + c] : 0.0f;
     [[maybe_unused]] ChebyOps<1> cop;
@@ -573,7 +581,7 @@ __device__ __forceinline__ void packed_rows(const IP* __restrict__ indptr, const
     int64_t beg = 0;
     int len = 0;
     if (rv) {
-        if constexpr (EX == kEpiSpan) {
+        if constexpr (kIsSpan<EX>) {
             if (epi.slot_beg) {
                 beg = epi.slot_beg[slot];
                 len = (int)(epi.slot_end[slot] - beg);
@@ -594,6 +602,7 @@ __device__ __forceinline__ void packed_rows(const IP* __restrict__ indptr, const
     }
     maxlen = __builtin_amdgcn_readfirstlane(maxlen);
     float* __restrict__ yrow = Y + (int64_t)row * ldy;
+    if constexpr (EX == kEpiSpanRA) accumulate = rv && beg != epi.row_first[row];
     // the Chebyshev epilogue never aggregates nor accumulates (its entry rejects both): dropping
     // them statically keeps its registers (the prefetched operands) within 5 waves per SIMD
     float* __restrict__ arow = (EX != kEpiCheby && epi.agg) ? epi.agg + (int64_t)row * epi.lda : nullptr;
@@ -695,6 +704,7 @@ k_spmm(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
     if (w >= n_rows) return;
     const int row = order ? order[w] : w;
     float* __restrict__ yrow = Y + (int64_t)row * ldy;
+    if constexpr (EX == kEpiSpanRA) accumulate = (int64_t)indptr[row] != epi.row_first[row];
     for (int c0 = 0; c0 < d; c0 += 64 * VEC) {
         const int col = c0 + lane * VEC;
         const bool act = col < d;
@@ -707,7 +717,7 @@ k_spmm(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
         [[maybe_unused]] ChebyOps<VEC> cop;
         if constexpr (EX == kEpiCheby)
             if (FULL || act) cheby_load<VEC>(epi, row, col, X, ldx, cop);
-        row_gather<float, VEC, U, FULL, IP, EX == kEpiSpan>(acc, indptr, indices, vals, row, X, ldx, col, act,
+        row_gather<float, VEC, U, FULL, IP, kIsSpan<EX>>(acc, indptr, indices, vals, row, X, ldx, col, act,
                                                             epi.row_end);
         if (FULL || act) {
             if constexpr (EX == kEpiCheby) cheby_epi<VEC>(epi, row, col, acc, cop);
@@ -1701,6 +1711,9 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
     SideStream* ss = nullptr;
     std::unique_lock<std::mutex> side_lock(g_side_mu, std::defer_lock);
     const bool fast = (flags & SRG_SPMM_FAST) && (EX == kEpiPlain || EX == kEpiSpan) && !epi.agg;
+    if (EX == kEpiSpanRA && n_hub > 0)
+        return fail(SRG_ERR_INVALID, "per-row accumulation (row_first) takes no hub rows: n_hub=%lld", (long long)n_hub);
+    if constexpr (EX != kEpiSpanRA) {
     if (n_hub > 0 && fast) {   // fork: the hub rows' segments, then their sums, beside the main launch
         side_lock.lock();
         int rc = side_stream_locked(s, &ss);
@@ -1780,6 +1793,7 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
             SRG_HIP_CHECK(hipGetLastError());
         }
     }
+    }   // EX != kEpiSpanRA
 
     const int32_t* morder = order ? order + n_hub : nullptr;
     const int64_t m_rows = n_rows - n_hub;
@@ -2119,6 +2133,25 @@ int srg_spmm_span_f32(const int64_t* row_beg, const int64_t* row_end, const int3
     e.row_end = row_end;
     rc = launch_spmm<int64_t, kEpiSpan>(row_beg, indices, values, n_rows, row_order, n_hub, n_heavy, X, ldx, Y, ldy,
                                         d, flags, static_cast<hipStream_t>(stream), e);
+    return rc ? rc : ok();
+}
+
+int srg_spmm_span_rowacc_f32(const int64_t* row_beg, const int64_t* row_end, const int64_t* row_first,
+                             const int32_t* indices, const float* values, int64_t n_rows, const int32_t* row_order,
+                             int64_t n_heavy, const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t d,
+                             uint32_t flags, void* stream)
+{
+    SRG_DEVICE_GUARD(stream);
+    int rc = check_spmm_args(row_beg, indices, values, n_rows, X, ldx, Y, ldy, d);
+    if (rc) return rc;
+    if (n_rows > 0 && (!row_end || !row_first)) return fail(SRG_ERR_INVALID, "null row_end / row_first");
+    if (flags & (SRG_SPMM_ACCUMULATE | SRG_SPMM_FAST | SRG_SPMM_HUB_NOJOIN | SRG_SPMM_HUB_CONTINUE))
+        return fail(SRG_ERR_INVALID, "flags 0x%x: the accumulation is per row here, and there are no hub rows", flags);
+    Epi e{};
+    e.row_end = row_end;
+    e.row_first = row_first;
+    rc = launch_spmm<int64_t, kEpiSpanRA>(row_beg, indices, values, n_rows, row_order, 0, n_heavy, X, ldx, Y, ldy, d,
+                                          flags, static_cast<hipStream_t>(stream), e);
     return rc ? rc : ok();
 }
 

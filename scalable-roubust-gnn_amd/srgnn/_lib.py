@@ -69,6 +69,7 @@ EXPORTED_SYMBOLS = (
     "srg_hop_accumulate_f32",
     "srg_spmm_agg_f32",
     "srg_spmm_span_f32",
+    "srg_spmm_span_rowacc_f32",
     "srg_spmm_send_f32",
     "srg_spmm_cheby_f32",
     "srg_tail_record_f32",
@@ -193,6 +194,8 @@ def _declare(lib):
     lib.srg_comm_size.restype = ctypes.c_int
     lib.srg_dist_propagate_khop_f32.argtypes = [_p, _p, ctypes.c_int, _p, _i64, _i32, _i32]
     lib.srg_dist_propagate_khop_f32.restype = ctypes.c_int
+    lib.srg_spmm_span_rowacc_f32.argtypes = [_p, _p, _p, _p, _p, _i64, _p, _i64, _p, _i64, _p, _i64, _i32, _u32, _p]
+    lib.srg_spmm_span_rowacc_f32.restype = ctypes.c_int
     lib.srg_halo_plan_build.argtypes = [_p, _p, _i64, _i32, _i32, _i32, _i64, _i64, _i32, ctypes.POINTER(_p)]
     lib.srg_halo_plan_destroy.argtypes = [_p]
     lib.srg_halo_plan_info.argtypes = [_p, ctypes.POINTER(HaloInfo)]

@@ -267,6 +267,18 @@ AUTO_HALO_HUB_BLOCKS = int(os.environ.get("SRGNN_HALO_HUB_BLOCKS", "1"))
 # of rows, so its entries are already read in nearly the order its launch takes them
 LAUNCH_ORDER = os.environ.get("SRGNN_HALO_LAUNCH_ORDER", "0") != "0"
 
+# Medium hub rows as column spans inside the row chunks (GPU ranks; SRGNN_HALO_MEDIUM_SPANS=0 for
+# the A/B): the hub group's rows of at most `giant_threshold` entries (products at 8 ranks: ~1,050
+# rows of 2.6 K - 10 K entries per rank, 30 % of its nonzeros) are not hub workgroups beside the
+# chunks any more; chunk c computes span c of each of them -- its entries whose GLOBAL column ids lie
+# in [ceil(c n / C), ceil((c+1) n / C)) -- as slice waves, continuing the chain left by chunk c - 1
+# (srg_spmm_span_rowacc_f32: per-row accumulation), so every row is still one fma chain in CSR
+# order.  Each chunk then gathers those rows' entries from one column block of the panel (the
+# locality column blocks give one GPU) instead of the hub workgroups gathering from everywhere;
+# only the giant rows stay hub workgroups.  They finish with the last chunk and are exchanged
+# with the hub group, as before.
+MEDIUM_SPANS = os.environ.get("SRGNN_HALO_MEDIUM_SPANS", "1") != "0"
+
 
 class HaloPartitionedOperator:
     """Rank p's share of Â for the halo-exchange multi-GPU propagation.
@@ -297,9 +309,10 @@ class HaloPartitionedOperator:
                  heavy_threshold=None, hub_threshold=None, device=None, rank=None, world=None,
                  local_spmm=None, ghost_max_degree=None, hub_launches=None, giant_weight=None,
                  calibrate_link: bool = True, fast: bool = False, col_blocks=None, early_degree=None,
-                 hub_col_blocks=None):
+                 hub_col_blocks=None, medium_spans=None, giant_threshold=None):
         from .csr import (DEFAULT_HEAVY_THRESHOLD, DEFAULT_HUB_THRESHOLD, NARROW_HEAVY_THRESHOLD,
                           auto_heavy_threshold, auto_hub_threshold)
+        self._narrow_heavy = NARROW_HEAVY_THRESHOLD
         self.group = group
         # tolerance mode for the hub group (SRG_SPMM_FAST: each hub row as 64 exact segment chains
         # plus their ordered sum; the other rows stay bit-exact)
@@ -308,6 +321,12 @@ class HaloPartitionedOperator:
         self.col_blocks = col_blocks
         # column blocks of the hub group's launch (None: the automatic rule of _hub_blocks_for)
         self.hub_col_blocks = hub_col_blocks
+        # medium hub rows as column spans in the row chunks (None: MEDIUM_SPANS); rows of the hub
+        # group longer than giant_threshold stay hub workgroups (None: auto_hub_threshold of the
+        # rank's nonzeros for one launch, nnz / 1024: a span per chunk then stays well inside the
+        # chunk's launch as slice waves)
+        self.medium_spans = MEDIUM_SPANS if medium_spans is None else bool(medium_spans)
+        self.giant_threshold = giant_threshold
         self._cb = {}
         self._lo_ok = None             # launch-ordered copies fit (_launch_op), decided on first use
         self.virtual = rank is not None
@@ -638,6 +657,66 @@ class HaloPartitionedOperator:
         self._cb[key] = blocks
         return blocks
 
+    def _medium_plan(self):
+        """(giant hub view or None, [chunk c's span view]) when medium hub rows run as column spans
+        inside the row chunks (see MEDIUM_SPANS), else None.  Chunk c's view schedules its own rows
+        whole ([lip[r], lip[r+1])) and span c of every medium row (its entries with global column
+        ids in block c of C, empty spans skipped), longest first; launched with per-row
+        accumulation (a span that starts at its row's first entry starts from +0.0f).  Cached."""
+        if "medium" in self._cb:
+            return self._cb["medium"]
+        res = None
+        C = self.C
+        if (self._hip and self.medium_spans and not self.fast and C > 1 and self.views[C][1]
+                and self._col_blocks_for(128) < 2 and self._hub_blocks_for(128) < 2):
+            from .csr import DeviceCSR, auto_heavy_threshold, auto_hub_threshold
+            lip = self._lip
+            deg = lip[1:] - lip[:-1]
+            hub_rows = self.views[C][0].to(torch.int64)                 # longest first
+            giant_t = auto_hub_threshold(self.nnz_local, launches=1) if self.giant_threshold is None \
+                else int(self.giant_threshold)
+            med_mask = deg[hub_rows] <= giant_t
+            med, giant = hub_rows[med_mask], hub_rows[~med_mask]
+            if med.numel():
+                bounds, _ = self._block_bounds(C)
+                heavy_t = auto_heavy_threshold(self.nnz_local, launches=C) if self._auto_heavy \
+                    else self._heavy_explicit
+                gview = None
+                if giant.numel():
+                    gview = DeviceCSR(lip, self._lix, self._lvv, int(giant.numel()), self.ncols_local,
+                                      giant.to(torch.int32).contiguous(), 0, int(giant.numel()), None,
+                                      row_space=self.rows)
+                views = []
+                for c in range(C):
+                    own = self.views[c][0].to(torch.int64)
+                    beg = lip[: self.rows].clone()
+                    end = lip[1: self.rows + 1].clone()
+                    mb, me = bounds[c][med], bounds[c + 1][med]
+                    beg[med], end[med] = mb, me
+                    rows_c = torch.cat([own, med[me > mb]])
+                    lens = end[rows_c] - beg[rows_c]
+                    srt = torch.sort(lens, descending=True, stable=True)
+                    order = rows_c[srt.indices].to(torch.int32).contiguous()
+                    n_heavy = int((srt.values > heavy_t).sum()) if heavy_t >= 0 else 0
+                    narrow = int((srt.values > self._narrow_heavy).sum()) if self._auto_heavy else None
+                    views.append(DeviceCSR(beg, self._lix, self._lvv, int(order.numel()), self.ncols_local, order,
+                                           n_heavy, 0, narrow, row_end=end, row_space=self.rows))
+                res = (gview, views)
+        self._cb["medium"] = res
+        return res
+
+    def _medium_chunk(self, c: int, src: torch.Tensor, out: torch.Tensor):
+        """Row chunk c with its span of every medium hub row (srg_spmm_span_rowacc_f32)."""
+        from . import _lib
+        A = self._medium_plan()[1][c]
+        if A.n_rows == 0:
+            return
+        d = src.shape[1]
+        _lib.call(src.device, "srg_spmm_span_rowacc_f32", A.indptr.data_ptr(), A.row_end.data_ptr(),
+                  self._lip.data_ptr(), A.indices.data_ptr(), A.values.data_ptr(), A.n_rows, A.order.data_ptr(),
+                  A.heavy(d), src.data_ptr(), src.stride(0), out.data_ptr(), out.stride(0), d, 0,
+                  _lib.stream(src.device))
+
     def _launch_op(self, g: int):
         """Group g's operator as its launch takes it: on GPU ranks a copy of its entries laid out in
         its schedule's order (DeviceCSR.schedule_ordered, cached on the operator; the same chains),
@@ -772,23 +851,35 @@ class HaloPartitionedOperator:
             return
         from . import _lib
         from .spmm import spmm, spmm_send
-        fork = bool(self.views[C][1] and self.views[C][3] and self._hip and packed is None)
-        if self.views[C][1]:
-            if packed is not None:
-                spmm_send(self._A[C], src, out, packed, self._send_ptr, self._send_slot)
-            elif fork:
-                self._hub_launch(src, out)
-            else:
-                self._spmm(self._launch_op(C), src, out)
-        blocks = self.chunk_blocks(src.shape[1]) if packed is None else None
-        for c in range(C):
-            if self.views[c][1]:
+        med = self._medium_plan() if packed is None else None
+        if med is not None:
+            # the giant hub rows forked beside the chunks; every chunk carries one column span of
+            # each medium hub row
+            fork = med[0] is not None
+            if fork:
+                spmm(med[0], src, out=out, hub_nojoin=True)
+            for c in range(C):
+                self._medium_chunk(c, src, out)
+                if after_group is not None:
+                    after_group(c)
+        else:
+            fork = bool(self.views[C][1] and self.views[C][3] and self._hip and packed is None)
+            if self.views[C][1]:
                 if packed is not None:
-                    spmm_send(self._A[c], src, out, packed, self._send_ptr, self._send_slot)
+                    spmm_send(self._A[C], src, out, packed, self._send_ptr, self._send_slot)
+                elif fork:
+                    self._hub_launch(src, out)
                 else:
-                    self._chunk_spmm(c, src, out, blocks)
-            if after_group is not None:
-                after_group(c)
+                    self._spmm(self._launch_op(C), src, out)
+            blocks = self.chunk_blocks(src.shape[1]) if packed is None else None
+            for c in range(C):
+                if self.views[c][1]:
+                    if packed is not None:
+                        spmm_send(self._A[c], src, out, packed, self._send_ptr, self._send_slot)
+                    else:
+                        self._chunk_spmm(c, src, out, blocks)
+                if after_group is not None:
+                    after_group(c)
         if ghosts and self.n_ghost:
             self._spmm(self._launch_op(self.n_groups) if packed is None else gA, src, dst)
         if fork:
@@ -923,7 +1014,7 @@ def _virtual_exchange(shares, panels, ghosts: bool = False):
 
 def simulate_halo_propagate(indptr, indices, values, n: int, x: torch.Tensor, K: int, world: int,
                             chunks: int = 3, heavy_threshold=None, hub_threshold=None, device=None,
-                            ghost_max_degree=None, shares=None, col_blocks=None, hub_col_blocks=None):
+                            ghost_max_degree=None, shares=None, col_blocks=None, hub_col_blocks=None, **kw):
     """P virtual halo-exchange ranks in ONE process (all_to_all emulated by copies); returns the
     K+1 full [n, d] panels.  Exercises the group split, ghost rows, halo layout and column remap
     on a device."""
@@ -931,7 +1022,7 @@ def simulate_halo_propagate(indptr, indices, values, n: int, x: torch.Tensor, K:
         shares = [HaloPartitionedOperator(indptr, indices, values, n, chunks=chunks, heavy_threshold=heavy_threshold,
                                           hub_threshold=hub_threshold, device=device, rank=q, world=world,
                                           ghost_max_degree=ghost_max_degree, col_blocks=col_blocks,
-                                          hub_col_blocks=hub_col_blocks)
+                                          hub_col_blocks=hub_col_blocks, **kw)
                   for q in range(world)]
     d = x.shape[1]
     panels = [[s.new_panel(d) for _ in range(K + 1)] for s in shares]

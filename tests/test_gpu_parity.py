@@ -907,3 +907,71 @@ def test_schedule_ordered_one_launch_bit_exact(name):
     for k in range(1, c.k + 1):
         c.check_hop(k, hops[k].cpu().numpy())
     c.check_hop(1, spmm_mod.hop(A, X, torch.empty_like(X), col_blocks=1).cpu().numpy())
+
+
+@pytest.mark.parametrize("world,chunks,ghost,giant,d,medium", [(8, 6, 2, 1000, 128, True), (4, 4, 8, 400, 64, True),
+                                                              (2, 3, None, None, 256, True), (8, 6, 2, 1000, 32, True),
+                                                              (3, 5, 0, 600, 130, True), (8, 6, 2, None, 128, False)])
+def test_halo_medium_spans_bitwise(world, chunks, ghost, giant, d, medium):
+    """Medium hub rows as column spans inside the row chunks (srgnn.dist.MEDIUM_SPANS: chunk c runs
+    its own rows whole and span c of every medium hub row with per-row accumulation,
+    srg_spmm_span_rowacc_f32; the rows above the giant threshold stay hub workgroups beside the
+    chunks): every hop bitwise equal to the single-device propagation, for wide, narrow and ragged
+    panels, with and without giant rows, and with the mode off."""
+    from srgnn import synth
+    from srgnn.csr import DeviceCSR
+    from srgnn.dist import HaloPartitionedOperator, simulate_halo_propagate
+    from srgnn.normalize import sym_norm_binary
+    from srgnn.spmm import propagate
+    n = 20000
+    u, v = synth.rmat_undirected_t(n, 150000, seed=22, device="cuda")
+    ip, ix = synth.symmetric_csr_t(n, u, v)
+    ip, ix, vals = sym_norm_binary(ip, ix, n, 0.5)
+    x = synth.uniform_features_t(n, d, device="cuda")
+    want = propagate(DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, device="cuda"), x, 3)
+    shares = [HaloPartitionedOperator(ip, ix, vals, n, chunks=chunks, hub_threshold=150, device="cuda", rank=q,
+                                      world=world, ghost_max_degree=ghost, medium_spans=medium,
+                                      giant_threshold=giant) for q in range(world)]
+    plans = [s._medium_plan() for s in shares]
+    if medium:
+        assert all(p is not None for p in plans)
+        if giant is not None:
+            assert any(p[0] is not None for p in plans)       # some giant rows stay hub workgroups
+    else:
+        assert all(p is None for p in plans)
+    got = simulate_halo_propagate(ip, ix, vals, n, x, 3, world, shares=shares)
+    for k in range(1, 4):
+        assert torch.equal(got[k], want[k]), f"hop {k} differs with {world} virtual halo ranks"
+
+
+def test_span_rowacc_entry_checks():
+    """srg_spmm_span_rowacc_f32 rejects hub / accumulate / FAST flags and missing span arrays."""
+    from srgnn import _lib
+    L = _lib.lib()
+    X = torch.zeros((4, 8), device="cuda")
+    ip = torch.tensor([0, 1, 2, 3, 4], dtype=torch.int64, device="cuda")
+    ix = torch.arange(4, dtype=torch.int32, device="cuda")
+    vv = torch.ones(4, device="cuda")
+    order = torch.arange(4, dtype=torch.int32, device="cuda")
+    s = _lib.stream(X.device)
+    args = (ip.data_ptr(), ip[1:].data_ptr(), ip.data_ptr(), ix.data_ptr(), vv.data_ptr(), 4, order.data_ptr(), 0,
+            X.data_ptr(), 8, X.data_ptr(), 8, 8)
+    for f in (_lib.SRG_SPMM_ACCUMULATE, _lib.SRG_SPMM_FAST, _lib.SRG_SPMM_HUB_NOJOIN):
+        assert L.srg_spmm_span_rowacc_f32(*args, f, s) == _lib.SRG_ERR_INVALID
+    bad = list(args)
+    bad[2] = None
+    assert L.srg_spmm_span_rowacc_f32(*bad, 0, s) == _lib.SRG_ERR_INVALID
+    Y = torch.full((4, 8), 5.0, device="cuda")
+    X2 = torch.arange(32, dtype=torch.float32, device="cuda").reshape(4, 8)
+    # row_first == row_beg: every row starts from zero -> Y = X (identity pattern)
+    good = list(args)
+    good[8], good[10] = X2.data_ptr(), Y.data_ptr()
+    assert L.srg_spmm_span_rowacc_f32(*good, 0, s) == _lib.SRG_OK
+    torch.cuda.synchronize()
+    assert torch.equal(Y, X2)
+    # row_first != row_beg: every row continues from Y -> Y = X2 + X2
+    first = ip.clone() - 1
+    good[2] = first.data_ptr()
+    assert L.srg_spmm_span_rowacc_f32(*good, 0, s) == _lib.SRG_OK
+    torch.cuda.synchronize()
+    assert torch.equal(Y, 2 * X2)
