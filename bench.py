@@ -101,6 +101,9 @@ def parse():
     ap.add_argument("--pmc", default="auto", choices=["auto", "on", "off"],
                     help="measure the hop's HBM traffic with rocprofv3 --pmc passes of tools/spmm_probe.py "
                          "before this process touches the GPU (auto: one GPU, K-hop, not under a profiler)")
+    ap.add_argument("--dist-parity", default="auto", choices=["auto", "sampled"],
+                    help="N > 1: auto = bitwise against the whole-graph one-GPU hops when they fit beside a "
+                         "rank's share, else sampled rows against the oracle; sampled = always the latter")
     ap.add_argument("--parity-rows", type=int, default=2000,
                     help="one GPU: random rows (plus the 20 longest) checked against the oracle after timing")
     ap.add_argument("--mode", default="auto", choices=["auto", "panels", "last"],
@@ -789,7 +792,7 @@ def main():
 
     stream = torch.cuda.current_stream(dev)
     mode = a.mode
-    ref_full = reference_hops(ip, ix, vals, n, X, K, dev) if world > 1 else None
+    ref_full = reference_hops(ip, ix, vals, n, X, K, dev) if world > 1 and a.dist_parity == "auto" else None
     if world == 1:
         A = DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, heavy_threshold=a.heavy_threshold, device=dev)
         if mode == "auto":
@@ -949,7 +952,8 @@ def main():
         elif a.exchange == "halo" and not a.fast:
             # the whole graph's panels do not fit beside a rank's share: sampled own rows of hop 1
             # and hop K against the oracle, and sampled halo rows against their owners
-            parity = {"whole_graph_reference": "does not fit beside a rank's share",
+            parity = {"whole_graph_reference": ("not computed (--dist-parity sampled)" if a.dist_parity == "sampled"
+                                                else "does not fit beside a rank's share"),
                       "sampled_vs_oracle": dist_sampled_parity(op, panels, K)}
         else:
             parity = {"skipped": "the whole graph's panels do not fit beside a rank's share"}

@@ -83,7 +83,11 @@ extern "C" {
  * are deterministic and within fp32 re-association error of the reference chain (the tests hold
  * them to the forward-error bound and 1e-5 relative); every other row is bit-exact.  The longest
  * row's latency drops ~64-fold: the straggler of a row-partitioned hop.  Plain and span entries
- * only (the aggregation / send / Chebyshev epilogues run exact). */
+ * only (the aggregation / send / Chebyshev epilogues run exact).
+ * DIAGNOSTIC / tolerance studies only: no configuration measured so far gains from it (one GPU:
+ * the top row's exact chain runs beside the hop; 8 ranks: the hub group is bound by its share of
+ * HBM beside the chunks, not by the top row's chain -- 1.09-1.11 ms per hop against 1.05-1.08
+ * exact), so no default path sets it. */
 #define SRG_SPMM_FAST 0x40u
 
 /* =============================================================================================

@@ -1599,9 +1599,11 @@ int side_stream_locked(hipStream_t caller, SideStream** out)
     if (!ss.stream) {
         // highest queue priority: the hub workgroups (9 waves, ~136 KB LDS each) must get CUs
         // before the main launch's many small blocks occupy them all
+        // (SRGNN_HUB_PRIORITY=normal: the caller streams' priority instead, for A/B runs)
         int least = 0, greatest = 0;
         SRG_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-        SRG_HIP_CHECK(hipStreamCreateWithPriority(&ss.stream, hipStreamNonBlocking, greatest));
+        static const bool normal = [] { const char* e = getenv("SRGNN_HUB_PRIORITY"); return e && !strcmp(e, "normal"); }();
+        SRG_HIP_CHECK(hipStreamCreateWithPriority(&ss.stream, hipStreamNonBlocking, normal ? least : greatest));
         SRG_HIP_CHECK(hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming));
         SRG_HIP_CHECK(hipEventCreateWithFlags(&ss.join, hipEventDisableTiming));
     }

@@ -277,7 +277,11 @@ LAUNCH_ORDER = os.environ.get("SRGNN_HALO_LAUNCH_ORDER", "0") != "0"
 # locality column blocks give one GPU) instead of the hub workgroups gathering from everywhere;
 # only the giant rows stay hub workgroups.  They finish with the last chunk and are exchanged
 # with the hub group, as before.
-MEDIUM_SPANS = os.environ.get("SRGNN_HALO_MEDIUM_SPANS", "1") != "0"
+# Measured opt-in (round 4, tools/halo_ranks.py on products at P = 8, profiles/r04_halo_medium_spans_negative.txt):
+# the per-rank fabric traffic falls from 5.59 to 5.02 GB per hop, but the hop takes 1.11-1.13 ms
+# against 1.02: slice waves keep 8 KiB of gathers in flight per wave where the hub workgroups keep
+# ~128 KiB per workgroup, so the spans run latency-bound (4.9 TB/s against 5.6 at the gather ceiling)
+MEDIUM_SPANS = os.environ.get("SRGNN_HALO_MEDIUM_SPANS", "0") != "0"
 
 
 class HaloPartitionedOperator:
@@ -673,8 +677,9 @@ class HaloPartitionedOperator:
             lip = self._lip
             deg = lip[1:] - lip[:-1]
             hub_rows = self.views[C][0].to(torch.int64)                 # longest first
-            giant_t = auto_hub_threshold(self.nnz_local, launches=1) if self.giant_threshold is None \
-                else int(self.giant_threshold)
+            giant_env = os.environ.get("SRGNN_HALO_GIANT_THRESHOLD")
+            giant_t = int(self.giant_threshold) if self.giant_threshold is not None else \
+                int(giant_env) if giant_env else auto_hub_threshold(self.nnz_local, launches=1)
             med_mask = deg[hub_rows] <= giant_t
             med, giant = hub_rows[med_mask], hub_rows[~med_mask]
             if med.numel():

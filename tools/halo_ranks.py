@@ -44,6 +44,11 @@ def main():
                     help="column blocks of the row chunks' launches: one value or a comma list (default: auto)")
     ap.add_argument("--hub-col-blocks", default=None,
                     help="column blocks of the hub group's launch: one value or a comma list (default: auto)")
+    ap.add_argument("--quick", action="store_true",
+                    help="time only each rank's hop compute (op.compute), no breakdowns: for A/B sweeps")
+    ap.add_argument("--medium", default=None, choices=["on", "off"],
+                    help="medium hub rows as column spans in the chunks (default: srgnn.dist.MEDIUM_SPANS)")
+    ap.add_argument("--giant-threshold", type=int, default=None)
     ap.add_argument("--ghost", default="auto",
                     help="ghost row degree cap(s): 'auto' (the operator's cost model) or a comma list")
     a = ap.parse_args()
@@ -62,13 +67,31 @@ def main():
             op = HaloPartitionedOperator(ip, ix, vals, n, chunks=a.chunks, device=dev, rank=q, world=P,
                                          ghost_max_degree=ghost, hub_launches=a.hub_launches,
                                          giant_weight=a.giant_weight, fast=a.fast, col_blocks=cb,
-                                         early_degree=a.early_degree, hub_col_blocks=hcb)
+                                         early_degree=a.early_degree, hub_col_blocks=hcb,
+                                         medium_spans=None if a.medium is None else a.medium == "on",
+                                         giant_threshold=a.giant_threshold)
             src = op.new_panel(d)
             src[: op.rows].copy_(x[op.r0:op.r1])
             src[op.rows:].uniform_(-1, 1)
             dst = op.new_panel(d)
             times = {}
             G = op.n_groups            # op._A[G] is the ghost rows' launch (into dst's halo)
+            if a.quick:
+                for _ in range(2):
+                    op.compute(src, dst)
+                ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * a.reps)]
+                for r in range(a.reps):
+                    ev[2 * r].record()
+                    op.compute(src, dst)
+                    ev[2 * r + 1].record()
+                torch.cuda.synchronize()
+                ms = sorted(ev[2 * r].elapsed_time(ev[2 * r + 1]) for r in range(a.reps))
+                ranks.append({"rank": q, "rows": op.rows, "nnz": op.nnz_local, "hub_rows": op.views[op.C][1],
+                              "ms_compute": ms[len(ms) // 2]})
+                print(f"  P={P} rank {q}: compute {ms[len(ms) // 2]:.3f} ms", file=sys.stderr, flush=True)
+                del op, src, dst
+                torch.cuda.empty_cache()
+                continue
             for name, groups in (("all", range(G + 1)), ("hub", [op.C]), ("chunks", list(range(op.C)) + [G]),
                                  ("ghosts", [G])):
                 ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * a.reps)]
@@ -170,6 +193,12 @@ def main():
                   f"compute {times['compute']:.3f} ms", file=sys.stderr, flush=True)
             del op, src, dst
             torch.cuda.empty_cache()
+        if a.quick:
+            key = f"{P}"
+            out["worlds"][key] = {"ranks": ranks, "max_hop_compute_ms": max(r["ms_compute"] for r in ranks)}
+            print(f"P={P}: hop compute {out['worlds'][key]['max_hop_compute_ms']:.3f} ms (max over ranks)",
+                  file=sys.stderr, flush=True)
+            continue
         worst = max(ranks, key=lambda r: max(r["ms_hub"], r["ms_chunks"]))
         key = (f"{P}" if a.ghost == "auto" else f"{P}/ghost{ghost}") + ("" if cb is None else f"/cb{cb}") + \
             ("" if hcb is None else f"/hcb{hcb}")
