@@ -89,6 +89,12 @@ extern "C" {
  * HBM beside the chunks, not by the top row's chain -- 1.09-1.11 ms per hop against 1.05-1.08
  * exact), so no default path sets it. */
 #define SRG_SPMM_FAST 0x40u
+/* Hub workgroups of 4 producer waves + the consumer (256-nonzero windows) instead of 8 + 1: the same
+ * gathers in flight with 5 waves instead of 9 (134 VGPRs instead of 92 per wave, 680 instead of 864
+ * VGPR-waves per workgroup), so launches beside hundreds of hub workgroups keep more of each CU.
+ * SRGNN_HUB_PRODUCERS=4 selects it for every launch with more hub workgroups than CUs.  Results are
+ * identical either way. */
+#define SRG_SPMM_HUB_LITE 0x100u
 
 /* =============================================================================================
  * (A) drop-in entry points

@@ -762,9 +762,9 @@ constexpr int kHubThreads = 64 * (kHubProducers + 1);
 // both the producers' transposed ds_write_b32 (lanes: 4 nonzeros x 8 column chunks) and the
 // consumer's ds_read_b128 (lanes: 32 columns, 16-lane groups) are bank-conflict-free (exhaustive
 // check over all window offsets; the 4 (mod 64) stride of the first version made the reads 2-way)
-template <int W>
+template <int W, int NP = kHubProducers>
 struct HubGeom {
-    static constexpr int UW = W / (kHubProducers * 8);       // gathers per producer lane per window
+    static constexpr int UW = W / (NP * 8);                  // gathers per producer lane per window
     static constexpr int LD = W + 16;
     static constexpr int TILE = kSliceCols * LD;             // floats per tile
     static constexpr size_t LDS_BYTES = (size_t)(2 * TILE + 2 * W) * sizeof(float);
@@ -814,8 +814,11 @@ __device__ __forceinline__ void hub_links16(float& acc, const typename Vec<float
 // chains; 2 = the producers skip gathers and LDS writes; 3 = the consumer's fmas read registers
 // only (no LDS reads); 4 = producers gather but skip the LDS writes; 5 / 6 = the consumer reads
 // only the tile / only the values from LDS.
-template <bool SFULL, typename IP, int ABL = 0, int EX = kEpiPlain, int W = kHubW>
-__global__ void __launch_bounds__(kHubThreads)
+// NP producer waves (8 by default; 4 -- the "lite" workgroup of the halo path's hub groups, 5 waves
+// instead of 9 -- keeps the same gathers in flight with half the waves and registers, so the row
+// chunks running beside hundreds of hub workgroups keep more of each CU)
+template <bool SFULL, typename IP, int ABL = 0, int EX = kEpiPlain, int W = kHubW, int NP = kHubProducers>
+__global__ void __launch_bounds__(64 * (NP + 1))
 k_spmm_hub(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
            const float* __restrict__ vals, const int32_t* __restrict__ hub_rows, int n_slices,
            const float* __restrict__ X, int64_t ldx, float* __restrict__ Y, int64_t ldy, int d,
@@ -823,8 +826,8 @@ k_spmm_hub(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
 {
     typedef typename Vec<float, 4>::type V4;
     extern __shared__ __attribute__((aligned(16))) float hub_lds[];
-    // [2 tiles][32 columns][HubGeom<W>::LD] then [2][W] values
-    float* aval_base = hub_lds + 2 * HubGeom<W>::TILE;
+    // [2 tiles][32 columns][HubGeom<W, NP>::LD] then [2][W] values
+    float* aval_base = hub_lds + 2 * HubGeom<W, NP>::TILE;
     const int item = blockIdx.x;
     const int row = hub_rows[item / n_slices];
     const int slice = item % n_slices;
@@ -851,7 +854,7 @@ k_spmm_hub(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
         for (int h = 0; h < n_win; ++h) {
             __syncthreads();                      // window h is in tile h & 1
             if (lane < kSliceCols) {
-                const float* tcol = hub_lds + (h & 1) * HubGeom<W>::TILE + c * HubGeom<W>::LD;
+                const float* tcol = hub_lds + (h & 1) * HubGeom<W, NP>::TILE + c * HubGeom<W, NP>::LD;
                 const float* av = aval_base + (h & 1) * W;
                 const int64_t sb = beg + (int64_t)h * W;
                 const int nb = (end - sb) < W ? (int)(end - sb) : W;
@@ -886,7 +889,7 @@ k_spmm_hub(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
                     constexpr int NK = W / 16;
                     const float* tb[8];
 #pragma unroll
-                    for (int k = 0; k < 8; ++k) tb[k] = hub_lds + (h & 1) * HubGeom<W>::TILE + c * HubGeom<W>::LD + ((k ^ sw) << 2);
+                    for (int k = 0; k < 8; ++k) tb[k] = hub_lds + (h & 1) * HubGeom<W, NP>::TILE + c * HubGeom<W, NP>::LD + ((k ^ sw) << 2);
                     const float* avl = av + 4 * (lane & 3);
                     auto rt = [&](int grp) { return *reinterpret_cast<const V4*>(tb[grp & 7] + (grp >> 3) * 32); };
                     auto rv = [&](int k) { return *reinterpret_cast<const V4*>(avl + 16 * k); };
@@ -924,7 +927,7 @@ k_spmm_hub(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
                     constexpr int NG = W / 4;
                     const float* tb[8];
 #pragma unroll
-                    for (int k = 0; k < 8; ++k) tb[k] = hub_lds + (h & 1) * HubGeom<W>::TILE + c * HubGeom<W>::LD + ((k ^ sw) << 2);
+                    for (int k = 0; k < 8; ++k) tb[k] = hub_lds + (h & 1) * HubGeom<W, NP>::TILE + c * HubGeom<W, NP>::LD + ((k ^ sw) << 2);
                     auto rt = [&](int grp) { return *reinterpret_cast<const V4*>(tb[grp & 7] + (grp >> 3) * 32); };
                     auto ra = [&](int grp) { return *reinterpret_cast<const V4*>(av + (grp << 2)); };
                     V4 t[kHubL], a[kHubL];
@@ -1017,38 +1020,38 @@ k_spmm_hub(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
     const int qq = lane & 7;          // 16-byte chunk = columns qq*4 .. qq*4+3 of the slice
     const int qcol = slice * kSliceCols + qq * 4;
     const bool gact = SFULL || qcol < d;
-    V4 x0[HubGeom<W>::UW], x1[HubGeom<W>::UW];        // gathered windows, two register sets (even / odd windows)
-    float a0[HubGeom<W>::UW], a1[HubGeom<W>::UW];
-    int cn[HubGeom<W>::UW];                   // column ids / values of the next window to gather
-    float an[HubGeom<W>::UW];
+    V4 x0[HubGeom<W, NP>::UW], x1[HubGeom<W, NP>::UW];        // gathered windows, two register sets (even / odd windows)
+    float a0[HubGeom<W, NP>::UW], a1[HubGeom<W, NP>::UW];
+    int cn[HubGeom<W, NP>::UW];                   // column ids / values of the next window to gather
+    float an[HubGeom<W, NP>::UW];
     auto load_ids = [&](int w) {
         const int64_t sb = beg + (int64_t)w * W;
 #pragma unroll
-        for (int b = 0; b < HubGeom<W>::UW; ++b) {
-            int64_t jj = sb + (p * HubGeom<W>::UW + b) * 8 + g;
+        for (int b = 0; b < HubGeom<W, NP>::UW; ++b) {
+            int64_t jj = sb + (p * HubGeom<W, NP>::UW + b) * 8 + g;
             jj = jj < end ? jj : end - 1;
             cn[b] = indices[jj];
             an[b] = vals[jj];
         }
     };
-    auto gather = [&](V4 (&x)[HubGeom<W>::UW], float (&a)[HubGeom<W>::UW]) {
+    auto gather = [&](V4 (&x)[HubGeom<W, NP>::UW], float (&a)[HubGeom<W, NP>::UW]) {
 #pragma unroll
-        for (int b = 0; b < HubGeom<W>::UW; ++b) {
+        for (int b = 0; b < HubGeom<W, NP>::UW; ++b) {
             x[b] = (gact && ABL != 2) ? gload<float, 4>(X + (int64_t)cn[b] * ldx + qcol) : vzero<float, 4>();
             a[b] = an[b];
         }
     };
-    auto put = [&](int w, const V4 (&x)[HubGeom<W>::UW], const float (&a)[HubGeom<W>::UW]) {
+    auto put = [&](int w, const V4 (&x)[HubGeom<W, NP>::UW], const float (&a)[HubGeom<W, NP>::UW]) {
         if (ABL == 2 || ABL == 4) return;
-        float* tile = hub_lds + (w & 1) * HubGeom<W>::TILE;
+        float* tile = hub_lds + (w & 1) * HubGeom<W, NP>::TILE;
         float* av = aval_base + (w & 1) * W;
 #pragma unroll
-        for (int b = 0; b < HubGeom<W>::UW; ++b) {
-            const int nl = (p * HubGeom<W>::UW + b) * 8 + g;   // nonzero within the window
+        for (int b = 0; b < HubGeom<W, NP>::UW; ++b) {
+            const int nl = (p * HubGeom<W, NP>::UW + b) * 8 + g;   // nonzero within the window
 #pragma unroll
             for (int i = 0; i < 4; ++i) {             // transposed, swizzled: conflict-free
                 const int cc = qq * 4 + i;
-                tile[cc * HubGeom<W>::LD + ((((nl >> 2) ^ hub_swz(cc)) << 2) | (nl & 3))] = x[b][i];
+                tile[cc * HubGeom<W, NP>::LD + ((((nl >> 2) ^ hub_swz(cc)) << 2) | (nl & 3))] = x[b][i];
             }
             if (qq == 0) av[nl] = a[b];
         }
@@ -1520,6 +1523,13 @@ int packed_u_setting()
     return v;
 }
 
+// producer waves of the wide hub launches' workgroups: 8, or 4 (SRGNN_HUB_PRODUCERS)
+int hub_producers()
+{
+    static const int np = [] { const char* e = getenv("SRGNN_HUB_PRODUCERS"); return (e && atoi(e) == 4) ? 4 : 8; }();
+    return np;
+}
+
 int hub_delay_us()
 {
     static const int us = [] { const char* e = getenv("SRGNN_HUB_DISPATCH_DELAY_US"); return e ? atoi(e) : 10; }();
@@ -1563,6 +1573,11 @@ int hub_attrs()
                            (const void*)k_spmm_hub<true, IP, 0, kEpiCheby, 256>, (const void*)k_spmm_hub<false, IP, 0, kEpiCheby, 256>,
                            (const void*)k_spmm_hub<true, IP, 0, kEpiSpan, 256>, (const void*)k_spmm_hub<false, IP, 0, kEpiSpan, 256>})
         SRG_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)HubGeom<256>::LDS_BYTES));
+    for (const void* fn : {(const void*)k_spmm_hub<true, IP, 0, false, 256, 4>, (const void*)k_spmm_hub<false, IP, 0, false, 256, 4>,
+                           (const void*)k_spmm_hub<true, IP, 0, kEpiSend, 256, 4>, (const void*)k_spmm_hub<false, IP, 0, kEpiSend, 256, 4>,
+                           (const void*)k_spmm_hub<true, IP, 0, kEpiCheby, 256, 4>, (const void*)k_spmm_hub<false, IP, 0, kEpiCheby, 256, 4>,
+                           (const void*)k_spmm_hub<true, IP, 0, kEpiSpan, 256, 4>, (const void*)k_spmm_hub<false, IP, 0, kEpiSpan, 256, 4>})
+        SRG_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)HubGeom<256, 4>::LDS_BYTES));
     return SRG_OK;
 }
 
@@ -1774,16 +1789,20 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
         } else {
             static const int wide_env = [] { const char* e = getenv("SRGNN_HUB_WIDE_LAUNCH"); return e ? atoi(e) : -1; }();
             const int64_t wide = wide_env >= 0 ? wide_env : kHubWideLaunch;
-            const bool w256 = n_hub * n_slices > wide || (flags & SRG_SPMM_HUB_W256);
-#define SRG_LAUNCH_HUB(SF, WW)                                                                             \
-    hipLaunchKernelGGL((k_spmm_hub<SF, IP, 0, EX, WW>), hgrid, dim3(kHubThreads), HubGeom<WW>::LDS_BYTES, \
+            const bool w256 = n_hub * n_slices > wide || (flags & (SRG_SPMM_HUB_W256 | SRG_SPMM_HUB_LITE));
+            // the wide launches (more hub workgroups than CUs) may take the 4-producer workgroup
+            const bool lite = (w256 && hub_producers() == 4) || (flags & SRG_SPMM_HUB_LITE);
+#define SRG_LAUNCH_HUB(SF, WW, NPP)                                                                                 \
+    hipLaunchKernelGGL((k_spmm_hub<SF, IP, 0, EX, WW, NPP>), hgrid, dim3(64 * (NPP + 1)), (HubGeom<WW, NPP>::LDS_BYTES), \
                        ss->stream, indptr, indices, vals, order, n_slices, X, ldx, Y, ldy, d, acc, nt, epi)
             if (sfull) {
-                if (w256) SRG_LAUNCH_HUB(true, 256);
-                else SRG_LAUNCH_HUB(true, 512);
+                if (lite) SRG_LAUNCH_HUB(true, 256, 4);
+                else if (w256) SRG_LAUNCH_HUB(true, 256, 8);
+                else SRG_LAUNCH_HUB(true, 512, 8);
             } else {
-                if (w256) SRG_LAUNCH_HUB(false, 256);
-                else SRG_LAUNCH_HUB(false, 512);
+                if (lite) SRG_LAUNCH_HUB(false, 256, 4);
+                else if (w256) SRG_LAUNCH_HUB(false, 256, 8);
+                else SRG_LAUNCH_HUB(false, 512, 8);
             }
 #undef SRG_LAUNCH_HUB
         }

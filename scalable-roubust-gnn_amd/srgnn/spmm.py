@@ -257,14 +257,15 @@ def _check_panel(X: torch.Tensor, rows: int, name: str, d=None):
 def spmm(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor | None = None, accumulate: bool = False,
          nt_store: bool = False, wide_rows: bool = False, hub_w256: bool = False,
          hub_nojoin: bool = False, packed_u2: bool = False, fast: bool = False,
-         hub_continue: bool = False) -> torch.Tensor:
+         hub_continue: bool = False, hub_lite: bool = False) -> torch.Tensor:
     """out[r, :] (+)= A[r, :] @ X  for the rows of A (one hop; exact fma chains in CSR order).
     fast: tolerance mode (SRG_SPMM_FAST): A's hub rows are summed as 64 exact segment chains whose
     partial sums are then added in order -- deterministic, within fp32 re-association error of the
     exact chain, ~64x shorter latency for the longest rows; every other row stays bit-exact.
     wide_rows: diagnostic, one row per wave for every light row (no narrow or packed rows);
     hub_w256: diagnostic, 256-nonzero
-    hub windows for any hub launch (same results either way).  hub_nojoin: A's hub rows are left
+    hub windows for any hub launch (same results either way); hub_lite: 4-producer hub workgroups
+    (SRG_SPMM_HUB_LITE, same results).  hub_nojoin: A's hub rows are left
     running on the library's side stream; the caller must make a stream wait for them
     (srg_hub_join) before reading them.  hub_continue (with hub_nojoin, after an unjoined fork):
     the hub rows are appended to the side stream without a new fork (SRG_SPMM_HUB_CONTINUE)."""
@@ -283,7 +284,8 @@ def spmm(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor | None = None, accumul
     flags = (_lib.SRG_SPMM_ACCUMULATE if accumulate else 0) | (_lib.SRG_SPMM_NT_STORE if nt_store else 0) | \
         (_lib.SRG_SPMM_WIDE_ROWS if wide_rows else 0) | (_lib.SRG_SPMM_HUB_W256 if hub_w256 else 0) | \
         (_lib.SRG_SPMM_HUB_NOJOIN if hub_nojoin else 0) | (_lib.SRG_SPMM_PACKED_U2 if packed_u2 else 0) | \
-        (_lib.SRG_SPMM_FAST if fast else 0) | (_lib.SRG_SPMM_HUB_CONTINUE if hub_continue else 0)
+        (_lib.SRG_SPMM_FAST if fast else 0) | (_lib.SRG_SPMM_HUB_CONTINUE if hub_continue else 0) | \
+        (_lib.SRG_SPMM_HUB_LITE if hub_lite else 0)
     if A.is_span:
         _span_call(A, X, out, d, flags, None, 0, 0.0, False)
         return out

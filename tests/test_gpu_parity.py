@@ -701,7 +701,8 @@ def test_halo_whole_x_hop0_gather(world, ghost):
 @pytest.mark.parametrize("name", ["rand_d128_r05", "rand_d36_ppr", "cora_sym_k3"])
 def test_hub_window_256_bit_exact(name, oracle_mod):
     """Hub workgroups with 256-nonzero windows (two per CU; the default once a launch has more hub
-    workgroups than CUs) and with 512: every row a hub row, both bit-identical to the reference."""
+    workgroups than CUs), with 512, and the 4-producer "lite" workgroup (SRG_SPMM_HUB_LITE): every
+    row a hub row, all bit-identical to the reference."""
     from srgnn.spmm import spmm
     c = G.Case(name)
     A = _csr(c, (0, 0))
@@ -713,8 +714,8 @@ def test_hub_window_256_bit_exact(name, oracle_mod):
         x = np.ascontiguousarray(x[:, : x.shape[1] // 4 * 4])
         want = oracle_mod.spmm(*c.ahat(), x)
     X = torch.from_numpy(x).cuda()
-    for w256 in (True, False):
-        y = spmm(A, X, hub_w256=w256)
+    for w256, lite in ((True, False), (False, False), (False, True)):
+        y = spmm(A, X, hub_w256=w256, hub_lite=lite)
         if x.shape[1] != c.x().shape[1]:
             np.testing.assert_array_equal(y.cpu().numpy(), want)
         else:
@@ -729,8 +730,8 @@ def test_hub_window_256_bit_exact(name, oracle_mod):
     x = rng.standard_normal((3000, 64)).astype(np.float32)
     B = DeviceCSR.from_tensors(ip, ix, vv, n_cols=3000, heavy_threshold=0, hub_threshold=0, device="cuda")
     want = None
-    for w256 in (True, False):
-        y = spmm(B, torch.from_numpy(x).cuda(), hub_w256=w256).cpu().numpy()
+    for w256, lite in ((True, False), (False, False), (False, True)):
+        y = spmm(B, torch.from_numpy(x).cuda(), hub_w256=w256, hub_lite=lite).cpu().numpy()
         want = y if want is None else want
         assert np.array_equal(y, want)
     assert np.array_equal(want, oracle_mod.spmm(ip, ix, vv, x))
