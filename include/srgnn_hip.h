@@ -347,6 +347,15 @@ int srg_hub_side_streams(void);
 int srg_csr_col_splits(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t n_cols,
                        int32_t n_blocks, int64_t* splits, void* stream);
 
+/* Span copy (the compact column blocks of srgnn.csr.DeviceCSR: a launch's entries laid out in the
+ * order it takes its rows): for i < n_order, row r = order[i] has its span [beg[r], end[r]) of
+ * indices / values copied to [pos[i], pos[i] + end[r] - beg[r]) of out_indices / out_values, and
+ * out_beg[r] / out_end[r] set to that range (pos: the exclusive prefix sum of the spans' lengths in
+ * `order`; rows not in `order` keep their out_beg / out_end).  Asynchronous on `stream`. */
+int srg_csr_copy_spans(const int32_t* order, int64_t n_order, const int64_t* beg, const int64_t* end,
+                       const int32_t* indices, const float* values, const int64_t* pos, int32_t* out_indices,
+                       float* out_values, int64_t* out_beg, int64_t* out_end, void* stream);
+
 /* Mirror positions (device construct_adj, srgnn/construct.py; SSRG/operators/utils.py:91 transposes
  * A+I): for a CSR whose rows hold strictly increasing column ids, mirror[e] = the position of entry
  * (c, r) in row c for entry e = (r, c) (rows[e] = r, int64 [nnz]), or -1 when row c has no column r.

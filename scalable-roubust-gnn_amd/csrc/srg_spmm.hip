@@ -1427,6 +1427,32 @@ k_col_splits(const int64_t* __restrict__ indptr, const int32_t* __restrict__ ind
     splits[t] = lo;
 }
 
+// Span copy (DeviceCSR compact copies: the entries of a launch laid out in the order it takes its
+// rows): row order[i]'s span [beg, end) of (indices, values) goes to [pos[i], pos[i] + len) of the
+// output arrays, and out_beg / out_end of that row get the new span.  16 lanes per row, each lane
+// copying every 16th entry (coalesced runs of the row); 4 rows per wave, a grid stride over rows.
+__global__ void __launch_bounds__(256)
+k_copy_spans(const int32_t* __restrict__ order, int64_t n, const int64_t* __restrict__ beg,
+             const int64_t* __restrict__ end, const int32_t* __restrict__ ix, const float* __restrict__ v,
+             const int64_t* __restrict__ pos, int32_t* __restrict__ oix, float* __restrict__ ov,
+             int64_t* __restrict__ obeg, int64_t* __restrict__ oend)
+{
+    const int l = threadIdx.x & 15;
+    const int64_t stride = (int64_t)gridDim.x * (blockDim.x / 16);
+    for (int64_t i = (int64_t)blockIdx.x * (blockDim.x / 16) + (threadIdx.x >> 4); i < n; i += stride) {
+        const int r = order[i];
+        const int64_t b = beg[r], len = end[r] - b, p = pos[i];
+        for (int64_t e = l; e < len; e += 16) {
+            oix[p + e] = ix[b + e];
+            ov[p + e] = v[b + e];
+        }
+        if (l == 0) {
+            obeg[r] = p;
+            oend[r] = p + len;
+        }
+    }
+}
+
 // Mirror positions of a CSR with sorted rows: mirror[e] = the position of entry (c, r) in row c for
 // entry e = (r, c), or -1 when row c holds no column r (one binary search per entry).  All entries
 // found <=> the structure is symmetric, and then the transpose of the matrix is the same structure
@@ -2558,6 +2584,23 @@ int srg_csr_col_splits(const int64_t* indptr, const int32_t* indices, int64_t n_
     if ((work + 255) / 256 > INT32_MAX) return fail(SRG_ERR_INVALID, "grid too large");
     hipLaunchKernelGGL(k_col_splits, dim3((unsigned)((work + 255) / 256)), dim3(256), 0,
                        static_cast<hipStream_t>(stream), indptr, indices, n_rows, n_cols, (int)n_blocks, splits);
+    SRG_HIP_CHECK(hipGetLastError());
+    return ok();
+}
+
+int srg_csr_copy_spans(const int32_t* order, int64_t n_order, const int64_t* beg, const int64_t* end,
+                       const int32_t* indices, const float* values, const int64_t* pos, int32_t* out_indices,
+                       float* out_values, int64_t* out_beg, int64_t* out_end, void* stream)
+{
+    SRG_DEVICE_GUARD(stream);
+    if (n_order < 0) return fail(SRG_ERR_INVALID, "n_order=%lld < 0", (long long)n_order);
+    if (n_order == 0) return ok();
+    if (!order || !beg || !end || !pos || !out_beg || !out_end)
+        return fail(SRG_ERR_INVALID, "null order / span / position array");
+    const int64_t rows_per_block = 256 / 16;
+    const unsigned blocks = (unsigned)std::min<int64_t>((n_order + rows_per_block - 1) / rows_per_block, 1 << 20);
+    hipLaunchKernelGGL(k_copy_spans, dim3(blocks), dim3(256), 0, static_cast<hipStream_t>(stream), order, n_order,
+                       beg, end, indices, values, pos, out_indices, out_values, out_beg, out_end);
     SRG_HIP_CHECK(hipGetLastError());
     return ok();
 }

@@ -85,6 +85,7 @@ EXPORTED_SYMBOLS = (
     "srg_hub_join",
     "srg_hub_side_streams",
     "srg_csr_col_splits",
+    "srg_csr_copy_spans",
     "srg_csr_mirror",
     "srg_csr_validate",
     "srg_comm_unique_id",
@@ -195,6 +196,8 @@ def _declare(lib):
     lib.srg_comm_size.restype = ctypes.c_int
     lib.srg_dist_propagate_khop_f32.argtypes = [_p, _p, ctypes.c_int, _p, _i64, _i32, _i32]
     lib.srg_dist_propagate_khop_f32.restype = ctypes.c_int
+    lib.srg_csr_copy_spans.argtypes = [_p, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p]
+    lib.srg_csr_copy_spans.restype = ctypes.c_int
     lib.srg_spmm_span_rowacc_f32.argtypes = [_p, _p, _p, _p, _p, _i64, _p, _i64, _p, _i64, _p, _i64, _i32, _u32, _p]
     lib.srg_spmm_span_rowacc_f32.restype = ctypes.c_int
     lib.srg_halo_plan_build.argtypes = [_p, _p, _i64, _i32, _i32, _i32, _i64, _i64, _i32, ctypes.POINTER(_p)]

@@ -263,20 +263,30 @@ class DeviceCSR:
         """(beg, end, indices, values): the entries of `rows` (int64 row ids) copied out one row after
         the other in that order, row r's at [beg[r], end[r]) of the copies (rows not listed: empty)."""
         ip = self.indptr
+        dev = ip.device
         b0 = ip[rows]
         deg = (self.row_end[rows] if self.is_span else ip[rows + 1]) - b0
-        pos = torch.zeros(rows.numel() + 1, dtype=torch.int64, device=ip.device)
+        pos = torch.zeros(rows.numel() + 1, dtype=torch.int64, device=dev)
         torch.cumsum(deg, 0, out=pos[1:])
         nnz = int(pos[-1].item())
-        # entry e of the copy is entry b0[i] + (e - pos[i]) of row i of the list
-        idx = torch.repeat_interleave(b0 - pos[:-1], deg, output_size=nnz)
-        idx += torch.arange(nnz, dtype=torch.int64, device=ip.device)
-        beg = torch.zeros(self.out_rows, dtype=torch.int64, device=ip.device)
-        end = torch.zeros(self.out_rows, dtype=torch.int64, device=ip.device)
-        beg[rows] = pos[:-1]
-        end[rows] = pos[1:]
-        ix, v = self.indices[idx], self.values[idx]
-        del idx
+        beg = torch.zeros(self.out_rows, dtype=torch.int64, device=dev)
+        end = torch.zeros(self.out_rows, dtype=torch.int64, device=dev)
+        if self.indices.dtype != torch.int32 or self.values.dtype != torch.float32:
+            # entry e of the copy is entry b0[i] + (e - pos[i]) of row i of the list
+            idx = torch.repeat_interleave(b0 - pos[:-1], deg, output_size=nnz)
+            idx += torch.arange(nnz, dtype=torch.int64, device=dev)
+            beg[rows] = pos[:-1]
+            end[rows] = pos[1:]
+            return beg, end, self.indices[idx], self.values[idx]
+        ix = torch.empty(nnz, dtype=self.indices.dtype, device=dev)
+        v = torch.empty(nnz, dtype=self.values.dtype, device=dev)
+        # srg_csr_copy_spans: one pass over the spans (the torch formulation, an int64 gather index of
+        # nnz entries built with repeat_interleave, took 4.6 ms more on products' six blocks)
+        order = rows.to(torch.int32).contiguous()
+        row_end = self.row_end if self.is_span else ip[1:]
+        _lib.call(dev, "srg_csr_copy_spans", order.data_ptr(), order.numel(), ip.data_ptr(), row_end.data_ptr(),
+                  self.indices.data_ptr(), self.values.data_ptr(), pos.data_ptr(), ix.data_ptr(), v.data_ptr(),
+                  beg.data_ptr(), end.data_ptr(), _lib.stream(dev))
         return beg, end, ix, v
 
     def schedule_ordered(self) -> "DeviceCSR":
