@@ -273,6 +273,12 @@ constexpr int kSliceCols = 32;
 #define SRG_SLICE_LDS_BUFS 1
 #endif
 constexpr int kSliceLdsBufs = SRG_SLICE_LDS_BUFS;
+// packed light rows of span launches stage a wave's consecutive entries in its LDS slot (packed_rows);
+// -DSRG_STAGE_ENTRIES=0 builds the unstaged loop (A/B)
+#ifndef SRG_STAGE_ENTRIES
+#define SRG_STAGE_ENTRIES 1
+#endif
+constexpr bool kStageEntries = SRG_STAGE_ENTRIES != 0;
 
 // Epilogues of the SpMM kernels (every output element y a kernel stores may also go to):
 //  * fused hop aggregation (srgnn.aggregate): with agg != nullptr it is folded into the accumulator
@@ -569,7 +575,7 @@ __device__ __forceinline__ void packed_rows(const IP* __restrict__ indptr, const
                                             const float* __restrict__ vals, const int32_t* __restrict__ order,
                                             int n_rows, int first, const float* __restrict__ X, int64_t ldx,
                                             float* __restrict__ Y, int64_t ldy, int accumulate, int nt,
-                                            const Epi& epi)
+                                            const Epi& epi, float* __restrict__ wlds)
 {
     typedef typename Vec<float, 4>::type V4;
     constexpr int S = 64 / LR;
@@ -601,6 +607,40 @@ __device__ __forceinline__ void packed_rows(const IP* __restrict__ indptr, const
         maxlen = o > maxlen ? o : maxlen;
     }
     maxlen = __builtin_amdgcn_readfirstlane(maxlen);
+    // Staged entry stream (span launches with slot spans, kStageEntries): when the wave's rows are
+    // consecutive in the entry arrays -- a compact copy laid out in launch order -- and hold at most
+    // 128 entries in all, the wave loads them with two coalesced loads into its LDS slot and the
+    // rows' chains then read their (column id, value) pairs from LDS (16-lane broadcast) instead of
+    // issuing a dependent global load per gather round.  Same entries, same order: same bits.
+    [[maybe_unused]] int spos = 0;     // the row's first entry in the staged stream
+    [[maybe_unused]] bool staged = false;
+    if constexpr (kIsSpan<EX> && kStageEntries) {
+        if (epi.slot_beg) {
+            // prefix of the row lengths over the wave's row groups (entry g * S holds row g's length)
+            int pre = 0, tot = 0;
+#pragma unroll
+            for (int h = 0; h < LR; ++h) {
+                const int lh = __shfl(len, h * S);
+                pre += h < g ? lh : 0;
+                tot += lh;
+            }
+            const int64_t w0 = epi.slot_beg[first];             // wave-uniform: the first row's span start
+            const bool contig = !rv || beg == w0 + pre;
+            staged = tot <= 128 && __all(contig);
+            if (staged) {
+                spos = pre;
+                int* sid = reinterpret_cast<int*>(wlds);
+                float* sva = wlds + 128;
+                for (int q = lane; q < tot; q += 64) {
+                    sid[q] = indices[w0 + q];
+                    sva[q] = vals[w0 + q];
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+        }
+    }
     float* __restrict__ yrow = Y + (int64_t)row * ldy;
     if constexpr (EX == kEpiSpanRA) accumulate = rv && beg != epi.row_first[row];
     // the Chebyshev epilogue never aggregates nor accumulates (its entry rejects both): dropping
@@ -619,12 +659,22 @@ __device__ __forceinline__ void packed_rows(const IP* __restrict__ indptr, const
     for (int j = 0; j < maxlen; j += U) {
         int cv[U];
         float av[U];
+        if (staged) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const bool ok = j + u < len;
-            const int64_t p = beg + (ok ? j + u : 0);
-            cv[u] = ok ? indices[p] : 0;
-            av[u] = ok ? vals[p] : 0.0f;
+            for (int u = 0; u < U; ++u) {
+                const bool ok = j + u < len;
+                const int q = spos + (ok ? j + u : 0);
+                cv[u] = ok ? reinterpret_cast<const int*>(wlds)[q] : 0;
+                av[u] = ok ? wlds[128 + q] : 0.0f;
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const bool ok = j + u < len;
+                const int64_t p = beg + (ok ? j + u : 0);
+                cv[u] = ok ? indices[p] : 0;
+                av[u] = ok ? vals[p] : 0.0f;
+            }
         }
         __builtin_amdgcn_sched_barrier(0);   // every id load ahead of the first gather
         V4 x[U][LQ];
@@ -691,7 +741,8 @@ k_spmm(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
     if constexpr (LR > 0) {   // wide panel: LR light rows per wave
         const int first = __builtin_amdgcn_readfirstlane((bid - nb_heavy) * kWavesPerBlock + wib) * LR + n_heavy;
         if (first >= n_rows) return;
-        packed_rows<LR, LQ, U, IP, EX>(indptr, indices, vals, order, n_rows, first, X, ldx, Y, ldy, accumulate, nt, epi);
+        packed_rows<LR, LQ, U, IP, EX>(indptr, indices, vals, order, n_rows, first, X, ldx, Y, ldy, accumulate, nt, epi,
+                                       lds + wib * kSliceLdsBufs * 256);
         return;
     }
     if constexpr (NS > 0) {   // narrow panel: 64 / NS light rows per wave

@@ -21,8 +21,11 @@ def main():
     ap.add_argument("dir")
     ap.add_argument("counter")
     ap.add_argument("--per", default="hub")
+    ap.add_argument("--cycle", type=int, default=0,
+                    help="also average the k_spmm dispatches by position in a cycle of this many (one hop's "
+                         "launches, in dispatch order)")
     a = ap.parse_args()
-    vals, disp = {}, {}
+    vals, disp, spmm = {}, {}, {}
     for f in glob.glob(os.path.join(a.dir, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for r in csv.DictReader(fh):
@@ -31,9 +34,16 @@ def main():
                 k = short(r.get("Kernel_Name", ""))
                 vals[k] = vals.get(k, 0.0) + float(r["Counter_Value"])
                 disp.setdefault(k, set()).add((f, r.get("Dispatch_Id")))
+                if k == "spmm":
+                    key = (f, int(r.get("Dispatch_Id", 0)))
+                    spmm[key] = spmm.get(key, 0.0) + float(r["Counter_Value"])
     n = len(disp.get(a.per, ())) or 1
     out = {"counter": a.counter, "per": a.per, "units": n,
            "families": {k: {"total": v, "dispatches": len(disp[k]), "per_unit": v / n} for k, v in vals.items()}}
+    if a.cycle > 0 and spmm:
+        seq = [v for _, v in sorted(spmm.items())]
+        seq = seq[len(seq) % a.cycle:]                      # whole cycles, the last ones
+        out["spmm_by_position"] = [sum(seq[i::a.cycle]) / max(1, len(seq[i::a.cycle])) for i in range(a.cycle)]
     print(json.dumps(out))
 
 
