@@ -273,10 +273,11 @@ constexpr int kSliceCols = 32;
 #define SRG_SLICE_LDS_BUFS 1
 #endif
 constexpr int kSliceLdsBufs = SRG_SLICE_LDS_BUFS;
-// packed light rows of span launches stage a wave's consecutive entries in its LDS slot (packed_rows);
-// -DSRG_STAGE_ENTRIES=0 builds the unstaged loop (A/B)
+// -DSRG_STAGE_ENTRIES=1: packed light rows of span launches stage a wave's consecutive entries in its
+// LDS slot (packed_rows).  Off by default: on products it measured 5.96 ms per hop and 34.7 GB of
+// traffic against 5.85 ms and 32.6 GB unstaged (profiles/r04h_stage_entries_negative.txt)
 #ifndef SRG_STAGE_ENTRIES
-#define SRG_STAGE_ENTRIES 1
+#define SRG_STAGE_ENTRIES 0
 #endif
 constexpr bool kStageEntries = SRG_STAGE_ENTRIES != 0;
 

@@ -56,10 +56,11 @@ def _split_block0(A: DeviceCSR, d: int) -> bool:
 # tools/probes/colblock_build_time.py; 21 ms when the blocks were copies of the ids and values):
 # it is cut for a run of at least this many hops, or when its blocks already exist.
 MIN_HOPS_TO_CUT = 4
-# Runs of this many hops copy the blocks' spans into compact arrays (DeviceCSR.compact_column_blocks:
-# 1 % less traffic per hop for one more copy of the ids and values, ~3 ms on products), when the
-# copy fits in a quarter of the free memory.
-MIN_HOPS_TO_COMPACT = 48
+# Runs of this many hops copy the blocks' spans into compact arrays (DeviceCSR.compact_column_blocks,
+# the srg_csr_copy_spans kernel), when the copy fits in a quarter of the free memory.  Products, K = 10
+# (profiles/r04h_one_shot_products.json): the layout costs 4.6 ms more and each hop 0.40 ms less
+# (6.09 against 6.49 ms), so the copy pays after ~12 hops.
+MIN_HOPS_TO_COMPACT = 16
 _COMPACT = os.environ.get("SRGNN_COMPACT_BLOCKS", "1") != "0"     # 0: spans only (A/B)
 
 
