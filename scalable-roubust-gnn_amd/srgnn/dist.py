@@ -253,8 +253,14 @@ def ghost_plan(halos, elig, deg, owner, gip, starts, caps=GHOST_CAPS, link_bps=N
 
 
 # column blocks per row-chunk launch of the halo path for large local panels (1 = off);
-# SRGNN_HALO_COL_BLOCKS overrides.  Bitwise the same hops either way.
-AUTO_HALO_COL_BLOCKS = int(os.environ.get("SRGNN_HALO_COL_BLOCKS", "1"))
+# SRGNN_HALO_COL_BLOCKS overrides.  Bitwise the same hops either way.  Default: 8 for local panels of
+# >= 8 GiB at d >= 256 (RMAT-26 at P = 8, 23.8 GB of [own | halo] rows of 1 KiB: per-rank hop 46.4 ms
+# at B = 1, 43.6 at 4, 40.7 at 8, 41.3 at 12, 43.6 at 32), else 1 (papers100M at d = 128 is flat over
+# B = 1..16, products at P = 8 slower; profiles/r04_halo_col_blocks_p8.txt)
+_HALO_COL_BLOCKS_ENV = os.environ.get("SRGNN_HALO_COL_BLOCKS")
+AUTO_HALO_COL_BLOCKS = int(_HALO_COL_BLOCKS_ENV) if _HALO_COL_BLOCKS_ENV else 1
+WIDE_HALO_COL_BLOCKS = 8
+WIDE_HALO_PANEL = 8 << 30
 # column blocks of the hub group's launch (chained on the hub side stream; 1 = one launch);
 # SRGNN_HALO_HUB_BLOCKS overrides.  Bitwise the same hops either way.
 AUTO_HALO_HUB_BLOCKS = int(os.environ.get("SRGNN_HALO_HUB_BLOCKS", "1"))
@@ -562,13 +568,15 @@ class HaloPartitionedOperator:
 
     def _col_blocks_for(self, d: int) -> int:
         """Column blocks per row-chunk launch for a panel of d columns: `col_blocks` if given, else
-        AUTO_HALO_COL_BLOCKS for local panels ([own | halo] rows) of >= 256 MiB at d >= 64 (HIP
-        ranks only)."""
+        WIDE_HALO_COL_BLOCKS for local panels ([own | halo] rows) of >= WIDE_HALO_PANEL at d >= 256,
+        else AUTO_HALO_COL_BLOCKS for panels of >= 256 MiB at d >= 64 (HIP ranks only)."""
         if not self._hip:
             return 1
         if self.col_blocks is not None:
             return max(1, int(self.col_blocks))
         panel = (self.rows + self.halo) * d * 4
+        if _HALO_COL_BLOCKS_ENV is None and d >= 256 and panel >= WIDE_HALO_PANEL:
+            return WIDE_HALO_COL_BLOCKS
         return AUTO_HALO_COL_BLOCKS if d >= 64 and panel >= (256 << 20) else 1
 
     def chunk_blocks(self, d: int):

@@ -194,9 +194,9 @@ def main():
             del op, src, dst
             torch.cuda.empty_cache()
         if a.quick:
-            key = f"{P}"
+            key = f"{P}" + ("" if cb is None else f"/cb{cb}") + ("" if hcb is None else f"/hcb{hcb}")
             out["worlds"][key] = {"ranks": ranks, "max_hop_compute_ms": max(r["ms_compute"] for r in ranks)}
-            print(f"P={P}: hop compute {out['worlds'][key]['max_hop_compute_ms']:.3f} ms (max over ranks)",
+            print(f"P={P} col blocks {cb} hub blocks {hcb}: hop compute {out['worlds'][key]['max_hop_compute_ms']:.3f} ms (max over ranks)",
                   file=sys.stderr, flush=True)
             continue
         worst = max(ranks, key=lambda r: max(r["ms_hub"], r["ms_chunks"]))
