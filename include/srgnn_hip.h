@@ -486,10 +486,20 @@ int srg_halo_plan_info(const srg_halo_plan* plan, srg_halo_info* info);
 int srg_halo_plan_array(const srg_halo_plan* plan, int32_t what, int32_t index, const void** data, int64_t* count);
 /* The share on `device`: local CSR (values gathered from the GLOBAL fp32 host array `values`),
  * schedules, send lists, a send buffer for panels up to d_max columns, a comm stream and events.
- * The plan must outlive the share. */
+ * The plan must outlive the share.  The row chunks run in column blocks when d_max's panel asks for
+ * them (srg_halo_share_col_blocks' automatic rule). */
 int srg_halo_share_create(const srg_halo_plan* plan, const float* values, int device, int32_t d_max,
                           srg_halo_share** share);
 int srg_halo_share_destroy(srg_halo_share* share);
+/* Column blocks of the row chunks' launches (srgnn/dist.py HaloPartitionedOperator.chunk_blocks):
+ * each chunk runs as n_blocks span launches over the own rows' spans whose GLOBAL column ids lie in
+ * [ceil(b n / B), ceil((b+1) n / B)), rows of <= 32 entries whole in block 0, later blocks continuing
+ * the chains (ACCUMULATE): bitwise the unblocked hop, with column locality for wide panels.
+ * n_blocks in [1, 64] (1: unblocked) applies to every d; SRG_HALO_AUTO (the share's default) picks 8
+ * for local panels ([own | halo] rows x d x 4 B) of >= 8 GiB at d >= 256, else 1, per call's d
+ * (SRGNN_HALO_COL_BLOCKS overrides the automatic count for panels of >= 256 MiB at d >= 64).
+ * Builds the split points and schedules on the host and uploads them (synchronous). */
+int srg_halo_share_col_blocks(srg_halo_share* share, int32_t n_blocks);
 /* Panel 0 from the WHOLE feature matrix X [n, ldx] on the share's device (as GraphOp.propagate is
  * handed the whole feature): own rows, then the halo rows gathered by global id.  Then pass
  * SRG_HALO_X_HALO_FILLED to srg_halo_propagate_f32 (no exchange of X). */

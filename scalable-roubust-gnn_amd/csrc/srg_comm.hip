@@ -514,10 +514,27 @@ int srg_halo_propagate_f32(srg_comm* comm, srg_halo_share* const* shares, int n_
             SRG_HIPC(hipSetDevice(shares[i]->device));
             if ((rc = launch(i, C, SRG_SPMM_HUB_NOJOIN))) return rc;
         }
+        // a row chunk: one launch, or its column blocks in order (the share's, when d asks for as many)
+        auto chunk = [&](int i, int c) -> int {
+            const srg_halo_share* S = shares[i];
+            const SrgHaloBlocks& Kb = S->blocks;
+            if (Kb.B < 2 || (!Kb.forced && srg_halo_col_blocks(S->plan->rows + S->plan->halo, d) != Kb.B))
+                return launch(i, c, 0);
+            const uint32_t u2 = d >= 128 ? SRG_SPMM_PACKED_U2 : 0u;
+            for (int b = 0; b < Kb.B; ++b) {
+                const SrgHaloView& V = Kb.views[c][b];
+                if (V.n == 0) continue;
+                const int e = srg_spmm_span_f32(Kb.bounds[b], Kb.bounds[b + 1], S->lix, S->lvv, V.n, Kb.orders[c][b], 0,
+                                                view_heavy(V, d), panels[i][k - 1], ld, panels[i][k], ld, d,
+                                                (b > 0 ? SRG_SPMM_ACCUMULATE : 0u) | u2, nullptr, 0, 0.0f, 0, st(i));
+                if (e) return e;
+            }
+            return SRG_OK;
+        };
         for (int c = 0; c < C; ++c) {
             for (int i = 0; i < n_shards; ++i) {
                 SRG_HIPC(hipSetDevice(shares[i]->device));
-                if ((rc = launch(i, c, 0))) return rc;
+                if ((rc = chunk(i, c))) return rc;
                 if (ex && (rc = halo_pack(shares[i], c, panels[i][k], d, st(i)))) return rc;
             }
             if (ex && (rc = halo_transport(r, comm, shares, n_shards, c, panel_k(k), d))) return rc;

@@ -22,6 +22,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <thread>
@@ -81,7 +82,112 @@ void sort_by_degree(std::vector<int32_t>& rows, const std::vector<int64_t>& deg_
     std::stable_sort(rows.begin(), rows.end(), [&](int32_t a, int32_t b) { return deg_of[a] > deg_of[b]; });
 }
 
+int64_t env_int(const char* name, int64_t dflt)
+{
+    const char* v = getenv(name);
+    return (v && *v) ? strtoll(v, nullptr, 10) : dflt;
+}
+
+void free_blocks(SrgHaloBlocks& K)
+{
+    for (auto* sp : K.splits) (void)hipFree(sp);
+    for (auto& oc : K.orders)
+        for (auto* o : oc) (void)hipFree(o);
+    K = SrgHaloBlocks();
+}
+
+// The chunks' column blocks of share S (SrgHaloBlocks): split points on the host from the entries'
+// global column ids (the binary search of srg_csr_col_splits), per (chunk, block) schedules sorted by
+// span length (stable, from the chunk's degree order), uploaded.
+int build_blocks(srg_halo_share* S, int B)
+{
+    const srg_halo_plan& pl = *S->plan;
+    SrgHaloBlocks& K = S->blocks;
+    const int64_t rows = pl.rows;
+    const int C = pl.C;
+    const int64_t whole_max = env_int("SRGNN_BLOCK_WHOLE_MAX", 32);
+    std::vector<std::vector<int64_t>> sp((size_t)B - 1, std::vector<int64_t>((size_t)rows));
+    auto glob = [&](int32_t l) -> int64_t { return l < rows ? pl.r0 + l : pl.halo_ids[(size_t)(l - rows)]; };
+    for (int64_t r = 0; r < rows; ++r) {
+        const int64_t beg = pl.lip[r], end = pl.lip[r + 1];
+        const bool whole = whole_max > 0 && end - beg <= whole_max;
+        for (int b = 1; b < B; ++b) {
+            if (whole) { sp[b - 1][r] = end; continue; }
+            const int64_t bound = ((int64_t)b * pl.n + B - 1) / B;
+            int64_t lo = beg, hi = end;
+            while (lo < hi) {
+                const int64_t mid = lo + (hi - lo) / 2;
+                if (glob(pl.lix[mid]) < bound) lo = mid + 1; else hi = mid;
+            }
+            sp[b - 1][r] = lo;
+        }
+    }
+    auto bound_at = [&](int b, int64_t r) { return b == 0 ? pl.lip[r] : b == B ? pl.lip[r + 1] : sp[b - 1][r]; };
+    const int64_t heavy_t = pl.auto_heavy ? auto_heavy(pl.b1 - pl.b0, C * B) : pl.heavy_threshold;
+    K.views.assign(C, std::vector<SrgHaloView>(B));
+    for (int c = 0; c < C; ++c) {
+        const std::vector<int32_t>& rows_c = pl.views[c].order;
+        std::vector<int32_t> cut;
+        for (int32_t r : rows_c)
+            if (!(whole_max > 0 && pl.lip[r + 1] - pl.lip[r] <= whole_max)) cut.push_back(r);
+        for (int b = 0; b < B; ++b) {
+            SrgHaloView& V = K.views[c][b];
+            V.order = b == 0 ? rows_c : cut;
+            std::vector<int64_t> len(V.order.size());
+            for (size_t i = 0; i < V.order.size(); ++i) len[i] = bound_at(b + 1, V.order[i]) - bound_at(b, V.order[i]);
+            std::vector<int32_t> idx(V.order.size());
+            for (size_t i = 0; i < idx.size(); ++i) idx[i] = (int32_t)i;
+            std::stable_sort(idx.begin(), idx.end(), [&](int32_t a, int32_t b2) { return len[a] > len[b2]; });
+            std::vector<int32_t> o(idx.size());
+            for (size_t i = 0; i < idx.size(); ++i) o[i] = V.order[idx[i]];
+            V.order.swap(o);
+            V.n = (int64_t)V.order.size();
+            for (int64_t l : len) {
+                V.n_heavy += (heavy_t >= 0 && l > heavy_t) ? 1 : 0;
+                V.n_heavy_narrow += l > kNarrowHeavy ? 1 : 0;
+            }
+            if (!pl.auto_heavy) V.n_heavy_narrow = V.n_heavy;
+        }
+    }
+    // device arrays
+    K.B = B;
+    K.splits.assign((size_t)B - 1, nullptr);
+    K.bounds.assign((size_t)B + 1, nullptr);
+    K.bounds[0] = S->lip;
+    K.bounds[B] = S->lip + 1;
+    for (int b = 1; b < B; ++b) {
+        if (rows == 0) continue;
+        if (hipMalloc((void**)&K.splits[b - 1], (size_t)rows * sizeof(int64_t)) != hipSuccess)
+            return hfail(SRG_ERR_ALLOC, "column block split points (%lld rows)", (long long)rows);
+        SRG_HALO_HIP(hipMemcpy(K.splits[b - 1], sp[b - 1].data(), (size_t)rows * sizeof(int64_t), hipMemcpyHostToDevice));
+        K.bounds[b] = K.splits[b - 1];
+    }
+    K.orders.assign(C, std::vector<int32_t*>(B, nullptr));
+    for (int c = 0; c < C; ++c)
+        for (int b = 0; b < B; ++b) {
+            std::vector<int32_t>& o = K.views[c][b].order;
+            if (!o.empty()) {
+                if (hipMalloc((void**)&K.orders[c][b], o.size() * sizeof(int32_t)) != hipSuccess)
+                    return hfail(SRG_ERR_ALLOC, "column block schedule (%zu rows)", o.size());
+                SRG_HALO_HIP(hipMemcpy(K.orders[c][b], o.data(), o.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+            }
+            std::vector<int32_t>().swap(o);
+        }
+    return SRG_OK;
+}
+
 }  // namespace
+
+int srg_halo_col_blocks(int64_t nloc, int d)
+{
+    const int64_t panel = nloc * (int64_t)d * 4;
+    const char* env = getenv("SRGNN_HALO_COL_BLOCKS");
+    if (env && *env) {
+        const int64_t b = strtoll(env, nullptr, 10);
+        return (d >= 64 && panel >= (256ll << 20)) ? (int)std::min<int64_t>(std::max<int64_t>(b, 1), 64) : 1;
+    }
+    return (d >= 256 && panel >= (8ll << 30)) ? 8 : 1;
+}
 
 extern "C" {
 
@@ -260,6 +366,7 @@ int srg_halo_plan_build(const int64_t* indptr, const int32_t* indices, int64_t n
     const bool auto_h = heavy_threshold == SRG_HALO_AUTO;
     const int64_t heavy_t = auto_h ? auto_heavy(pl.b1 - pl.b0, C) : heavy_threshold;
     pl.heavy_threshold = heavy_t;
+    pl.auto_heavy = auto_h;
     pl.views.assign(G + 1, {});
     for (int64_t i = 0; i < pl.rows; ++i) pl.views[grp[r0 + i]].order.push_back((int32_t)i);
     for (int64_t j = 0; j < pl.n_ghost; ++j) pl.views[G].order.push_back((int32_t)(pl.rows + pl.n_recv + j));
@@ -398,6 +505,8 @@ int srg_halo_share_create(const srg_halo_plan* plan, const float* values, int de
     if (S->send_off.back() > 0 &&
         hipMalloc((void**)&S->sendbuf, (size_t)S->send_off.back() * (size_t)d_max * sizeof(float)) != hipSuccess)
         return fail_free(hfail(SRG_ERR_ALLOC, "send buffer of %lld rows x %d", (long long)S->send_off.back(), d_max));
+    const int B = srg_halo_col_blocks(pl.rows + pl.halo, d_max);
+    if (B > 1 && (rc = build_blocks(S, B))) return fail_free(rc);
     S->packed.assign(G + 1, nullptr);
     for (auto& e : S->packed)
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
@@ -421,6 +530,7 @@ int srg_halo_share_destroy(srg_halo_share* S)
     (void)hipFree(S->lix);
     (void)hipFree(S->lvv);
     for (auto* o : S->orders) (void)hipFree(o);
+    free_blocks(S->blocks);
     for (auto* s : S->send_idx) (void)hipFree(s);
     (void)hipFree(S->sendbuf);
     for (auto e : S->packed) if (e) (void)hipEventDestroy(e);
@@ -428,6 +538,29 @@ int srg_halo_share_destroy(srg_halo_share* S)
     if (S->comm_stream) (void)hipStreamDestroy(S->comm_stream);
     if (prev >= 0) (void)hipSetDevice(prev);
     delete S;
+    return SRG_OK;
+}
+
+int srg_halo_share_col_blocks(srg_halo_share* S, int32_t n_blocks)
+{
+    if (!S || !S->plan) return hfail(SRG_ERR_INVALID, "null share");
+    if (n_blocks != SRG_HALO_AUTO && (n_blocks < 1 || n_blocks > 64))
+        return hfail(SRG_ERR_INVALID, "n_blocks=%d not in [1, 64] nor SRG_HALO_AUTO", n_blocks);
+    int prev = -1;
+    if (hipGetDevice(&prev) != hipSuccess) return hfail(SRG_ERR_HIP, "no HIP device");
+    SRG_HALO_HIP(hipSetDevice(S->device));
+    struct Restore { int d; ~Restore() { (void)hipSetDevice(d); } } restore{prev};
+    SRG_HALO_HIP(hipDeviceSynchronize());          // no launch of this share may still read the old arrays
+    free_blocks(S->blocks);
+    const srg_halo_plan& pl = *S->plan;
+    const int B = n_blocks == SRG_HALO_AUTO ? srg_halo_col_blocks(pl.rows + pl.halo, (int)S->d_cap) : n_blocks;
+    int rc = B > 1 ? build_blocks(S, B) : SRG_OK;
+    if (rc) {
+        free_blocks(S->blocks);
+        return rc;
+    }
+    S->blocks.forced = n_blocks != SRG_HALO_AUTO;
+    srg_clear_error();
     return SRG_OK;
 }
 

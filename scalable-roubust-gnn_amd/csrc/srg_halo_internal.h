@@ -31,6 +31,7 @@ struct srg_halo_plan {
     int64_t n_recv = 0, n_ghost = 0, halo = 0;
     int32_t ghost_max_degree = 0;
     int64_t heavy_threshold = 0;                   // the chunks' slice-wave threshold used
+    bool auto_heavy = true;                        // heavy_threshold was SRG_HALO_AUTO
     std::vector<int64_t> hub_thresholds;           // per owner rank
     std::vector<int64_t> starts;                   // [P + 1] row blocks
     std::vector<int64_t> chunk_ranges;             // [C + 1] local row bounds of this rank's chunks
@@ -49,12 +50,32 @@ struct srg_halo_plan {
     std::vector<int64_t> halo_ids;                 // global ids of the halo rows, panel order
 };
 
+// The row chunks' column blocks (srgnn/dist.py HaloPartitionedOperator.chunk_blocks): block b of an own
+// row is its span [bounds[b][r], bounds[b+1][r]) of the local CSR, cut where the entries' GLOBAL column
+// ids cross ceil(b n / B); rows of <= BLOCK_WHOLE_MAX entries run whole in block 0.  Chunk c's block 0
+// schedules all its rows, blocks 1.. its cut rows; each launch continues the chains of the one before
+// (ACCUMULATE), so every row is the unblocked fma chain.
+struct SrgHaloBlocks {
+    int B = 1;                                     // 1: the chunks run unblocked
+    bool forced = false;                           // set by srg_halo_share_col_blocks: for every d
+    std::vector<const int64_t*> bounds;            // [B + 1] device: lip, the B - 1 split arrays, lip + 1
+    std::vector<int64_t*> splits;                  // the B - 1 allocated split arrays [rows]
+    std::vector<std::vector<SrgHaloView>> views;   // [C][B]: rows, heavy counts (order kept on the host only while built)
+    std::vector<std::vector<int32_t*>> orders;     // [C][B] device schedules
+};
+
+// column blocks per row-chunk launch for a d-column panel of `nloc` rows (dist.py _col_blocks_for):
+// SRGNN_HALO_COL_BLOCKS (for panels >= 256 MiB at d >= 64) if set, else 8 for panels >= 8 GiB at
+// d >= 256, else 1
+int srg_halo_col_blocks(int64_t nloc, int d);
+
 struct srg_halo_share {
     int device = 0;
     const srg_halo_plan* plan = nullptr;           // borrowed: must outlive the share
     int64_t* lip = nullptr;
     int32_t* lix = nullptr;
     float* lvv = nullptr;
+    SrgHaloBlocks blocks;                          // for d_max's block count
     std::vector<int32_t*> orders;                  // per view (device)
     std::vector<int64_t*> send_idx;                // per group (device), then the ghost sends
     std::vector<int64_t> send_off;                 // [G + 2] rows of the send buffer per group, ghosts last

@@ -100,6 +100,7 @@ EXPORTED_SYMBOLS = (
     "srg_halo_plan_array",
     "srg_halo_share_create",
     "srg_halo_share_destroy",
+    "srg_halo_share_col_blocks",
     "srg_halo_fill_x_halo",
     "srg_halo_propagate_f32",
     "srg_comm_init_loopback",
@@ -206,11 +207,12 @@ def _declare(lib):
     lib.srg_halo_plan_array.argtypes = [_p, _i32, _i32, ctypes.POINTER(_p), ctypes.POINTER(_i64)]
     lib.srg_halo_share_create.argtypes = [_p, _p, ctypes.c_int, _i32, ctypes.POINTER(_p)]
     lib.srg_halo_share_destroy.argtypes = [_p]
+    lib.srg_halo_share_col_blocks.argtypes = [_p, _i32]
     lib.srg_halo_fill_x_halo.argtypes = [_p, _p, _i64, _p, _i64, _i32, _p]
     lib.srg_halo_propagate_f32.argtypes = [_p, _p, ctypes.c_int, _p, _i64, _i32, _i32, _u32, _p]
     lib.srg_comm_init_loopback.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(_p)]
     for name in ("srg_halo_plan_build", "srg_halo_plan_destroy", "srg_halo_plan_info", "srg_halo_plan_array",
-                 "srg_halo_share_create", "srg_halo_share_destroy", "srg_halo_fill_x_halo", "srg_halo_propagate_f32",
+                 "srg_halo_share_create", "srg_halo_share_destroy", "srg_halo_share_col_blocks", "srg_halo_fill_x_halo", "srg_halo_propagate_f32",
                  "srg_comm_init_loopback"):
         getattr(lib, name).restype = ctypes.c_int
     lib.srg_last_error.argtypes = []

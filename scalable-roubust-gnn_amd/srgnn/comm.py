@@ -158,6 +158,12 @@ class HaloShare:
         self._h, self.plan, self.device = h, plan, torch.device("cuda", int(device))
         self.rows, self.halo = plan.info["n_rows"], plan.info["halo"]
 
+    def col_blocks(self, n_blocks: int = _lib.SRG_HALO_AUTO):
+        """srg_halo_share_col_blocks: the row chunks in n_blocks column blocks (1: unblocked) for every
+        d, or the automatic rule per d (SRG_HALO_AUTO)."""
+        _lib.call_host("srg_halo_share_col_blocks", self._h, int(n_blocks))
+        return self
+
     def new_panel(self, d: int) -> torch.Tensor:
         return torch.zeros((self.rows + self.halo, d), dtype=torch.float32, device=self.device)
 

@@ -69,6 +69,39 @@ def test_loopback_ranks_bitwise_equal_one_gpu(world, chunks, ghost, x_filled, hu
             s.destroy()
 
 
+@pytest.mark.parametrize("world,chunks,ghost,blocks,d", [(2, 3, 0, 2, 64), (4, 3, 2, 3, 128), (8, 6, 0, 8, 256),
+                                                        (3, 2, 8, 5, 32), (1, 2, 0, 4, 128)])
+def test_loopback_ranks_column_blocks_bitwise(world, chunks, ghost, blocks, d):
+    """srg_halo_share_col_blocks: every row chunk in `blocks` column-block span launches (rows of
+    <= 32 entries whole in block 0, later blocks continuing the chains) -- bitwise the one-GPU hops,
+    and the same after switching the share back to unblocked."""
+    from srgnn.comm import HaloPlan, HaloShare, halo_propagate, loopback
+    ip, ix, vals, X, n = _graph(n=30000, e=400000, d=d, seed=9)
+    K = 3
+    want = _one_gpu(ip, ix, vals, X, n, K)
+    ipn, ixn, vn = ip.cpu().numpy(), ix.cpu().numpy(), vals.cpu().numpy()
+    plans = [HaloPlan(ipn, ixn, n, world, r, chunks=chunks, ghost_max_degree=ghost, hub_threshold=128)
+             for r in range(world)]
+    shares = [HaloShare(p, vn, 0, d).col_blocks(blocks) for p in plans]
+    comm = loopback(world, 0)
+    try:
+        for nb in (blocks, 1):
+            for s in shares:
+                s.col_blocks(nb)
+            panels = [[s.new_panel(d) for _ in range(K + 1)] for s in shares]
+            for s, ps in zip(shares, panels):
+                s.fill_x_halo(X, ps[0])
+            halo_propagate(comm, shares, panels, K, x_halo_filled=True)
+            torch.cuda.synchronize()
+            for k in range(K + 1):
+                got = torch.cat([ps[k][: s.rows] for s, ps in zip(shares, panels)])
+                assert torch.equal(got, want[k]), f"blocks {nb} hop {k}"
+    finally:
+        comm.destroy()
+        for s in shares:
+            s.destroy()
+
+
 def test_one_rccl_rank_runs_the_halo_loop():
     from srgnn.comm import Comm, HaloPlan, HaloShare, halo_propagate, unique_id
     ip, ix, vals, X, n = _graph(n=6000, e=60000)
@@ -107,6 +140,9 @@ def test_halo_entry_argument_checks():
         wide = [[torch.zeros((s.rows + s.halo, 32), device="cuda") for _ in range(3)] for s in shares]
         with pytest.raises(_lib.SrgError, match="d_max"):
             halo_propagate(comm, shares, wide, 2)
+        for bad in (0, 65, -2):
+            with pytest.raises(_lib.SrgError, match="n_blocks"):
+                shares[0].col_blocks(bad)
         # a loopback communicator is not an RCCL one
         from srgnn.comm import Comm
         from srgnn.csr import DeviceCSR
