@@ -95,6 +95,12 @@ extern "C" {
  * SRGNN_HUB_PRODUCERS=4 selects it for every launch with more hub workgroups than CUs.  Results are
  * identical either way. */
 #define SRG_SPMM_HUB_LITE 0x100u
+/* The row kernel's launch reserves LDS so that at most 5 of its 4-wave blocks share a CU
+ * (SRGNN_SPMM_WAVES sets the cap, 0 = none): fewer rows gather at once and the L2 re-serves more of
+ * the lines they re-read.  For panels far beyond the caches (srgnn.spmm passes it for hops over
+ * panels of >= 512 MiB): products 5.84 -> 5.81 ms per hop; arxiv's 87 MB panel is 3 % faster without.
+ * Results are identical either way. */
+#define SRG_SPMM_CAP_WAVES 0x200u
 
 /* =============================================================================================
  * (A) drop-in entry points

@@ -280,6 +280,18 @@ constexpr int kSliceLdsBufs = SRG_SLICE_LDS_BUFS;
 #define SRG_STAGE_ENTRIES 0
 #endif
 constexpr bool kStageEntries = SRG_STAGE_ENTRIES != 0;
+// The row waves' (column id, value) loads for the next group of entries are issued right after the
+// current group's gathers, so their latency overlaps the gathers and the fma links instead of
+// preceding the next gathers.  SRG_PREFETCH_IDS bit 0: packed_rows, bit 1: slice_wave.  Products
+// (one box, profiles/r04u_prefetch_ab.txt): none 6.02 ms per hop, slice waves 5.82, packed rows 6.06,
+// both 6.01 -- the packed rows' prefetch, like their LDS-staged ids, raises the traffic (+2.3 GB per
+// hop).  The slice waves' prefetch costs 2 UH registers (73 instead of 54-70: 6 waves per SIMD).
+// Same entries in the same order: same bits.
+#ifndef SRG_PREFETCH_IDS
+#define SRG_PREFETCH_IDS 2
+#endif
+constexpr bool kPrefetchIds = (SRG_PREFETCH_IDS & 1) != 0;
+constexpr bool kPrefetchSliceIds = (SRG_PREFETCH_IDS & 2) != 0;
 
 // Epilogues of the SpMM kernels (every output element y a kernel stores may also go to):
 //  * fused hop aggregation (srgnn.aggregate): with agg != nullptr it is folded into the accumulator
@@ -449,21 +461,31 @@ __device__ __forceinline__ void slice_wave(const IP* __restrict__ indptr,
     if constexpr (EX == kEpiCheby)
         if (cact) cheby_load<1>(epi, row, ccol, X, ldx, cop);
     const int64_t end = row_stop<EX>(indptr, epi, row);
+    float av[UH];
+    int cv[UH];
+    auto load_ids = [&](int64_t j0, int* c, float* a) {   // clamped: no branches
+#pragma unroll
+        for (int b = 0; b < UH; ++b) {
+            int64_t jj = j0 + b * 8 + g;
+            jj = jj < end ? jj : end - 1;
+            c[b] = indices[jj];
+            a[b] = vals[jj];
+        }
+    };
+    if (kPrefetchSliceIds && beg < end) load_ids(beg, cv, av);
     for (int64_t j = beg; j < end; j += 8 * UH) {
         V4 x[UH];
-        float av[UH];
-        int cv[UH];
-#pragma unroll
-        for (int b = 0; b < UH; ++b) {   // all index/value loads first (clamped: no branches) ...
-            int64_t jj = j + b * 8 + g;
-            jj = jj < end ? jj : end - 1;
-            cv[b] = indices[jj];
-            av[b] = vals[jj];
-        }
+        if constexpr (!kPrefetchSliceIds) load_ids(j, cv, av);   // all index/value loads first ...
         __builtin_amdgcn_sched_barrier(0);   // keep every index load ahead of the first gather
 #pragma unroll
         for (int b = 0; b < UH; ++b)     // ... then UH dependent gathers in flight
             x[b] = gact ? gload<float, 4>(X + (int64_t)cv[b] * ldx + qcol) : vzero<float, 4>();
+        [[maybe_unused]] int ncv[UH];
+        [[maybe_unused]] float nav[UH];
+        if constexpr (kPrefetchSliceIds) {    // the next group's ids behind the gathers
+            if (j + 8 * UH < end) load_ids(j + 8 * UH, ncv, nav);
+            __builtin_amdgcn_sched_barrier(0);
+        }
 #pragma unroll
         for (int b = 0; b < UH; ++b) {
             const int64_t jb = j + b * 8;
@@ -485,6 +507,13 @@ __device__ __forceinline__ void slice_wave(const IP* __restrict__ indptr,
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        if constexpr (kPrefetchSliceIds) {
+#pragma unroll
+            for (int b = 0; b < UH; ++b) {
+                cv[b] = ncv[b];
+                av[b] = nav[b];
+            }
         }
     }
     if (cact) {
@@ -657,26 +686,30 @@ __device__ __forceinline__ void packed_rows(const IP* __restrict__ indptr, const
         if constexpr (EX == kEpiCheby)
             if (rv) cheby_load<4>(epi, row, col, X, ldx, cop[q]);
     }
-    for (int j = 0; j < maxlen; j += U) {
-        int cv[U];
-        float av[U];
+    int cv[U];
+    float av[U];
+    auto load_ids = [&](int j0, int* c, float* a) {
         if (staged) {
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const bool ok = j + u < len;
-                const int q = spos + (ok ? j + u : 0);
-                cv[u] = ok ? reinterpret_cast<const int*>(wlds)[q] : 0;
-                av[u] = ok ? wlds[128 + q] : 0.0f;
+                const bool ok = j0 + u < len;
+                const int q = spos + (ok ? j0 + u : 0);
+                c[u] = ok ? reinterpret_cast<const int*>(wlds)[q] : 0;
+                a[u] = ok ? wlds[128 + q] : 0.0f;
             }
         } else {
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const bool ok = j + u < len;
-                const int64_t p = beg + (ok ? j + u : 0);
-                cv[u] = ok ? indices[p] : 0;
-                av[u] = ok ? vals[p] : 0.0f;
+                const bool ok = j0 + u < len;
+                const int64_t p = beg + (ok ? j0 + u : 0);
+                c[u] = ok ? indices[p] : 0;
+                a[u] = ok ? vals[p] : 0.0f;
             }
         }
+    };
+    if (kPrefetchIds && maxlen > 0) load_ids(0, cv, av);
+    for (int j = 0; j < maxlen; j += U) {
+        if constexpr (!kPrefetchIds) load_ids(j, cv, av);
         __builtin_amdgcn_sched_barrier(0);   // every id load ahead of the first gather
         V4 x[U][LQ];
 #pragma unroll
@@ -685,11 +718,24 @@ __device__ __forceinline__ void packed_rows(const IP* __restrict__ indptr, const
             for (int q = 0; q < LQ; ++q)
                 x[u][q] = (j + u < len) ? gload<float, 4>(X + (int64_t)cv[u] * ldx + q * 4 * S + 4 * l)
                                         : vzero<float, 4>();
+        [[maybe_unused]] int ncv[U];
+        [[maybe_unused]] float nav[U];
+        if constexpr (kPrefetchIds) {        // the next entries' ids behind the gathers
+            if (j + U < maxlen) load_ids(j + U, ncv, nav);
+            __builtin_amdgcn_sched_barrier(0);
+        }
 #pragma unroll
         for (int u = 0; u < U; ++u)
             if (j + u < len)
 #pragma unroll
                 for (int q = 0; q < LQ; ++q) chain<float, 4>(acc[q], av[u], x[u][q]);
+        if constexpr (kPrefetchIds) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                cv[u] = ncv[u];
+                av[u] = nav[u];
+            }
+        }
     }
     if (!rv) return;
 #pragma unroll
@@ -716,7 +762,8 @@ k_spmm(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
 {
     typedef typename Vec<float, VEC>::type V;
     const int bid = block_base + (int)blockIdx.x;
-    __shared__ __attribute__((aligned(16))) float lds[kWavesPerBlock * kSliceLdsBufs * 256];
+    // dynamic: at least kSpmmLdsBytes, more when the launch caps its blocks per CU (spmm_lds_bytes)
+    extern __shared__ __attribute__((aligned(16))) float lds[];
     const int lane = threadIdx.x & 63;
     const int wib = threadIdx.x >> 6;
     if (bid < nb_heavy) {
@@ -1591,6 +1638,26 @@ bool xcd_heavy_setting()
     static const bool v = [] { const char* e = getenv("SRGNN_XCD_HEAVY"); return e ? atoi(e) != 0 : true; }();
     return v;
 }
+// LDS a k_spmm block needs (its waves' slice tiles), and what a launch reserves: with
+// SRG_SPMM_CAP_WAVES and a cap of W waves per SIMD (SRGNN_SPMM_WAVES, default kSpmmWavesDefault;
+// 0 = none) each 4-wave block reserves ~160 KiB / (W + 0.5), so at most W blocks -- W waves per
+// SIMD -- share a CU.  Fewer waves gather from fewer rows at once and the L2 re-serves more of their
+// lines: products 6.08 -> 5.96 ms per hop and 35.4 -> 31.3 GB of traffic at W = 5 without the slice
+// waves' id prefetch, 5.84 -> 5.81 ms with it (whose registers already hold the kernel at 6 waves);
+// arxiv (an 87 MB panel) is 3 % faster uncapped, the halo chunks flat (profiles/r04v_*, r04w_*, r04x_*).
+constexpr int kSpmmLdsBytes = kWavesPerBlock * kSliceLdsBufs * 256 * (int)sizeof(float);
+constexpr int kSpmmWavesDefault = 5;
+int spmm_lds_bytes(uint32_t flags)
+{
+    static const int v = [] {
+        const char* e = getenv("SRGNN_SPMM_WAVES");
+        const int w = e ? atoi(e) : kSpmmWavesDefault;
+        if (w <= 0 || w >= 8) return kSpmmLdsBytes;
+        const int b = (int)((160.0 * 1024.0) / (w + 0.5)) / 512 * 512;
+        return b > kSpmmLdsBytes ? b : kSpmmLdsBytes;
+    }();
+    return (flags & SRG_SPMM_CAP_WAVES) ? v : kSpmmLdsBytes;
+}
 int packed_u_setting()
 {
     static const int v = [] {
@@ -1935,26 +2002,27 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
     }
     const int nr = (int)m_rows, nh = (int)n_heavy;
     const int pu = (flags & SRG_SPMM_PACKED_U2) ? 2 : packed_u_setting();
+    const unsigned shm = (unsigned)spmm_lds_bytes(flags);
     for (int64_t b0 = 0; b0 < blocks; b0 += kMaxLaunchBlocks) {
         const dim3 grid((unsigned)std::min<int64_t>(kMaxLaunchBlocks, blocks - b0));
         const int bb = (int)b0;
 #define SRG_LAUNCH_SPMM(V, F, SF)                                                               \
-    hipLaunchKernelGGL((k_spmm<V, kUnroll, kUnrollHeavy, F, SF, IP, 0, EX>), grid, dim3(kBlock), 0, s,     \
+    hipLaunchKernelGGL((k_spmm<V, kUnroll, kUnrollHeavy, F, SF, IP, 0, EX>), grid, dim3(kBlock), shm, s,   \
                        indptr, indices, vals, morder, nr, nh, n_slices, nb_heavy, X, ldx, Y, ldy, \
                        d, acc, nt, bb, epi)
         const bool full = d % (64 * vec) == 0;        // implies d % 32 == 0
 #define SRG_LAUNCH_NARROW(NSV, SF)                                                                 \
-    hipLaunchKernelGGL((k_spmm<1, kUnroll, kUnrollHeavy, false, SF, IP, NSV, EX>), grid, dim3(kBlock), 0, s, \
+    hipLaunchKernelGGL((k_spmm<1, kUnroll, kUnrollHeavy, false, SF, IP, NSV, EX>), grid, dim3(kBlock), shm, s, \
                        indptr, indices, vals, morder, nr, nh, n_slices, nb_heavy, X, ldx, Y, ldy,     \
                        d, acc, nt, bb, epi)
 #define SRG_LAUNCH_PACKED(LRV, LQV, UV)                                                              \
     do {                                                                                              \
         if (xh)                                                                                       \
             hipLaunchKernelGGL((k_spmm<1, UV, kUnrollHeavy, false, true, IP, 0, EX, LRV, LQV, true>), grid, dim3(kBlock), \
-                               0, s, indptr, indices, vals, morder, nr, nh, n_slices, nb_heavy_launch, X, ldx, Y, ldy, \
+                               shm, s, indptr, indices, vals, morder, nr, nh, n_slices, nb_heavy_launch, X, ldx, Y, ldy, \
                                d, acc, nt, bb, epi);                                                  \
         else                                                                                          \
-            hipLaunchKernelGGL((k_spmm<1, UV, kUnrollHeavy, false, true, IP, 0, EX, LRV, LQV>), grid, dim3(kBlock), 0, s, \
+            hipLaunchKernelGGL((k_spmm<1, UV, kUnrollHeavy, false, true, IP, 0, EX, LRV, LQV>), grid, dim3(kBlock), shm, s, \
                                indptr, indices, vals, morder, nr, nh, n_slices, nb_heavy, X, ldx, Y, ldy, \
                                d, acc, nt, bb, epi);                                                  \
     } while (0)

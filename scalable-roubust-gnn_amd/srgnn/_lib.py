@@ -28,6 +28,7 @@ SRG_SPMM_PACKED_U2 = 0x20
 SRG_SPMM_FAST = 0x40
 SRG_SPMM_HUB_CONTINUE = 0x80
 SRG_SPMM_HUB_LITE = 0x100
+SRG_SPMM_CAP_WAVES = 0x200
 
 SRG_CHEBY_INIT = 0
 SRG_CHEBY_STEP = 1

@@ -114,6 +114,11 @@ def auto_col_blocks(A: DeviceCSR, d: int, hops: int | None = None) -> int:
     return B
 
 
+# Hops over panels of at least this many bytes cap the row kernel's occupancy (SRG_SPMM_CAP_WAVES):
+# products 5.84 -> 5.81 ms per hop, arxiv (87 MB) 3 % slower capped (profiles/r04x_waves_ab.txt)
+CAP_WAVES_MIN_PANEL = 512 << 20
+
+
 def launches_per_hop(A: DeviceCSR, B: int, d: int, agg: bool = False) -> int:
     """k_spmm launches of one hop of A over a d-column panel in B column blocks (hop()): B, plus
     one when block 0 runs as its cut spans and its whole rows (_split_block0, or the aggregation
@@ -142,7 +147,8 @@ def _hop_plan(A: DeviceCSR, d: int, B: int, nt_store: bool = False, fast: bool =
     # whole rows -- are in no other launch, so its hub rows never matter)
     chain = len(blocks) > 1 and not fast and _HUB_CHAIN and \
         _same_hub_rows(A, B, ([split[0]] + blocks[1:]) if split is not None else blocks, agg=split is not None)
-    base = (_lib.SRG_SPMM_NT_STORE if nt_store else 0) | (_lib.SRG_SPMM_PACKED_U2 if u2 else 0)
+    base = (_lib.SRG_SPMM_NT_STORE if nt_store else 0) | (_lib.SRG_SPMM_PACKED_U2 if u2 else 0) | \
+        (_lib.SRG_SPMM_CAP_WAVES if A.n_cols * d * 4 >= CAP_WAVES_MIN_PANEL else 0)
     seq = []     # (operator, accumulate, kind)
     for b, Ab in enumerate(blocks):
         if split is not None and b == 0:
