@@ -1595,7 +1595,10 @@ int pick_vec(int d, int64_t ldx, int64_t ldy, const void* X, const void* Y, size
     return 1;
 }
 
-constexpr int kUnrollHeavy = 8;
+#ifndef SRG_UNROLL_HEAVY
+#define SRG_UNROLL_HEAVY 8
+#endif
+constexpr int kUnrollHeavy = SRG_UNROLL_HEAVY;   // slice-wave groups of 8 entries in flight
 
 // One wave that sleeps ~`us` microseconds (s_memrealtime ticks at 100 MHz).  Enqueued on the main
 // stream right after the hub workgroups are forked onto the side stream, so they are dispatched
