@@ -373,10 +373,13 @@ def make_schedule(indptr: torch.Tensor, heavy_threshold=None, hub_threshold=None
                                  heavy_threshold, hub_threshold)
 
 
-# Column blocks' spans take the slice waves from a lower length per nonzero of the launch: nnz_b /
-# BLOCK_HEAVY_PER (products, five blocks: 300-500 best, 6.13 ms per hop; 160: 6.43, 600: 6.19, the
-# whole-operator rule nnz_b / 100000 ~ 230: 6.18; profiles/r03_ab_heavy_threshold_B5.txt)
-BLOCK_HEAVY_PER = 60000
+# Column blocks' spans take the slice waves above nnz_b / BLOCK_HEAVY_PER entries.  Round 3 (five
+# blocks): 300-500 best, 6.13 ms per hop; 160: 6.43, 600: 6.19 (profiles/r03_ab_heavy_threshold_B5.txt).
+# Round 4, with the slice waves' id prefetch and the occupancy cap, longer packed spans pay: products
+# (six blocks, nnz_b ~ 19 M) 5.79 ms at 60000 (~320 entries), 5.62-5.64 at 30000 / 20000 / 15000
+# (650-1300; 2000+ entries: 6.84); papers100M 239.0 -> 237.4 ms, RMAT-26 307.7 -> 306.2
+# (profiles/r04ab_*, r04ac_*, r04ad_*).  SRGNN_BLOCK_HEAVY_PER overrides.
+BLOCK_HEAVY_PER = int(os.environ.get("SRGNN_BLOCK_HEAVY_PER", "20000"))
 
 
 def schedule_from_degrees(deg: torch.Tensor, nnz: int, heavy_threshold=None, hub_threshold=None,
