@@ -499,7 +499,7 @@ int srg_halo_share_create(const srg_halo_plan* plan, const float* values, int de
 int srg_halo_share_destroy(srg_halo_share* share);
 /* Column blocks of the row chunks' launches (srgnn/dist.py HaloPartitionedOperator.chunk_blocks):
  * each chunk runs as n_blocks span launches over the own rows' spans whose GLOBAL column ids lie in
- * [ceil(b n / B), ceil((b+1) n / B)), rows of <= 32 entries whole in block 0, later blocks continuing
+ * [ceil(b n / B), ceil((b+1) n / B)), rows of <= 48 entries whole in block 0, later blocks continuing
  * the chains (ACCUMULATE): bitwise the unblocked hop, with column locality for wide panels.
  * n_blocks in [1, 64] (1: unblocked) applies to every d; SRG_HALO_AUTO (the share's default) picks 8
  * for local panels ([own | halo] rows x d x 4 B) of >= 8 GiB at d >= 256, else 1, per call's d

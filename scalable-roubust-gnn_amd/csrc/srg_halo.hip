@@ -105,7 +105,7 @@ int build_blocks(srg_halo_share* S, int B)
     SrgHaloBlocks& K = S->blocks;
     const int64_t rows = pl.rows;
     const int C = pl.C;
-    const int64_t whole_max = env_int("SRGNN_BLOCK_WHOLE_MAX", 32);
+    const int64_t whole_max = env_int("SRGNN_BLOCK_WHOLE_MAX", 48);   // csr.BLOCK_WHOLE_MAX
     std::vector<std::vector<int64_t>> sp((size_t)B - 1, std::vector<int64_t>((size_t)rows));
     auto glob = [&](int32_t l) -> int64_t { return l < rows ? pl.r0 + l : pl.halo_ids[(size_t)(l - rows)]; };
     for (int64_t r = 0; r < rows; ++r) {

@@ -52,7 +52,7 @@ struct srg_halo_plan {
 
 // The row chunks' column blocks (srgnn/dist.py HaloPartitionedOperator.chunk_blocks): block b of an own
 // row is its span [bounds[b][r], bounds[b+1][r]) of the local CSR, cut where the entries' GLOBAL column
-// ids cross ceil(b n / B); rows of <= BLOCK_WHOLE_MAX entries run whole in block 0.  Chunk c's block 0
+// ids cross ceil(b n / B); rows of <= BLOCK_WHOLE_MAX (48) entries run whole in block 0.  Chunk c's block 0
 // schedules all its rows, blocks 1.. its cut rows; each launch continues the chains of the one before
 // (ACCUMULATE), so every row is the unblocked fma chain.
 struct SrgHaloBlocks {

@@ -38,7 +38,9 @@ DEFAULT_HEAVY_THRESHOLD = None if _HEAVY_ENV == "auto" else int(_HEAVY_ENV)
 NARROW_HEAVY_THRESHOLD = int(os.environ.get("SRGNN_NARROW_HEAVY_THRESHOLD", "32"))
 # Column blocks: rows of at most this many nonzeros are not cut but computed whole in block 0
 # (DeviceCSR.column_blocks); 0 cuts every row.
-BLOCK_WHOLE_MAX = int(os.environ.get("SRGNN_BLOCK_WHOLE_MAX", "32"))
+# Round 4: 48 (products 5.63 -> 5.58 ms per hop at six blocks, 5.53 at seven; 64: the same, 96: 5.62;
+# papers100M 236.7 -> 236.1 ms, RMAT-26 307.6 -> 307.1; profiles/r04ag_*, r04ah_*).  Round 2: 32.
+BLOCK_WHOLE_MAX = int(os.environ.get("SRGNN_BLOCK_WHOLE_MAX", "48"))
 # "auto": rows whose slice-wave time (~40 ns per nonzero, measured) would exceed about half of the
 # expected hop time (~nnz / 13.5e9 s at the measured hop rate) go to the hub path:
 # threshold = nnz // 1024, at least 8192.  Products on 1 GPU -> only the top hub; 1/8 of it -> ~15 K.

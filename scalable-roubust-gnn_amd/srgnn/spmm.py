@@ -94,8 +94,10 @@ def column_blocks_for(A: DeviceCSR, B: int, hops: int | None = None):
 def auto_col_blocks(A: DeviceCSR, d: int, hops: int | None = None) -> int:
     """Column blocks per hop for a panel of d columns (1 = the one-launch hop), if A's blocks exist
     or `hops` hops will amortise cutting it: for panels of >= 512 MiB at d >= 64, one block per
-    ~200 MiB of panel (a slice well inside the 256 MiB Infinity Cache), 4 to 8; 4 for panels of
-    >= 16 GiB.  Round 3, block 0 in two launches, compact blocks in launch order
+    ~150 MiB of panel (a slice well inside the 256 MiB Infinity Cache), 4 to 8; 4 for panels of
+    >= 16 GiB.  Round 4 (slice waves from ~1000-entry spans, rows of <= 48 entries whole): products
+    d = 128 5.63 ms at B = 6, 5.60-5.61 at 7 and 8; with 48-entry whole rows 5.58 / 5.53 / 5.51-5.52 at
+    6 / 7 / 8 (profiles/r04af_*, r04ag_*, r04ah_*).  Round 3, block 0 in two launches, compact blocks in launch order
     (profiles/r03_ab_col_blocks_round3.txt): products d = 128 (1.25 GB) 5.98 ms at B = 6 against
     6.00-6.01 at 5 and 7, 6.03 at 8, 6.10 at 4; d = 256 (2.5 GB) 12.35 ms at 7-8 against 12.40 at 6
     (before the launch order: 12.55 at 6, 12.67 at 5, 12.70 at 10, 12.91 at 4); d = 64 (0.63 GB) flat
@@ -108,7 +110,7 @@ def auto_col_blocks(A: DeviceCSR, d: int, hops: int | None = None) -> int:
     elif panel >= SPLIT_BLOCK0_MAX_PANEL:
         B = 4
     else:
-        B = min(8, max(4, int(round(panel / (200 << 20)))))
+        B = min(8, max(4, int(round(panel / (150 << 20)))))
     if B > 1 and B not in A._blocks and (hops is None or hops < MIN_HOPS_TO_CUT):
         return 1
     return B
