@@ -75,6 +75,7 @@ std::vector<int64_t> balanced(const int64_t* ip, int64_t n, int parts, int64_t b
 int64_t auto_hub(int64_t nnz, int launches) { return std::max<int64_t>(2048, nnz / (1024 * std::max(1, launches))); }
 int64_t auto_heavy(int64_t nnz, int launches) { return std::max<int64_t>(96, nnz / (100000 * std::max(1, launches))); }
 constexpr int64_t kNarrowHeavy = 32;   // csr.NARROW_HEAVY_THRESHOLD
+constexpr int64_t kHaloHeavyMin = 192; // dist.HALO_HEAVY_MIN: the chunks' slice-wave threshold floor
 
 // rows sorted by decreasing degree, ties in the given order (torch.sort(..., descending, stable))
 void sort_by_degree(std::vector<int32_t>& rows, const std::vector<int64_t>& deg_of)
@@ -364,7 +365,7 @@ int srg_halo_plan_build(const int64_t* indptr, const int32_t* indices, int64_t n
     std::vector<int64_t> ldeg(nloc);
     for (int64_t i = 0; i < nloc; ++i) ldeg[i] = pl.lip[i + 1] - pl.lip[i];
     const bool auto_h = heavy_threshold == SRG_HALO_AUTO;
-    const int64_t heavy_t = auto_h ? auto_heavy(pl.b1 - pl.b0, C) : heavy_threshold;
+    const int64_t heavy_t = auto_h ? std::max<int64_t>(kHaloHeavyMin, auto_heavy(pl.b1 - pl.b0, C)) : heavy_threshold;
     pl.heavy_threshold = heavy_t;
     pl.auto_heavy = auto_h;
     pl.views.assign(G + 1, {});

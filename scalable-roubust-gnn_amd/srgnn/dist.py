@@ -252,6 +252,12 @@ def ghost_plan(halos, elig, deg, owner, gip, starts, caps=GHOST_CAPS, link_bps=N
     return best, model
 
 
+# The row chunks' slice waves take rows above max(HALO_HEAVY_MIN, nnz_local / (100000 C)) entries.
+# Products at P = 8 (where the second term is below 96): per-rank hop 1.149-1.152 ms at 96, 1.123-1.129
+# at 128, 1.110-1.112 at 160-200, 1.131 at 256, 1.165 at 300 (round 4, with the slice waves' id
+# prefetch; profiles/r04ak_*, r04al_halo_heavy_ab.txt).  papers100M / RMAT-26 ranks are above it.
+HALO_HEAVY_MIN = 192
+
 # column blocks per row-chunk launch of the halo path for large local panels (1 = off);
 # SRGNN_HALO_COL_BLOCKS overrides.  Bitwise the same hops either way.  Default: 8 for local panels of
 # >= 8 GiB at d >= 256 (RMAT-26 at P = 8, 23.8 GB of [own | halo] rows of 1 KiB: per-rank hop 46.4 ms
@@ -503,7 +509,8 @@ class HaloPartitionedOperator:
             heavy_threshold = DEFAULT_HEAVY_THRESHOLD
         # per launch: the rank's nonzeros split over its row chunks, as for the hub threshold
         auto_heavy = heavy_threshold is None
-        heavy_t = auto_heavy_threshold(int(lip[self.rows]), launches=C) if auto_heavy else heavy_threshold
+        heavy_t = max(HALO_HEAVY_MIN, auto_heavy_threshold(int(lip[self.rows]), launches=C)) if auto_heavy \
+            else heavy_threshold
         self._auto_heavy = auto_heavy
         self._heavy_explicit = heavy_threshold
         self.views = []
