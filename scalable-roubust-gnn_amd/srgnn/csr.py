@@ -380,8 +380,10 @@ def make_schedule(indptr: torch.Tensor, heavy_threshold=None, hub_threshold=None
 # Round 4, with the slice waves' id prefetch and the occupancy cap, longer packed spans pay: products
 # (six blocks, nnz_b ~ 19 M) 5.79 ms at 60000 (~320 entries), 5.62-5.64 at 30000 / 20000 / 15000
 # (650-1300; 2000+ entries: 6.84); papers100M 239.0 -> 237.4 ms, RMAT-26 307.7 -> 306.2
-# (profiles/r04ab_*, r04ac_*, r04ad_*).  SRGNN_BLOCK_HEAVY_PER overrides.
-BLOCK_HEAVY_PER = int(os.environ.get("SRGNN_BLOCK_HEAVY_PER", "20000"))
+# (profiles/r04ab_*, r04ac_*, r04ad_*).  At eight blocks (nnz_b ~ 14.5 M, shorter launches) the cliff
+# comes sooner: 5.51 ms at 30000 and 20000 (~485 / ~730 entries), 7.04 at 12000 (~1200;
+# r04ap_*), so 30000 keeps the margin.  SRGNN_BLOCK_HEAVY_PER overrides.
+BLOCK_HEAVY_PER = int(os.environ.get("SRGNN_BLOCK_HEAVY_PER", "30000"))
 
 
 def schedule_from_degrees(deg: torch.Tensor, nnz: int, heavy_threshold=None, hub_threshold=None,
