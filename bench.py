@@ -257,21 +257,27 @@ def _scipy_rate(ip, ix32, v32, x, n, budget_s):
 
 
 def pmc_traffic(config, launches_per_hop=1, measured=None):
-    """(HBM bytes per hop, source): from this run's PMC passes (`measured`), else from the committed
-    profiles/pmc_<config>.json (tools/pmc_traffic.py) when it was taken with the same hop layout."""
+    """(fabric bytes per hop, source, read bytes per hop): from this run's PMC passes (`measured`),
+    else from the committed profiles/pmc_<config>.json (tools/pmc_traffic.py) when it was taken with
+    the same hop layout.  The bytes are L2 -> fabric bytes (2 * FETCH_SIZE + WRITE_SIZE), Infinity-
+    Cache hits included: an upper bound on DRAM bytes."""
     if measured is not None and int(measured.get("launches_per_hop", 1)) == int(launches_per_hop):
-        return float(measured["hbm_bytes_per_hop"]), measured["source"]
+        return (float(measured["hbm_bytes_per_hop"]), measured["source"],
+                2.0 * float(measured["fetch_kib_per_hop"]) * 1024)
     path = os.path.join(HERE, "profiles", f"pmc_{config}.json")
     if not os.path.exists(path):
-        return None, None
+        return None, None, None
     try:
         with open(path) as f:
             rec = json.load(f)
         if int(rec.get("launches_per_hop", 1)) != int(launches_per_hop):
-            return None, None       # measured with another hop layout
-        return float(rec["hbm_bytes_per_launch"]), f"committed profiles/pmc_{config}.json (tools/pmc_traffic.py)"
+            return None, None, None       # measured with another hop layout
+        b = rec["hbm_bytes_per_hop"] if "hbm_bytes_per_hop" in rec else rec["hbm_bytes_per_launch"]   # pre-round-5 key
+        rd = rec.get("hbm_read_bytes_per_hop", rec.get("hbm_read_bytes_per_launch"))
+        return float(b), f"committed profiles/pmc_{config}.json (tools/pmc_traffic.py)", \
+            (float(rd) if rd is not None else None)
     except Exception:  # noqa: BLE001
-        return None, None
+        return None, None, None
 
 
 def _under_profiler() -> bool:
@@ -662,7 +668,8 @@ def run_wavelet(a, dev, world=1, rank=0, pmc=None):
                            + " (bit-identical to the fused Chebyshev kernel)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
                      "frac": achieved / peak, "traffic": traffic,
-                     "achieved_basis": ("HBM bytes per order's SpMM from PMC counters (traffic) / its time" if traffic
+                     "achieved_basis": ("L2 -> fabric bytes per order's SpMM (Infinity-Cache hits included; PMC "
+                                        "2 * FETCH_SIZE + WRITE_SIZE = traffic) / its time" if traffic
                                         else "compulsory bytes / the SpMM's time (no counter run: a lower bound)"),
                      "traffic_source": pmc["source"] if traffic else None,
                      "unit_of_work": f"one Chebyshev order's SpMM over a {cb}-column block ({B} column blocks, {LB} launches)",
@@ -995,8 +1002,12 @@ def main():
     b_alg = roofline.bytes_no_reuse(local_rows, local_nnz, d)
     b_comp = roofline.bytes_compulsory(local_rows, local_nnz, d, n_cols=n)
     peak = roofline.MI355X_HBM_PEAK_GBS
-    traffic, traffic_src = pmc_traffic(a.config, launches_per_hop=launches, measured=pmc) if world == 1 \
-        else (None, None)
+    traffic, traffic_src, traffic_rd = pmc_traffic(a.config, launches_per_hop=launches, measured=pmc) if world == 1 \
+        else (None, None, None)
+    # the same bytes with the gather read calibration applied (reads / PMC_READ_CALIBRATION: the
+    # counters read 3.8 % above the bytes a random-row gather asks for, profiles/r04_pmc_gather_calibration.txt)
+    traffic_cal = (traffic_rd / roofline.PMC_READ_CALIBRATION + (traffic - traffic_rd)) \
+        if traffic and traffic_rd is not None else None
     # achieved: HBM bytes the counters saw per hop / hop time (a lower bound -- the compulsory
     # bytes -- where no counter run exists for this layout)
     achieved = (traffic if traffic else b_comp) / kern_s / 1e9
@@ -1040,8 +1051,13 @@ def main():
                    **exchange_stats},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
                      "frac": achieved / peak, "traffic": traffic,
-                     "achieved_basis": ("HBM bytes per hop from PMC counters (traffic) / hop time" if traffic else
+                     "achieved_basis": ("L2 -> fabric bytes per hop (Infinity-Cache hits included; PMC "
+                                        "2 * FETCH_SIZE + WRITE_SIZE = traffic) / hop time" if traffic else
                                         "compulsory bytes per hop / hop time (no counter run for this layout: a lower bound)"),
+                     "frac_calibrated": (traffic_cal / kern_s / 1e9 / peak) if traffic_cal else None,
+                     "traffic_calibrated": traffic_cal,
+                     "calibration": (f"reads / {roofline.PMC_READ_CALIBRATION} (profiles/r04_pmc_gather_calibration.txt)"
+                                     if traffic_cal else None),
                      "traffic_source": traffic_src,
                      "unit_of_work": "one hop" + (f" = {col_blocks} column blocks in {launches} launches" if col_blocks > 1
                                                   else " (one launch)")

@@ -186,6 +186,32 @@ typedef struct srg_hop_launch {
 int srg_propagate_plan_f32(const srg_hop_launch* launches, int32_t n_launch, int32_t join_hub,
                            float* const* panels, int64_t ld, int32_t d, int32_t K, void* stream);
 
+/* ---- the light rows of a launch as LDS-DMA entry streams (srg_stream.hip) ----------------------
+ * A launch's light rows (the schedule after its hub and slice-wave rows) laid out as one stream:
+ * row order[i]'s span [beg[r], end[r]) of (indices, values) copied, in schedule order, as int32 pairs
+ * (column id, value bits) into ent; with `accumulate` every row gets a leading pseudo entry
+ * (-1 - row, 1.0f) that reads the row's partial sum from Y (the chain then starts from -0.0f, so
+ * fma(1, y, -0) == y: the same chain as SRG_SPMM_ACCUMULATE).  st_end[i] = the end of row i in the
+ * stream, st_row[i] = order[i], st_wave[w] = the first row of wave w's run (about wave_entries
+ * entries each).  Sizes first (synchronous): srg_stream_layout_size gives the entries and waves for
+ * the buffers (ent: 2 * entries int32, st_end / st_row: n, st_wave: waves + 1).  wave_entries in
+ * [4, 4096].  Asynchronous on `stream`. */
+int srg_stream_layout_size(const int32_t* order, int64_t n, const int64_t* beg, const int64_t* end,
+                           int32_t accumulate, int64_t wave_entries, int64_t* entries, int64_t* waves, void* stream);
+int srg_stream_layout_build(const int32_t* order, int64_t n, const int64_t* beg, const int64_t* end,
+                            const int32_t* indices, const float* values, int32_t accumulate, int64_t wave_entries,
+                            int64_t entries, int64_t waves, int32_t* ent, int64_t* st_end, int32_t* st_row,
+                            int32_t* st_wave, void* stream);
+/* Y[st_row[i], :] = (row i's stream) * X for every row of a layout: one wave per run, each streaming
+ * its entries' X rows into an LDS ring by LDS-DMA (3 tiles of 8 KiB in flight) and running every
+ * row's fma chain in stored order -- bitwise srg_spmm_span_f32 over the same rows.  flags:
+ * SRG_SPMM_ACCUMULATE must match the layout's `accumulate`; SRG_SPMM_NT_STORE.  d in {64, 128, 256},
+ * 16-byte aligned panels with ld % 4 == 0.  Replaces the light-row part of one call of
+ * csr_sparse_dense_matmul inside GraphOp.propagate's hop loop (SSRG/operators/base_operator.py:33-35). */
+int srg_spmm_stream_f32(const int32_t* ent, const int64_t* st_end, const int32_t* st_row, const int32_t* st_wave,
+                        int64_t waves, int64_t wave_entries, const float* X, int64_t ldx, float* Y, int64_t ldy,
+                        int32_t d, uint32_t flags, void* stream);
+
 /* Chebyshev heat-kernel filter bank (wavelet basis), SSRG/models/base_scalable/base_model.py:
  * 184-191, 236-265 via pygsp cheby_op.  One fused launch per Chebyshev order:
  *   mode SRG_CHEBY_INIT (order 1):  Tn = (A*Tc - a2*Tc) / a1;   R_s  = (c0_s/2)*Tc + c1_s*Tn

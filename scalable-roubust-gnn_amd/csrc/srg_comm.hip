@@ -3,20 +3,26 @@
 // srgnn/dist.py).
 //
 // Partition: rank r owns rows [row_starts[r], row_starts[r+1]) of Â (a 1-D, contiguous row block with
-// global column ids) and the same rows of every hop panel.  Per hop, every rank's block of the previous
-// panel is exchanged with grouped ncclSend / ncclRecv (variable block sizes, every peer at once: a
-// direct all-gather over xGMI's point-to-point links), the own block is copied device-to-device, and the
-// rank's rows are multiplied by srg_spmm_csr_f32 on the gathered panel.  Each row's fma chain is the
-// one-GPU chain, so every hop is bitwise the one-GPU hop.
+// global column ids) and the same rows of every hop panel.  srg_dist_propagate_khop_f32 is SURVEY §8(e)'s
+// all-gather, chunked by owner and overlapped with the SpMM: per hop every pair of ranks exchanges its
+// blocks of the previous panel in a grouped ncclSend / ncclRecv on a stream of that pair (all links at
+// once), and each rank multiplies its rows in P column blocks -- block q = the entries whose column ids
+// lie in rank q's rows, a span of every row since Â's rows hold sorted ids -- in ascending q, block q
+// as soon as rank q's rows have arrived (the own block first copied locally), blocks 1.. continuing
+// the chains of block 0 (SRG_SPMM_ACCUMULATE).  Every row's fma chain is the one-GPU chain in CSR order,
+// so every hop is bitwise the one-GPU hop.  The halo exchange (srg_halo_*, below) moves only the rows
+// each rank references and is the faster path.
 //
 // RCCL is loaded at run time (dlopen, RTLD_LOCAL): a process that already holds an RCCL (PyTorch's) keeps
 // using that one, and the library itself has no link-time dependency on it.  SRGNN_RCCL_LIB names a
-// specific librccl.
+// specific librccl (the tests load an in-process stand-in, tests/fake_rccl.cpp, to run these RCCL paths
+// with several ranks on one GPU).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <dlfcn.h>
 
+#include <algorithm>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -129,7 +135,120 @@ struct srg_comm {
     bool loopback = false;
     hipStream_t lb_stream = nullptr;
     hipEvent_t lb_done = nullptr;
+    // srg_dist_propagate_khop_f32: per local rank, a stream and an arrival event per peer, and the
+    // "previous panel ready" event (created on first use)
+    std::vector<std::vector<hipStream_t>> peer_stream;
+    std::vector<std::vector<hipEvent_t>> peer_arrived;
+    std::vector<hipEvent_t> panel_ready;
 };
+
+namespace {
+
+// splits[(b - 1) * n + r] = the first entry of row r whose column id is >= bounds[b], b = 1 .. P - 1 (one
+// wave per row: a binary search per boundary, and a check that the row's ids never decrease -- else
+// a block would read rows of another owner before they arrive)
+__global__ void __launch_bounds__(256)
+k_owner_splits(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices, int64_t n,
+               const int64_t* __restrict__ bounds, int P, int64_t* __restrict__ splits, int* __restrict__ bad)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t waves = (int64_t)gridDim.x * (blockDim.x / 64);
+    for (int64_t r = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); r < n; r += waves) {
+        const int64_t b0 = indptr[r], b1 = indptr[r + 1];
+        int unsorted = 0;
+        for (int64_t e = b0 + lane; e + 1 < b1; e += 64) unsorted |= indices[e] > indices[e + 1];
+        if (__any(unsorted) && lane == 0) atomicOr(bad, 1);
+        for (int b = 1 + lane; b < P; b += 64) {
+            int64_t lo = b0, hi = b1;
+            while (lo < hi) {
+                const int64_t mid = lo + (hi - lo) / 2;
+                if ((int64_t)indices[mid] < bounds[b])
+                    lo = mid + 1;
+                else
+                    hi = mid;
+            }
+            splits[(int64_t)(b - 1) * n + r] = lo;
+        }
+    }
+}
+
+// the pair streams and events of srg_dist_propagate_khop_f32 (created once per communicator)
+int dist_streams(srg_comm* comm)
+{
+    const size_t L = comm->comms.size();
+    if (comm->peer_stream.size() == L) return SRG_OK;
+    comm->peer_stream.assign(L, std::vector<hipStream_t>(comm->nranks, nullptr));
+    comm->peer_arrived.assign(L, std::vector<hipEvent_t>(comm->nranks, nullptr));
+    comm->panel_ready.assign(L, nullptr);
+    for (size_t i = 0; i < L; ++i) {
+        SRG_HIPC(hipSetDevice(comm->devices[i]));
+        SRG_HIPC(hipEventCreateWithFlags(&comm->panel_ready[i], hipEventDisableTiming));
+        for (int q = 0; q < comm->nranks; ++q) {
+            if (q == comm->ranks[i]) continue;
+            SRG_HIPC(hipStreamCreateWithFlags(&comm->peer_stream[i][q], hipStreamNonBlocking));
+            SRG_HIPC(hipEventCreateWithFlags(&comm->peer_arrived[i][q], hipEventDisableTiming));
+        }
+    }
+    return SRG_OK;
+}
+
+// One hop's exchange: for every pair of ranks (a, b), a < b, in ascending order, one group with the
+// local ranks' send of their block to the other and receive of the other's block into x_full, on the
+// pair's stream (which first waits for the previous panel), then the arrival event.  A rank meets its
+// peers in ascending order, so the blocks it needs first are sent first; the pairs' streams run
+// side by side (every xGMI link at once).
+int dist_exchange(const Rccl* r, srg_comm* comm, const srg_shard_f32* shards, int n_shards, const int64_t* row_starts,
+                  int64_t ld, int k)
+{
+    const int P = comm->nranks;
+    for (int a = 0; a < P; ++a)
+        for (int b = a + 1; b < P; ++b) {
+            int local[2] = {-1, -1};
+            for (int i = 0; i < n_shards; ++i) {
+                if (comm->ranks[i] == a) local[0] = i;
+                if (comm->ranks[i] == b) local[1] = i;
+            }
+            if (local[0] < 0 && local[1] < 0) continue;
+            for (int side = 0; side < 2; ++side) {
+                const int i = local[side];
+                if (i < 0) continue;
+                const int peer = side ? a : b;
+                SRG_HIPC(hipSetDevice(shards[i].device));
+                SRG_HIPC(hipStreamWaitEvent(comm->peer_stream[i][peer], comm->panel_ready[i], 0));
+            }
+            SRG_NCCL(r, r->GroupStart());
+            int rc = SRG_OK;
+            for (int side = 0; side < 2 && !rc; ++side) {
+                const int i = local[side];
+                if (i < 0) continue;
+                const srg_shard_f32& s = shards[i];
+                const int peer = side ? a : b;
+                const hipStream_t ps = comm->peer_stream[i][peer];
+                const size_t n_me = (size_t)s.n_rows * (size_t)ld;
+                const size_t n_peer = (size_t)(row_starts[peer + 1] - row_starts[peer]) * (size_t)ld;
+                ncclResult_t e = ncclSuccess;
+                // the previous panel's own rows (complete at panel_ready)
+                if (n_me) e = r->Send(s.panels[k - 1], n_me, ncclFloat32, peer, comm->comms[i], ps);
+                if (e == ncclSuccess && n_peer)
+                    e = r->Recv(s.x_full + (size_t)row_starts[peer] * ld, n_peer, ncclFloat32, peer, comm->comms[i], ps);
+                if (e != ncclSuccess) rc = comm_fail(SRG_ERR_HIP, "ncclSend / ncclRecv failed: %s", r->GetErrorString(e));
+            }
+            // every exit closes the group (RCCL's group state is thread-local and shared with torch)
+            const ncclResult_t ge = r->GroupEnd();
+            if (rc) return rc;
+            if (ge != ncclSuccess) return comm_fail(SRG_ERR_HIP, "ncclGroupEnd failed: %s", r->GetErrorString(ge));
+            for (int side = 0; side < 2; ++side) {
+                const int i = local[side];
+                if (i < 0) continue;
+                const int peer = side ? a : b;
+                SRG_HIPC(hipSetDevice(shards[i].device));
+                SRG_HIPC(hipEventRecord(comm->peer_arrived[i][peer], comm->peer_stream[i][peer]));
+            }
+        }
+    return SRG_OK;
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -236,6 +355,20 @@ int srg_comm_destroy(srg_comm* comm)
         delete comm;
         return SRG_OK;
     }
+    {
+        DeviceScope scope;
+        for (size_t i = 0; i < comm->peer_stream.size(); ++i) {
+            (void)hipSetDevice(comm->devices[i]);
+            for (auto st : comm->peer_stream[i])
+                if (st) {
+                    (void)hipStreamSynchronize(st);
+                    (void)hipStreamDestroy(st);
+                }
+            for (auto ev : comm->peer_arrived[i])
+                if (ev) (void)hipEventDestroy(ev);
+            if (comm->panel_ready[i]) (void)hipEventDestroy(comm->panel_ready[i]);
+        }
+    }
     const Rccl* r = nullptr;
     int rc = load_rccl(&r);
     if (rc) return rc;
@@ -250,26 +383,6 @@ int srg_comm_destroy(srg_comm* comm)
 }
 
 int srg_comm_size(const srg_comm* comm) { return comm ? comm->nranks : 0; }
-
-// The sends and receives of hop k's exchange (inside the caller's GroupStart / GroupEnd bracket).
-static int group_sends(const Rccl* r, srg_comm* comm, const srg_shard_f32* shards, int n_shards,
-                       const int64_t* row_starts, int64_t ld, int k, int P)
-{
-    for (int i = 0; i < n_shards; ++i) {
-        const srg_shard_f32& s = shards[i];
-        const int me = comm->ranks[i];
-        SRG_HIPC(hipSetDevice(s.device));
-        hipStream_t st = static_cast<hipStream_t>(s.stream);
-        for (int q = 0; q < P; ++q) {
-            if (q == me) continue;
-            const size_t nq = (size_t)(row_starts[q + 1] - row_starts[q]) * (size_t)ld;
-            const size_t nme = (size_t)s.n_rows * (size_t)ld;
-            if (nme) SRG_NCCL(r, r->Send(s.panels[k - 1], nme, ncclFloat32, q, comm->comms[i], st));
-            if (nq) SRG_NCCL(r, r->Recv(s.x_full + (size_t)row_starts[q] * ld, nq, ncclFloat32, q, comm->comms[i], st));
-        }
-    }
-    return SRG_OK;
-}
 
 int srg_dist_propagate_khop_f32(srg_comm* comm, const srg_shard_f32* shards, int n_shards,
                                 const int64_t* row_starts, int64_t ld, int32_t d, int32_t K)
@@ -293,36 +406,100 @@ int srg_dist_propagate_khop_f32(srg_comm* comm, const srg_shard_f32* shards, int
             return comm_fail(SRG_ERR_INVALID, "shard %d on device %d, its communicator on %d", i, s.device,
                              comm->devices[i]);
         if (!s.x_full || !s.panels) return comm_fail(SRG_ERR_INVALID, "shard %d: null buffers", i);
+        if (s.n_rows > 0 && !s.indptr) return comm_fail(SRG_ERR_INVALID, "shard %d: null indptr", i);
     }
     if (K == 0 || d == 0) return SRG_OK;
     const Rccl* r = nullptr;
     int rc = load_rccl(&r);
     if (rc) return rc;
     DeviceScope scope;
-    const size_t esz = sizeof(float);
-    for (int k = 1; k <= K; ++k) {
-        // exchange: every rank's block of panel k-1 into every other rank's gathered panel
-        SRG_NCCL(r, r->GroupStart());
-        // every exit from the bracket closes the group: an error inside it must not leave RCCL's
-        // thread-local group open (later RCCL calls of the process, torch's included, would be
-        // folded into it); the first error is the one returned
-        rc = group_sends(r, comm, shards, n_shards, row_starts, ld, k, P);
-        const ncclResult_t ge = r->GroupEnd();
-        if (rc) return rc;
-        if (ge != ncclSuccess) return comm_fail(SRG_ERR_HIP, "ncclGroupEnd failed: %s", r->GetErrorString(ge));
-        for (int i = 0; i < n_shards; ++i) {
-            const srg_shard_f32& s = shards[i];
-            SRG_HIPC(hipSetDevice(s.device));
-            hipStream_t st = static_cast<hipStream_t>(s.stream);
-            if (s.n_rows)
-                SRG_HIPC(hipMemcpyAsync(s.x_full + (size_t)s.row0 * ld, s.panels[k - 1], (size_t)s.n_rows * ld * esz,
-                                        hipMemcpyDeviceToDevice, st));
-            int e = srg_spmm_csr_f32(s.indptr, s.indices, s.values, s.n_rows, s.row_order, s.n_hub, s.n_heavy,
-                                     s.x_full, ld, s.panels[k], ld, d, 0, s.stream);
-            if (e) return e;
+    if ((rc = dist_streams(comm))) return rc;
+    auto st = [&](int i) { return static_cast<hipStream_t>(shards[i].stream); };
+    // the owner-block split points of every shard's rows (and the check that the rows are sorted:
+    // block q must read only rows rank q owns, which have arrived when it runs)
+    std::vector<int64_t*> splits(n_shards, nullptr);
+    int* bad = nullptr;
+    auto release = [&]() {
+        for (int i = 0; i < n_shards; ++i)
+            if (splits[i]) {
+                (void)hipSetDevice(shards[i].device);
+                (void)hipFreeAsync(splits[i], st(i));
+            }
+    };
+    for (int i = 0; i < n_shards; ++i) {
+        const srg_shard_f32& s = shards[i];
+        SRG_HIPC(hipSetDevice(s.device));
+        // [P + 1] bounds, [P - 1][n_rows] split points, one status word
+        const size_t bytes = (size_t)(P + 1) * 8 + (size_t)(P - 1) * (size_t)s.n_rows * 8 + 8;
+        if (hipMallocAsync(reinterpret_cast<void**>(&splits[i]), bytes, st(i)) != hipSuccess) {
+            release();
+            return comm_fail(SRG_ERR_HIP, "shard %d: hipMallocAsync of %zu bytes failed", i, bytes);
+        }
+        int64_t* bounds = splits[i] + (size_t)(P - 1) * s.n_rows;
+        bad = reinterpret_cast<int*>(bounds + P + 1);
+        hipError_t e = hipMemcpyAsync(bounds, row_starts, (size_t)(P + 1) * 8, hipMemcpyHostToDevice, st(i));
+        if (e == hipSuccess) e = hipMemsetAsync(bad, 0, 4, st(i));
+        if (e == hipSuccess && s.n_rows > 0) {
+            const unsigned grid = (unsigned)std::min<int64_t>((s.n_rows * 64 + 255) / 256, 1 << 20);
+            hipLaunchKernelGGL(k_owner_splits, dim3(grid), dim3(256), 0, st(i), s.indptr, s.indices, s.n_rows, bounds,
+                               P, splits[i], bad);
+            e = hipGetLastError();
+        }
+        int flag = 0;
+        if (e == hipSuccess) e = hipMemcpyAsync(&flag, bad, 4, hipMemcpyDeviceToHost, st(i));
+        if (e == hipSuccess) e = hipStreamSynchronize(st(i));
+        if (e != hipSuccess) {
+            release();
+            return comm_fail(SRG_ERR_HIP, "shard %d: owner splits failed: %s", i, hipGetErrorString(e));
+        }
+        if (flag) {
+            release();
+            return comm_fail(SRG_ERR_INVALID, "shard %d: a row's column ids are not sorted (the owner-chunked exchange "
+                                              "needs Â's canonical rows, SSRG/operators/utils.py:81-93)", i);
         }
     }
-    return SRG_OK;
+    for (int k = 1; k <= K && !rc; ++k) {
+        for (int i = 0; i < n_shards && !rc; ++i) {
+            const srg_shard_f32& s = shards[i];
+            if (hipSetDevice(s.device) != hipSuccess || hipEventRecord(comm->panel_ready[i], st(i)) != hipSuccess)
+                rc = comm_fail(SRG_ERR_HIP, "shard %d: panel event failed", i);
+            // the own block is in place at once; the peers' blocks arrive on the pair streams
+            else if (s.n_rows && hipMemcpyAsync(s.x_full + (size_t)s.row0 * ld, s.panels[k - 1],
+                                                (size_t)s.n_rows * ld * sizeof(float), hipMemcpyDeviceToDevice,
+                                                st(i)) != hipSuccess)
+                rc = comm_fail(SRG_ERR_HIP, "shard %d: own block copy failed", i);
+        }
+        if (!rc) rc = dist_exchange(r, comm, shards, n_shards, row_starts, ld, k);
+        // block q of every row once rank q's rows are in x_full, ascending q: the chains in CSR order
+        for (int i = 0; i < n_shards && !rc; ++i) {
+            const srg_shard_f32& s = shards[i];
+            const int me = comm->ranks[i];
+            if (hipSetDevice(s.device) != hipSuccess) {
+                rc = comm_fail(SRG_ERR_HIP, "hipSetDevice(%d) failed", s.device);
+                break;
+            }
+            for (int q = 0; q < P && !rc; ++q) {
+                if (q != me && hipStreamWaitEvent(st(i), comm->peer_arrived[i][q], 0) != hipSuccess) {
+                    rc = comm_fail(SRG_ERR_HIP, "shard %d: wait for rank %d failed", i, q);
+                    break;
+                }
+                if (s.n_rows == 0) continue;
+                const int64_t* beg = q == 0 ? s.indptr : splits[i] + (size_t)(q - 1) * s.n_rows;
+                const int64_t* end = q == P - 1 ? s.indptr + 1 : splits[i] + (size_t)q * s.n_rows;
+                rc = srg_spmm_span_f32(beg, end, s.indices, s.values, s.n_rows, s.row_order, s.n_hub, s.n_heavy, s.x_full,
+                                       ld, s.panels[k], ld, d, q > 0 ? SRG_SPMM_ACCUMULATE : 0u, nullptr, 0, 0.0f, 0,
+                                       s.stream);
+            }
+        }
+    }
+    // the shards' streams also wait for their last sends (the caller may reuse panel K - 1 after them)
+    for (int i = 0; i < n_shards; ++i) {
+        (void)hipSetDevice(shards[i].device);
+        for (int q = 0; q < P; ++q)
+            if (q != comm->ranks[i]) (void)hipStreamWaitEvent(st(i), comm->peer_arrived[i][q], 0);
+    }
+    release();
+    return rc;
 }
 
 }  // extern "C"
@@ -419,6 +596,87 @@ int halo_transport(const Rccl* r, srg_comm* comm, srg_halo_share* const* shares,
     return SRG_OK;
 }
 
+// Before a share's first exchange over RCCL: every rank sends each peer what it will send it -- the
+// rows of every group and of X's ghost rows, plus (n, nnz) of the plan's graph -- and checks that
+// against what it expects to receive.  Plans built with different arguments (chunks, thresholds, ghost
+// caps, graphs) then fail with SRG_ERR_INVALID instead of hanging in ncclGroupEnd or filling the halo
+// with the wrong rows.  One small grouped exchange and a host sync per share, once.
+int verify_counts(const Rccl* r, srg_comm* comm, srg_halo_share* const* shares, int n)
+{
+    bool all = true;
+    for (int i = 0; i < n; ++i) all &= shares[i]->counts_verified;
+    if (all) return SRG_OK;
+    const int P = comm->nranks;
+    const int NG = shares[0]->plan->C + 4;        // groups 0..C, ghosts (C + 1), then n and nnz
+    std::vector<int64_t*> buf(n, nullptr);
+    auto release = [&]() {
+        for (int i = 0; i < n; ++i)
+            if (buf[i]) {
+                (void)hipSetDevice(shares[i]->device);
+                (void)hipFree(buf[i]);
+            }
+    };
+    std::vector<std::vector<int64_t>> mine(n, std::vector<int64_t>((size_t)P * NG, 0));
+    for (int i = 0; i < n; ++i) {
+        const srg_halo_plan& pl = *shares[i]->plan;
+        for (int q = 0; q < P; ++q) {
+            for (int g = 0; g <= pl.C + 1; ++g) mine[i][(size_t)q * NG + g] = send_count(pl, g, q);
+            mine[i][(size_t)q * NG + pl.C + 2] = pl.n;
+            mine[i][(size_t)q * NG + pl.C + 3] = pl.nnz_total;
+        }
+        if (hipSetDevice(shares[i]->device) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void**>(&buf[i]), (size_t)2 * P * NG * sizeof(int64_t)) != hipSuccess ||
+            hipMemcpy(buf[i], mine[i].data(), (size_t)P * NG * sizeof(int64_t), hipMemcpyHostToDevice) != hipSuccess) {
+            release();
+            return comm_fail(SRG_ERR_HIP, "share %d: count buffers failed", i);
+        }
+    }
+    int rc = SRG_OK;
+    if (r->GroupStart() != ncclSuccess) {
+        release();
+        return comm_fail(SRG_ERR_HIP, "ncclGroupStart failed");
+    }
+    for (int i = 0; i < n && !rc; ++i) {
+        const int me = comm->ranks[i];
+        for (int q = 0; q < P && !rc; ++q) {
+            if (q == me) continue;
+            ncclResult_t e = r->Send(buf[i] + (size_t)q * NG, NG, ncclInt64, q, comm->comms[i], shares[i]->comm_stream);
+            if (e == ncclSuccess)
+                e = r->Recv(buf[i] + (size_t)(P + q) * NG, NG, ncclInt64, q, comm->comms[i], shares[i]->comm_stream);
+            if (e != ncclSuccess) rc = comm_fail(SRG_ERR_HIP, "count exchange failed: %s", r->GetErrorString(e));
+        }
+    }
+    const ncclResult_t ge = r->GroupEnd();
+    if (!rc && ge != ncclSuccess) rc = comm_fail(SRG_ERR_HIP, "count exchange: ncclGroupEnd failed: %s", r->GetErrorString(ge));
+    for (int i = 0; i < n && !rc; ++i) {
+        std::vector<int64_t> theirs((size_t)P * NG, 0);
+        if (hipSetDevice(shares[i]->device) != hipSuccess || hipStreamSynchronize(shares[i]->comm_stream) != hipSuccess ||
+            hipMemcpy(theirs.data(), buf[i] + (size_t)P * NG, (size_t)P * NG * sizeof(int64_t), hipMemcpyDeviceToHost) !=
+                hipSuccess) {
+            rc = comm_fail(SRG_ERR_HIP, "share %d: count exchange readback failed", i);
+            break;
+        }
+        const srg_halo_plan& pl = *shares[i]->plan;
+        for (int q = 0; q < P && !rc; ++q) {
+            if (q == comm->ranks[i]) continue;
+            const int64_t* t = theirs.data() + (size_t)q * NG;
+            if (t[pl.C + 2] != pl.n || t[pl.C + 3] != pl.nnz_total)
+                rc = comm_fail(SRG_ERR_INVALID, "rank %d's plan is of a graph with n=%lld nnz=%lld, rank %d's of n=%lld "
+                               "nnz=%lld", q, (long long)t[pl.C + 2], (long long)t[pl.C + 3], comm->ranks[i],
+                               (long long)pl.n, (long long)pl.nnz_total);
+            for (int g = 0; g <= pl.C + 1 && !rc; ++g)
+                if (t[g] != recv_count(pl, g, q))
+                    rc = comm_fail(SRG_ERR_INVALID, "plans disagree: rank %d sends %lld rows of group %d to rank %d, which "
+                                   "expects %lld (build every rank's plan with the same arguments)", q, (long long)t[g],
+                                   g, comm->ranks[i], (long long)recv_count(pl, g, q));
+        }
+    }
+    release();
+    if (!rc)
+        for (int i = 0; i < n; ++i) shares[i]->counts_verified = true;
+    return rc;
+}
+
 // every shard's stream waits for the exchanges issued so far (on the device, not the host)
 int halo_finish(srg_comm* comm, srg_halo_share* const* shares, int n, void* const* streams)
 {
@@ -476,11 +734,12 @@ int srg_halo_propagate_f32(srg_comm* comm, srg_halo_share* const* shares, int n_
                                          (long long)send_count(*shares[s]->plan, g, q));
     if (K == 0 || d == 0) return SRG_OK;
     const Rccl* r = nullptr;
+    DeviceScope scope;
     if (!comm->loopback) {
         int rc = load_rccl(&r);
+        if (!rc) rc = verify_counts(r, comm, shares, n_shards);
         if (rc) return rc;
     }
-    DeviceScope scope;
     const int G = C + 1;
     auto st = [&](int i) { return streams ? static_cast<hipStream_t>(streams[i]) : nullptr; };
     std::vector<float*> dst(n_shards);

@@ -84,6 +84,7 @@ struct srg_halo_share {
     std::vector<hipEvent_t> packed;                // per group + ghosts: the pack is on the shard's stream
     hipStream_t comm_stream = nullptr;             // RCCL's stream of this shard
     hipEvent_t comm_done = nullptr;
+    bool counts_verified = false;                  // its peers agreed on every exchange count (first RCCL call)
 };
 
 #endif  // SRG_HALO_INTERNAL_H_

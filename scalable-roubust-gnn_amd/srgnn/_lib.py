@@ -65,6 +65,9 @@ EXPORTED_SYMBOLS = (
     "srg_spmm_csr_f32",
     "srg_propagate_khop_f32",
     "srg_propagate_plan_f32",
+    "srg_stream_layout_size",
+    "srg_stream_layout_build",
+    "srg_spmm_stream_f32",
     "srg_cheby_step_f64",
     "srg_cheby_step_f32",
     "srg_cheby_epilogue_f32",
@@ -134,6 +137,12 @@ def _declare(lib):
     lib.srg_propagate_khop_f32.restype = ctypes.c_int
     lib.srg_propagate_plan_f32.argtypes = [_p, _i32, _i32, _p, _i64, _i32, _i32, _p]
     lib.srg_propagate_plan_f32.restype = ctypes.c_int
+    lib.srg_stream_layout_size.argtypes = [_p, _i64, _p, _p, _i32, _i64, ctypes.POINTER(_i64), ctypes.POINTER(_i64), _p]
+    lib.srg_stream_layout_size.restype = ctypes.c_int
+    lib.srg_stream_layout_build.argtypes = [_p, _i64, _p, _p, _p, _p, _i32, _i64, _i64, _i64, _p, _p, _p, _p, _p]
+    lib.srg_stream_layout_build.restype = ctypes.c_int
+    lib.srg_spmm_stream_f32.argtypes = [_p, _p, _p, _p, _i64, _i64, _p, _i64, _p, _i64, _i32, _u32, _p]
+    lib.srg_spmm_stream_f32.restype = ctypes.c_int
     lib.srg_cheby_step_f64.argtypes = [_p, _p, _p, _i64, _p, _p, _p, _p, _i64, _i32, ctypes.c_int,
                                        _f64, _f64, _p, _p, _i32, _p, _i64, _p]
     lib.srg_cheby_step_f64.restype = ctypes.c_int

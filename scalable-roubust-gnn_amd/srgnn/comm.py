@@ -115,6 +115,13 @@ class HaloPlan:
         import numpy as np
         self._ip = np.ascontiguousarray(np.asarray(indptr), dtype=np.int64)
         self._ix = np.ascontiguousarray(np.asarray(indices), dtype=np.int32)
+        # the planner reads indptr[0 .. n] and indices[0 .. indptr[n]): short arrays would be host
+        # over-reads, so their sizes are checked here (the C side validates their contents)
+        if self._ip.ndim != 1 or self._ip.size != int(n) + 1:
+            raise ValueError(f"indptr must have n + 1 = {int(n) + 1} entries, got {self._ip.size}")
+        if self._ix.ndim != 1 or self._ix.size != int(self._ip[-1]):
+            raise ValueError(f"indices must have indptr[n] = {int(self._ip[-1])} entries, got {self._ix.size}")
+        self.nnz = int(self._ip[-1])
         h = ctypes.c_void_p()
         _lib.call_host("srg_halo_plan_build", self._ip.ctypes.data, self._ix.ctypes.data if self._ix.size else None,
                        int(n), int(nranks), int(rank), int(chunks), int(hub_threshold), int(heavy_threshold),
@@ -152,6 +159,8 @@ class HaloShare:
     def __init__(self, plan: HaloPlan, values, device: int, d_max: int):
         import numpy as np
         v = np.ascontiguousarray(np.asarray(values), dtype=np.float32)
+        if v.ndim != 1 or v.size != plan.nnz:
+            raise ValueError(f"values must hold the global CSR's {plan.nnz} entries, got {v.size}")
         h = ctypes.c_void_p()
         _lib.call_host("srg_halo_share_create", plan._h, v.ctypes.data if v.size else None, int(device), int(d_max),
                        ctypes.byref(h))
@@ -167,8 +176,22 @@ class HaloShare:
     def new_panel(self, d: int) -> torch.Tensor:
         return torch.zeros((self.rows + self.halo, d), dtype=torch.float32, device=self.device)
 
+    def check_panel(self, p: torch.Tensor, d: int, what: str):
+        """A [rows + halo, d] float32 contiguous panel on the share's device (the C side trusts it)."""
+        if not isinstance(p, torch.Tensor) or p.dtype != torch.float32 or p.device != self.device or \
+                tuple(p.shape) != (self.rows + self.halo, d) or not p.is_contiguous():
+            raise ValueError(f"{what} must be a contiguous float32 [{self.rows + self.halo}, {d}] tensor on "
+                             f"{self.device}, got {getattr(p, 'dtype', None)} {tuple(getattr(p, 'shape', ()))} "
+                             f"on {getattr(p, 'device', None)}")
+
     def fill_x_halo(self, X: torch.Tensor, panel0: torch.Tensor):
         """Panel 0 from the whole X: own rows, then the halo rows gathered by global id."""
+        d = int(X.shape[1]) if isinstance(X, torch.Tensor) and X.dim() == 2 else -1
+        if d < 0 or X.dtype != torch.float32 or X.device != self.device or X.stride(1) != 1 or \
+                X.shape[0] != int(self.plan._ip.size - 1):
+            raise ValueError("X must be the whole float32 [n, d] feature matrix (unit column stride) on the "
+                             "share's device")
+        self.check_panel(panel0, d, "panel0")
         _lib.call(self.device, "srg_halo_fill_x_halo", self._h, X.data_ptr(), X.stride(0), panel0.data_ptr(),
                   panel0.stride(0), X.shape[1], _lib.stream(self.device))
 
@@ -196,12 +219,22 @@ def halo_propagate(comm: Comm, shares: list[HaloShare], panels: list[list[torch.
     """srg_halo_propagate_f32 over the local shares (loopback: every rank, in order); panels[i][k]
     [rows + halo, d] of share i; asynchronous on each share's stream (torch's current one by
     default)."""
-    d = int(panels[0][0].shape[1])
     n = len(shares)
+    if n == 0 or len(panels) != n:
+        raise ValueError(f"one panel list per share: {len(panels)} lists for {n} shares")
+    if K < 0:
+        raise ValueError("K must be >= 0")
+    d = int(panels[0][0].shape[1])
+    for i, (s, ps) in enumerate(zip(shares, panels)):
+        if len(ps) != K + 1:
+            raise ValueError(f"share {i}: K + 1 = {K + 1} panels needed, got {len(ps)}")
+        for k, p in enumerate(ps):
+            s.check_panel(p, d, f"panels[{i}][{k}]")
     arrs = [(ctypes.c_void_p * (K + 1))(*[p.data_ptr() for p in ps]) for ps in panels]
     parr = (ctypes.c_void_p * n)(*[ctypes.cast(a, ctypes.c_void_p) for a in arrs])
     sh = (ctypes.c_void_p * n)(*[s._h for s in shares])
     strm = (ctypes.c_void_p * n)(*[(streams[i] if streams else torch.cuda.current_stream(s.device).cuda_stream)
                                    for i, s in enumerate(shares)])
-    _lib.call_host("srg_halo_propagate_f32", comm._h, sh, n, parr, d, d, int(K),
+    # every panel is contiguous [rows + halo, d]: its leading dimension is d
+    _lib.call_host("srg_halo_propagate_f32", comm._h, sh, n, parr, panels[0][0].stride(0), d, int(K),
                    _lib.SRG_HALO_X_HALO_FILLED if x_halo_filled else 0, strm)

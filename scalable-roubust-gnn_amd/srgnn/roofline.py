@@ -9,6 +9,9 @@ pointers; the model keeps the survey's definition so numbers compare across impl
 """
 MI355X_HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (8.0 TB/s spec)
 MI355X_HBM_MEASURED_GBS = 6290.0      # ditto, float4 copy
+# 2 * FETCH_SIZE over the bytes a random-row gather asks for (tools/spmm_probe.py --permutation at the
+# products size, d = 128: profiles/r04_pmc_gather_calibration.txt); reads / this = calibrated reads
+PMC_READ_CALIBRATION = 1.038
 
 
 def s_ptr(nnz: int) -> int:

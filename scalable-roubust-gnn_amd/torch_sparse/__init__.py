@@ -10,8 +10,10 @@ reference pins no version; these are the published torch_sparse 0.6.x semantics,
       SparseTensor(A) @ SparseTensor(B) (spspmm_sum): per output row, the products of A's entries
       in stored order with B's rows, each rounded then added from 0; zero sums dropped; entries
       sorted by (row, col).  With coalesced=False the inputs are taken as sorted by row (torch_sparse
-      builds its row pointers from them as given); coalesced=True coalesces both inputs first
-      (sorted by (row, col), duplicate entries summed in stored order).
+      builds its row pointers from them as given); coalesced=True sorts both inputs by (row, col)
+      first and KEEPS duplicate entries (0.6.x builds SparseTensor(..., is_sorted=not coalesced),
+      which sorts without summing, whatever its docstring says: a1*b and a2*b are rounded and added
+      separately).  Parity unpinned: torch_sparse is absent and the reference never passes it.
       -> srgnn.sparse.spgemm (srg_spgemm_f32).
   spmm(index, value, m, n, matrix) -> [m, ...] dense
       index_select, mul, scatter_add: each output row is the sum of its entries' rounded products in
@@ -55,15 +57,8 @@ def spspmm(indexA, valueA, indexB, valueB, m, k, n, coalesced=False):
     for v in (vA, vB):
         if v.dtype != torch.float32:
             raise TypeError(f"spspmm computes in float32, got {v.dtype}")
-    if coalesced:
-        # torch_sparse: "coalesced=True will coalesce both input sparse matrices" -- duplicate
-        # (row, col) entries are summed in their stored order before the product, so a1*b + a2*b
-        # becomes (a1 + a2)*b
-        from srgnn.directed import _coalesce, segment_sum
-        r, c, out = _coalesce(iA[0].to(torch.int64), iA[1].to(torch.int64), [vA], int(k), segment_sum)
-        iA, vA = torch.stack([r, c]), out[0]
-        r, c, out = _coalesce(iB[0].to(torch.int64), iB[1].to(torch.int64), [vB], int(n), segment_sum)
-        iB, vB = torch.stack([r, c]), out[0]
+    # coalesced=True: both inputs sorted by (row, col), duplicates kept in their stored order
+    # (torch_sparse 0.6.x: SparseTensor(row, col, value, is_sorted=not coalesced) sorts, never sums)
     a = csr_from_coo(iA[0], iA[1], vA, int(m), sort_cols=bool(coalesced))
     b = csr_from_coo(iB[0], iB[1], vB, int(k), sort_cols=bool(coalesced))
     if a[1].numel() and int(a[1].max()) >= int(k):

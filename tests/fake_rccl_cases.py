@@ -1,0 +1,106 @@
+"""Run in a child process by tests/test_fake_rccl_gpu.py with SRGNN_RCCL_LIB pointing at the test-only
+tests/_build/libfake_rccl.so: the library's RCCL code paths -- srg_dist_propagate_khop_f32 (the
+owner-chunked all-gather overlapped with the column-block SpMM) and the RCCL branch of
+srg_halo_propagate_f32's exchange (halo_transport, srg_comm.hip) -- with P = 2, 3 and 8 ranks of one
+process on one GPU (real RCCL refuses a repeated device).  Every rank's rows of every hop are compared
+bitwise with the one-GPU hops.  Prints one JSON line {"cases": [...], "ok": bool}."""
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(HERE, "scalable-roubust-gnn_amd"))
+
+import torch  # noqa: E402
+
+
+def graph(n, e, d, seed):
+    from srgnn import synth
+    from srgnn.normalize import sym_norm_binary
+    u, v = synth.rmat_undirected_t(n, e, seed=seed, device="cuda")
+    ip, ix = synth.symmetric_csr_t(n, u, v)
+    ip, ix, vals = sym_norm_binary(ip, ix, n, 0.5)
+    return ip, ix, vals, synth.uniform_features_t(n, d, device="cuda")
+
+
+def main():
+    assert os.environ.get("SRGNN_RCCL_LIB", "").endswith("libfake_rccl.so"), "run with the fake RCCL"
+    from srgnn import _lib
+    from srgnn.comm import Comm, HaloPlan, HaloShare, halo_propagate
+    from srgnn.csr import DeviceCSR
+    from srgnn.spmm import propagate
+    cases = []
+    ip, ix, vals, X = graph(20000, 200000, 64, 5)
+    n, d, K = X.shape[0], X.shape[1], 4
+    A = DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, device="cuda")
+    want = propagate(A, X, K, col_blocks=1)
+    ipn, ixn, vn = ip.cpu().numpy(), ix.cpu().numpy(), vals.cpu().numpy()
+    for P in (2, 3, 8):
+        # srg_dist_propagate_khop_f32: uneven contiguous row blocks (one empty at P = 8)
+        starts = [0] + [min(n, (i * n) // P + (37 * i if i < P - 1 else 0)) for i in range(1, P)] + [n]
+        if P == 8:
+            starts[3] = starts[2]
+        comm = Comm.init_all([0] * P)
+        try:
+            blocks = [A.rows(starts[i], starts[i + 1]) for i in range(P)]
+            out = comm.propagate(blocks, starts, [X[starts[i]:starts[i + 1]].clone() for i in range(P)], K)
+            ok = all(torch.equal(torch.cat([out[i][k] for i in range(P)]), want[k]) for k in range(K + 1))
+            cases.append({"path": "srg_dist_propagate_khop_f32", "P": P, "bitwise_equal_one_gpu": ok})
+        finally:
+            comm.destroy()
+        # srg_halo_propagate_f32 through RCCL grouped send / receive (not the loopback copies)
+        for chunks, ghost, x_filled in ((3, 0, False), (6, 2, True)):
+            plans = [HaloPlan(ipn, ixn, n, P, r, chunks=chunks, ghost_max_degree=ghost, hub_threshold=256)
+                     for r in range(P)]
+            shares = [HaloShare(p, vn, 0, d) for p in plans]
+            panels = [[s.new_panel(d) for _ in range(K + 1)] for s in shares]
+            for s, ps in zip(shares, panels):
+                if x_filled:
+                    s.fill_x_halo(X, ps[0])
+                else:
+                    ps[0][: s.rows].copy_(X[s.plan.info["row0"]:s.plan.info["row0"] + s.rows])
+            streams = [torch.cuda.Stream() for _ in range(P)]
+            for st in streams:
+                st.wait_stream(torch.cuda.current_stream())
+            comm = Comm.init_all([0] * P)
+            try:
+                halo_propagate(comm, shares, panels, K, x_halo_filled=x_filled, streams=[st.cuda_stream for st in streams])
+                torch.cuda.synchronize()
+                ok = all(torch.equal(torch.cat([ps[k][: s.rows] for s, ps in zip(shares, panels)]), want[k])
+                         for k in range(K + 1))
+                halo_ok = True
+                for s, ps in zip(shares, panels):
+                    ids = torch.from_numpy(s.plan.array(_lib.SRG_HALO_HALO_IDS)).cuda()
+                    if ids.numel():
+                        halo_ok &= bool(torch.equal(ps[K - 1][s.rows:s.rows + s.halo], want[K - 1][ids]))
+                cases.append({"path": "srg_halo_propagate_f32 (RCCL branch)", "P": P, "chunks": chunks, "ghost": ghost,
+                              "x_halo_filled": x_filled, "bitwise_equal_one_gpu": ok, "halo_rows_equal_owners": halo_ok})
+            finally:
+                comm.destroy()
+                for s in shares:
+                    s.destroy()
+    # plans that disagree across ranks (different ghost caps): the exchange must fail, not hang
+    P = 3
+    plans = [HaloPlan(ipn, ixn, n, P, r, chunks=3, ghost_max_degree=(4 if r == 1 else 0), hub_threshold=256)
+             for r in range(P)]
+    shares = [HaloShare(p, vn, 0, d) for p in plans]
+    panels = [[s.new_panel(d) for _ in range(3)] for s in shares]
+    comm = Comm.init_all([0] * P)
+    try:
+        halo_propagate(comm, shares, panels, 2)
+        torch.cuda.synchronize()
+        mismatch = "not detected"
+    except _lib.SrgError as e:
+        mismatch = str(e)
+    finally:
+        comm.destroy()
+        for s in shares:
+            s.destroy()
+    cases.append({"path": "mismatched plans", "error": mismatch})
+    ok = all(c.get("bitwise_equal_one_gpu", True) and c.get("halo_rows_equal_owners", True) for c in cases) and \
+        mismatch != "not detected"
+    print(json.dumps({"cases": cases, "ok": ok}))
+
+
+if __name__ == "__main__":
+    main()

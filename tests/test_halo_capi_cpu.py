@@ -78,3 +78,8 @@ def test_c_planner_argument_checks():
     # no hub rows at all
     pl = HaloPlan(ip.numpy(), ix.numpy(), n, 3, 1, chunks=2, hub_threshold=_lib.SRG_HALO_NONE)
     assert pl.info["hub_rows"] == 0
+    # array sizes are checked before the planner reads them (short arrays were host over-reads)
+    with pytest.raises(ValueError, match="n \\+ 1"):
+        HaloPlan(ip.numpy()[:-1], ix.numpy(), n, 2, 0)
+    with pytest.raises(ValueError, match="indices must have"):
+        HaloPlan(ip.numpy(), ix.numpy()[:-3], n, 2, 0)

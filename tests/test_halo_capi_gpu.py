@@ -136,7 +136,27 @@ def test_halo_entry_argument_checks():
         with pytest.raises(_lib.SrgError, match="shares for"):
             halo_propagate(comm, shares[:1], panels[:1], 2)
         with pytest.raises(_lib.SrgError, match="rank"):
-            halo_propagate(comm, shares[::-1], panels, 2)
+            halo_propagate(comm, shares[::-1], panels[::-1], 2)
+        # the Python wrapper checks what the C side trusts: panel count, shape, dtype,
+        # layout and device of every panel
+        with pytest.raises(ValueError, match="panels needed"):
+            halo_propagate(comm, shares, [ps[:2] for ps in panels], 2)
+        with pytest.raises(ValueError, match="panel list per share"):
+            halo_propagate(comm, shares, panels[:1], 2)
+        strided = [[torch.zeros((s.rows + s.halo, 32), device="cuda")[:, :16] for _ in range(3)] for s in shares]
+        with pytest.raises(ValueError, match="contiguous"):
+            halo_propagate(comm, shares, strided, 2)
+        short = [[torch.zeros((s.rows, 16), device="cuda") for _ in range(3)] for s in shares]
+        with pytest.raises(ValueError, match="contiguous float32"):
+            halo_propagate(comm, shares, short, 2)
+        f64 = [[torch.zeros((s.rows + s.halo, 16), device="cuda", dtype=torch.float64) for _ in range(3)]
+               for s in shares]
+        with pytest.raises(ValueError, match="float32"):
+            halo_propagate(comm, shares, f64, 2)
+        with pytest.raises(ValueError, match="panel0"):
+            shares[0].fill_x_halo(X, panels[0][0][:, :8])
+        with pytest.raises(ValueError, match="global CSR"):
+            HaloShare(plans[0], vn[:-1], 0, 16)
         wide = [[torch.zeros((s.rows + s.halo, 32), device="cuda") for _ in range(3)] for s in shares]
         with pytest.raises(_lib.SrgError, match="d_max"):
             halo_propagate(comm, shares, wide, 2)

@@ -142,7 +142,7 @@ def test_spspmm_equals_scipy_product(m, k, n, da, db):
 
 def test_spspmm_unsorted_duplicates_and_coalesced():
     """B rows with repeated column ids (each B row walked in order by one lane) and coalesced=True
-    with shuffled COO input (sorted by (row, col) first)."""
+    with shuffled COO input (sorted by (row, col) first, duplicates kept)."""
     import torch_sparse
     rng = np.random.default_rng(7)
     m, k, n = 50, 40, 30
@@ -167,20 +167,21 @@ def test_spspmm_unsorted_duplicates_and_coalesced():
     keys = sorted(kk for kk, v in want.items() if v != 0)
     np.testing.assert_array_equal(idx.numpy().T, np.array(keys).reshape(-1, 2))
     np.testing.assert_array_equal(val.numpy(), np.array([want[kk] for kk in keys], np.float32))
-    # coalesced=True coalesces both inputs first (torch_sparse's docstring): B's duplicate (row, col)
-    # entries are summed in their stored order, then every product uses the summed value; A's
-    # shuffled entries are sorted by (row, col)
+    # coalesced=True sorts both inputs by (row, col) and keeps duplicates (torch_sparse 0.6.x builds
+    # SparseTensor(..., is_sorted=False), which sorts without summing): every duplicate's product is
+    # rounded and added on its own, in the stably sorted order
     perm = rng.permutation(ia.shape[1])
-    idx2, val2 = torch_sparse.spspmm(ia[:, perm], va[perm], ib, torch.from_numpy(vb), m, k, n, coalesced=True)
-    bsum = {}
-    for q in range(rows.size):                  # rows are sorted, duplicates in stored order
-        key = (int(rows[q]), int(cols[q]))
-        bsum[key] = np.float32(bsum.get(key, np.float32(0)) + vb[q])
+    bperm = rng.permutation(rows.size)
+    ib2 = ib[:, bperm]
+    vb2 = vb[bperm]
+    idx2, val2 = torch_sparse.spspmm(ia[:, perm], va[perm], ib2, torch.from_numpy(vb2), m, k, n, coalesced=True)
+    r2, c2 = ib2[0].numpy(), ib2[1].numpy()
+    bord = np.lexsort((np.arange(rows.size), c2, r2))   # stable by (row, col)
     brow = {}
-    for (r, cc), v in sorted(bsum.items()):
-        brow.setdefault(r, []).append((cc, v))
+    for q in bord:
+        brow.setdefault(int(r2[q]), []).append((int(c2[q]), vb2[q]))
     want2 = {}
-    As = Ad.sorted_indices()                    # coalesced: A's entries by (row, col)
+    As = Ad.sorted_indices()                    # A's entries by (row, col)
     for i in range(m):
         for e in range(As.indptr[i], As.indptr[i + 1]):
             kk, a = As.indices[e], As.data[e]
@@ -188,7 +189,7 @@ def test_spspmm_unsorted_duplicates_and_coalesced():
                 key = (i, cc)
                 want2[key] = np.float32(want2.get(key, np.float32(0)) + np.float32(a * v))
     keys2 = sorted(kk for kk, v in want2.items() if v != 0)
-    assert len(bsum) < rows.size                # the fixture has duplicates to sum
+    assert len({(int(r), int(c)) for r, c in zip(rows, cols)}) < rows.size   # the fixture has duplicates
     np.testing.assert_array_equal(idx2.numpy().T, np.array(keys2).reshape(-1, 2))
     np.testing.assert_array_equal(val2.numpy(), np.array([want2[kk] for kk in keys2], np.float32))
 

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Per-hop HBM traffic of the SpMM kernel from rocprofv3 --pmc runs of tools/spmm_probe.py (a hop
-is one launch, or one per column block; the "_per_launch" keys hold per-hop sums).
+is one launch, or one per column block; the "_per_hop" keys hold the sums over a hop's launches;
+the bytes are L2 -> fabric bytes, Infinity-Cache hits included, not DRAM bytes).
 
     python tools/pmc_traffic.py --fetch DIR --write DIR [--hits DIR] --probe probe.json --out OUT.json
 
@@ -60,17 +61,17 @@ def main():
                                                "hub workgroups excluded)", "n_heavy": probe.get("n_heavy"),
            "launches": f[1], "launches_per_hop": B,
            "fetch_size_kib": f[0], "write_size_kib": w[0],
-           "hbm_read_bytes_per_launch": 2.0 * f[0] * 1024, "hbm_write_bytes_per_launch": w[0] * 1024}
-    rec["hbm_bytes_per_launch"] = rec["hbm_read_bytes_per_launch"] + rec["hbm_write_bytes_per_launch"]
+           "hbm_read_bytes_per_hop": 2.0 * f[0] * 1024, "hbm_write_bytes_per_hop": w[0] * 1024}
+    rec["hbm_bytes_per_hop"] = rec["hbm_read_bytes_per_hop"] + rec["hbm_write_bytes_per_hop"]
     if a.hits:
         h = per_launch(a.hits, ["TCC_HIT_sum", "TCC_MISS_sum"], hops=hops)
         hit, miss = h["TCC_HIT_sum"][0], h["TCC_MISS_sum"][0]
         rec["l2_hit_rate"] = hit / (hit + miss)
-        rec["l2_miss_bytes_per_launch"] = miss * 128.0
-    rec["algorithmic_bytes_per_launch"] = probe["algorithmic_bytes"]
-    rec["compulsory_bytes_per_launch"] = probe["compulsory_bytes"]
-    rec["traffic_over_algorithmic"] = rec["hbm_bytes_per_launch"] / probe["algorithmic_bytes"]
-    rec["traffic_over_compulsory"] = rec["hbm_bytes_per_launch"] / probe["compulsory_bytes"]
+        rec["l2_miss_bytes_per_hop"] = miss * 128.0
+    rec["algorithmic_bytes_per_hop"] = probe["algorithmic_bytes"]
+    rec["compulsory_bytes_per_hop"] = probe["compulsory_bytes"]
+    rec["traffic_over_algorithmic"] = rec["hbm_bytes_per_hop"] / probe["algorithmic_bytes"]
+    rec["traffic_over_compulsory"] = rec["hbm_bytes_per_hop"] / probe["compulsory_bytes"]
     with open(a.out, "w") as fh:
         json.dump(rec, fh, indent=1)
     print(json.dumps(rec, indent=1))
