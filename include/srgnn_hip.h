@@ -89,14 +89,8 @@ extern "C" {
  * HBM beside the chunks, not by the top row's chain -- 1.09-1.11 ms per hop against 1.05-1.08
  * exact), so no default path sets it. */
 #define SRG_SPMM_FAST 0x40u
-/* Hub workgroups of 4 producer waves + the consumer (256-nonzero windows) instead of 8 + 1: the same
- * gathers in flight with 5 waves instead of 9 (134 VGPRs instead of 92 per wave, 680 instead of 864
- * VGPR-waves per workgroup), so launches beside hundreds of hub workgroups keep more of each CU.
- * SRGNN_HUB_PRODUCERS=4 selects it for every launch with more hub workgroups than CUs.  Results are
- * identical either way. */
-#define SRG_SPMM_HUB_LITE 0x100u
-/* The row kernel's launch reserves LDS so that at most 5 of its 4-wave blocks share a CU
- * (SRGNN_SPMM_WAVES sets the cap, 0 = none): fewer rows gather at once and the L2 re-serves more of
+/* The row kernel's launch reserves LDS so that at most 5 of its 4-wave blocks share a CU (gfx950's
+ * 160 KiB of LDS per CU): fewer rows gather at once and the L2 re-serves more of
  * the lines they re-read.  For panels far beyond the caches (srgnn.spmm passes it for hops over
  * panels of >= 512 MiB): products 5.84 -> 5.81 ms per hop; arxiv's 87 MB panel is 3 % faster without.
  * Results are identical either way. */
@@ -185,32 +179,6 @@ typedef struct srg_hop_launch {
  * caller must srg_hub_join(stream) after the call, before anything reads the hub rows. */
 int srg_propagate_plan_f32(const srg_hop_launch* launches, int32_t n_launch, int32_t join_hub,
                            float* const* panels, int64_t ld, int32_t d, int32_t K, void* stream);
-
-/* ---- the light rows of a launch as LDS-DMA entry streams (srg_stream.hip) ----------------------
- * A launch's light rows (the schedule after its hub and slice-wave rows) laid out as one stream:
- * row order[i]'s span [beg[r], end[r]) of (indices, values) copied, in schedule order, as int32 pairs
- * (column id, value bits) into ent; with `accumulate` every row gets a leading pseudo entry
- * (-1 - row, 1.0f) that reads the row's partial sum from Y (the chain then starts from -0.0f, so
- * fma(1, y, -0) == y: the same chain as SRG_SPMM_ACCUMULATE).  st_end[i] = the end of row i in the
- * stream, st_row[i] = order[i], st_wave[w] = the first row of wave w's run (about wave_entries
- * entries each).  Sizes first (synchronous): srg_stream_layout_size gives the entries and waves for
- * the buffers (ent: 2 * entries int32, st_end / st_row: n, st_wave: waves + 1).  wave_entries in
- * [4, 4096].  Asynchronous on `stream`. */
-int srg_stream_layout_size(const int32_t* order, int64_t n, const int64_t* beg, const int64_t* end,
-                           int32_t accumulate, int64_t wave_entries, int64_t* entries, int64_t* waves, void* stream);
-int srg_stream_layout_build(const int32_t* order, int64_t n, const int64_t* beg, const int64_t* end,
-                            const int32_t* indices, const float* values, int32_t accumulate, int64_t wave_entries,
-                            int64_t entries, int64_t waves, int32_t* ent, int64_t* st_end, int32_t* st_row,
-                            int32_t* st_wave, void* stream);
-/* Y[st_row[i], :] = (row i's stream) * X for every row of a layout: one wave per run, each streaming
- * its entries' X rows into an LDS ring by LDS-DMA (3 tiles of 8 KiB in flight) and running every
- * row's fma chain in stored order -- bitwise srg_spmm_span_f32 over the same rows.  flags:
- * SRG_SPMM_ACCUMULATE must match the layout's `accumulate`; SRG_SPMM_NT_STORE.  d in {64, 128, 256},
- * 16-byte aligned panels with ld % 4 == 0.  Replaces the light-row part of one call of
- * csr_sparse_dense_matmul inside GraphOp.propagate's hop loop (SSRG/operators/base_operator.py:33-35). */
-int srg_spmm_stream_f32(const int32_t* ent, const int64_t* st_end, const int32_t* st_row, const int32_t* st_wave,
-                        int64_t waves, int64_t wave_entries, const float* X, int64_t ldx, float* Y, int64_t ldy,
-                        int32_t d, uint32_t flags, void* stream);
 
 /* Chebyshev heat-kernel filter bank (wavelet basis), SSRG/models/base_scalable/base_model.py:
  * 184-191, 236-265 via pygsp cheby_op.  One fused launch per Chebyshev order:
@@ -302,31 +270,6 @@ int srg_spmm_span_f32(const int64_t* row_beg, const int64_t* row_end, const int3
                       const float* values, int64_t n_rows, const int32_t* row_order, int64_t n_hub,
                       int64_t n_heavy, const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t d,
                       uint32_t flags, float* agg, int64_t lda, float w, int agg_init, void* stream);
-
-/* A span launch in which each row decides for itself whether its chain starts from +0.0f or
- * continues from Y: row r accumulates iff row_beg[r] != row_first[r] (its span does not start at
- * the row's first entry; row_first: the full CSR's row pointers).  One launch can then finish some
- * rows whole and carry on others from an earlier launch's partial chain -- the halo path's row
- * chunks each compute their own rows plus one column span of every medium hub row (spans in
- * ascending column order over the chunks, so the chains stay exact; srgnn/dist.py).  No hub rows,
- * no ACCUMULATE / FAST / HUB_* flags; otherwise as srg_spmm_span_f32 (n_heavy slice-wave rows
- * first in row_order).  No reference counterpart: the reference is single process. */
-int srg_spmm_span_rowacc_f32(const int64_t* row_beg, const int64_t* row_end, const int64_t* row_first,
-                             const int32_t* indices, const float* values, int64_t n_rows, const int32_t* row_order,
-                             int64_t n_heavy, const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t d,
-                             uint32_t flags, void* stream);
-
-/* srg_spmm_csr_f32 with the halo pack of the multi-GPU exchange fused into its epilogue
- * (srgnn/dist.py HaloPartitionedOperator; no reference counterpart -- the reference is single
- * process): every row r it computes is also stored, unchanged, into the send-buffer rows
- * send_slot[send_ptr[r] .. send_ptr[r+1]) (leading dimension lds), one per peer that needs it.
- * Y is bitwise the same as srg_spmm_csr_f32's; send rows equal the gathered rows of Y.
- * send_ptr: int64 [n_rows + 1] over the local rows; send_slot: int32 row ids in `send`. */
-int srg_spmm_send_f32(const int64_t* indptr, const int32_t* indices, const float* values,
-                      int64_t n_rows, const int32_t* row_order, int64_t n_hub, int64_t n_heavy,
-                      const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t d, uint32_t flags,
-                      float* send, int64_t lds, const int64_t* send_ptr, const int32_t* send_slot,
-                      void* stream);
 
 /* The last flat elements (< SRG_TAIL_MAX of them) of a torch dim-0 sum take its scalar row_sum
  * order (4 interleaved partials).  srg_tail_record_f32 stores w * y[flat_start + e] (flat index of
@@ -428,11 +371,16 @@ int srg_spmm_muladd_f32(const int64_t* indptr, const int32_t* indices, const flo
 /* ---- multi-GPU: communicators and the row-partitioned K-hop propagation ---------------------------
  * SURVEY.md §8(b) item 5, for C / C++ hosts (the Python package drives the same kernels through
  * torch.distributed: srgnn/dist.py).  RCCL is loaded at run time.  Rank r owns rows
- * [row_starts[r], row_starts[r+1]) of Â and of every hop panel; per hop the blocks are exchanged
- * with grouped ncclSend / ncclRecv to every peer (variable block sizes) and each rank multiplies its
- * rows by the gathered panel (srg_spmm_csr_f32).  Every hop is bitwise the one-GPU hop (each row's
- * fma chain is unchanged).  Replaces the reference's single-process hop loop,
- * SSRG/operators/base_operator.py:32-35. */
+ * [row_starts[r], row_starts[r+1]) of Â and of every hop panel.  srg_dist_propagate_khop_f32 is
+ * SURVEY §8(e)'s all-gather, chunked by owner and overlapped with the SpMM: per hop every pair of
+ * ranks swaps its blocks of the previous panel (grouped ncclSend / ncclRecv on a stream of that
+ * pair: all links at once, lower ranks first), and each rank multiplies its rows in P column blocks
+ * (block q = the entries whose columns rank q owns: a span of every row, since Â's rows hold sorted
+ * ids), in ascending q, block q as soon as rank q's rows have arrived, blocks 1.. continuing the
+ * chains (SRG_SPMM_ACCUMULATE).  Every hop is bitwise the one-GPU hop (each row's fma chain is
+ * unchanged).  Rows with unsorted column ids are rejected (SRG_ERR_INVALID).  The halo exchange
+ * below (srg_halo_*) moves only the referenced rows and is the faster path.  Replaces the
+ * reference's single-process hop loop, SSRG/operators/base_operator.py:32-35. */
 typedef struct srg_comm srg_comm;
 #define SRG_COMM_ID_BYTES 128
 /* RCCL unique id (SRG_COMM_ID_BYTES bytes) to share out of band before srg_comm_init_rank. */
@@ -460,7 +408,9 @@ typedef struct {
 
 /* panels[k] = (rank's rows of Â) * (panel k-1 gathered from every rank), k = 1..K, for every local
  * shard (shards[i] belongs to the communicator's i-th local rank).  Asynchronous on each shard's
- * stream; the exchange is a grouped RCCL call across the local ranks. */
+ * stream, apart from one host sync per call (the owner split points and the sortedness check);
+ * library-owned pair streams carry the exchange, and scratch for the split points comes from the
+ * stream-ordered pool ((P - 1) * n_rows int64 per shard, freed at the end of the call). */
 int srg_dist_propagate_khop_f32(srg_comm* comm, const srg_shard_f32* shards, int n_shards,
                                 const int64_t* row_starts, int64_t ld, int32_t d, int32_t K);
 
@@ -529,7 +479,6 @@ int srg_halo_share_destroy(srg_halo_share* share);
  * the chains (ACCUMULATE): bitwise the unblocked hop, with column locality for wide panels.
  * n_blocks in [1, 64] (1: unblocked) applies to every d; SRG_HALO_AUTO (the share's default) picks 8
  * for local panels ([own | halo] rows x d x 4 B) of >= 8 GiB at d >= 256, else 1, per call's d
- * (SRGNN_HALO_COL_BLOCKS overrides the automatic count for panels of >= 256 MiB at d >= 64).
  * Builds the split points and schedules on the host and uploads them (synchronous). */
 int srg_halo_share_col_blocks(srg_halo_share* share, int32_t n_blocks);
 /* Panel 0 from the WHOLE feature matrix X [n, ldx] on the share's device (as GraphOp.propagate is

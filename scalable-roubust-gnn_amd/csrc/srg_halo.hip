@@ -83,11 +83,8 @@ void sort_by_degree(std::vector<int32_t>& rows, const std::vector<int64_t>& deg_
     std::stable_sort(rows.begin(), rows.end(), [&](int32_t a, int32_t b) { return deg_of[a] > deg_of[b]; });
 }
 
-int64_t env_int(const char* name, int64_t dflt)
-{
-    const char* v = getenv(name);
-    return (v && *v) ? strtoll(v, nullptr, 10) : dflt;
-}
+// rows of at most this many entries run whole in block 0 (= srgnn.csr.BLOCK_WHOLE_MAX)
+constexpr int64_t kBlockWholeMax = 48;
 
 void free_blocks(SrgHaloBlocks& K)
 {
@@ -106,7 +103,7 @@ int build_blocks(srg_halo_share* S, int B)
     SrgHaloBlocks& K = S->blocks;
     const int64_t rows = pl.rows;
     const int C = pl.C;
-    const int64_t whole_max = env_int("SRGNN_BLOCK_WHOLE_MAX", 48);   // csr.BLOCK_WHOLE_MAX
+    const int64_t whole_max = kBlockWholeMax;
     std::vector<std::vector<int64_t>> sp((size_t)B - 1, std::vector<int64_t>((size_t)rows));
     auto glob = [&](int32_t l) -> int64_t { return l < rows ? pl.r0 + l : pl.halo_ids[(size_t)(l - rows)]; };
     for (int64_t r = 0; r < rows; ++r) {
@@ -182,11 +179,6 @@ int build_blocks(srg_halo_share* S, int B)
 int srg_halo_col_blocks(int64_t nloc, int d)
 {
     const int64_t panel = nloc * (int64_t)d * 4;
-    const char* env = getenv("SRGNN_HALO_COL_BLOCKS");
-    if (env && *env) {
-        const int64_t b = strtoll(env, nullptr, 10);
-        return (d >= 64 && panel >= (256ll << 20)) ? (int)std::min<int64_t>(std::max<int64_t>(b, 1), 64) : 1;
-    }
     return (d >= 256 && panel >= (8ll << 30)) ? 8 : 1;
 }
 

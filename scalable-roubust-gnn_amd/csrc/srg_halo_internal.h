@@ -65,8 +65,7 @@ struct SrgHaloBlocks {
 };
 
 // column blocks per row-chunk launch for a d-column panel of `nloc` rows (dist.py _col_blocks_for):
-// SRGNN_HALO_COL_BLOCKS (for panels >= 256 MiB at d >= 64) if set, else 8 for panels >= 8 GiB at
-// d >= 256, else 1
+// 8 for panels >= 8 GiB at d >= 256, else 1 (srg_halo_share_col_blocks sets a count for every d)
 int srg_halo_col_blocks(int64_t nloc, int d);
 
 struct srg_halo_share {

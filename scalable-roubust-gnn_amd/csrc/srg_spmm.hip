@@ -94,20 +94,12 @@ __device__ __forceinline__ typename Vec<T, VEC>::type vload(const T* p)
 {
     return *reinterpret_cast<const typename Vec<T, VEC>::type*>(p);
 }
-// Gather of one X row piece.  SRG_GATHER_NT=1 builds issue every gather non-temporally
-// (experiment hook; measured 35 % slower on the products-shaped graph: the gathered rows are
-// re-read from L2 / Infinity Cache).
-#ifndef SRG_GATHER_NT
-#define SRG_GATHER_NT 0
-#endif
+// Gather of one X row piece (plain loads: the gathered rows are re-read from L2 / Infinity Cache;
+// non-temporal gathers measured 35 % slower on the products-shaped graph).
 template <typename T, int VEC>
 __device__ __forceinline__ typename Vec<T, VEC>::type gload(const T* p)
 {
-    typedef typename Vec<T, VEC>::type V;
-    if constexpr (SRG_GATHER_NT != 0)
-        return __builtin_nontemporal_load(reinterpret_cast<const V*>(p));
-    else
-        return *reinterpret_cast<const V*>(p);
+    return *reinterpret_cast<const typename Vec<T, VEC>::type*>(p);
 }
 
 template <typename T, int VEC>
@@ -269,37 +261,22 @@ constexpr int kSliceCols = 32;
 // operations complete in issue order, so the next group's write cannot overtake this group's reads.
 // Two (the round-1 layout) cost 8 KB per k_spmm block, which beside the hub group's 72 KB workgroups
 // (halo exchange) left room for only two row blocks per CU.
-#ifndef SRG_SLICE_LDS_BUFS
-#define SRG_SLICE_LDS_BUFS 1
-#endif
-constexpr int kSliceLdsBufs = SRG_SLICE_LDS_BUFS;
-// -DSRG_STAGE_ENTRIES=1: packed light rows of span launches stage a wave's consecutive entries in its
-// LDS slot (packed_rows).  Off by default: on products it measured 5.96 ms per hop and 34.7 GB of
-// traffic against 5.85 ms and 32.6 GB unstaged (profiles/r04h_stage_entries_negative.txt)
-#ifndef SRG_STAGE_ENTRIES
-#define SRG_STAGE_ENTRIES 0
-#endif
-constexpr bool kStageEntries = SRG_STAGE_ENTRIES != 0;
+constexpr int kSliceLdsBufs = 1;
 // The row waves' (column id, value) loads for the next group of entries are issued right after the
 // current group's gathers, so their latency overlaps the gathers and the fma links instead of
 // preceding the next gathers.  SRG_PREFETCH_IDS bit 0: packed_rows, bit 1: slice_wave.  Products
 // (one box, profiles/r04u_prefetch_ab.txt): none 6.02 ms per hop, slice waves 5.82, packed rows 6.06,
 // both 6.01 -- the packed rows' prefetch, like their LDS-staged ids, raises the traffic (+2.3 GB per
 // hop).  The slice waves' prefetch costs 2 UH registers (73 instead of 54-70: 6 waves per SIMD).
-// Same entries in the same order: same bits.
-#ifndef SRG_PREFETCH_IDS
-#define SRG_PREFETCH_IDS 2
-#endif
-constexpr bool kPrefetchIds = (SRG_PREFETCH_IDS & 1) != 0;
-constexpr bool kPrefetchSliceIds = (SRG_PREFETCH_IDS & 2) != 0;
+// Same entries in the same order: same bits.  The packed rows' variant (and the LDS-staged entries
+// of round 4, profiles/r04h_stage_entries_negative.txt) measured slower and were removed in round 5.
+constexpr bool kPrefetchIds = false;
+constexpr bool kPrefetchSliceIds = true;
 
 // Epilogues of the SpMM kernels (every output element y a kernel stores may also go to):
 //  * fused hop aggregation (srgnn.aggregate): with agg != nullptr it is folded into the accumulator
 //    panel, agg = (init ? 0 : agg) + w*y, with separate multiply and add -- the same arithmetic as a
 //    following srg_hop_accumulate_f32 step, without re-reading Y;
-//  * fused halo pack (srgnn.dist): with send != nullptr row r is also stored into the send-buffer
-//    rows send_slot[send_ptr[r] .. send_ptr[r+1]) (one per peer that needs it), so the exchange
-//    reads a ready buffer instead of gathering the rows again;
 //  * fused Chebyshev step (srgnn.wavelet, srg_spmm_cheby_f32): y = A*T_k becomes T_{k+1} before it
 //    is stored and every scale's output is updated, with k_cheby_epilogue's arithmetic --
 //      INIT: T1 = (y - a2*T0) / a1,  R_s = (c0_s/2)*T0 + c1_s*T1   (T0 = X, the gathered panel)
@@ -318,10 +295,6 @@ struct Epi {
     int64_t lda;
     float w;
     int init;
-    float* send;
-    int64_t lds;
-    const int64_t* send_ptr;
-    const int32_t* send_slot;
     // fused Chebyshev step (EX == kEpiCheby only)
     const float* cto;     // T_{k-1} (STEP)
     int64_t ldo;
@@ -339,10 +312,6 @@ struct Epi {
     // row-indexed arrays: consecutive slots, consecutive addresses (srg_propagate_plan_f32)
     const int64_t* slot_beg;
     const int64_t* slot_end;
-    // kEpiSpanRA only: row r's chain continues from Y (accumulate) iff its span does not start at
-    // the row's first entry, row_first[r] -- one launch then starts some rows from +0.0f and continues
-    // others (the halo path's row chunks, which also carry one column span of each medium hub row)
-    const int64_t* row_first;
 };
 
 // Epilogue kinds (template parameter EX of the SpMM kernels).  Every call site sits under
@@ -350,9 +319,10 @@ struct Epi {
 // (the reference-bound acc) changed the gather loop's schedule (+10 % per hop on products);
 // guarded, the kEpiPlain kernels are instruction-for-instruction the plain ones.  kEpiSpan is the
 // plain epilogue (aggregation included) over row spans.
-constexpr int kEpiPlain = 0, kEpiSend = 1, kEpiCheby = 2, kEpiSpan = 3, kEpiSpanRA = 4;
-// row spans (kEpiSpan, and kEpiSpanRA: spans with the accumulate decision per row)
-template <int EX> constexpr bool kIsSpan = EX == kEpiSpan || EX == kEpiSpanRA;
+// (round 5 removed the fused halo pack, kEpiSend, and the per-row accumulation of the medium-span
+// probe, kEpiSpanRA: both measured slower)
+constexpr int kEpiPlain = 0, kEpiCheby = 2, kEpiSpan = 3;
+template <int EX> constexpr bool kIsSpan = EX == kEpiSpan;
 
 // End of row `row`'s entries: the next row's start, or the span's end.
 template <int EX, typename IP>
@@ -364,13 +334,6 @@ __device__ __forceinline__ int64_t row_stop(const IP* __restrict__ indptr, const
         return (int64_t)indptr[row + 1];
 }
 
-template <int VEC>
-__device__ __forceinline__ void send_row(const Epi& e, int row, int col, const typename Vec<float, VEC>::type& v)
-{
-    const int64_t s0 = e.send_ptr[row], s1 = e.send_ptr[row + 1];
-    for (int64_t s = s0; s < s1; ++s)
-        vstore<float, VEC>(e.send + (int64_t)e.send_slot[s] * e.lds + col, v, false);
-}
 
 // Operands of the Chebyshev epilogue at (row, col), loaded before the chain so that their latency
 // hides under the gathers (loaded after it, the R round trips were the end of every light row:
@@ -454,7 +417,6 @@ __device__ __forceinline__ void slice_wave(const IP* __restrict__ indptr,
     float* __restrict__ yrow = Y + (int64_t)row * ldy;
     float acc = 0.0f;
     const int64_t beg = indptr[row];
-    if constexpr (EX == kEpiSpanRA) accumulate = beg != epi.row_first[row];
     if (accumulate && cact) acc = yrow[ccol];
     const float aprev = (epi.agg && !epi.init && cact) ? epi.agg[(int64_t)row * epi.lda + ccol] : 0.0f;
     [[maybe_unused]] ChebyOps<1> cop;
@@ -523,7 +485,6 @@ __device__ __forceinline__ void slice_wave(const IP* __restrict__ indptr,
         else
             yrow[ccol] = acc;
         if (epi.agg) epi.agg[(int64_t)row * epi.lda + ccol] = __fadd_rn(aprev, __fmul_rn(epi.w, acc));
-        if constexpr (EX == kEpiSend) send_row<1>(epi, row, ccol, acc);
     }
 }
 
@@ -556,7 +517,6 @@ __device__ __forceinline__ void narrow_rows(const IP* __restrict__ indptr, const
     }
     maxlen = __builtin_amdgcn_readfirstlane(maxlen);
     float* __restrict__ yrow = Y + (int64_t)row * ldy;
-    if constexpr (EX == kEpiSpanRA) accumulate = rv && beg != epi.row_first[row];
     float acc = (accumulate && act) ? yrow[c] : 0.0f;
     const float aprev = (epi.agg && !epi.init && act) ? epi.agg[(int64_t)row * epi.lda + c] : 0.0f;
     [[maybe_unused]] ChebyOps<1> cop;
@@ -588,7 +548,6 @@ __device__ __forceinline__ void narrow_rows(const IP* __restrict__ indptr, const
         else
             yrow[c] = acc;
         if (epi.agg) epi.agg[(int64_t)row * epi.lda + c] = __fadd_rn(aprev, __fmul_rn(epi.w, acc));
-        if constexpr (EX == kEpiSend) send_row<1>(epi, row, c, acc);
     }
 }
 
@@ -605,7 +564,7 @@ __device__ __forceinline__ void packed_rows(const IP* __restrict__ indptr, const
                                             const float* __restrict__ vals, const int32_t* __restrict__ order,
                                             int n_rows, int first, const float* __restrict__ X, int64_t ldx,
                                             float* __restrict__ Y, int64_t ldy, int accumulate, int nt,
-                                            const Epi& epi, float* __restrict__ wlds)
+                                            const Epi& epi)
 {
     typedef typename Vec<float, 4>::type V4;
     constexpr int S = 64 / LR;
@@ -637,42 +596,7 @@ __device__ __forceinline__ void packed_rows(const IP* __restrict__ indptr, const
         maxlen = o > maxlen ? o : maxlen;
     }
     maxlen = __builtin_amdgcn_readfirstlane(maxlen);
-    // Staged entry stream (span launches with slot spans, kStageEntries): when the wave's rows are
-    // consecutive in the entry arrays -- a compact copy laid out in launch order -- and hold at most
-    // 128 entries in all, the wave loads them with two coalesced loads into its LDS slot and the
-    // rows' chains then read their (column id, value) pairs from LDS (16-lane broadcast) instead of
-    // issuing a dependent global load per gather round.  Same entries, same order: same bits.
-    [[maybe_unused]] int spos = 0;     // the row's first entry in the staged stream
-    [[maybe_unused]] bool staged = false;
-    if constexpr (kIsSpan<EX> && kStageEntries) {
-        if (epi.slot_beg) {
-            // prefix of the row lengths over the wave's row groups (entry g * S holds row g's length)
-            int pre = 0, tot = 0;
-#pragma unroll
-            for (int h = 0; h < LR; ++h) {
-                const int lh = __shfl(len, h * S);
-                pre += h < g ? lh : 0;
-                tot += lh;
-            }
-            const int64_t w0 = epi.slot_beg[first];             // wave-uniform: the first row's span start
-            const bool contig = !rv || beg == w0 + pre;
-            staged = tot <= 128 && __all(contig);
-            if (staged) {
-                spos = pre;
-                int* sid = reinterpret_cast<int*>(wlds);
-                float* sva = wlds + 128;
-                for (int q = lane; q < tot; q += 64) {
-                    sid[q] = indices[w0 + q];
-                    sva[q] = vals[w0 + q];
-                }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            }
-        }
-    }
     float* __restrict__ yrow = Y + (int64_t)row * ldy;
-    if constexpr (EX == kEpiSpanRA) accumulate = rv && beg != epi.row_first[row];
     // the Chebyshev epilogue never aggregates nor accumulates (its entry rejects both): dropping
     // them statically keeps its registers (the prefetched operands) within 5 waves per SIMD
     float* __restrict__ arow = (EX != kEpiCheby && epi.agg) ? epi.agg + (int64_t)row * epi.lda : nullptr;
@@ -689,22 +613,12 @@ __device__ __forceinline__ void packed_rows(const IP* __restrict__ indptr, const
     int cv[U];
     float av[U];
     auto load_ids = [&](int j0, int* c, float* a) {
-        if (staged) {
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const bool ok = j0 + u < len;
-                const int q = spos + (ok ? j0 + u : 0);
-                c[u] = ok ? reinterpret_cast<const int*>(wlds)[q] : 0;
-                a[u] = ok ? wlds[128 + q] : 0.0f;
-            }
-        } else {
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const bool ok = j0 + u < len;
-                const int64_t p = beg + (ok ? j0 + u : 0);
-                c[u] = ok ? indices[p] : 0;
-                a[u] = ok ? vals[p] : 0.0f;
-            }
+        for (int u = 0; u < U; ++u) {
+            const bool ok = j0 + u < len;
+            const int64_t p = beg + (ok ? j0 + u : 0);
+            c[u] = ok ? indices[p] : 0;
+            a[u] = ok ? vals[p] : 0.0f;
         }
     };
     if (kPrefetchIds && maxlen > 0) load_ids(0, cv, av);
@@ -748,7 +662,6 @@ __device__ __forceinline__ void packed_rows(const IP* __restrict__ indptr, const
             for (int i = 0; i < 4; ++i) aprev[q][i] = __fadd_rn(aprev[q][i], __fmul_rn(epi.w, acc[q][i]));
             vstore<float, 4>(arow + col, aprev[q], false);
         }
-        if constexpr (EX == kEpiSend) send_row<4>(epi, row, col, acc[q]);
     }
 }
 
@@ -789,8 +702,7 @@ k_spmm(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
     if constexpr (LR > 0) {   // wide panel: LR light rows per wave
         const int first = __builtin_amdgcn_readfirstlane((bid - nb_heavy) * kWavesPerBlock + wib) * LR + n_heavy;
         if (first >= n_rows) return;
-        packed_rows<LR, LQ, U, IP, EX>(indptr, indices, vals, order, n_rows, first, X, ldx, Y, ldy, accumulate, nt, epi,
-                                       lds + wib * kSliceLdsBufs * 256);
+        packed_rows<LR, LQ, U, IP, EX>(indptr, indices, vals, order, n_rows, first, X, ldx, Y, ldy, accumulate, nt, epi);
         return;
     }
     if constexpr (NS > 0) {   // narrow panel: 64 / NS light rows per wave
@@ -803,7 +715,6 @@ k_spmm(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
     if (w >= n_rows) return;
     const int row = order ? order[w] : w;
     float* __restrict__ yrow = Y + (int64_t)row * ldy;
-    if constexpr (EX == kEpiSpanRA) accumulate = (int64_t)indptr[row] != epi.row_first[row];
     for (int c0 = 0; c0 < d; c0 += 64 * VEC) {
         const int col = c0 + lane * VEC;
         const bool act = col < d;
@@ -826,7 +737,6 @@ k_spmm(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
                 for (int i = 0; i < VEC; ++i) elem(aprev, i) = __fadd_rn(elem(aprev, i), __fmul_rn(epi.w, elem(acc, i)));
                 vstore<float, VEC>(arow + col, aprev, false);
             }
-            if constexpr (EX == kEpiSend) send_row<VEC>(epi, row, col, acc);
         }
     }
 }
@@ -870,13 +780,8 @@ struct HubGeom {
 };
 constexpr int kHubWideLaunch = 256;   // more hub workgroups than this (the CU count) -> W = 256
 __device__ __forceinline__ int hub_swz(int c) { return (c >> 2) & 7; }
-constexpr int kHubL = 7;   // consumer: (tile, value) LDS read pairs in flight in a full window
-// Full windows take their link values by DPP quad broadcast (hub_links16); SRG_HUB_DPP=0 builds the
-// value-read-per-4-links loop instead (A/B)
-#ifndef SRG_HUB_DPP
-#define SRG_HUB_DPP 1
-#endif
-constexpr bool kHubDpp = SRG_HUB_DPP != 0;
+// Full windows take their link values by DPP quad broadcast (hub_links16; the value-read-per-4-links
+// loop it replaced in round 3 was removed in round 5)
 constexpr int kHubDppL = 3;   // 16-link sets in flight (4 tile reads + 1 value read each)
 
 // 16 links of one column chain: link 4i + j multiplies x = t[i][j] by the value that quad lane i
@@ -909,15 +814,10 @@ __device__ __forceinline__ void hub_links16(float& acc, const typename Vec<float
 #undef SRG_QP
 }
 
-// ABL (diagnostic ablations, SRGNN_HUB_ABLATION): 0 = the kernel; 1 = the consumer skips its
-// chains; 2 = the producers skip gathers and LDS writes; 3 = the consumer's fmas read registers
-// only (no LDS reads); 4 = producers gather but skip the LDS writes; 5 / 6 = the consumer reads
-// only the tile / only the values from LDS.
-// NP producer waves (8 by default; 4 -- the "lite" workgroup of the halo path's hub groups, 5 waves
-// instead of 9 -- keeps the same gathers in flight with half the waves and registers, so the row
-// chunks running beside hundreds of hub workgroups keep more of each CU)
-template <bool SFULL, typename IP, int ABL = 0, int EX = kEpiPlain, int W = kHubW, int NP = kHubProducers>
-__global__ void __launch_bounds__(64 * (NP + 1))
+// kHubProducers producer waves + the consumer (the round-1 ablations and the round-4 4-producer
+// "lite" workgroup were removed in round 5: DESIGN.md §5.1, §7)
+template <bool SFULL, typename IP, int EX = kEpiPlain, int W = kHubW>
+__global__ void __launch_bounds__(kHubThreads)
 k_spmm_hub(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
            const float* __restrict__ vals, const int32_t* __restrict__ hub_rows, int n_slices,
            const float* __restrict__ X, int64_t ldx, float* __restrict__ Y, int64_t ldy, int d,
@@ -925,8 +825,8 @@ k_spmm_hub(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
 {
     typedef typename Vec<float, 4>::type V4;
     extern __shared__ __attribute__((aligned(16))) float hub_lds[];
-    // [2 tiles][32 columns][HubGeom<W, NP>::LD] then [2][W] values
-    float* aval_base = hub_lds + 2 * HubGeom<W, NP>::TILE;
+    // [2 tiles][32 columns][HubGeom<W>::LD] then [2][W] values
+    float* aval_base = hub_lds + 2 * HubGeom<W>::TILE;
     const int item = blockIdx.x;
     const int row = hub_rows[item / n_slices];
     const int slice = item % n_slices;
@@ -953,7 +853,7 @@ k_spmm_hub(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
         for (int h = 0; h < n_win; ++h) {
             __syncthreads();                      // window h is in tile h & 1
             if (lane < kSliceCols) {
-                const float* tcol = hub_lds + (h & 1) * HubGeom<W, NP>::TILE + c * HubGeom<W, NP>::LD;
+                const float* tcol = hub_lds + (h & 1) * HubGeom<W>::TILE + c * HubGeom<W>::LD;
                 const float* av = aval_base + (h & 1) * W;
                 const int64_t sb = beg + (int64_t)h * W;
                 const int nb = (end - sb) < W ? (int)(end - sb) : W;
@@ -962,8 +862,8 @@ k_spmm_hub(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
 #pragma unroll
                     for (int i = 0; i < G; ++i) {
                         const int grp = set * G + i;
-                        if (ABL != 6) t[i] = *reinterpret_cast<const V4*>(tcol + ((grp ^ sw) << 2));
-                        if (ABL != 5) a[i] = *reinterpret_cast<const V4*>(av + (grp << 2));   // broadcast
+                        t[i] = *reinterpret_cast<const V4*>(tcol + ((grp ^ sw) << 2));
+                        a[i] = *reinterpret_cast<const V4*>(av + (grp << 2));   // broadcast
                     }
                 };
                 auto run = [&](const V4 (&t)[G], const V4 (&a)[G]) {
@@ -975,8 +875,7 @@ k_spmm_hub(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
                         acc = __builtin_fmaf(a[i][3], t[i][3], acc);
                     }
                 };
-                if (ABL == 1) continue;
-                if (kHubDpp && (ABL == 0 || ABL == 2 || ABL == 4) && nb == W) {
+                if (nb == W) {
                     // full window, values by DPP: per 16 links one ds_read_b128 of values (lane l
                     // reads values 16k + 4 (l & 3) .. +3, so register j of quad lane i holds value
                     // 16k + 4i + j) and four tile reads (4 links each); link 4i + j is
@@ -988,7 +887,7 @@ k_spmm_hub(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
                     constexpr int NK = W / 16;
                     const float* tb[8];
 #pragma unroll
-                    for (int k = 0; k < 8; ++k) tb[k] = hub_lds + (h & 1) * HubGeom<W, NP>::TILE + c * HubGeom<W, NP>::LD + ((k ^ sw) << 2);
+                    for (int k = 0; k < 8; ++k) tb[k] = hub_lds + (h & 1) * HubGeom<W>::TILE + c * HubGeom<W>::LD + ((k ^ sw) << 2);
                     const float* avl = av + 4 * (lane & 3);
                     auto rt = [&](int grp) { return *reinterpret_cast<const V4*>(tb[grp & 7] + (grp >> 3) * 32); };
                     auto rv = [&](int k) { return *reinterpret_cast<const V4*>(avl + 16 * k); };
@@ -1017,47 +916,6 @@ k_spmm_hub(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
                     }
                     continue;
                 }
-                if ((ABL == 0 || ABL == 2 || ABL == 4) && nb == W) {
-                    // full window, fully unrolled: every LDS read is a per-lane base (the XOR swizzle
-                    // of group k & 7 folded in, hoisted per window) or the value base, plus an
-                    // immediate offset -- no address arithmetic between the fmas.  A ring of kHubL
-                    // (tile, value) read pairs in flight (2 * kHubL <= 15 = lgkmcnt's range).
-                    // Same links, same order: the chain is unchanged.
-                    constexpr int NG = W / 4;
-                    const float* tb[8];
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) tb[k] = hub_lds + (h & 1) * HubGeom<W, NP>::TILE + c * HubGeom<W, NP>::LD + ((k ^ sw) << 2);
-                    auto rt = [&](int grp) { return *reinterpret_cast<const V4*>(tb[grp & 7] + (grp >> 3) * 32); };
-                    auto ra = [&](int grp) { return *reinterpret_cast<const V4*>(av + (grp << 2)); };
-                    V4 t[kHubL], a[kHubL];
-#pragma unroll
-                    for (int i = 0; i < kHubL; ++i) {
-                        t[i] = rt(i);
-                        a[i] = ra(i);
-                    }
-#pragma unroll
-                    for (int g0 = 0; g0 < NG; g0 += kHubL) {
-#pragma unroll
-                        for (int i = 0; i < kHubL; ++i) {
-                            const int grp = g0 + i;
-                            if (grp < NG) {
-                                acc = __builtin_fmaf(a[i][0], t[i][0], acc);
-                                acc = __builtin_fmaf(a[i][1], t[i][1], acc);
-                                acc = __builtin_fmaf(a[i][2], t[i][2], acc);
-                                acc = __builtin_fmaf(a[i][3], t[i][3], acc);
-                                if (grp + kHubL < NG) {
-                                    t[i] = rt(grp + kHubL);
-                                    a[i] = ra(grp + kHubL);
-                                }
-                                __builtin_amdgcn_sched_barrier(0);
-                            }
-                        }
-                    }
-                    continue;
-                }
-                if (ABL == 5 || ABL == 6)
-                    for (int i = 0; i < G; ++i)
-                        tA[i] = tB[i] = tC[i] = tD[i] = aA[i] = aB[i] = aC[i] = aD[i] = vzero<float, 4>();
                 // unconditional: sets past nc read stale tile / value words, never used (and the
                 // waitcnt pass then sees one issue order on every path into the loop)
                 ld(0, tA, aA);
@@ -1066,26 +924,25 @@ k_spmm_hub(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
                 __builtin_amdgcn_sched_barrier(0);
                 ld(2, tC, aC);
                 __builtin_amdgcn_sched_barrier(0);
-                if (ABL == 3) ld(3, tD, aD);
                 int k = 0;
                 // ring of four 8-link sets: every read is issued three sets (24 links) before its
                 // fmas, with at most 12 LDS reads outstanding (lgkmcnt counts 15).  The loop's
                 // loads are unconditional (k + 6 < nc) and the scheduling barriers keep the ring's
                 // order; the last <= 6 sets run after it.
                 for (; k + 7 <= nc; k += 4) {
-                    if (ABL != 3) ld(k + 3, tD, aD);
+                    ld(k + 3, tD, aD);
                     __builtin_amdgcn_sched_barrier(0);
                     run(tA, aA);
                     __builtin_amdgcn_sched_barrier(0);
-                    if (ABL != 3) ld(k + 4, tA, aA);
+                    ld(k + 4, tA, aA);
                     __builtin_amdgcn_sched_barrier(0);
                     run(tB, aB);
                     __builtin_amdgcn_sched_barrier(0);
-                    if (ABL != 3) ld(k + 5, tB, aB);
+                    ld(k + 5, tB, aB);
                     __builtin_amdgcn_sched_barrier(0);
                     run(tC, aC);
                     __builtin_amdgcn_sched_barrier(0);
-                    if (ABL != 3) ld(k + 6, tC, aC);
+                    ld(k + 6, tC, aC);
                     __builtin_amdgcn_sched_barrier(0);
                     run(tD, aD);
                     __builtin_amdgcn_sched_barrier(0);
@@ -1094,7 +951,7 @@ k_spmm_hub(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
                 if (k + 1 < nc) run(tB, aB);
                 if (k + 2 < nc) run(tC, aC);
                 for (int j = k + 3; j < nc; ++j) {
-                    if (ABL != 3) ld(j, tD, aD);
+                    ld(j, tD, aD);
                     run(tD, aD);
                 }
                 for (int q = nc * 4 * G; q < nb; ++q)
@@ -1108,8 +965,7 @@ k_spmm_hub(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
             else
                 yrow[ccol] = acc;
             if (epi.agg) epi.agg[(int64_t)row * epi.lda + ccol] = __fadd_rn(aprev, __fmul_rn(epi.w, acc));
-            if constexpr (EX == kEpiSend) send_row<1>(epi, row, ccol, acc);
-        }
+            }
         return;
     }
 
@@ -1119,38 +975,37 @@ k_spmm_hub(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
     const int qq = lane & 7;          // 16-byte chunk = columns qq*4 .. qq*4+3 of the slice
     const int qcol = slice * kSliceCols + qq * 4;
     const bool gact = SFULL || qcol < d;
-    V4 x0[HubGeom<W, NP>::UW], x1[HubGeom<W, NP>::UW];        // gathered windows, two register sets (even / odd windows)
-    float a0[HubGeom<W, NP>::UW], a1[HubGeom<W, NP>::UW];
-    int cn[HubGeom<W, NP>::UW];                   // column ids / values of the next window to gather
-    float an[HubGeom<W, NP>::UW];
+    V4 x0[HubGeom<W>::UW], x1[HubGeom<W>::UW];        // gathered windows, two register sets (even / odd windows)
+    float a0[HubGeom<W>::UW], a1[HubGeom<W>::UW];
+    int cn[HubGeom<W>::UW];                   // column ids / values of the next window to gather
+    float an[HubGeom<W>::UW];
     auto load_ids = [&](int w) {
         const int64_t sb = beg + (int64_t)w * W;
 #pragma unroll
-        for (int b = 0; b < HubGeom<W, NP>::UW; ++b) {
-            int64_t jj = sb + (p * HubGeom<W, NP>::UW + b) * 8 + g;
+        for (int b = 0; b < HubGeom<W>::UW; ++b) {
+            int64_t jj = sb + (p * HubGeom<W>::UW + b) * 8 + g;
             jj = jj < end ? jj : end - 1;
             cn[b] = indices[jj];
             an[b] = vals[jj];
         }
     };
-    auto gather = [&](V4 (&x)[HubGeom<W, NP>::UW], float (&a)[HubGeom<W, NP>::UW]) {
+    auto gather = [&](V4 (&x)[HubGeom<W>::UW], float (&a)[HubGeom<W>::UW]) {
 #pragma unroll
-        for (int b = 0; b < HubGeom<W, NP>::UW; ++b) {
-            x[b] = (gact && ABL != 2) ? gload<float, 4>(X + (int64_t)cn[b] * ldx + qcol) : vzero<float, 4>();
+        for (int b = 0; b < HubGeom<W>::UW; ++b) {
+            x[b] = gact ? gload<float, 4>(X + (int64_t)cn[b] * ldx + qcol) : vzero<float, 4>();
             a[b] = an[b];
         }
     };
-    auto put = [&](int w, const V4 (&x)[HubGeom<W, NP>::UW], const float (&a)[HubGeom<W, NP>::UW]) {
-        if (ABL == 2 || ABL == 4) return;
-        float* tile = hub_lds + (w & 1) * HubGeom<W, NP>::TILE;
+    auto put = [&](int w, const V4 (&x)[HubGeom<W>::UW], const float (&a)[HubGeom<W>::UW]) {
+        float* tile = hub_lds + (w & 1) * HubGeom<W>::TILE;
         float* av = aval_base + (w & 1) * W;
 #pragma unroll
-        for (int b = 0; b < HubGeom<W, NP>::UW; ++b) {
-            const int nl = (p * HubGeom<W, NP>::UW + b) * 8 + g;   // nonzero within the window
+        for (int b = 0; b < HubGeom<W>::UW; ++b) {
+            const int nl = (p * HubGeom<W>::UW + b) * 8 + g;   // nonzero within the window
 #pragma unroll
             for (int i = 0; i < 4; ++i) {             // transposed, swizzled: conflict-free
                 const int cc = qq * 4 + i;
-                tile[cc * HubGeom<W, NP>::LD + ((((nl >> 2) ^ hub_swz(cc)) << 2) | (nl & 3))] = x[b][i];
+                tile[cc * HubGeom<W>::LD + ((((nl >> 2) ^ hub_swz(cc)) << 2) | (nl & 3))] = x[b][i];
             }
             if (qq == 0) av[nl] = a[b];
         }
@@ -1612,77 +1467,27 @@ __global__ void k_dispatch_delay(int us)
     while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(16);
 }
 
-// Light rows per wave for wide panels (packed_rows).  Default: 512 / d rows, so that every lane holds
-// two 16-byte column chunks (d = 128: 4 rows, 16 lanes each; d = 256: 2 rows of 32 lanes; measured
-// best, profiles/r02_ab_d256.txt: 4 rows at d = 256 are 2 % slower than one row per wave).
-// SRGNN_PACKED_ROWS = 0 (one row per wave), 2, 4 or 8 overrides it; SRGNN_PACKED_U = gathers in
-// flight per row (2, 4 or 8).  Results are identical for every setting.
-constexpr int kPackedUDefault = 4;
-int packed_rows_setting(int d)
-{
-    static const int v = [] {
-        const char* e = getenv("SRGNN_PACKED_ROWS");
-        if (!e) return -1;
-        const int x = atoi(e);
-        return (x == 2 || x == 4 || x == 8) ? x : 0;
-    }();
-    if (v >= 0) return v;
-    // d = 32 (8 rows of 8 lanes, one chunk each) measured even with the narrow path on products
-    // (3.46 vs 3.42 ms per hop) and within 3 % on the RMAT-26 wavelet blocks: off unless asked for
-    // (SRGNN_PACKED_D32=1; profiles/r02_ab_d32.txt)
-    static const bool d32 = [] { const char* e = getenv("SRGNN_PACKED_D32"); return e ? atoi(e) != 0 : false; }();
-    return d == 32 ? (d32 ? 8 : 0) : d == 64 ? 8 : d == 128 ? 4 : d == 256 ? 2 : 0;
-}
-// XCD-aware slice waves (k_spmm<..., XH>), on by default; SRGNN_XCD_HEAVY=0 turns them off.  Results are
-// identical either way.  Measured (profiles/r02_ab_xh*.txt): products hop 7.49 -> 7.31 ms at the same
-// threshold, 7.18-7.23 ms over thresholds 128-1024; arxiv, papers100M and RMAT-26 unchanged.
-bool xcd_heavy_setting()
-{
-    static const bool v = [] { const char* e = getenv("SRGNN_XCD_HEAVY"); return e ? atoi(e) != 0 : true; }();
-    return v;
-}
-// LDS a k_spmm block needs (its waves' slice tiles), and what a launch reserves: with
-// SRG_SPMM_CAP_WAVES and a cap of W waves per SIMD (SRGNN_SPMM_WAVES, default kSpmmWavesDefault;
-// 0 = none) each 4-wave block reserves ~160 KiB / (W + 0.5), so at most W blocks -- W waves per
-// SIMD -- share a CU.  Fewer waves gather from fewer rows at once and the L2 re-serves more of their
-// lines: products 6.08 -> 5.96 ms per hop and 35.4 -> 31.3 GB of traffic at W = 5 without the slice
-// waves' id prefetch, 5.84 -> 5.81 ms with it (whose registers already hold the kernel at 6 waves);
-// arxiv (an 87 MB panel) is 3 % faster uncapped, the halo chunks flat (profiles/r04v_*, r04w_*, r04x_*).
+// Light rows per wave for wide panels (packed_rows): 512 / d rows, so that every lane holds two
+// 16-byte column chunks (d = 64: 8 rows of 8 lanes, d = 128: 4 rows of 16 lanes, d = 256: 2 rows of 32
+// lanes; measured best, profiles/r02_ab_d256.txt: 4 rows at d = 256 are 2 % slower than one row per
+// wave; d = 32 packed measured even with the narrow path, profiles/r02_ab_d32.txt), 4 gathers per row in
+// flight (2 with SRG_SPMM_PACKED_U2; 8 measured slower).  Results are identical for every setting.
+constexpr int kPackedU = 4;
+constexpr int packed_rows_for(int d) { return d == 64 ? 8 : d == 128 ? 4 : d == 256 ? 2 : 0; }
+// LDS a k_spmm block needs (its waves' slice tiles), and what a launch reserves with
+// SRG_SPMM_CAP_WAVES: ~160 KiB / (5 + 0.5) per 4-wave block, so at most 5 blocks -- 5 waves per SIMD --
+// share a CU (gfx950's 160 KiB LDS; below the 64 KiB default dynamic-LDS limit).  Fewer waves gather
+// from fewer rows at once and the L2 re-serves more of their lines: products 6.08 -> 5.96 ms per hop
+// and 35.4 -> 31.3 GB of traffic at 5 waves without the slice waves' id prefetch, 5.84 -> 5.81 ms with
+// it (whose registers already hold the kernel at 6 waves); 4 and 3 waves lose; arxiv (an 87 MB panel)
+// is 3 % faster uncapped, the halo chunks flat (profiles/r04v_*, r04w_*, r04x_*).
 constexpr int kSpmmLdsBytes = kWavesPerBlock * kSliceLdsBufs * 256 * (int)sizeof(float);
-constexpr int kSpmmWavesDefault = 5;
-int spmm_lds_bytes(uint32_t flags)
-{
-    static const int v = [] {
-        const char* e = getenv("SRGNN_SPMM_WAVES");
-        const int w = e ? atoi(e) : kSpmmWavesDefault;
-        if (w <= 0 || w >= 8) return kSpmmLdsBytes;
-        const int b = (int)((160.0 * 1024.0) / (w + 0.5)) / 512 * 512;
-        return b > kSpmmLdsBytes ? b : kSpmmLdsBytes;
-    }();
-    return (flags & SRG_SPMM_CAP_WAVES) ? v : kSpmmLdsBytes;
-}
-int packed_u_setting()
-{
-    static const int v = [] {
-        const char* e = getenv("SRGNN_PACKED_U");
-        const int x = e ? atoi(e) : kPackedUDefault;
-        return (x == 2 || x == 4 || x == 8) ? x : kPackedUDefault;
-    }();
-    return v;
-}
-
-// producer waves of the wide hub launches' workgroups: 8, or 4 (SRGNN_HUB_PRODUCERS)
-int hub_producers()
-{
-    static const int np = [] { const char* e = getenv("SRGNN_HUB_PRODUCERS"); return (e && atoi(e) == 4) ? 4 : 8; }();
-    return np;
-}
-
-int hub_delay_us()
-{
-    static const int us = [] { const char* e = getenv("SRGNN_HUB_DISPATCH_DELAY_US"); return e ? atoi(e) : 10; }();
-    return us;
-}
+constexpr int kSpmmCapLdsBytes = (int)((160.0 * 1024.0) / 5.5) / 512 * 512;
+static_assert(kSpmmCapLdsBytes > kSpmmLdsBytes && kSpmmCapLdsBytes <= 65536, "k_spmm's capped LDS reservation");
+constexpr int spmm_lds_bytes(uint32_t flags) { return (flags & SRG_SPMM_CAP_WAVES) ? kSpmmCapLdsBytes : kSpmmLdsBytes; }
+// the single-wave delay after a hub fork (10 us: 0 and 5 stay bimodal, 20 is 1-3 % slower,
+// profiles/r01_dispatch_delay_sweep.txt)
+constexpr int kHubDelayUs = 10;
 
 // Hub side streams.  One per (device, caller stream), created on first use, each with its own
 // fork / join events: callers on different streams never share events.  The whole fork sequence
@@ -1709,23 +1514,13 @@ template <typename IP>
 int hub_attrs()
 {
     for (const void* fn : {(const void*)k_spmm_hub<true, IP>, (const void*)k_spmm_hub<false, IP>,
-                           (const void*)k_spmm_hub<true, IP, 0, kEpiSend>, (const void*)k_spmm_hub<false, IP, 0, kEpiSend>,
-                           (const void*)k_spmm_hub<true, IP, 0, kEpiCheby>, (const void*)k_spmm_hub<false, IP, 0, kEpiCheby>,
-                           (const void*)k_spmm_hub<true, IP, 0, kEpiSpan>, (const void*)k_spmm_hub<false, IP, 0, kEpiSpan>,
-                           (const void*)k_spmm_hub<true, IP, 1>, (const void*)k_spmm_hub<true, IP, 2>,
-                           (const void*)k_spmm_hub<true, IP, 3>, (const void*)k_spmm_hub<true, IP, 4>,
-                           (const void*)k_spmm_hub<true, IP, 5>, (const void*)k_spmm_hub<true, IP, 6>})
+                           (const void*)k_spmm_hub<true, IP, kEpiCheby>, (const void*)k_spmm_hub<false, IP, kEpiCheby>,
+                           (const void*)k_spmm_hub<true, IP, kEpiSpan>, (const void*)k_spmm_hub<false, IP, kEpiSpan>})
         SRG_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kHubLdsBytes));
-    for (const void* fn : {(const void*)k_spmm_hub<true, IP, 0, false, 256>, (const void*)k_spmm_hub<false, IP, 0, false, 256>,
-                           (const void*)k_spmm_hub<true, IP, 0, kEpiSend, 256>, (const void*)k_spmm_hub<false, IP, 0, kEpiSend, 256>,
-                           (const void*)k_spmm_hub<true, IP, 0, kEpiCheby, 256>, (const void*)k_spmm_hub<false, IP, 0, kEpiCheby, 256>,
-                           (const void*)k_spmm_hub<true, IP, 0, kEpiSpan, 256>, (const void*)k_spmm_hub<false, IP, 0, kEpiSpan, 256>})
+    for (const void* fn : {(const void*)k_spmm_hub<true, IP, kEpiPlain, 256>, (const void*)k_spmm_hub<false, IP, kEpiPlain, 256>,
+                           (const void*)k_spmm_hub<true, IP, kEpiCheby, 256>, (const void*)k_spmm_hub<false, IP, kEpiCheby, 256>,
+                           (const void*)k_spmm_hub<true, IP, kEpiSpan, 256>, (const void*)k_spmm_hub<false, IP, kEpiSpan, 256>})
         SRG_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)HubGeom<256>::LDS_BYTES));
-    for (const void* fn : {(const void*)k_spmm_hub<true, IP, 0, false, 256, 4>, (const void*)k_spmm_hub<false, IP, 0, false, 256, 4>,
-                           (const void*)k_spmm_hub<true, IP, 0, kEpiSend, 256, 4>, (const void*)k_spmm_hub<false, IP, 0, kEpiSend, 256, 4>,
-                           (const void*)k_spmm_hub<true, IP, 0, kEpiCheby, 256, 4>, (const void*)k_spmm_hub<false, IP, 0, kEpiCheby, 256, 4>,
-                           (const void*)k_spmm_hub<true, IP, 0, kEpiSpan, 256, 4>, (const void*)k_spmm_hub<false, IP, 0, kEpiSpan, 256, 4>})
-        SRG_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)HubGeom<256, 4>::LDS_BYTES));
     return SRG_OK;
 }
 
@@ -1761,12 +1556,11 @@ int side_stream_locked(hipStream_t caller, SideStream** out)
     ss.last_use = ++g_side_tick;
     if (!ss.stream) {
         // highest queue priority: the hub workgroups (9 waves, ~136 KB LDS each) must get CUs
-        // before the main launch's many small blocks occupy them all
-        // (SRGNN_HUB_PRIORITY=normal: the caller streams' priority instead, for A/B runs)
+        // before the main launch's many small blocks occupy them all (normal priority measured the
+        // same or slower: DESIGN.md §7, round 4)
         int least = 0, greatest = 0;
         SRG_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-        static const bool normal = [] { const char* e = getenv("SRGNN_HUB_PRIORITY"); return e && !strcmp(e, "normal"); }();
-        SRG_HIP_CHECK(hipStreamCreateWithPriority(&ss.stream, hipStreamNonBlocking, normal ? least : greatest));
+        SRG_HIP_CHECK(hipStreamCreateWithPriority(&ss.stream, hipStreamNonBlocking, greatest));
         SRG_HIP_CHECK(hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming));
         SRG_HIP_CHECK(hipEventCreateWithFlags(&ss.join, hipEventDisableTiming));
     }
@@ -1876,9 +1670,6 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
     SideStream* ss = nullptr;
     std::unique_lock<std::mutex> side_lock(g_side_mu, std::defer_lock);
     const bool fast = (flags & SRG_SPMM_FAST) && (EX == kEpiPlain || EX == kEpiSpan) && !epi.agg;
-    if (EX == kEpiSpanRA && n_hub > 0)
-        return fail(SRG_ERR_INVALID, "per-row accumulation (row_first) takes no hub rows: n_hub=%lld", (long long)n_hub);
-    if constexpr (EX != kEpiSpanRA) {
     if (n_hub > 0 && fast) {   // fork: the hub rows' segments, then their sums, beside the main launch
         side_lock.lock();
         int rc = side_stream_locked(s, &ss);
@@ -1927,42 +1718,27 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
             SRG_HIP_CHECK(hipStreamWaitEvent(ss->stream, ss->fork, 0));
         }
         const dim3 hgrid((unsigned)(n_hub * n_slices));
-        static const int abl = [] { const char* e = getenv("SRGNN_HUB_ABLATION"); return e ? atoi(e) : 0; }();
-        if (EX == kEpiPlain && sfull && abl >= 1 && abl <= 6) {
-            auto k = abl == 1 ? k_spmm_hub<true, IP, 1> : abl == 2 ? k_spmm_hub<true, IP, 2>
-                   : abl == 3 ? k_spmm_hub<true, IP, 3> : abl == 4 ? k_spmm_hub<true, IP, 4>
-                   : abl == 5 ? k_spmm_hub<true, IP, 5> : k_spmm_hub<true, IP, 6>;
-            hipLaunchKernelGGL(k, hgrid, dim3(kHubThreads), kHubLdsBytes, ss->stream, indptr, indices, vals,
-                               order, n_slices, X, ldx, Y, ldy, d, acc, nt, epi);
+        // 256-nonzero windows (two workgroups per CU) once a launch has more hub workgroups than CUs
+        const bool w256 = n_hub * n_slices > kHubWideLaunch || (flags & SRG_SPMM_HUB_W256);
+#define SRG_LAUNCH_HUB(SF, WW)                                                                                      \
+    hipLaunchKernelGGL((k_spmm_hub<SF, IP, EX, WW>), hgrid, dim3(kHubThreads), (HubGeom<WW>::LDS_BYTES), ss->stream, \
+                       indptr, indices, vals, order, n_slices, X, ldx, Y, ldy, d, acc, nt, epi)
+        if (sfull) {
+            if (w256) SRG_LAUNCH_HUB(true, 256);
+            else SRG_LAUNCH_HUB(true, 512);
         } else {
-            static const int wide_env = [] { const char* e = getenv("SRGNN_HUB_WIDE_LAUNCH"); return e ? atoi(e) : -1; }();
-            const int64_t wide = wide_env >= 0 ? wide_env : kHubWideLaunch;
-            const bool w256 = n_hub * n_slices > wide || (flags & (SRG_SPMM_HUB_W256 | SRG_SPMM_HUB_LITE));
-            // the wide launches (more hub workgroups than CUs) may take the 4-producer workgroup
-            const bool lite = (w256 && hub_producers() == 4) || (flags & SRG_SPMM_HUB_LITE);
-#define SRG_LAUNCH_HUB(SF, WW, NPP)                                                                                 \
-    hipLaunchKernelGGL((k_spmm_hub<SF, IP, 0, EX, WW, NPP>), hgrid, dim3(64 * (NPP + 1)), (HubGeom<WW, NPP>::LDS_BYTES), \
-                       ss->stream, indptr, indices, vals, order, n_slices, X, ldx, Y, ldy, d, acc, nt, epi)
-            if (sfull) {
-                if (lite) SRG_LAUNCH_HUB(true, 256, 4);
-                else if (w256) SRG_LAUNCH_HUB(true, 256, 8);
-                else SRG_LAUNCH_HUB(true, 512, 8);
-            } else {
-                if (lite) SRG_LAUNCH_HUB(false, 256, 4);
-                else if (w256) SRG_LAUNCH_HUB(false, 256, 8);
-                else SRG_LAUNCH_HUB(false, 512, 8);
-            }
-#undef SRG_LAUNCH_HUB
+            if (w256) SRG_LAUNCH_HUB(false, 256);
+            else SRG_LAUNCH_HUB(false, 512);
         }
+#undef SRG_LAUNCH_HUB
         SRG_HIP_CHECK(hipGetLastError());
         SRG_HIP_CHECK(hipEventRecord(ss->join, ss->stream));
         ss->pending = (flags & SRG_SPMM_HUB_NOJOIN) != 0;
-        if (!cont && hub_delay_us() > 0) {
-            hipLaunchKernelGGL(k_dispatch_delay, dim3(1), dim3(64), 0, s, hub_delay_us());
+        if (!cont) {
+            hipLaunchKernelGGL(k_dispatch_delay, dim3(1), dim3(64), 0, s, kHubDelayUs);
             SRG_HIP_CHECK(hipGetLastError());
         }
     }
-    }   // EX != kEpiSpanRA
 
     const int32_t* morder = order ? order + n_hub : nullptr;
     const int64_t m_rows = n_rows - n_hub;
@@ -1970,23 +1746,22 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
     const int64_t n_light = m_rows - n_heavy;
     // light rows: LR rows per wave (packed_rows) when the column tiles line up; else, for d <= 32,
     // 64 / S rows per wave (narrow_rows); else one row per wave
-    int lr = 0, lq = 0;
+    int lr = 0;
     if (!(flags & SRG_SPMM_WIDE_ROWS)) {
-        const int cand = packed_rows_setting(d);
+        const int cand = packed_rows_for(d);
         const int S = cand ? 64 / cand : 0;
         const int q = cand ? d / (4 * S) : 0;
-        const bool ok = cand && d % (4 * S) == 0 && (q == 1 || q == 2 || q == 4) && ldx % 4 == 0 &&
+        const bool ok = cand && d % (4 * S) == 0 && q == 2 && ldx % 4 == 0 &&
                         ldy % 4 == 0 && aligned(X, 16) && aligned(Y, 16) &&
                         (!epi.agg || (epi.lda % 4 == 0 && aligned(epi.agg, 16))) &&
-                        (!epi.send || (epi.lds % 4 == 0 && aligned(epi.send, 16))) &&
                         (EX != kEpiCheby || (epi.ldo % 4 == 0 && aligned(epi.cto, 16) && epi.ldr % 4 == 0 &&
                                              epi.r_stride % 4 == 0 && aligned(epi.R, 16)));
-        if (ok) { lr = cand; lq = q; }
+        if (ok) lr = cand;
     }
     const int ns = (!lr && d <= 32 && !(flags & SRG_SPMM_WIDE_ROWS)) ? (d <= 1 ? 1 : d <= 2 ? 2 : d <= 4 ? 4 : d <= 8 ? 8 : d <= 16 ? 16 : 32) : 0;
     const int64_t rows_per_block = (int64_t)kWavesPerBlock * (ns ? 64 / ns : lr ? lr : 1);
     // XCD-aware slice waves (k_spmm<..., XH>) with packed light rows, 2 / 4 / 8 slices
-    const bool xh = xcd_heavy_setting() && lr && (n_slices == 2 || n_slices == 4 || n_slices == 8);
+    const bool xh = lr && (n_slices == 2 || n_slices == 4 || n_slices == 8);
     int nb_heavy_launch = nb_heavy;
     if (xh) {
         const int64_t per = 8 / n_slices;
@@ -1997,14 +1772,13 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
     const int64_t blocks = nb_heavy_launch + (n_light + rows_per_block - 1) / rows_per_block;
     if (blocks > INT32_MAX) return fail(SRG_ERR_INVALID, "grid too large");
     int vec = pick_vec(d, ldx, ldy, X, Y, sizeof(float));
-    if (epi.send) vec = std::min(vec, pick_vec(d, epi.lds, epi.lds, epi.send, epi.send, sizeof(float)));
     if (epi.agg) vec = std::min(vec, pick_vec(d, epi.lda, epi.lda, epi.agg, epi.agg, sizeof(float)));
     if (EX == kEpiCheby) {
         vec = std::min(vec, pick_vec(d, epi.ldo, epi.ldr, epi.cto, epi.R, sizeof(float)));
         while (vec > 1 && epi.r_stride % vec) vec /= 2;
     }
     const int nr = (int)m_rows, nh = (int)n_heavy;
-    const int pu = (flags & SRG_SPMM_PACKED_U2) ? 2 : packed_u_setting();
+    const int pu = (flags & SRG_SPMM_PACKED_U2) ? 2 : kPackedU;
     const unsigned shm = (unsigned)spmm_lds_bytes(flags);
     for (int64_t b0 = 0; b0 < blocks; b0 += kMaxLaunchBlocks) {
         const dim3 grid((unsigned)std::min<int64_t>(kMaxLaunchBlocks, blocks - b0));
@@ -2031,22 +1805,16 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
     } while (0)
 #define SRG_LAUNCH_PACKED_U(LRV, LQV)                                                                 \
     do {                                                                                              \
-        if (pu == 4) SRG_LAUNCH_PACKED(LRV, LQV, 4);                                                  \
-        else if (pu == 2) SRG_LAUNCH_PACKED(LRV, LQV, 2);                                             \
-        else SRG_LAUNCH_PACKED(LRV, LQV, 8);                                                          \
+        if (pu == 2) SRG_LAUNCH_PACKED(LRV, LQV, 2);                                                  \
+        else SRG_LAUNCH_PACKED(LRV, LQV, 4);                                                          \
     } while (0)
+        // packed_rows_for gives two 16-byte chunks per lane (LQ = 2) at d = 64 / 128 / 256
         if (lr == 2) {
-            if (lq == 1) SRG_LAUNCH_PACKED_U(2, 1);
-            else if (lq == 2) SRG_LAUNCH_PACKED_U(2, 2);
-            else SRG_LAUNCH_PACKED_U(2, 4);
+            SRG_LAUNCH_PACKED_U(2, 2);
         } else if (lr == 4) {
-            if (lq == 1) SRG_LAUNCH_PACKED_U(4, 1);
-            else if (lq == 2) SRG_LAUNCH_PACKED_U(4, 2);
-            else SRG_LAUNCH_PACKED_U(4, 4);
+            SRG_LAUNCH_PACKED_U(4, 2);
         } else if (lr == 8) {
-            if (lq == 1) SRG_LAUNCH_PACKED_U(8, 1);
-            else if (lq == 2) SRG_LAUNCH_PACKED_U(8, 2);
-            else SRG_LAUNCH_PACKED_U(8, 4);
+            SRG_LAUNCH_PACKED_U(8, 2);
         } else if (ns == 32) {
             if (sfull) SRG_LAUNCH_NARROW(32, true);
             else SRG_LAUNCH_NARROW(32, false);
@@ -2280,7 +2048,7 @@ int srg_spmm_agg_f32(const int64_t* indptr, const int32_t* indices, const float*
         return fail(SRG_ERR_INVALID, "aggregation panel: agg=%p lda=%lld < d=%d", (void*)agg, (long long)lda, d);
     if (agg && agg == Y) return fail(SRG_ERR_INVALID, "agg must not alias Y");
     rc = launch_spmm<int64_t>(indptr, indices, values, n_rows, row_order, n_hub, n_heavy, X, ldx, Y, ldy, d, flags,
-                              static_cast<hipStream_t>(stream), Epi{agg, lda, w, agg_init ? 1 : 0, nullptr, 0, nullptr, nullptr});
+                              static_cast<hipStream_t>(stream), Epi{agg, lda, w, agg_init ? 1 : 0});
     return rc ? rc : ok();
 }
 
@@ -2303,44 +2071,6 @@ int srg_spmm_span_f32(const int64_t* row_beg, const int64_t* row_end, const int3
     e.row_end = row_end;
     rc = launch_spmm<int64_t, kEpiSpan>(row_beg, indices, values, n_rows, row_order, n_hub, n_heavy, X, ldx, Y, ldy,
                                         d, flags, static_cast<hipStream_t>(stream), e);
-    return rc ? rc : ok();
-}
-
-int srg_spmm_span_rowacc_f32(const int64_t* row_beg, const int64_t* row_end, const int64_t* row_first,
-                             const int32_t* indices, const float* values, int64_t n_rows, const int32_t* row_order,
-                             int64_t n_heavy, const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t d,
-                             uint32_t flags, void* stream)
-{
-    SRG_DEVICE_GUARD(stream);
-    int rc = check_spmm_args(row_beg, indices, values, n_rows, X, ldx, Y, ldy, d);
-    if (rc) return rc;
-    if (n_rows > 0 && (!row_end || !row_first)) return fail(SRG_ERR_INVALID, "null row_end / row_first");
-    if (flags & (SRG_SPMM_ACCUMULATE | SRG_SPMM_FAST | SRG_SPMM_HUB_NOJOIN | SRG_SPMM_HUB_CONTINUE))
-        return fail(SRG_ERR_INVALID, "flags 0x%x: the accumulation is per row here, and there are no hub rows", flags);
-    Epi e{};
-    e.row_end = row_end;
-    e.row_first = row_first;
-    rc = launch_spmm<int64_t, kEpiSpanRA>(row_beg, indices, values, n_rows, row_order, 0, n_heavy, X, ldx, Y, ldy, d,
-                                          flags, static_cast<hipStream_t>(stream), e);
-    return rc ? rc : ok();
-}
-
-int srg_spmm_send_f32(const int64_t* indptr, const int32_t* indices, const float* values,
-                      int64_t n_rows, const int32_t* row_order, int64_t n_hub, int64_t n_heavy,
-                      const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t d, uint32_t flags,
-                      float* send, int64_t lds, const int64_t* send_ptr, const int32_t* send_slot,
-                      void* stream)
-{
-    SRG_DEVICE_GUARD(stream);
-    int rc = check_spmm_args(indptr, indices, values, n_rows, X, ldx, Y, ldy, d);
-    if (rc) return rc;
-    if (n_rows > 0 && d > 0 && send && (lds < d || !send_ptr || !send_slot))
-        return fail(SRG_ERR_INVALID, "send buffer: lds=%lld < d=%d or null slot map", (long long)lds, d);
-    rc = send ? launch_spmm<int64_t, kEpiSend>(indptr, indices, values, n_rows, row_order, n_hub, n_heavy, X, ldx, Y, ldy,
-                                           d, flags, static_cast<hipStream_t>(stream),
-                                           Epi{nullptr, 0, 0.0f, 0, send, lds, send_ptr, send_slot})
-              : launch_spmm<int64_t>(indptr, indices, values, n_rows, row_order, n_hub, n_heavy, X, ldx, Y, ldy, d,
-                                     flags, static_cast<hipStream_t>(stream));
     return rc ? rc : ok();
 }
 

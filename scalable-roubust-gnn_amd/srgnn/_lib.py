@@ -27,7 +27,6 @@ SRG_SPMM_HUB_NOJOIN = 0x10
 SRG_SPMM_PACKED_U2 = 0x20
 SRG_SPMM_FAST = 0x40
 SRG_SPMM_HUB_CONTINUE = 0x80
-SRG_SPMM_HUB_LITE = 0x100
 SRG_SPMM_CAP_WAVES = 0x200
 
 SRG_CHEBY_INIT = 0
@@ -65,17 +64,12 @@ EXPORTED_SYMBOLS = (
     "srg_spmm_csr_f32",
     "srg_propagate_khop_f32",
     "srg_propagate_plan_f32",
-    "srg_stream_layout_size",
-    "srg_stream_layout_build",
-    "srg_spmm_stream_f32",
     "srg_cheby_step_f64",
     "srg_cheby_step_f32",
     "srg_cheby_epilogue_f32",
     "srg_hop_accumulate_f32",
     "srg_spmm_agg_f32",
     "srg_spmm_span_f32",
-    "srg_spmm_span_rowacc_f32",
-    "srg_spmm_send_f32",
     "srg_spmm_cheby_f32",
     "srg_tail_record_f32",
     "srg_tail_rowsum_f32",
@@ -137,12 +131,6 @@ def _declare(lib):
     lib.srg_propagate_khop_f32.restype = ctypes.c_int
     lib.srg_propagate_plan_f32.argtypes = [_p, _i32, _i32, _p, _i64, _i32, _i32, _p]
     lib.srg_propagate_plan_f32.restype = ctypes.c_int
-    lib.srg_stream_layout_size.argtypes = [_p, _i64, _p, _p, _i32, _i64, ctypes.POINTER(_i64), ctypes.POINTER(_i64), _p]
-    lib.srg_stream_layout_size.restype = ctypes.c_int
-    lib.srg_stream_layout_build.argtypes = [_p, _i64, _p, _p, _p, _p, _i32, _i64, _i64, _i64, _p, _p, _p, _p, _p]
-    lib.srg_stream_layout_build.restype = ctypes.c_int
-    lib.srg_spmm_stream_f32.argtypes = [_p, _p, _p, _p, _i64, _i64, _p, _i64, _p, _i64, _i32, _u32, _p]
-    lib.srg_spmm_stream_f32.restype = ctypes.c_int
     lib.srg_cheby_step_f64.argtypes = [_p, _p, _p, _i64, _p, _p, _p, _p, _i64, _i32, ctypes.c_int,
                                        _f64, _f64, _p, _p, _i32, _p, _i64, _p]
     lib.srg_cheby_step_f64.restype = ctypes.c_int
@@ -162,9 +150,6 @@ def _declare(lib):
     lib.srg_csr_col_splits.restype = ctypes.c_int
     lib.srg_csr_mirror.argtypes = [_p, _p, _p, _i64, _i64, _p, _p]
     lib.srg_csr_mirror.restype = ctypes.c_int
-    lib.srg_spmm_send_f32.argtypes = [_p, _p, _p, _i64, _p, _i64, _i64, _p, _i64, _p, _i64, _i32, ctypes.c_uint32,
-                                      _p, _i64, _p, _p, _p]
-    lib.srg_spmm_send_f32.restype = ctypes.c_int
     lib.srg_spmm_cheby_f32.argtypes = [_p, _p, _p, _i64, _p, _i64, _i64, _p, _i64, _p, _i64, _i32, ctypes.c_uint32,
                                        ctypes.c_int, _f32, _f32, _p, _i64, _p, _p, _i32, _p, _i64, _i64, _p]
     lib.srg_spmm_cheby_f32.restype = ctypes.c_int
@@ -209,8 +194,6 @@ def _declare(lib):
     lib.srg_dist_propagate_khop_f32.restype = ctypes.c_int
     lib.srg_csr_copy_spans.argtypes = [_p, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p]
     lib.srg_csr_copy_spans.restype = ctypes.c_int
-    lib.srg_spmm_span_rowacc_f32.argtypes = [_p, _p, _p, _p, _p, _i64, _p, _i64, _p, _i64, _p, _i64, _i32, _u32, _p]
-    lib.srg_spmm_span_rowacc_f32.restype = ctypes.c_int
     lib.srg_halo_plan_build.argtypes = [_p, _p, _i64, _i32, _i32, _i32, _i64, _i64, _i32, ctypes.POINTER(_p)]
     lib.srg_halo_plan_destroy.argtypes = [_p]
     lib.srg_halo_plan_info.argtypes = [_p, ctypes.POINTER(HaloInfo)]

@@ -19,7 +19,6 @@ only decides which wave works on what and when (power-law hubs start first).
 """
 from __future__ import annotations
 
-import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -28,24 +27,24 @@ import torch
 from . import _lib
 
 # Rows longer than the heavy threshold take the slice-wave path; shorter ones the row path (packed
-# 512 / d rows per wave at d = 64, 128, 256).  "auto" (default): auto_heavy_threshold(nnz).
-_HEAVY_ENV = os.environ.get("SRGNN_HEAVY_THRESHOLD", "auto")
-DEFAULT_HEAVY_THRESHOLD = None if _HEAVY_ENV == "auto" else int(_HEAVY_ENV)
+# 512 / d rows per wave at d = 64, 128, 256).  None (default): auto_heavy_threshold(nnz); callers pass
+# heavy_threshold to force one.
+DEFAULT_HEAVY_THRESHOLD = None
 # Narrow panels (d <= 32) run their light rows as 64 / S single-lane-per-column rows per wave, whose
 # cost per nonzero is a full dependent gather: they keep the slice waves from 32 up (profiles/
 # r02_ab_auto.txt: d = 8 hop 3.34 ms at 32 vs 3.76 at the wide auto threshold; the RMAT-26 wavelet
 # in 32-column blocks 63.8 vs 98.9 ms per block).  Used when the wide threshold is automatic.
-NARROW_HEAVY_THRESHOLD = int(os.environ.get("SRGNN_NARROW_HEAVY_THRESHOLD", "32"))
+NARROW_HEAVY_THRESHOLD = 32
 # Column blocks: rows of at most this many nonzeros are not cut but computed whole in block 0
 # (DeviceCSR.column_blocks); 0 cuts every row.
 # Round 4: 48 (products 5.63 -> 5.58 ms per hop at six blocks, 5.53 at seven; 64: the same, 96: 5.62;
 # papers100M 236.7 -> 236.1 ms, RMAT-26 307.6 -> 307.1; profiles/r04ag_*, r04ah_*).  Round 2: 32.
-BLOCK_WHOLE_MAX = int(os.environ.get("SRGNN_BLOCK_WHOLE_MAX", "48"))
+BLOCK_WHOLE_MAX = 48             # = kBlockWholeMax of the C halo planner (srg_halo.hip)
 # "auto": rows whose slice-wave time (~40 ns per nonzero, measured) would exceed about half of the
 # expected hop time (~nnz / 13.5e9 s at the measured hop rate) go to the hub path:
 # threshold = nnz // 1024, at least 8192.  Products on 1 GPU -> only the top hub; 1/8 of it -> ~15 K.
-_HUB_ENV = os.environ.get("SRGNN_HUB_THRESHOLD", "auto")
-DEFAULT_HUB_THRESHOLD = None if _HUB_ENV == "auto" else int(_HUB_ENV)
+# None (default): automatic; callers pass hub_threshold to force one.
+DEFAULT_HUB_THRESHOLD = None
 
 
 def auto_hub_threshold(nnz: int, launches: int = 1) -> int:
@@ -382,8 +381,8 @@ def make_schedule(indptr: torch.Tensor, heavy_threshold=None, hub_threshold=None
 # (650-1300; 2000+ entries: 6.84); papers100M 239.0 -> 237.4 ms, RMAT-26 307.7 -> 306.2
 # (profiles/r04ab_*, r04ac_*, r04ad_*).  At eight blocks (nnz_b ~ 14.5 M, shorter launches) the cliff
 # comes sooner: 5.51 ms at 30000 and 20000 (~485 / ~730 entries), 7.04 at 12000 (~1200;
-# r04ap_*), so 30000 keeps the margin.  SRGNN_BLOCK_HEAVY_PER overrides.
-BLOCK_HEAVY_PER = int(os.environ.get("SRGNN_BLOCK_HEAVY_PER", "30000"))
+# r04ap_*), so 30000 keeps the margin.
+BLOCK_HEAVY_PER = 30000
 
 
 def schedule_from_degrees(deg: torch.Tensor, nnz: int, heavy_threshold=None, hub_threshold=None,

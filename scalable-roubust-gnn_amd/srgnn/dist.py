@@ -20,7 +20,6 @@ GPU: the multi-GPU results are bitwise equal to the single-GPU ones.
 """
 from __future__ import annotations
 
-import os
 
 import numpy as np
 import torch
@@ -258,42 +257,19 @@ def ghost_plan(halos, elig, deg, owner, gip, starts, caps=GHOST_CAPS, link_bps=N
 # prefetch; profiles/r04ak_*, r04al_halo_heavy_ab.txt).  papers100M / RMAT-26 ranks are above it.
 HALO_HEAVY_MIN = 192
 
-# column blocks per row-chunk launch of the halo path for large local panels (1 = off);
-# SRGNN_HALO_COL_BLOCKS overrides.  Bitwise the same hops either way.  Default: 8 for local panels of
-# >= 8 GiB at d >= 256 (RMAT-26 at P = 8, 23.8 GB of [own | halo] rows of 1 KiB: per-rank hop 46.4 ms
-# at B = 1, 43.6 at 4, 40.7 at 8, 41.3 at 12, 43.6 at 32), else 1 (papers100M at d = 128 is flat over
-# B = 1..16, products at P = 8 slower; profiles/r04_halo_col_blocks_p8.txt)
-_HALO_COL_BLOCKS_ENV = os.environ.get("SRGNN_HALO_COL_BLOCKS")
-AUTO_HALO_COL_BLOCKS = int(_HALO_COL_BLOCKS_ENV) if _HALO_COL_BLOCKS_ENV else 1
+# column blocks per row-chunk launch of the halo path for large local panels (1 = off; the
+# operator's col_blocks argument forces a count).  Bitwise the same hops either way.  Default: 8 for
+# local panels of >= 8 GiB at d >= 256 (RMAT-26 at P = 8, 23.8 GB of [own | halo] rows of 1 KiB: per-rank
+# hop 46.4 ms at B = 1, 43.6 at 4, 40.7 at 8, 41.3 at 12, 43.6 at 32), else 1 (papers100M at d = 128 is
+# flat over B = 1..16, products at P = 8 slower; profiles/r04_halo_col_blocks_p8.txt)
 WIDE_HALO_COL_BLOCKS = 8
 WIDE_HALO_PANEL = 8 << 30
-# column blocks of the hub group's launch (chained on the hub side stream; 1 = one launch);
-# SRGNN_HALO_HUB_BLOCKS overrides.  Bitwise the same hops either way.
-AUTO_HALO_HUB_BLOCKS = int(os.environ.get("SRGNN_HALO_HUB_BLOCKS", "1"))
-
-
-# GPU ranks may launch their groups from copies of the entries laid out in schedule order
-# (_launch_op, SRGNN_HALO_LAUNCH_ORDER=1).  Off: unlike one GPU's column blocks (+2 %), the halo
-# groups gain nothing -- products per-rank hop 3.74 / 2.01 / 1.07 ms at P = 2 / 4 / 8 against
-# 3.74 / 1.91 / 1.03 (profiles/r03_halo_launch_order_negative.txt): a row chunk is a contiguous range
-# of rows, so its entries are already read in nearly the order its launch takes them
-LAUNCH_ORDER = os.environ.get("SRGNN_HALO_LAUNCH_ORDER", "0") != "0"
-
-# Medium hub rows as column spans inside the row chunks (GPU ranks; SRGNN_HALO_MEDIUM_SPANS=0 for
-# the A/B): the hub group's rows of at most `giant_threshold` entries (products at 8 ranks: ~1,050
-# rows of 2.6 K - 10 K entries per rank, 30 % of its nonzeros) are not hub workgroups beside the
-# chunks any more; chunk c computes span c of each of them -- its entries whose GLOBAL column ids lie
-# in [ceil(c n / C), ceil((c+1) n / C)) -- as slice waves, continuing the chain left by chunk c - 1
-# (srg_spmm_span_rowacc_f32: per-row accumulation), so every row is still one fma chain in CSR
-# order.  Each chunk then gathers those rows' entries from one column block of the panel (the
-# locality column blocks give one GPU) instead of the hub workgroups gathering from everywhere;
-# only the giant rows stay hub workgroups.  They finish with the last chunk and are exchanged
-# with the hub group, as before.
-# Measured opt-in (round 4, tools/halo_ranks.py on products at P = 8, profiles/r04_halo_medium_spans_negative.txt):
-# the per-rank fabric traffic falls from 5.59 to 5.02 GB per hop, but the hop takes 1.11-1.13 ms
-# against 1.02: slice waves keep 8 KiB of gathers in flight per wave where the hub workgroups keep
-# ~128 KiB per workgroup, so the spans run latency-bound (4.9 TB/s against 5.6 at the gather ceiling)
-MEDIUM_SPANS = os.environ.get("SRGNN_HALO_MEDIUM_SPANS", "0") != "0"
+# Measured and removed (round 5: they cost time at every setting; DESIGN.md §7 keeps the numbers): the
+# hub group in column blocks (profiles/r03_halo_hub_blocks_negative.txt, r04n_*), the groups launched
+# from launch-ordered copies (r03_halo_launch_order_negative.txt), medium hub rows as column spans in
+# the chunks (r04_halo_medium_spans_negative.txt), long rows moved into the first chunk
+# (r03_halo_p8_early_rows_negative.txt) and the halo pack fused into the SpMM epilogue
+# (r01_halo_ranks_products_fused_pack_probe.json).
 
 
 class HaloPartitionedOperator:
@@ -324,8 +300,7 @@ class HaloPartitionedOperator:
     def __init__(self, indptr, indices, values, n: int, group=None, chunks: int = 4,
                  heavy_threshold=None, hub_threshold=None, device=None, rank=None, world=None,
                  local_spmm=None, ghost_max_degree=None, hub_launches=None, giant_weight=None,
-                 calibrate_link: bool = True, fast: bool = False, col_blocks=None, early_degree=None,
-                 hub_col_blocks=None, medium_spans=None, giant_threshold=None):
+                 calibrate_link: bool = True, fast: bool = False, col_blocks=None):
         from .csr import (DEFAULT_HEAVY_THRESHOLD, DEFAULT_HUB_THRESHOLD, NARROW_HEAVY_THRESHOLD,
                           auto_heavy_threshold, auto_hub_threshold)
         self._narrow_heavy = NARROW_HEAVY_THRESHOLD
@@ -335,16 +310,7 @@ class HaloPartitionedOperator:
         self.fast = bool(fast)
         # column blocks of the row chunks' launches (None: the automatic rule of _col_blocks_for)
         self.col_blocks = col_blocks
-        # column blocks of the hub group's launch (None: the automatic rule of _hub_blocks_for)
-        self.hub_col_blocks = hub_col_blocks
-        # medium hub rows as column spans in the row chunks (None: MEDIUM_SPANS); rows of the hub
-        # group longer than giant_threshold stay hub workgroups (None: auto_hub_threshold of the
-        # rank's nonzeros for one launch, nnz / 1024: a span per chunk then stays well inside the
-        # chunk's launch as slice waves)
-        self.medium_spans = MEDIUM_SPANS if medium_spans is None else bool(medium_spans)
-        self.giant_threshold = giant_threshold
         self._cb = {}
-        self._lo_ok = None             # launch-ordered copies fit (_launch_op), decided on first use
         self.virtual = rank is not None
         self.rank = rank if rank is not None else (dist.get_rank(group) if dist.is_initialized() else 0)
         self.world = world if world is not None else (dist.get_world_size(group) if dist.is_initialized() else 1)
@@ -383,12 +349,6 @@ class HaloPartitionedOperator:
                 # local row range of each chunk (its hub rows included: they belong to group C)
                 self.chunk_ranges = [(cb[c], cb[c + 1]) for c in range(C)]
         grp[is_hub] = C
-        # early_degree: non-hub rows longer than this join the first chunk, whose launch starts the
-        # hop, so their slice-wave chains (~38 ns per nonzero) run beside the rest of the hop's work
-        # instead of outlasting a later chunk (probe of a raised hub threshold, tools/halo_ranks.py)
-        self._early = early_degree is not None
-        if early_degree is not None:
-            grp[(deg > int(early_degree)) & ~is_hub] = 0
         self.n_groups = C + 1
         G = self.n_groups
         r0, r1 = self.starts[p], self.starts[p + 1]
@@ -464,21 +424,6 @@ class HaloPartitionedOperator:
             self.send_cat.append(torch.cat(parts) if parts else torch.zeros(0, dtype=torch.int64, device=dev))
         parts = [self.ghost_send_idx[q] for q in range(P) if q != p and self.ghost_send_counts[q] > 0]
         self.ghost_send_cat = torch.cat(parts) if parts else torch.zeros(0, dtype=torch.int64, device=dev)
-        # fused pack: all groups' send rows in one buffer [group 0 | group 1 | ...]; every local row
-        # lists the buffer rows it goes to (srg_spmm_send_f32 stores them as it computes the row)
-        self.send_offsets = [0]
-        for g in range(G):
-            self.send_offsets.append(self.send_offsets[-1] + int(self.send_cat[g].numel()))
-        rows_all = torch.cat(self.send_cat) if self.send_offsets[-1] else torch.zeros(0, dtype=torch.int64, device=dev)
-        self._send_slot = torch.argsort(rows_all, stable=True).to(torch.int32).contiguous()
-        self._send_ptr = torch.zeros(self.rows + 1, dtype=torch.int64, device=dev)
-        if rows_all.numel():
-            self._send_ptr[1:] = torch.cumsum(torch.bincount(rows_all, minlength=self.rows), 0)
-        self._send_buf = None
-        # opt-in: measured slower on products (P = 8 chunks 0.84 -> 1.61 ms with the pack fused, vs
-        # 1.08 ms for the chunks plus the separate index_select pack; the per-row slot lookups sit
-        # at the end of every row's chain), profiles/r01_halo_ranks_products_fused_pack_probe.json
-        self.fused_pack = False
         # --- local operator over the panel rows [own | received (empty rows) | ghosts], columns
         # remapped into the same layout
         self._halo_ids = torch.cat([need, gh]).contiguous()
@@ -548,7 +493,7 @@ class HaloPartitionedOperator:
         else:
             self._A = [(lip, lix, lvv, order) for (order, _, _, _) in self.views + [self.ghost_view]]
             self._spmm = local_spmm
-        self._hip = local_spmm is None and dev.type == "cuda"      # the HIP kernels (fused pack possible)
+        self._hip = local_spmm is None and dev.type == "cuda"      # the HIP kernels
 
     # ------------------------------------------------------------------------------------------
     def new_panel(self, d: int) -> torch.Tensor:
@@ -563,7 +508,6 @@ class HaloPartitionedOperator:
         lvv = self._local_values(values)
         other._lvv = lvv
         other._cb = {}                 # column blocks hold the values: rebuilt for `other` on use
-        other._lo_ok = None
         if isinstance(self._A[0], tuple):
             other._A = [(a[0], a[1], lvv, a[3]) for a in self._A]
         else:
@@ -576,15 +520,13 @@ class HaloPartitionedOperator:
     def _col_blocks_for(self, d: int) -> int:
         """Column blocks per row-chunk launch for a panel of d columns: `col_blocks` if given, else
         WIDE_HALO_COL_BLOCKS for local panels ([own | halo] rows) of >= WIDE_HALO_PANEL at d >= 256,
-        else AUTO_HALO_COL_BLOCKS for panels of >= 256 MiB at d >= 64 (HIP ranks only)."""
+        else 1 (HIP ranks only; the C planner's srg_halo_col_blocks is the same rule)."""
         if not self._hip:
             return 1
         if self.col_blocks is not None:
             return max(1, int(self.col_blocks))
         panel = (self.rows + self.halo) * d * 4
-        if _HALO_COL_BLOCKS_ENV is None and d >= 256 and panel >= WIDE_HALO_PANEL:
-            return WIDE_HALO_COL_BLOCKS
-        return AUTO_HALO_COL_BLOCKS if d >= 64 and panel >= (256 << 20) else 1
+        return WIDE_HALO_COL_BLOCKS if d >= 256 and panel >= WIDE_HALO_PANEL else 1
 
     def chunk_blocks(self, d: int):
         """The row chunks' column blocks for a panel of d columns: per chunk, B DeviceCSRs over row
@@ -648,122 +590,10 @@ class HaloPartitionedOperator:
         self._cb[key] = ([lip[:-1]] + [splits[b] for b in range(B - 1)] + [lip[1:]], whole)
         return self._cb[key]
 
-    def _hub_blocks_for(self, d: int) -> int:
-        """Column blocks of the hub group's launches: `hub_col_blocks` if given, else
-        AUTO_HALO_HUB_BLOCKS (HIP ranks, exact mode, d >= 64; FAST hub rows are one launch)."""
-        if not self._hip or self.fast or not (self.views[self.C][1] and self.views[self.C][3]):
-            return 1
-        if self.hub_col_blocks is not None:
-            return max(1, int(self.hub_col_blocks))
-        return AUTO_HALO_HUB_BLOCKS if d >= 64 else 1
-
-    def hub_blocks(self, d: int):
-        """The hub group's column blocks for a panel of d columns: B DeviceCSRs over the row spans
-        of _block_bounds(B), every hub row in every block (so the launches chain on the hub side
-        stream with SRG_SPMM_HUB_CONTINUE: each hub row's workgroups of block b run after its block
-        b-1 workgroups), or None for one launch.  Bitwise the one launch, as for the chunks."""
-        B = self._hub_blocks_for(d)
-        if B < 2:
-            return None
-        key = ("hub", B)
-        if key in self._cb:
-            return self._cb[key]
-        from .csr import DeviceCSR
-        bounds, _ = self._block_bounds(B)
-        order, n_g, _, n_hub = self.views[self.C]
-        blocks = [DeviceCSR(bounds[b], self._lix, self._lvv, n_g, self.ncols_local, order, 0, n_hub, None,
-                            row_end=bounds[b + 1], row_space=self.rows) for b in range(B)]
-        self._cb[key] = blocks
-        return blocks
-
-    def _medium_plan(self):
-        """(giant hub view or None, [chunk c's span view]) when medium hub rows run as column spans
-        inside the row chunks (see MEDIUM_SPANS), else None.  Chunk c's view schedules its own rows
-        whole ([lip[r], lip[r+1])) and span c of every medium row (its entries with global column
-        ids in block c of C, empty spans skipped), longest first; launched with per-row
-        accumulation (a span that starts at its row's first entry starts from +0.0f).  Cached."""
-        if "medium" in self._cb:
-            return self._cb["medium"]
-        res = None
-        C = self.C
-        if (self._hip and self.medium_spans and not self.fast and C > 1 and self.views[C][1]
-                and self._col_blocks_for(128) < 2 and self._hub_blocks_for(128) < 2):
-            from .csr import DeviceCSR, auto_heavy_threshold, auto_hub_threshold
-            lip = self._lip
-            deg = lip[1:] - lip[:-1]
-            hub_rows = self.views[C][0].to(torch.int64)                 # longest first
-            giant_env = os.environ.get("SRGNN_HALO_GIANT_THRESHOLD")
-            giant_t = int(self.giant_threshold) if self.giant_threshold is not None else \
-                int(giant_env) if giant_env else auto_hub_threshold(self.nnz_local, launches=1)
-            med_mask = deg[hub_rows] <= giant_t
-            med, giant = hub_rows[med_mask], hub_rows[~med_mask]
-            if med.numel():
-                bounds, _ = self._block_bounds(C)
-                heavy_t = auto_heavy_threshold(self.nnz_local, launches=C) if self._auto_heavy \
-                    else self._heavy_explicit
-                gview = None
-                if giant.numel():
-                    gview = DeviceCSR(lip, self._lix, self._lvv, int(giant.numel()), self.ncols_local,
-                                      giant.to(torch.int32).contiguous(), 0, int(giant.numel()), None,
-                                      row_space=self.rows)
-                views = []
-                for c in range(C):
-                    own = self.views[c][0].to(torch.int64)
-                    beg = lip[: self.rows].clone()
-                    end = lip[1: self.rows + 1].clone()
-                    mb, me = bounds[c][med], bounds[c + 1][med]
-                    beg[med], end[med] = mb, me
-                    rows_c = torch.cat([own, med[me > mb]])
-                    lens = end[rows_c] - beg[rows_c]
-                    srt = torch.sort(lens, descending=True, stable=True)
-                    order = rows_c[srt.indices].to(torch.int32).contiguous()
-                    n_heavy = int((srt.values > heavy_t).sum()) if heavy_t >= 0 else 0
-                    narrow = int((srt.values > self._narrow_heavy).sum()) if self._auto_heavy else None
-                    views.append(DeviceCSR(beg, self._lix, self._lvv, int(order.numel()), self.ncols_local, order,
-                                           n_heavy, 0, narrow, row_end=end, row_space=self.rows))
-                res = (gview, views)
-        self._cb["medium"] = res
-        return res
-
-    def _medium_chunk(self, c: int, src: torch.Tensor, out: torch.Tensor):
-        """Row chunk c with its span of every medium hub row (srg_spmm_span_rowacc_f32)."""
-        from . import _lib
-        A = self._medium_plan()[1][c]
-        if A.n_rows == 0:
-            return
-        d = src.shape[1]
-        _lib.call(src.device, "srg_spmm_span_rowacc_f32", A.indptr.data_ptr(), A.row_end.data_ptr(),
-                  self._lip.data_ptr(), A.indices.data_ptr(), A.values.data_ptr(), A.n_rows, A.order.data_ptr(),
-                  A.heavy(d), src.data_ptr(), src.stride(0), out.data_ptr(), out.stride(0), d, 0,
-                  _lib.stream(src.device))
-
-    def _launch_op(self, g: int):
-        """Group g's operator as its launch takes it: on GPU ranks a copy of its entries laid out in
-        its schedule's order (DeviceCSR.schedule_ordered, cached on the operator; the same chains),
-        which reads the id / value streams in order; else the operator itself.  Memory permitting
-        (a quarter of the free memory for the copies); opt-in, SRGNN_HALO_LAUNCH_ORDER=1."""
-        A = self._A[g]
-        if not (self._hip and LAUNCH_ORDER):
-            return A
-        if "sched" not in A._blocks:
-            if self._lo_ok is None:
-                free, _ = torch.cuda.mem_get_info(self.device)
-                need = self._lix.numel() * 8 + 16 * (self.rows + self.halo) * len(self._A)
-                self._lo_ok = need <= free // 4
-            if not self._lo_ok:
-                return A
-        return A.schedule_ordered()
-
     def _hub_launch(self, src: torch.Tensor, out: torch.Tensor):
-        """The hub group forked onto the library's hub side stream (joined by the caller): one
-        launch, or its column blocks chained on the side stream."""
+        """The hub group forked onto the library's hub side stream (joined by the caller)."""
         from .spmm import spmm
-        blocks = self.hub_blocks(src.shape[1])
-        if blocks is None:
-            spmm(self._launch_op(self.C), src, out=out, hub_nojoin=True, fast=self.fast)
-            return
-        for b, Ab in enumerate(blocks):
-            spmm(Ab, src, out=out, accumulate=b > 0, hub_nojoin=True, hub_continue=b > 0)
+        spmm(self._A[self.C], src, out=out, hub_nojoin=True, fast=self.fast)
 
     def _chunk_spmm(self, c: int, src: torch.Tensor, out: torch.Tensor, blocks=None):
         """Row chunk c's launch(es): one, or its column blocks in order (bitwise the same)."""
@@ -773,7 +603,7 @@ class HaloPartitionedOperator:
             for b, Ab in enumerate(blocks[c]):
                 spmm(Ab, src, out=out, accumulate=b > 0, packed_u2=u2)
         else:
-            self._spmm(self._launch_op(c), src, out)
+            self._spmm(self._A[c], src, out)
 
     def _local_values(self, values: torch.Tensor) -> torch.Tensor:
         """The local operator's values: the own rows' slice, then the ghost rows' entries."""
@@ -782,17 +612,10 @@ class HaloPartitionedOperator:
             own = torch.cat([own, values[self._ghost_pos.to(values.device)].to(self.device)])
         return own.contiguous()
 
-    def send_buffer(self, d: int) -> torch.Tensor:
-        """The fused-pack send rows of all groups, [sum of send counts, d] (allocated once per d)."""
-        if self._send_buf is None or self._send_buf.shape[1] != d:
-            self._send_buf = torch.empty((self.send_offsets[-1], d), dtype=torch.float32, device=self.device)
-        return self._send_buf
-
-    def _exchange_group(self, panel: torch.Tensor, g: int, packed: torch.Tensor | None = None,
-                        async_op: bool = False):
-        """all_to_all of group g's rows: from `packed` (the fused-pack buffer, already filled by
-        this group's kernels) or gathered from the panel's own rows here (on the current stream).
-        async_op: returns (work, send) -- the caller waits on the work before the halo is read."""
+    def _exchange_group(self, panel: torch.Tensor, g: int, async_op: bool = False):
+        """all_to_all of group g's rows, gathered from the panel's own rows here (on the current
+        stream).  async_op: returns (work, send) -- the caller waits on the work before the halo is
+        read."""
         P, p = self.world, self.rank
         off = self.rows + self.group_offsets[g]
         out_splits = [self.recv_counts[g][q] for q in range(P)]
@@ -801,9 +624,7 @@ class HaloPartitionedOperator:
         if P == 1 or (total_in == 0 and sum(in_splits) == 0 and not dist.is_initialized()):
             return None
         recv = panel[off:off + total_in]
-        if packed is not None:
-            send = packed[self.send_offsets[g]:self.send_offsets[g + 1]]
-        elif self.send_cat[g].numel():
+        if self.send_cat[g].numel():
             if self._hip:      # srg_gather_rows_f32: 16-byte row chunks, 12-15 % faster than index_select
                 from .spmm import gather_rows
                 send = gather_rows(panel[: self.rows], self.send_cat[g])
@@ -844,15 +665,13 @@ class HaloPartitionedOperator:
         if ghosts:
             self._exchange_ghosts(panel)
 
-    def _launch_groups(self, src: torch.Tensor, dst: torch.Tensor, packed: torch.Tensor | None = None,
-                       ghosts: bool = True, after_group=None):
+    def _launch_groups(self, src: torch.Tensor, dst: torch.Tensor, ghosts: bool = True, after_group=None):
         """dst[:rows] = local Â rows @ src, everything on the current stream: the hub group's
         workgroups forked onto the library's hub side stream (srg_spmm_csr_f32 with
         SRG_SPMM_HUB_NOJOIN; they run beside the chunks), the row chunks in order, the ghost rows
         into their halo slots of dst (ghosts=True), then the join of the hub side stream.
         after_group(g) is called right after group g's launch (chunks in order, the hub group after
-        its join): the hop issues group g's exchange there.  With `packed`, the kernels also store
-        every row peers need into it (fused pack; the hub group then runs before the chunks).
+        its join): the hop issues group g's exchange there.
         No other stream is used: a second torch stream may share a hardware queue with this one,
         and its waits would then stall the chunks behind the hub (measured: chunks + hub instead
         of the longer of the two)."""
@@ -870,51 +689,24 @@ class HaloPartitionedOperator:
                     after_group(g)
             return
         from . import _lib
-        from .spmm import spmm, spmm_send
-        med = self._medium_plan() if packed is None else None
-        if med is not None:
-            # the giant hub rows forked beside the chunks; every chunk carries one column span of
-            # each medium hub row
-            fork = med[0] is not None
+        fork = bool(self.views[C][1] and self.views[C][3] and self._hip)
+        if self.views[C][1]:
             if fork:
-                spmm(med[0], src, out=out, hub_nojoin=True)
-            for c in range(C):
-                self._medium_chunk(c, src, out)
-                if after_group is not None:
-                    after_group(c)
-        else:
-            fork = bool(self.views[C][1] and self.views[C][3] and self._hip and packed is None)
-            if self.views[C][1]:
-                if packed is not None:
-                    spmm_send(self._A[C], src, out, packed, self._send_ptr, self._send_slot)
-                elif fork:
-                    self._hub_launch(src, out)
-                else:
-                    self._spmm(self._launch_op(C), src, out)
-            blocks = self.chunk_blocks(src.shape[1]) if packed is None else None
-            for c in range(C):
-                if self.views[c][1]:
-                    if packed is not None:
-                        spmm_send(self._A[c], src, out, packed, self._send_ptr, self._send_slot)
-                    else:
-                        self._chunk_spmm(c, src, out, blocks)
-                if after_group is not None:
-                    after_group(c)
+                self._hub_launch(src, out)
+            else:
+                self._spmm(self._A[C], src, out)
+        blocks = self.chunk_blocks(src.shape[1])
+        for c in range(C):
+            if self.views[c][1]:
+                self._chunk_spmm(c, src, out, blocks)
+            if after_group is not None:
+                after_group(c)
         if ghosts and self.n_ghost:
-            self._spmm(self._launch_op(self.n_groups) if packed is None else gA, src, dst)
+            self._spmm(gA, src, dst)
         if fork:
             _lib.call(self.device, "srg_hub_join", _lib.stream(self.device))
         if after_group is not None:
             after_group(C)
-
-    def compute_packed(self, src: torch.Tensor, dst: torch.Tensor) -> torch.Tensor:
-        """compute() with the fused pack: returns the send buffer (all groups' rows peers need, in
-        exchange order), ordered on the current stream.  GPU ranks only."""
-        if not self._hip:
-            raise RuntimeError("the fused pack needs the HIP kernels (a CUDA operator without local_spmm)")
-        packed = self.send_buffer(src.shape[1])
-        self._launch_groups(src, dst, packed)
-        return packed
 
     def compute(self, src: torch.Tensor, dst: torch.Tensor, ghosts: bool = True):
         """dst[:rows] = local Â rows @ src (all groups, no exchange) and, with ghosts, the ghost
@@ -927,17 +719,14 @@ class HaloPartitionedOperator:
         stream right after its kernel and sent with an asynchronous all_to_all_single (RCCL runs it
         on its own stream while the later groups compute); the current stream waits for all of
         them at the end of the hop."""
-        packed = None
-        if exchange and self.fused_pack and self.world > 1 and not self.virtual and self._hip:
-            packed = self.send_buffer(src.shape[1])
         if not exchange or self.world == 1 or self.device.type != "cuda":
-            self._launch_groups(src, dst, packed, ghosts=exchange)   # no later hop reads the last ghosts
+            self._launch_groups(src, dst, ghosts=exchange)   # no later hop reads the last ghosts
             if exchange:
                 self.exchange(dst)
             return
         pending = []
-        self._launch_groups(src, dst, packed, ghosts=True,
-                            after_group=lambda g: pending.append(self._exchange_group(dst, g, packed, async_op=True)))
+        self._launch_groups(src, dst, ghosts=True,
+                            after_group=lambda g: pending.append(self._exchange_group(dst, g, async_op=True)))
         for item in pending:
             if item is not None:
                 item[0].wait()        # the current stream waits for RCCL's stream (the CPU does not)
@@ -952,8 +741,6 @@ class HaloPartitionedOperator:
         kernels (no ghost rows: the epilogue covers own rows only)."""
         if not (self._hip and self.world > 1 and not self.virtual) or self.n_ghost:
             raise RuntimeError("hop_with_epilogue needs real GPU ranks with the HIP kernels and no ghost rows")
-        if self._early:
-            raise RuntimeError("hop_with_epilogue needs every chunk's rows in its own row range (no early_degree)")
         from . import _lib
         from .spmm import spmm
         out = dst[: self.rows]
@@ -1034,15 +821,14 @@ def _virtual_exchange(shares, panels, ghosts: bool = False):
 
 def simulate_halo_propagate(indptr, indices, values, n: int, x: torch.Tensor, K: int, world: int,
                             chunks: int = 3, heavy_threshold=None, hub_threshold=None, device=None,
-                            ghost_max_degree=None, shares=None, col_blocks=None, hub_col_blocks=None, **kw):
+                            ghost_max_degree=None, shares=None, col_blocks=None, **kw):
     """P virtual halo-exchange ranks in ONE process (all_to_all emulated by copies); returns the
     K+1 full [n, d] panels.  Exercises the group split, ghost rows, halo layout and column remap
     on a device."""
     if shares is None:
         shares = [HaloPartitionedOperator(indptr, indices, values, n, chunks=chunks, heavy_threshold=heavy_threshold,
                                           hub_threshold=hub_threshold, device=device, rank=q, world=world,
-                                          ghost_max_degree=ghost_max_degree, col_blocks=col_blocks,
-                                          hub_col_blocks=hub_col_blocks, **kw)
+                                          ghost_max_degree=ghost_max_degree, col_blocks=col_blocks, **kw)
                   for q in range(world)]
     d = x.shape[1]
     panels = [[s.new_panel(d) for _ in range(K + 1)] for s in shares]

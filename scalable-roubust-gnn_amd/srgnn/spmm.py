@@ -6,7 +6,6 @@ on torch's current HIP stream of the operand's device, so torch events / synchro
 from __future__ import annotations
 
 import ctypes
-import os
 
 import torch
 
@@ -21,33 +20,34 @@ _stream = _lib.stream
 # of <= csr.BLOCK_WHOLE_MAX nonzeros are not cut (block 0 computes them whole).  Measured
 # (profiles/r02t-v_*): products d = 128 7.05 (one launch 7.31) -> 6.67 (B = 2) -> 6.30 ms (B = 4),
 # flat over B = 4..6, 6.47 at 8; d = 256 +9 % and papers100M / RMAT-26 +3 / +2 % for B = 4 over 2 / 1;
-# arxiv (X 87 MB, already cache-resident) 0.224 vs 0.163 ms at B = 2.  "auto": auto_col_blocks (4 to 8
-# blocks for panels of >= 512 MiB at d >= 64); SRGNN_COL_BLOCKS=<B> forces B.
-_COL_BLOCKS_ENV = os.environ.get("SRGNN_COL_BLOCKS", "auto")
+# arxiv (X 87 MB, already cache-resident) 0.224 vs 0.163 ms at B = 2.  auto_col_blocks: 4 to 8 blocks
+# for panels of >= 512 MiB at d >= 64 (callers pass col_blocks to force a count; FORCE_COL_BLOCKS
+# forces one for every automatic choice, a test hook).
+FORCE_COL_BLOCKS = None
 # column blocks' launches keep 2 gathers per packed light row in flight (SRG_SPMM_PACKED_U2) for
-# d >= 128: products 7.15 -> 7.03 ms per hop, d = 256 +1.3 %, d = 64 -3 % (so not there);
-# SRGNN_BLOCK_U2=0 turns it off (A/B, profiles/r02_ab_col_blocks.txt)
-_U2_BLOCKED = os.environ.get("SRGNN_BLOCK_U2", "1") != "0"
+# d >= 128: products 7.15 -> 7.03 ms per hop, d = 256 +1.3 %, d = 64 -3 % (so not there;
+# profiles/r02_ab_col_blocks.txt)
+_U2_BLOCKED = True
 # column-blocked hops: block b's hub rows continue block b-1's side-stream fork (SRG_SPMM_HUB_CONTINUE)
-# instead of a fork, dispatch delay and join per block; SRGNN_HUB_CHAIN=0 for the A/B
-_HUB_CHAIN = os.environ.get("SRGNN_HUB_CHAIN", "1") != "0"
+# instead of a fork, dispatch delay and join per block (profiles/r03_ab_hub_chain_products.txt)
+_HUB_CHAIN = True
 # span launches of the native plan loop hand the packed light rows their spans by schedule slot
-# (DeviceCSR.slot_spans); SRGNN_SLOT_SPANS=0 for the A/B
-_SLOT_SPANS = os.environ.get("SRGNN_SLOT_SPANS", "1") != "0"
+# (DeviceCSR.slot_spans; profiles/r03_ab_slot_spans.txt)
+_SLOT_SPANS = True
 # block 0 of a column-blocked hop as two launches over the same arrays (DeviceCSR.split_whole): the
 # cut rows' first spans, then the rows it computes whole.  Products (1.25 GB panel): 6.21 vs 6.24 ms
 # per hop, six alternations; the whole rows first, last or after the cut spans measure the same, and
 # beside the blocks on a second stream 6.80 ms.  The HBM-bound giants lose: papers100M (57 GB panel)
 # 245.6-246.1 vs 244.1-244.2 ms, RMAT-26 (68 GB) 314.3-315.8 vs 311.5-313.1 ms
-# (profiles/r03_ab_split_block0*.txt).  "auto": split for panels below SPLIT_BLOCK0_MAX_PANEL;
-# SRGNN_SPLIT_BLOCK0=1 / 0 forces it on / off
-_SPLIT_BLOCK0_ENV = os.environ.get("SRGNN_SPLIT_BLOCK0", "auto")
+# (profiles/r03_ab_split_block0*.txt): split for panels below SPLIT_BLOCK0_MAX_PANEL
 SPLIT_BLOCK0_MAX_PANEL = 16 << 30
+# None: automatic (tests force it on / off to check both layouts give the same bits)
+SPLIT_BLOCK0 = None
 
 
 def _split_block0(A: DeviceCSR, d: int) -> bool:
-    if _SPLIT_BLOCK0_ENV != "auto":
-        return _SPLIT_BLOCK0_ENV != "0"
+    if SPLIT_BLOCK0 is not None:
+        return bool(SPLIT_BLOCK0)
     return A.n_cols * d * 4 < SPLIT_BLOCK0_MAX_PANEL
 
 
@@ -61,7 +61,7 @@ MIN_HOPS_TO_CUT = 4
 # (profiles/r04h_one_shot_products.json): the layout costs 4.6 ms more and each hop 0.40 ms less
 # (6.09 against 6.49 ms), so the copy pays after ~12 hops.
 MIN_HOPS_TO_COMPACT = 16
-_COMPACT = os.environ.get("SRGNN_COMPACT_BLOCKS", "1") != "0"     # 0: spans only (A/B)
+_COMPACT = True                   # False: spans only (A/B of the round-2 / 3 layouts)
 
 
 def prepare(A: DeviceCSR, d: int, hops: int) -> int:
@@ -102,8 +102,8 @@ def auto_col_blocks(A: DeviceCSR, d: int, hops: int | None = None) -> int:
     6.00-6.01 at 5 and 7, 6.03 at 8, 6.10 at 4; d = 256 (2.5 GB) 12.35 ms at 7-8 against 12.40 at 6
     (before the launch order: 12.55 at 6, 12.67 at 5, 12.70 at 10, 12.91 at 4); d = 64 (0.63 GB) flat
     over 4-5; RMAT-26 (68 GB) 312.8 at 4 against 315.6 at 5, papers100M (57 GB) 242.9 against 242.0."""
-    if _COL_BLOCKS_ENV != "auto":
-        return max(1, int(_COL_BLOCKS_ENV))
+    if FORCE_COL_BLOCKS is not None:
+        return max(1, int(FORCE_COL_BLOCKS))
     panel = A.n_cols * d * 4
     if d < 64 or panel < (512 << 20):
         B = 1
@@ -266,15 +266,14 @@ def _check_panel(X: torch.Tensor, rows: int, name: str, d=None):
 def spmm(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor | None = None, accumulate: bool = False,
          nt_store: bool = False, wide_rows: bool = False, hub_w256: bool = False,
          hub_nojoin: bool = False, packed_u2: bool = False, fast: bool = False,
-         hub_continue: bool = False, hub_lite: bool = False) -> torch.Tensor:
+         hub_continue: bool = False) -> torch.Tensor:
     """out[r, :] (+)= A[r, :] @ X  for the rows of A (one hop; exact fma chains in CSR order).
     fast: tolerance mode (SRG_SPMM_FAST): A's hub rows are summed as 64 exact segment chains whose
     partial sums are then added in order -- deterministic, within fp32 re-association error of the
     exact chain, ~64x shorter latency for the longest rows; every other row stays bit-exact.
     wide_rows: diagnostic, one row per wave for every light row (no narrow or packed rows);
     hub_w256: diagnostic, 256-nonzero
-    hub windows for any hub launch (same results either way); hub_lite: 4-producer hub workgroups
-    (SRG_SPMM_HUB_LITE, same results).  hub_nojoin: A's hub rows are left
+    hub windows for any hub launch (same results either way).  hub_nojoin: A's hub rows are left
     running on the library's side stream; the caller must make a stream wait for them
     (srg_hub_join) before reading them.  hub_continue (with hub_nojoin, after an unjoined fork):
     the hub rows are appended to the side stream without a new fork (SRG_SPMM_HUB_CONTINUE)."""
@@ -293,8 +292,7 @@ def spmm(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor | None = None, accumul
     flags = (_lib.SRG_SPMM_ACCUMULATE if accumulate else 0) | (_lib.SRG_SPMM_NT_STORE if nt_store else 0) | \
         (_lib.SRG_SPMM_WIDE_ROWS if wide_rows else 0) | (_lib.SRG_SPMM_HUB_W256 if hub_w256 else 0) | \
         (_lib.SRG_SPMM_HUB_NOJOIN if hub_nojoin else 0) | (_lib.SRG_SPMM_PACKED_U2 if packed_u2 else 0) | \
-        (_lib.SRG_SPMM_FAST if fast else 0) | (_lib.SRG_SPMM_HUB_CONTINUE if hub_continue else 0) | \
-        (_lib.SRG_SPMM_HUB_LITE if hub_lite else 0)
+        (_lib.SRG_SPMM_FAST if fast else 0) | (_lib.SRG_SPMM_HUB_CONTINUE if hub_continue else 0)
     if A.is_span:
         _span_call(A, X, out, d, flags, None, 0, 0.0, False)
         return out
@@ -339,32 +337,6 @@ def spmm_agg(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, agg: torch.Tensor
               A.n_rows, A.order.data_ptr() if A.n_rows else None, A.n_hub, A.heavy(d), X.data_ptr(),
               X.stride(0), out.data_ptr(), out.stride(0), d, flags, agg.data_ptr(), agg.stride(0),
               float(w), 1 if init else 0, _stream(X.device))
-    return out
-
-
-def spmm_send(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, send: torch.Tensor, send_ptr: torch.Tensor,
-              send_slot: torch.Tensor) -> torch.Tensor:
-    """out = A @ X and, fused into the same kernels' epilogue, send[send_slot[send_ptr[r]:send_ptr[r+1]]]
-    = out[r] for every row r of A (srg_spmm_send_f32: the halo pack of srgnn.dist, bitwise the rows
-    of out).  send_ptr is indexed by the row ids A's schedule names (A may be a row-group view)."""
-    _no_spans(A, "spmm_send")
-    _check_panel(X, A.n_cols, "X")
-    d = X.shape[1]
-    _check_panel(out, A.out_rows, "out", d)
-    if not isinstance(send, torch.Tensor) or send.dtype != torch.float32 or send.dim() != 2 or \
-            send.shape[1] != d or send.stride(1) != 1 or send.device != A.device:
-        raise ValueError("send must be a float32 [m, d] row-major tensor on A's device")
-    if send_ptr.dtype != torch.int64 or send_ptr.dim() != 1 or send_ptr.numel() < 1 or send_slot.dtype != torch.int32 \
-            or send_ptr.device != A.device or send_slot.device != A.device:
-        raise ValueError("send_ptr must be int64 [rows + 1] (indexed by A's row ids) and send_slot int32, on A's device")
-    if send_slot.numel() and send.shape[0] == 0:
-        raise ValueError("send slots into an empty send buffer")
-    _lib.call(X.device, "srg_spmm_send_f32", A.indptr.data_ptr(), A.indices.data_ptr(), A.values.data_ptr(),
-              A.n_rows, A.order.data_ptr() if A.n_rows else None, A.n_hub, A.heavy(d), X.data_ptr(),
-              X.stride(0), out.data_ptr(), out.stride(0), d, 0,
-              send.data_ptr() if send.numel() else None, send.stride(0) if send.shape[0] > 1 else d,
-              send_ptr.data_ptr(), send_slot.data_ptr() if send_slot.numel() else None,
-              _stream(X.device))
     return out
 
 

@@ -24,7 +24,6 @@ same estimator (eigsh, tol 5e-3, x1.01) with a fixed start vector.
 from __future__ import annotations
 
 import ctypes
-import os
 
 import numpy as np
 import scipy.sparse as sp
@@ -169,8 +168,8 @@ class HeatWaveletFilter:
         del diag, l64
         self.lvals = lvals.to(dtype)
         # split path: the lean epilogue sequence (SRG_CHEBY_INIT_T / STEP_FIRST / NO_T); False runs
-        # INIT + STEP epilogues (same bits; SRGNN_WAVELET_LEAN=0 for A/B runs)
-        self.lean_epilogue = os.environ.get("SRGNN_WAVELET_LEAN", "1") != "0"
+        # INIT + STEP epilogues (same bits; set the attribute for A/B runs)
+        self.lean_epilogue = True
         self.order, self.n_heavy, self.n_hub = make_schedule(self.indptr, heavy_threshold, hub_threshold)
         self.n_heavy_narrow = narrow_heavy(self.indptr, self.n_hub) if _auto_heavy(heavy_threshold) else None
 

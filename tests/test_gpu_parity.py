@@ -205,7 +205,7 @@ def test_propagate_column_blocked_bit_exact(monkeypatch, name, B, compact, whole
 @pytest.mark.parametrize("compact", [False, True])
 def test_block0_split_launches_bit_exact(monkeypatch, name, compact):
     """Block 0 of a column-blocked hop as two launches (its cut spans, then its whole rows; the
-    default) or one (SRGNN_SPLIT_BLOCK0=0): the same bits as the reference either way, and
+    default) or one (spmm.SPLIT_BLOCK0 = False): the same bits as the reference either way, and
     launches_per_hop counts B + 1 or B launches."""
     from srgnn import csr as csr_mod
     from srgnn import spmm as spmm_mod
@@ -218,7 +218,7 @@ def test_block0_split_launches_bit_exact(monkeypatch, name, compact):
     d = X.shape[1]
     assert spmm_mod._split_block0(A, d)            # "auto": a small panel is split
     for split in (True, False):
-        monkeypatch.setattr(spmm_mod, "_SPLIT_BLOCK0_ENV", "1" if split else "0")
+        monkeypatch.setattr(spmm_mod, "SPLIT_BLOCK0", split)
         assert spmm_mod.launches_per_hop(A, 4, d) == (5 if split else 4)
         assert spmm_mod.launches_per_hop(A, 4, d, agg=True) == 5
         hops = spmm_mod.propagate(A, X, c.k, col_blocks=4)
@@ -226,7 +226,7 @@ def test_block0_split_launches_bit_exact(monkeypatch, name, compact):
         for k in range(1, c.k + 1):
             c.check_hop(k, hops[k].cpu().numpy())
     assert spmm_mod.launches_per_hop(A, 1, d) == 1
-    monkeypatch.setattr(spmm_mod, "_SPLIT_BLOCK0_ENV", "auto")
+    monkeypatch.setattr(spmm_mod, "SPLIT_BLOCK0", None)
     monkeypatch.setattr(spmm_mod, "SPLIT_BLOCK0_MAX_PANEL", 1)   # a "giant" panel: one launch
     assert spmm_mod.launches_per_hop(A, 4, d) == 4
 
@@ -414,16 +414,13 @@ def test_products_scale_sampled_rows_bit_exact(oracle_mod):
     assert bool((y[:, 1:] == y[:, :1]).all())
 
 
-@pytest.mark.parametrize("world,chunks,ghost,cb,hcb", [(2, 3, None, None, None), (8, 4, None, None, None),
-                                                       (2, 3, 0, None, None), (4, 2, 64, None, None),
-                                                       (8, 3, 8, None, None), (2, 3, None, 2, None),
-                                                       (8, 4, None, 3, None), (4, 2, 64, 4, None),
-                                                       (2, 3, None, None, 3), (8, 4, None, 2, 4)])
-def test_halo_virtual_ranks_bitwise(world, chunks, ghost, cb, hcb):
+@pytest.mark.parametrize("world,chunks,ghost,cb", [(2, 3, None, None), (8, 4, None, None), (2, 3, 0, None),
+                                                  (4, 2, 64, None), (8, 3, 8, None), (2, 3, None, 2),
+                                                  (8, 4, None, 3), (4, 2, 64, 4), (8, 4, None, 2)])
+def test_halo_virtual_ranks_bitwise(world, chunks, ghost, cb):
     """The halo-exchange multi-GPU layout (groups, remapped columns, hub group, ghost rows
-    computed into the halo, the row chunks' column blocks split by GLOBAL column ids, the hub
-    group's column blocks chained on the hub side stream) on one device with the real kernels:
-    bitwise equal to the single-device propagation."""
+    computed into the halo, the row chunks' column blocks split by GLOBAL column ids) on one
+    device with the real kernels: bitwise equal to the single-device propagation."""
     from srgnn import synth
     from srgnn.csr import DeviceCSR
     from srgnn.dist import simulate_halo_propagate
@@ -436,59 +433,9 @@ def test_halo_virtual_ranks_bitwise(world, chunks, ghost, cb, hcb):
     x = synth.uniform_features_t(n, 128, device="cuda")
     want = propagate(DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, device="cuda"), x, 3)
     got = simulate_halo_propagate(ip, ix, vals, n, x, 3, world, chunks=chunks, hub_threshold=300,
-                                  device="cuda", ghost_max_degree=ghost, col_blocks=cb, hub_col_blocks=hcb)
+                                  device="cuda", ghost_max_degree=ghost, col_blocks=cb)
     for k in range(1, 4):
         assert torch.equal(got[k], want[k]), f"hop {k} differs with {world} virtual halo ranks"
-
-
-@pytest.mark.parametrize("world,chunks,ghost", [(2, 3, None), (8, 4, 8), (4, 2, 64)])
-def test_halo_virtual_ranks_launch_order_bitwise(monkeypatch, world, chunks, ghost):
-    """The halo groups launched from launch-ordered copies of their entries (opt-in,
-    SRGNN_HALO_LAUNCH_ORDER=1): bitwise equal to the single-device propagation."""
-    from srgnn import dist as dist_mod, synth
-    from srgnn.csr import DeviceCSR
-    from srgnn.normalize import sym_norm_binary
-    from srgnn.spmm import propagate
-    monkeypatch.setattr(dist_mod, "LAUNCH_ORDER", True)
-    n = 20000
-    u, v = synth.rmat_undirected_t(n, 150000, seed=22, device="cuda")
-    ip, ix = synth.symmetric_csr_t(n, u, v)
-    ip, ix, vals = sym_norm_binary(ip, ix, n, 0.5)
-    x = synth.uniform_features_t(n, 128, device="cuda")
-    want = propagate(DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, device="cuda"), x, 3)
-    got = dist_mod.simulate_halo_propagate(ip, ix, vals, n, x, 3, world, chunks=chunks, hub_threshold=300,
-                                           device="cuda", ghost_max_degree=ghost)
-    for k in range(1, 4):
-        assert torch.equal(got[k], want[k]), f"hop {k} differs with {world} virtual halo ranks"
-
-
-@pytest.mark.parametrize("world,chunks,d", [(3, 2, 128), (8, 4, 128), (4, 3, 36), (2, 2, 7), (4, 2, 256)])
-def test_halo_fused_pack_equals_gathered_rows(world, chunks, d):
-    """srg_spmm_send_f32 (the halo pack fused into the SpMM epilogue, every path: row waves incl.
-    narrow panels, slice waves, hub workgroups): the panel is bitwise the plain kernels' and the
-    send buffer is exactly the rows peers need, gathered from it, for every virtual rank."""
-    from srgnn import synth
-    from srgnn.dist import HaloPartitionedOperator
-    from srgnn.normalize import sym_norm_binary
-    n = 20000
-    u, v = synth.rmat_undirected_t(n, 150000, seed=23, device="cuda")
-    ip, ix = synth.symmetric_csr_t(n, u, v)
-    ip, ix, vals = sym_norm_binary(ip, ix, n, 0.5)
-    for q in range(world):
-        op = HaloPartitionedOperator(ip, ix, vals, n, chunks=chunks, hub_threshold=300, device="cuda",
-                                     rank=q, world=world)
-        assert op.views[op.C][1] > 0 or world > 4     # the hub group is exercised
-        src = op.new_panel(d)
-        src.uniform_(-1, 1)
-        want = op.new_panel(d)
-        op.compute(src, want)
-        got = op.new_panel(d)
-        got.fill_(float("nan"))
-        packed = op.compute_packed(src, got)
-        torch.cuda.synchronize()
-        assert torch.equal(got[: op.rows], want[: op.rows])
-        ref = torch.cat([want[: op.rows].index_select(0, op.send_cat[g]) for g in range(op.n_groups)])
-        assert packed.shape == ref.shape and torch.equal(packed, ref), f"rank {q}/{world}"
 
 
 def test_launch_chunking_beyond_2e32_lanes(oracle_mod):
@@ -590,7 +537,7 @@ def test_packed_light_rows_bit_exact(oracle_mod, thr, d, ld):
     ACCUMULATE, the fused aggregation and halo-pack epilogues and strided panels."""
     from srgnn import synth
     from srgnn.csr import DeviceCSR
-    from srgnn.spmm import spmm, spmm_agg, spmm_send
+    from srgnn.spmm import spmm, spmm_agg
     n = 3000
     u, v = synth.rmat_undirected_t(n, 24000, seed=50 + d)
     ip, ix = synth.symmetric_csr_t(n, u, v)
@@ -610,18 +557,6 @@ def test_packed_light_rows_bit_exact(oracle_mod, thr, d, ld):
     out = torch.empty_like(y)
     spmm_agg(A, X, out, agg, -0.5, False)
     assert torch.equal(out, y) and torch.equal(agg, 2.0 + (-0.5) * y)
-    # halo pack: every third row stored into two send slots
-    rows = torch.arange(n)
-    cnt = ((rows % 3) == 0).to(torch.int64) * 2
-    ptr = torch.zeros(n + 1, dtype=torch.int64)
-    ptr[1:] = torch.cumsum(cnt, 0)
-    slot = torch.randperm(int(ptr[-1]), generator=torch.Generator().manual_seed(d)).to(torch.int32)
-    send = torch.full((int(ptr[-1]), d), float("nan"), device="cuda")
-    out2 = torch.empty_like(y)
-    spmm_send(A, X, out2, send, ptr.cuda(), slot.cuda())
-    assert torch.equal(out2, y)
-    src = torch.repeat_interleave(rows, cnt).cuda()
-    assert torch.equal(send[slot.long().cuda()], y[src])
 
 
 def test_papers100M_scale_sampled_rows_bit_exact(oracle_mod):
@@ -701,7 +636,7 @@ def test_halo_whole_x_hop0_gather(world, ghost):
 @pytest.mark.parametrize("name", ["rand_d128_r05", "rand_d36_ppr", "cora_sym_k3"])
 def test_hub_window_256_bit_exact(name, oracle_mod):
     """Hub workgroups with 256-nonzero windows (two per CU; the default once a launch has more hub
-    workgroups than CUs), with 512, and the 4-producer "lite" workgroup (SRG_SPMM_HUB_LITE): every
+    workgroups than CUs) and with 512: every
     row a hub row, all bit-identical to the reference."""
     from srgnn.spmm import spmm
     c = G.Case(name)
@@ -714,8 +649,8 @@ def test_hub_window_256_bit_exact(name, oracle_mod):
         x = np.ascontiguousarray(x[:, : x.shape[1] // 4 * 4])
         want = oracle_mod.spmm(*c.ahat(), x)
     X = torch.from_numpy(x).cuda()
-    for w256, lite in ((True, False), (False, False), (False, True)):
-        y = spmm(A, X, hub_w256=w256, hub_lite=lite)
+    for w256 in (True, False):
+        y = spmm(A, X, hub_w256=w256)
         if x.shape[1] != c.x().shape[1]:
             np.testing.assert_array_equal(y.cpu().numpy(), want)
         else:
@@ -730,8 +665,8 @@ def test_hub_window_256_bit_exact(name, oracle_mod):
     x = rng.standard_normal((3000, 64)).astype(np.float32)
     B = DeviceCSR.from_tensors(ip, ix, vv, n_cols=3000, heavy_threshold=0, hub_threshold=0, device="cuda")
     want = None
-    for w256, lite in ((True, False), (False, False), (False, True)):
-        y = spmm(B, torch.from_numpy(x).cuda(), hub_w256=w256, hub_lite=lite).cpu().numpy()
+    for w256 in (True, False):
+        y = spmm(B, torch.from_numpy(x).cuda(), hub_w256=w256).cpu().numpy()
         want = y if want is None else want
         assert np.array_equal(y, want)
     assert np.array_equal(want, oracle_mod.spmm(ip, ix, vv, x))
@@ -908,71 +843,3 @@ def test_schedule_ordered_one_launch_bit_exact(name):
     for k in range(1, c.k + 1):
         c.check_hop(k, hops[k].cpu().numpy())
     c.check_hop(1, spmm_mod.hop(A, X, torch.empty_like(X), col_blocks=1).cpu().numpy())
-
-
-@pytest.mark.parametrize("world,chunks,ghost,giant,d,medium", [(8, 6, 2, 1000, 128, True), (4, 4, 8, 400, 64, True),
-                                                              (2, 3, None, None, 256, True), (8, 6, 2, 1000, 32, True),
-                                                              (3, 5, 0, 600, 130, True), (8, 6, 2, None, 128, False)])
-def test_halo_medium_spans_bitwise(world, chunks, ghost, giant, d, medium):
-    """Medium hub rows as column spans inside the row chunks (srgnn.dist.MEDIUM_SPANS: chunk c runs
-    its own rows whole and span c of every medium hub row with per-row accumulation,
-    srg_spmm_span_rowacc_f32; the rows above the giant threshold stay hub workgroups beside the
-    chunks): every hop bitwise equal to the single-device propagation, for wide, narrow and ragged
-    panels, with and without giant rows, and with the mode off."""
-    from srgnn import synth
-    from srgnn.csr import DeviceCSR
-    from srgnn.dist import HaloPartitionedOperator, simulate_halo_propagate
-    from srgnn.normalize import sym_norm_binary
-    from srgnn.spmm import propagate
-    n = 20000
-    u, v = synth.rmat_undirected_t(n, 150000, seed=22, device="cuda")
-    ip, ix = synth.symmetric_csr_t(n, u, v)
-    ip, ix, vals = sym_norm_binary(ip, ix, n, 0.5)
-    x = synth.uniform_features_t(n, d, device="cuda")
-    want = propagate(DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, device="cuda"), x, 3)
-    shares = [HaloPartitionedOperator(ip, ix, vals, n, chunks=chunks, hub_threshold=150, device="cuda", rank=q,
-                                      world=world, ghost_max_degree=ghost, medium_spans=medium,
-                                      giant_threshold=giant) for q in range(world)]
-    plans = [s._medium_plan() for s in shares]
-    if medium:
-        assert all(p is not None for p in plans)
-        if giant is not None:
-            assert any(p[0] is not None for p in plans)       # some giant rows stay hub workgroups
-    else:
-        assert all(p is None for p in plans)
-    got = simulate_halo_propagate(ip, ix, vals, n, x, 3, world, shares=shares)
-    for k in range(1, 4):
-        assert torch.equal(got[k], want[k]), f"hop {k} differs with {world} virtual halo ranks"
-
-
-def test_span_rowacc_entry_checks():
-    """srg_spmm_span_rowacc_f32 rejects hub / accumulate / FAST flags and missing span arrays."""
-    from srgnn import _lib
-    L = _lib.lib()
-    X = torch.zeros((4, 8), device="cuda")
-    ip = torch.tensor([0, 1, 2, 3, 4], dtype=torch.int64, device="cuda")
-    ix = torch.arange(4, dtype=torch.int32, device="cuda")
-    vv = torch.ones(4, device="cuda")
-    order = torch.arange(4, dtype=torch.int32, device="cuda")
-    s = _lib.stream(X.device)
-    args = (ip.data_ptr(), ip[1:].data_ptr(), ip.data_ptr(), ix.data_ptr(), vv.data_ptr(), 4, order.data_ptr(), 0,
-            X.data_ptr(), 8, X.data_ptr(), 8, 8)
-    for f in (_lib.SRG_SPMM_ACCUMULATE, _lib.SRG_SPMM_FAST, _lib.SRG_SPMM_HUB_NOJOIN):
-        assert L.srg_spmm_span_rowacc_f32(*args, f, s) == _lib.SRG_ERR_INVALID
-    bad = list(args)
-    bad[2] = None
-    assert L.srg_spmm_span_rowacc_f32(*bad, 0, s) == _lib.SRG_ERR_INVALID
-    Y = torch.full((4, 8), 5.0, device="cuda")
-    X2 = torch.arange(32, dtype=torch.float32, device="cuda").reshape(4, 8)
-    # row_first == row_beg: every row starts from zero -> Y = X (identity pattern)
-    good = list(args)
-    good[8], good[10] = X2.data_ptr(), Y.data_ptr()
-    assert L.srg_spmm_span_rowacc_f32(*good, 0, s) == _lib.SRG_OK
-    torch.cuda.synchronize()
-    assert torch.equal(Y, X2)
-    # row_first != row_beg: every row continues from Y -> Y = X2 + X2
-    first = ip.clone() - 1
-    good[2] = first.data_ptr()
-    assert L.srg_spmm_span_rowacc_f32(*good, 0, s) == _lib.SRG_OK
-    torch.cuda.synchronize()
-    assert torch.equal(Y, 2 * X2)

@@ -147,12 +147,12 @@ def test_lean_epilogue_bit_identical(order, cb):
     assert torch.equal(fused, lean) and torch.equal(fused, plain)
 
 
-@pytest.mark.parametrize("B", ["2", "3"])
+@pytest.mark.parametrize("B", [2, 3])
 def test_split_path_column_blocked_bit_identical(monkeypatch, B):
     """The split path's SpMMs as column-blocked hops (spmm.hop, forced here; automatic for panels of
     512 MiB .. 16 GiB) == the fused kernel, bit for bit."""
     from srgnn import spmm as S_, wavelet as W
-    monkeypatch.setattr(S_, "_COL_BLOCKS_ENV", B)
+    monkeypatch.setattr(S_, "FORCE_COL_BLOCKS", B)
     a = graphs()["rmat3000"]
     L = W.laplacian_from_adj(a)
     f = W.HeatWaveletFilter(L, [-0.5, 0.5], order=3, lmax=None, dtype=torch.float32, device="cuda",

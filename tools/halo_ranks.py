@@ -32,23 +32,15 @@ def main():
     ap.add_argument("--chunks", type=int, default=4)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--d", type=int, default=None, help="feature width (default: the config's)")
-    ap.add_argument("--fused", action="store_true", help="also time the opt-in fused pack (srg_spmm_send_f32)")
     ap.add_argument("--hub-launches", type=int, default=None,
                     help="launch count the hub threshold assumes (default: the chunk count)")
     ap.add_argument("--giant-weight", type=float, default=None,
                     help="partition weight of giant rows (default: srgnn.dist.GIANT_WEIGHT)")
     ap.add_argument("--fast", action="store_true", help="the hub group in tolerance mode (SRG_SPMM_FAST)")
-    ap.add_argument("--early-degree", type=int, default=None,
-                    help="non-hub rows longer than this run in the first chunk (srgnn.dist early_degree)")
     ap.add_argument("--col-blocks", default=None,
                     help="column blocks of the row chunks' launches: one value or a comma list (default: auto)")
-    ap.add_argument("--hub-col-blocks", default=None,
-                    help="column blocks of the hub group's launch: one value or a comma list (default: auto)")
     ap.add_argument("--quick", action="store_true",
                     help="time only each rank's hop compute (op.compute), no breakdowns: for A/B sweeps")
-    ap.add_argument("--medium", default=None, choices=["on", "off"],
-                    help="medium hub rows as column spans in the chunks (default: srgnn.dist.MEDIUM_SPANS)")
-    ap.add_argument("--giant-threshold", type=int, default=None)
     ap.add_argument("--ghost", default="auto",
                     help="ghost row degree cap(s): 'auto' (the operator's cost model) or a comma list")
     a = ap.parse_args()
@@ -59,17 +51,13 @@ def main():
     out = {"config": a.config, "n": n, "nnz": int(ix.numel()), "d": d, "worlds": {}}
     ghosts = [None] if a.ghost == "auto" else [int(c) for c in a.ghost.split(",")]
     cbs = [None] if a.col_blocks is None else [int(c) for c in a.col_blocks.split(",")]
-    hcbs = [None] if a.hub_col_blocks is None else [int(c) for c in a.hub_col_blocks.split(",")]
-    for P, ghost, cb, hcb in [(int(w), gc, cb, h) for w in a.worlds.split(",") for gc in ghosts for cb in cbs
-                              for h in hcbs]:
+    hcb = None
+    for P, ghost, cb in [(int(w), gc, cb) for w in a.worlds.split(",") for gc in ghosts for cb in cbs]:
         ranks = []
         for q in range(P):
             op = HaloPartitionedOperator(ip, ix, vals, n, chunks=a.chunks, device=dev, rank=q, world=P,
                                          ghost_max_degree=ghost, hub_launches=a.hub_launches,
-                                         giant_weight=a.giant_weight, fast=a.fast, col_blocks=cb,
-                                         early_degree=a.early_degree, hub_col_blocks=hcb,
-                                         medium_spans=None if a.medium is None else a.medium == "on",
-                                         giant_threshold=a.giant_threshold)
+                                         giant_weight=a.giant_weight, fast=a.fast, col_blocks=cb)
             src = op.new_panel(d)
             src[: op.rows].copy_(x[op.r0:op.r1])
             src[op.rows:].uniform_(-1, 1)
@@ -172,20 +160,6 @@ def main():
                    "hub_rows": op.views[op.C][1],
                    "ms_all_serial": times["all"], "ms_hub": times["hub"], "ms_chunks": times["chunks"],
                    "ms_compute": times["compute"], "ms_hub_launch": times.get("hub_launch")}
-            if a.fused:
-                # the fused pack (srg_spmm_send_f32): the chunks' kernels store the send rows themselves
-                from srgnn.spmm import spmm_send
-                packed = op.send_buffer(d)
-                ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * a.reps)]
-                for r in range(a.reps):
-                    ev[2 * r].record()
-                    for g in range(op.C):
-                        if op.views[g][1]:
-                            spmm_send(op._A[g], src, dst[: op.rows], packed, op._send_ptr, op._send_slot)
-                    ev[2 * r + 1].record()
-                torch.cuda.synchronize()
-                ms = sorted(ev[2 * r].elapsed_time(ev[2 * r + 1]) for r in range(a.reps))
-                rec["ms_chunks_fused_pack"] = ms[len(ms) // 2]
             ranks.append(rec)
             print(f"  P={P} rank {q}: rows={op.rows} halo={op.halo} (received {op.n_recv}, ghosts {op.n_ghost} "
                   f"<= degree {op.ghost_max_degree}) chunks {times['chunks']:.3f} ms (ghosts {times['ghosts']:.3f}), "
