@@ -402,11 +402,11 @@ def parity_vs_oracle(sample, checks, tolerance=False):
 def one_shot(ip, ix, vals, n, X, K, dev, heavy_threshold=None):
     """The reference's own call pattern: NodeClassification.execute runs preprocess once per run
     (SSRG/tasks/node_classification.py:62), i.e. ONE propagate(K) on a freshly built operator.  Here:
-    a fresh DeviceCSR from the device arrays (row schedule), srgnn.spmm.propagate with its column
-    cut for a K-hop run (span blocks: a K-hop run does not amortise the compact copies the timed
-    operator gets) and the K output panels allocated inside the bracket; HIP events on the launch
-    stream plus the host wall clock around it.  Â and X already resident (GraphOp.propagate's
-    construct_adj and H2D / D2H are tools/e2e_api.py's)."""
+    a fresh DeviceCSR from the device arrays (validated; its row schedule is left to first use),
+    srgnn.spmm.propagate laying it out for a K-hop run with the native planner (srg_plan_build: column
+    blocks, compact launch-ordered copies from spmm.MIN_HOPS_TO_COMPACT hops) and the K output panels
+    allocated inside the bracket; HIP events on the launch stream plus the host wall clock around it.
+    Â and X already resident (GraphOp.propagate's construct_adj and H2D / D2H are tools/e2e_api.py's)."""
     from srgnn.csr import DeviceCSR
     from srgnn.spmm import auto_col_blocks, propagate
     stream = torch.cuda.current_stream(dev)

@@ -140,7 +140,11 @@ int srg_spmm_csr_f32(const int64_t* indptr, const int32_t* indices, const float*
 /* K hops: panels[k] = A * panels[k-1] for k = 1..K, panels[0] = X (read only).  `panels` is a
  * HOST array of K+1 device pointers, all with leading dimension ld.  Replaces the hop loop of
  * GraphOp.propagate, SSRG/operators/base_operator.py:32-35 (with the per-hop host round trips of
- * utils.py:38-47 removed).  A square (n_rows == rows of X). */
+ * utils.py:38-47 removed).  A square (n_rows == rows of X).  Given no schedule (row_order NULL,
+ * n_hub = n_heavy = 0) and flags within NT_STORE | FAST, the hops run through a plan built for them
+ * (srg_plan_build with automatic choices, released in stream order after the hops; the call then
+ * synchronises `stream` twice while it plans and takes the plan's memory for its duration); with a
+ * schedule, or other flags, every hop is one launch over the caller's CSR. */
 int srg_propagate_khop_f32(const int64_t* indptr, const int32_t* indices, const float* values,
                            int64_t n_rows, const int32_t* row_order, int64_t n_hub,
                            int64_t n_heavy, float* const* panels,
@@ -179,6 +183,57 @@ typedef struct srg_hop_launch {
  * caller must srg_hub_join(stream) after the call, before anything reads the hub rows. */
 int srg_propagate_plan_f32(const srg_hop_launch* launches, int32_t n_launch, int32_t join_hub,
                            float* const* panels, int64_t ld, int32_t d, int32_t K, void* stream);
+
+/* ---- the one-GPU planner (csrc/srg_plan.hip) ------------------------------------------------------
+ * The layout of a square operator for a run of `hops` hops over d-column panels, built on the device:
+ * column blocks as row spans (col_blocks: 0 = automatic -- 4..8 blocks for panels of >= 512 MiB at
+ * d >= 64 and runs of >= 4 hops, else 1), block 0 as its cut rows' spans and its whole rows (rows of
+ * <= 48 entries), per-launch schedules by decreasing span length with their hub / slice-wave counts,
+ * the hub spans chained on the side stream, spans by schedule slot and, for runs of at least
+ * SRG_PLAN_MIN_HOPS_TO_COMPACT hops when it fits in a quarter of the free memory, compact copies of
+ * the ids and values in launch order.  The same layout srgnn.spmm.prepare gives a DeviceCSR (the
+ * srgnn package builds its K-hop runs with this planner).  Replaces the reference's per-hop
+ * csr_sparse_dense_matmul setup inside GraphOp.propagate (SSRG/operators/base_operator.py:32-35,
+ * utils.py:17-47), which re-reads the scipy CSR every hop.
+ * Unlike the other (B) entries the plan allocates device memory (stream-ordered, hipMallocAsync on
+ * `stream`: the schedules, the spans by slot, the copies -- srg_plan_describe's device_bytes) and
+ * synchronises `stream` twice while it builds.  The plan BORROWS indptr / indices / values (span
+ * layouts read them every hop): they must outlive it.  indptr[n_rows + 1], indices / values
+ * [indptr[n_rows] - indptr[0]], column ids in [0, n_rows) (not validated here: srg_csr_validate). */
+typedef struct srg_plan srg_plan;
+#define SRG_PLAN_MIN_HOPS_TO_COMPACT 6
+#define SRG_PLAN_COMPACT 0x1u        /* copy the entries in launch order whatever the run length */
+#define SRG_PLAN_SPANS 0x2u          /* never copy: spans of the caller's arrays */
+#define SRG_PLAN_SPLIT_BLOCK0 0x4u   /* block 0 as two launches (default: panels < 16 GiB) */
+#define SRG_PLAN_WHOLE_BLOCK0 0x8u   /* block 0 as one launch */
+typedef struct {
+    int64_t n_rows, nnz;
+    int64_t device_bytes;            /* device memory the plan holds */
+    int32_t d;                       /* the panel width it was built for (any width runs it) */
+    int32_t col_blocks;              /* column blocks per hop (1: the one-launch hop) */
+    int32_t n_launch;                /* k_spmm launches per hop */
+    int32_t compact, split_block0, hub_chain;
+    int32_t device;
+} srg_plan_desc;
+int srg_plan_build(const int64_t* indptr, const int32_t* indices, const float* values, int64_t n_rows,
+                   int32_t d, int32_t hops, int32_t col_blocks, uint32_t opts, void* stream, srg_plan** plan);
+/* Releases the plan's device memory in stream order on `stream`: every hop that uses the plan must
+ * be ordered before that point of `stream` (enqueued on it, or joined into it). */
+int srg_plan_destroy(srg_plan* plan, void* stream);
+int srg_plan_describe(const srg_plan* plan, srg_plan_desc* desc);
+/* Launch i of one hop over a d-column panel, as srg_plan_propagate_f32 runs it (flags included), and
+ * whether the hops join the hub side stream at their ends: for callers that drive
+ * srg_propagate_plan_f32 themselves, and for layout tests.  A compact plan built for a 64 / 128 / 256
+ * column panel keeps row-indexed spans for its hub and slice-wave rows only (its light rows read the
+ * spans by slot); the first srg_plan_launch call (or a propagate over another width) completes them,
+ * enqueued on `stream`. */
+int srg_plan_launch(const srg_plan* plan, int32_t i, int32_t d, srg_hop_launch* launch, int32_t* join_hub,
+                    void* stream);
+/* K hops through the plan: panels[k] = A * panels[k-1], k = 1..K (HOST array of K+1 device pointers
+ * of leading dimension ld, d columns; any d, the layout was chosen for the build's d).  flags:
+ * SRG_SPMM_NT_STORE, SRG_SPMM_FAST.  Bitwise srg_propagate_khop_f32's hops (FAST: its tolerance). */
+int srg_plan_propagate_f32(const srg_plan* plan, float* const* panels, int64_t ld, int32_t d, int32_t K,
+                           uint32_t flags, void* stream);
 
 /* Chebyshev heat-kernel filter bank (wavelet basis), SSRG/models/base_scalable/base_model.py:
  * 184-191, 236-265 via pygsp cheby_op.  One fused launch per Chebyshev order:

@@ -1,0 +1,843 @@
+// srg_plan.hip -- the one-GPU propagate planner (srg_plan_build / srg_plan_propagate_f32): the layout a
+// long-lived operator gets for a run of K hops, built on the device in one pass, for C / C++ hosts and
+// for srgnn.spmm (the boundary the reference's GraphOp.propagate hop loop,
+// SSRG/operators/base_operator.py:32-35, is replaced behind).
+//
+// The layout:
+//   * column blocks: block b of row r is the span of its entries whose column ids lie in
+//     [ceil(b n / B), ceil((b+1) n / B)) (one binary search per row and boundary); rows of <= 48 entries
+//     run whole in block 0; B from the panel size (4..8 for panels of >= 512 MiB at d >= 64);
+//   * launches: block 0 as its cut rows' first spans and its whole rows (panels < 16 GiB), then blocks
+//     1..B-1 with ACCUMULATE -- every output element is the one-launch fma chain, continued;
+//   * schedules: each launch's rows by decreasing span length (stable: ties in row order), the first
+//     n_hub hub rows (> max(2048, nnz_L / 1024) entries), then n_heavy slice-wave rows
+//     (> max(96, nnz_L / 30000); the one-launch hop: nnz / 100000);
+//   * compact copies (long runs): the ids and values copied once more, launch after launch, each
+//     launch's rows in its schedule order, so no cache line of the streams is read by two launches;
+//   * spans by schedule slot (the packed light rows read consecutive slots);
+//   * hub spans chained on the side stream when every launch over cut rows has the same hub rows.
+// This is srgnn/spmm.py prepare + _hop_plan (the torch formulation kept for the aggregation and
+// wavelet paths), restated as one radix sort of (launch, span length) keys over every launch's rows,
+// one scan of the lengths (the copy positions and each launch's nnz) and one copy pass; two host
+// synchronisations (the degree statistics; the per-launch counts, checked before any span is derived).
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <new>
+#include <vector>
+
+#include "srgnn_hip.h"
+
+extern "C" void srg_set_error(int code, const char* msg);   // srg_spmm.hip: thread-local srg_last_error
+extern "C" void srg_clear_error(void);
+
+struct srg_plan {
+    struct Launch {
+        int block = 0;
+        const int64_t* row_beg = nullptr;
+        const int64_t* row_end = nullptr;    // nullptr: a CSR launch (row_beg has n + 1 pointers)
+        const int32_t* indices = nullptr;
+        const float* values = nullptr;
+        const int32_t* order = nullptr;
+        int64_t n_rows = 0, n_hub = 0, n_heavy = 0, n_narrow = 0, nnz = 0;
+        const int64_t* slot_beg = nullptr;
+        const int64_t* slot_end = nullptr;
+        int64_t item0 = 0;                   // the launch's first item (slot 0) among all the plan's items
+        bool whole_rows = false;             // block 0's whole rows (not in the hub chain)
+    };
+    int device = 0;
+    int64_t n = 0, nnz = 0, n_items = 0;
+    int32_t d = 0, B = 1;
+    bool split0 = false, compact = false, same_hubs = false;
+    // compact plans: whether the row-indexed spans hold every scheduled row (the light-row paths of
+    // panels other than 64 / 128 / 256 columns read them) or only the hub and slice-wave rows (the
+    // packed light rows read the spans by slot); completed on first need (complete_rows)
+    bool rows_full = true;
+    int64_t* blk_beg = nullptr;
+    int64_t* blk_end = nullptr;
+    std::vector<Launch> launches;
+    void* owned = nullptr;                   // one device allocation holds every array of the plan
+    int64_t bytes = 0;
+};
+
+namespace {
+
+int pfail(int code, const char* fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    srg_set_error(code, buf);
+    return code;
+}
+
+#define SRG_PLAN_HIP(expr)                                                                       \
+    do {                                                                                         \
+        hipError_t e_ = (expr);                                                                  \
+        if (e_ != hipSuccess)                                                                    \
+            return pfail(SRG_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(e_));            \
+    } while (0)
+
+// the constants of srgnn/csr.py and srgnn/spmm.py (DESIGN.md §3 has the measurements)
+constexpr int64_t kWholeMax = 48;              // csr.BLOCK_WHOLE_MAX
+constexpr int64_t kBlockHeavyPer = 30000;      // csr.BLOCK_HEAVY_PER
+constexpr int64_t kNarrowHeavy = 32;           // csr.NARROW_HEAVY_THRESHOLD
+constexpr int kMinHopsToCut = 4;               // spmm.MIN_HOPS_TO_CUT
+constexpr int64_t kSplitBlock0MaxPanel = 16ll << 30;   // spmm.SPLIT_BLOCK0_MAX_PANEL
+constexpr int64_t kCapWavesMinPanel = 512ll << 20;     // spmm.CAP_WAVES_MIN_PANEL
+constexpr int kMaxBlocks = 64;
+constexpr int kMaxLaunch = kMaxBlocks + 1;
+constexpr int kHubPrefix = 256;                // hub rows compared for the chain (more: no chain)
+constexpr int64_t kCopyChunk = 4096;           // entries of the copy per wave task
+
+// rows of a launch: every row, block 0's cut rows / whole rows
+enum RowSet { kAll = 0, kCut = 1, kWhole = 2 };
+
+struct LaunchTable {
+    int n_launch;
+    int lbits;                                 // launch id bits above the length bits
+    int lenbits;
+    int whole_rule;                            // 1: the one-launch hop's heavy threshold (nnz / 100000)
+    int64_t off[kMaxLaunch + 1];               // item offsets of the launches
+    int64_t rows_lim[kMaxLaunch];              // compact: items of launch L below off[L] + rows_lim[L] get row-indexed spans
+};
+
+// Bump allocation out of one device allocation (256-byte aligned pieces): a plan makes two
+// hipMalloc calls, one for what it keeps and one for its build's scratch.
+struct Arena {
+    char* base = nullptr;
+    size_t used = 0;
+    template <typename T>
+    T* take(size_t count)
+    {
+        used = (used + 255) & ~size_t(255);
+        T* p = reinterpret_cast<T*>(base ? base + used : nullptr);
+        used += std::max<size_t>(count, 1) * sizeof(T);
+        return p;
+    }
+};
+
+// stats[0] = the longest row, stats[1] = rows of <= kWholeMax entries; stats[2], [3] = indptr[0], indptr[n]
+__global__ void __launch_bounds__(256) k_plan_stats(const int64_t* __restrict__ ip, int64_t n,
+                                                    unsigned long long* __restrict__ stats)
+{
+    __shared__ unsigned long long smx[4], swh[4];
+    unsigned long long mx = 0, whole = 0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += stride) {
+        const int64_t deg = ip[r + 1] - ip[r];
+        mx = max(mx, (unsigned long long)max<int64_t>(deg, 0));
+        whole += deg <= kWholeMax ? 1 : 0;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        mx = max(mx, (unsigned long long)__shfl_xor((long long)mx, o));
+        whole += (unsigned long long)__shfl_xor((long long)whole, o);
+    }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { smx[w] = mx; swh[w] = whole; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int i = 1; i < (int)(blockDim.x >> 6); ++i) { mx = max(mx, smx[i]); whole += swh[i]; }
+        atomicMax(&stats[0], mx);
+        atomicAdd(&stats[1], whole);
+        if (blockIdx.x == 0) {
+            stats[2] = (unsigned long long)ip[0];
+            stats[3] = (unsigned long long)ip[n];
+        }
+    }
+}
+
+// split points of the column blocks (srg_csr_col_splits' lower bounds) for the cut rows; the whole rows
+// end in block 0 (only block 0's end is ever read for them), and the cut-row flags
+__global__ void __launch_bounds__(256) k_plan_splits(const int64_t* __restrict__ ip, const int32_t* __restrict__ ix,
+                                                     int64_t n, int B, int64_t* __restrict__ splits,
+                                                     int32_t* __restrict__ cut)
+{
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n * (B - 1)) return;
+    const int b = (int)(t / n) + 1;
+    const int64_t r = t % n;
+    const int64_t beg = ip[r], end = ip[r + 1];
+    const bool whole = end - beg <= kWholeMax;
+    if (b == 1) cut[r] = whole ? 0 : 1;
+    if (whole) {
+        if (b == 1) splits[t] = end;
+        return;
+    }
+    const int64_t bound = ((int64_t)b * n + B - 1) / B;
+    int64_t lo = beg, hi = end;
+    while (lo < hi) {
+        const int64_t mid = lo + (hi - lo) / 2;
+        if ((int64_t)ix[mid] < bound) lo = mid + 1; else hi = mid;
+    }
+    splits[t] = lo;
+}
+
+__device__ __forceinline__ int64_t bound_of(const int64_t* __restrict__ ip, const int64_t* __restrict__ splits,
+                                            int64_t n, int B, int b, int64_t r)
+{
+    return b == 0 ? ip[r] : (b == B ? ip[r + 1] : splits[(int64_t)(b - 1) * n + r]);
+}
+
+__device__ __forceinline__ int block_of(int L, bool split0) { return split0 ? (L <= 1 ? 0 : L - 1) : L; }
+
+// the sort items: one (launch, span length) key and the row id per (launch, row of it), the launch's
+// rows in ascending order (the stable sort keeps that order among equal lengths, as torch.sort does)
+__global__ void __launch_bounds__(256) k_plan_items(const int64_t* __restrict__ ip, const int64_t* __restrict__ splits,
+                                                    const int32_t* __restrict__ cutpos, int64_t n, int B, int split0,
+                                                    LaunchTable T, uint64_t* __restrict__ keys,
+                                                    int32_t* __restrict__ vals)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const uint64_t lmask = (1ull << T.lenbits) - 1;
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += stride) {
+        const int64_t deg = ip[r + 1] - ip[r];
+        auto put = [&](int L, int64_t pos, int64_t len) {
+            const int64_t i = T.off[L] + pos;
+            keys[i] = ((uint64_t)L << T.lenbits) | (lmask - (uint64_t)len);
+            vals[i] = (int32_t)r;
+        };
+        if (B == 1) {
+            put(0, r, deg);
+        } else if (deg > kWholeMax) {
+            const int64_t cp = cutpos[r];
+            put(0, split0 ? cp : r, bound_of(ip, splits, n, B, 1, r) - ip[r]);
+            for (int b = 1; b < B; ++b)
+                put(split0 ? b + 1 : b, cp,
+                    bound_of(ip, splits, n, B, b + 1, r) - bound_of(ip, splits, n, B, b, r));
+        } else {
+            put(split0 ? 1 : 0, split0 ? r - cutpos[r] : r, deg);
+        }
+    }
+}
+
+// every sorted item lies in its launch's segment (an item the items kernel did not write keeps the
+// all-ones fill and lands outside): a cheap guard before any span is derived from the keys
+__global__ void __launch_bounds__(256) k_plan_check(const uint64_t* __restrict__ keys, int64_t n_items, LaunchTable T,
+                                                    int32_t* __restrict__ bad)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    int b = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_items; i += stride) {
+        const uint64_t L = keys[i] >> T.lenbits;
+        b |= (L >= (uint64_t)T.n_launch || i < T.off[L] || i >= T.off[L + 1]) ? 1 : 0;
+    }
+    if (b) atomicOr(bad, 1);
+}
+
+struct KeyLen {
+    uint64_t lmask;
+    __host__ __device__ int64_t operator()(const uint64_t& k) const { return (int64_t)(lmask - (k & lmask)); }
+};
+
+// per launch: nnz, hub / slice-wave / narrow slice-wave rows (the sorted lengths decrease inside a
+// launch: a count of lengths above t is a binary search), the first hub rows
+__global__ void k_plan_counts(const uint64_t* __restrict__ keys, const int32_t* __restrict__ vals,
+                              const int64_t* __restrict__ pos, LaunchTable T, int64_t* __restrict__ counts,
+                              int32_t* __restrict__ hubs)
+{
+    const int L = threadIdx.x;
+    if (L >= T.n_launch) return;
+    const uint64_t lmask = (1ull << T.lenbits) - 1;
+    const int64_t o = T.off[L], m = T.off[L + 1] - o;
+    const int64_t nnz = pos[o + m] - pos[o];
+    auto above = [&](int64_t t) {
+        int64_t lo = 0, hi = m;
+        while (lo < hi) {
+            const int64_t mid = lo + (hi - lo) / 2;
+            if ((int64_t)(lmask - (keys[o + mid] & lmask)) > t) lo = mid + 1; else hi = mid;
+        }
+        return lo;
+    };
+    const int64_t hub_t = max<int64_t>(2048, nnz / 1024);
+    const int64_t heavy_t = max<int64_t>(96, nnz / (T.whole_rule ? 100000 : kBlockHeavyPer));
+    const int64_t n_hub = above(hub_t);
+    counts[4 * L + 0] = nnz;
+    counts[4 * L + 1] = n_hub;
+    counts[4 * L + 2] = max<int64_t>(0, above(heavy_t) - n_hub);
+    counts[4 * L + 3] = max<int64_t>(0, above(kNarrowHeavy) - n_hub);
+    for (int64_t j = 0; j < min<int64_t>(n_hub, kHubPrefix); ++j) hubs[(int64_t)L * kHubPrefix + j] = vals[o + j];
+}
+
+// The spans by slot (and, compact, the row-indexed spans of the first rows_lim[L] rows of each launch):
+// item i's span is [pos[i], pos[i+1]) of the copy (compact) or its span of the caller's arrays.
+__global__ void __launch_bounds__(256) k_plan_spans(const int64_t* __restrict__ ip, const int64_t* __restrict__ splits,
+                                                    int64_t n, int B, int split0, LaunchTable T, int compact,
+                                                    const uint64_t* __restrict__ keys, const int32_t* __restrict__ vals,
+                                                    const int64_t* __restrict__ pos, int64_t n_items,
+                                                    int64_t* __restrict__ slot_beg, int64_t* __restrict__ slot_end,
+                                                    int64_t* __restrict__ blk_beg, int64_t* __restrict__ blk_end)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_items; i += stride) {
+        const int L = (int)(keys[i] >> T.lenbits);
+        const int b = block_of(L, split0 != 0);
+        const int64_t len = pos[i + 1] - pos[i];
+        if (compact) {
+            const int64_t p = pos[i];
+            slot_beg[i] = p;
+            slot_end[i] = p + len;
+            if (i - T.off[L] < T.rows_lim[L]) {
+                const int64_t r = vals[i];
+                blk_beg[(int64_t)b * n + r] = p;
+                blk_end[(int64_t)b * n + r] = p + len;
+            }
+        } else {
+            const int64_t src = bound_of(ip, splits, n, B, b, vals[i]);
+            slot_beg[i] = src;
+            slot_end[i] = src + len;
+        }
+    }
+}
+
+// The compact copy: the entries of all items laid end to end (item i's at [pos[i], pos[i+1])).  Each
+// wave task copies kCopyChunk consecutive entries of the copy: it finds the item holding its first
+// entry (a binary search of pos), holds 64 items' (position, source) pairs in its lanes, and every
+// lane takes consecutive entries, finding its item among the lanes' positions with 6 shuffles -- so
+// the writes are whole contiguous runs and the reads contiguous within each span, whatever the span
+// lengths (5 M spans of ~23 entries on products: one span per 16-lane group read and wrote 64-byte
+// pieces and took 1.3 ms; tools/plan_probe).
+__global__ void __launch_bounds__(256) k_plan_copy(const int64_t* __restrict__ ip, const int64_t* __restrict__ splits,
+                                                   const int32_t* __restrict__ ix, const float* __restrict__ v,
+                                                   int64_t n, int B, int split0, int lenbits,
+                                                   const uint64_t* __restrict__ keys, const int32_t* __restrict__ vals,
+                                                   const int64_t* __restrict__ pos, int64_t n_items, int64_t nnz,
+                                                   int32_t* __restrict__ oix, float* __restrict__ ov)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t n_waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    const int64_t n_tasks = (nnz + kCopyChunk - 1) / kCopyChunk;
+    for (int64_t task = wave; task < n_tasks; task += n_waves) {
+        const int64_t e0 = task * kCopyChunk, e1 = min(e0 + kCopyChunk, nnz);
+        // the item holding entry e0: the last i with pos[i] <= e0 (pos[0] = 0)
+        int64_t lo = 0, hi = n_items;          // invariant: pos[lo] <= e0, answer in [lo, hi)
+        while (hi - lo > 1) {
+            const int64_t mid = lo + (hi - lo) / 2;
+            if (pos[mid] <= e0) lo = mid; else hi = mid;
+        }
+        int64_t ibase = lo;
+        int64_t e = e0;                        // wave-uniform: the first entry not yet copied
+        while (e < e1) {
+            const int64_t i = ibase + lane;
+            int64_t p = INT64_MAX, src = 0;
+            if (i < n_items) {
+                p = pos[i];
+                const int L = (int)(keys[i] >> lenbits);
+                src = bound_of(ip, splits, n, B, block_of(L, split0 != 0), vals[i]);
+            }
+            // the batch's items cover [pos[ibase], pos[ibase + 64])
+            const int64_t pend = ibase + 64 < n_items ? pos[ibase + 64] : nnz;
+            const int64_t stop = min(e1, pend);
+            for (int64_t eb = e; eb < stop; eb += 64) {
+                const int64_t me = eb + lane;
+                // the last lane j with p_j <= me
+                int j = 0;
+#pragma unroll
+                for (int step = 32; step > 0; step >>= 1) {
+                    const int64_t pj = __shfl((long long)p, j + step);
+                    if (pj <= me) j += step;
+                }
+                const int64_t pj = __shfl((long long)p, j), sj = __shfl((long long)src, j);
+                if (me < stop) {
+                    const int64_t from = sj + (me - pj);
+                    oix[me] = ix[from];
+                    ov[me] = v[from];
+                }
+            }
+            e = stop;
+            ibase += 64;
+        }
+    }
+}
+
+// The row-indexed spans of every scheduled row of a compact plan (the light-row paths that read them)
+__global__ void __launch_bounds__(256) k_plan_rows(int64_t n, const int32_t* __restrict__ order,
+                                                   const int64_t* __restrict__ item_launch_block, int n_launch,
+                                                   const int64_t* __restrict__ slot_beg, const int64_t* __restrict__ slot_end,
+                                                   int64_t n_items, int64_t* __restrict__ blk_beg, int64_t* __restrict__ blk_end)
+{
+    // item_launch_block: [n_launch + 1] item offsets, then [n_launch] blocks
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_items; i += stride) {
+        int L = 0;
+        while (L + 1 < n_launch && i >= item_launch_block[L + 1]) ++L;
+        const int64_t b = item_launch_block[n_launch + 1 + L];
+        const int64_t r = order[i];
+        blk_beg[b * n + r] = slot_beg[i];
+        blk_end[b * n + r] = slot_end[i];
+    }
+}
+
+int bits_for(uint64_t v)
+{
+    int b = 1;
+    while (b < 64 && (v >> b) != 0) ++b;
+    return b;
+}
+
+unsigned grid_for(int64_t work, int per_block, unsigned cap)
+{
+    const int64_t g = (work + per_block - 1) / per_block;
+    return (unsigned)std::max<int64_t>(1, std::min<int64_t>(g, cap));
+}
+
+struct DevGuard {
+    int prev = -1, rc = SRG_OK;
+    explicit DevGuard(hipStream_t s)
+    {
+        if (hipGetDevice(&prev) != hipSuccess) { (void)hipGetLastError(); prev = -1; return; }
+        if (!s) return;
+        hipDevice_t d = 0;
+        if (hipStreamGetDevice(s, &d) != hipSuccess) { rc = pfail(SRG_ERR_HIP, "hipStreamGetDevice failed"); return; }
+        if ((int)d != prev && hipSetDevice((int)d) != hipSuccess) rc = pfail(SRG_ERR_HIP, "hipSetDevice(%d) failed", (int)d);
+    }
+    ~DevGuard()
+    {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+// device memory released after the work enqueued on `s` so far (hipMalloc'd: the stream-ordered pool
+// lost track of plan memory reused across builds with the hub side stream in flight -- DESIGN.md §3)
+struct DevBuf {
+    void* p = nullptr;
+    hipStream_t s = nullptr;
+    ~DevBuf() { reset(); }
+    void reset()
+    {
+        if (!p) return;
+        (void)hipStreamSynchronize(s);
+        (void)hipFree(p);
+        p = nullptr;
+    }
+};
+
+void release(srg_plan* P, hipStream_t s)
+{
+    if (!P->owned) return;
+    (void)hipStreamSynchronize(s);
+    (void)hipFree(P->owned);
+    P->owned = nullptr;
+}
+
+// compact plans built with row-indexed spans for the hub and slice-wave rows only: fill the rest
+int complete_rows(srg_plan* P, hipStream_t s)
+{
+    if (P->rows_full || !P->compact) return SRG_OK;
+    const int nl = (int)P->launches.size();
+    std::vector<int64_t> tab((size_t)2 * nl + 1);
+    for (int L = 0; L < nl; ++L) {
+        tab[L] = P->launches[L].item0;
+        tab[(size_t)nl + 1 + L] = P->launches[L].block;
+    }
+    tab[nl] = P->n_items;
+    DevBuf t;
+    t.s = s;
+    SRG_PLAN_HIP(hipMalloc(&t.p, tab.size() * sizeof(int64_t)));
+    SRG_PLAN_HIP(hipMemcpyAsync(t.p, tab.data(), tab.size() * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    const srg_plan::Launch& L0 = P->launches[0];
+    hipLaunchKernelGGL(k_plan_rows, dim3(grid_for(P->n_items, 256, 1u << 20)), dim3(256), 0, s, P->n, L0.order, (const int64_t*)t.p, nl, L0.slot_beg, L0.slot_end, P->n_items, P->blk_beg, P->blk_end);
+    SRG_PLAN_HIP(hipGetLastError());
+    P->rows_full = true;
+    return SRG_OK;
+}
+
+bool packed_width(int d) { return d == 64 || d == 128 || d == 256; }
+
+}  // namespace
+
+extern "C" {
+
+int srg_plan_build(const int64_t* indptr, const int32_t* indices, const float* values, int64_t n_rows, int32_t d,
+                   int32_t hops, int32_t col_blocks, uint32_t opts, void* stream, srg_plan** plan)
+{
+    if (!plan) return pfail(SRG_ERR_INVALID, "null plan");
+    *plan = nullptr;
+    if (!indptr) return pfail(SRG_ERR_INVALID, "null indptr");
+    if (n_rows < 0 || n_rows >= (1ll << 31)) return pfail(SRG_ERR_INVALID, "n_rows=%lld outside [0, 2^31)", (long long)n_rows);
+    if (d <= 0 || hops < 0 || col_blocks < 0 || col_blocks > kMaxBlocks)
+        return pfail(SRG_ERR_INVALID, "d=%d, hops=%d, col_blocks=%d (0 = automatic, at most %d)", d, hops, col_blocks, kMaxBlocks);
+    const uint32_t known = SRG_PLAN_COMPACT | SRG_PLAN_SPANS | SRG_PLAN_SPLIT_BLOCK0 | SRG_PLAN_WHOLE_BLOCK0;
+    if ((opts & ~known) || ((opts & SRG_PLAN_COMPACT) && (opts & SRG_PLAN_SPANS)) ||
+        ((opts & SRG_PLAN_SPLIT_BLOCK0) && (opts & SRG_PLAN_WHOLE_BLOCK0)))
+        return pfail(SRG_ERR_INVALID, "opts=0x%x: unknown or conflicting options", opts);
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    DevGuard g(s);
+    if (g.rc) return g.rc;
+    srg_plan* P = new (std::nothrow) srg_plan();
+    if (!P) return pfail(SRG_ERR_ALLOC, "plan: host memory");
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) { delete P; return pfail(SRG_ERR_HIP, "hipGetDevice failed"); }
+    P->device = dev;
+    P->n = n_rows;
+    P->d = d;
+    auto bail = [&](int rc) { release(P, s); delete P; return rc; };
+    const int64_t n = n_rows;
+    DevBuf scratch;
+    scratch.s = s;
+    // ---- 1: degree statistics (host sync 1) ----
+    unsigned long long hs[4] = {0, 0, 0, 0};
+    {
+        DevBuf st;
+        st.s = s;
+        if (hipMalloc(&st.p, 4 * sizeof(unsigned long long)) != hipSuccess) { (void)hipGetLastError(); return bail(pfail(SRG_ERR_ALLOC, "plan: statistics")); }
+        unsigned long long* dstats = (unsigned long long*)st.p;
+        if (hipMemsetAsync(dstats, 0, 4 * sizeof(unsigned long long), s) != hipSuccess) return bail(pfail(SRG_ERR_HIP, "memset"));
+        hipLaunchKernelGGL(k_plan_stats, dim3(grid_for(std::max<int64_t>(n, 1), 256, 512)), dim3(256), 0, s, indptr, n, dstats);
+        if (hipMemcpyAsync(hs, dstats, sizeof(hs), hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+            return bail(pfail(SRG_ERR_HIP, "plan: degree statistics: %s", hipGetErrorString(hipGetLastError())));
+    }
+    const int64_t max_deg = (int64_t)hs[0], n_whole_rows = (int64_t)hs[1];
+    const int64_t nnz = (int64_t)hs[3] - (int64_t)hs[2];
+    if (nnz < 0) return bail(pfail(SRG_ERR_INVALID, "indptr[n] < indptr[0]"));
+    if (nnz > 0 && (!indices || !values)) return bail(pfail(SRG_ERR_INVALID, "null indices / values"));
+    P->nnz = nnz;
+    // ---- 2: the layout: blocks, launches, copies ----
+    const int64_t panel = n * (int64_t)d * 4;
+    int B = col_blocks;
+    if (B == 0) {
+        if (d < 64 || panel < (512ll << 20)) B = 1;
+        else if (panel >= kSplitBlock0MaxPanel) B = 4;
+        else B = (int)std::min<int64_t>(8, std::max<int64_t>(4, (int64_t)std::nearbyint((double)panel / (150 << 20))));
+        if (hops < kMinHopsToCut) B = 1;
+    }
+    if (n == 0 || nnz == 0) B = 1;
+    P->B = B;
+    P->split0 = B > 1 && ((opts & SRG_PLAN_SPLIT_BLOCK0) ? true : (opts & SRG_PLAN_WHOLE_BLOCK0) ? false : panel < kSplitBlock0MaxPanel);
+    bool compact = false;
+    if (opts & SRG_PLAN_COMPACT) compact = nnz > 0;
+    else if (!(opts & SRG_PLAN_SPANS) && hops >= SRG_PLAN_MIN_HOPS_TO_COMPACT && nnz > 0) {
+        size_t fr = 0, tot = 0;
+        if (hipMemGetInfo(&fr, &tot) != hipSuccess) { (void)hipGetLastError(); fr = 0; }
+        // the copies, and the build's keys / ids / positions (< 24 B per entry)
+        compact = (uint64_t)nnz * 8 + (uint64_t)nnz * 24 <= (uint64_t)fr / 4;
+    }
+    P->compact = compact;
+    const bool split0 = P->split0;
+    const int64_t n_cut = B > 1 ? n - n_whole_rows : 0;
+    std::vector<int> sets;     // row set per launch
+    std::vector<int> blocks;
+    if (B == 1) { sets = {kAll}; blocks = {0}; }
+    else {
+        if (split0) { sets = {kCut, kWhole}; blocks = {0, 0}; }
+        else { sets = {kAll}; blocks = {0}; }
+        for (int b = 1; b < B; ++b) { sets.push_back(kCut); blocks.push_back(b); }
+    }
+    LaunchTable T{};
+    T.n_launch = (int)sets.size();
+    T.whole_rule = B == 1 ? 1 : 0;
+    T.lenbits = bits_for((uint64_t)max_deg);
+    T.lbits = bits_for((uint64_t)std::max(0, T.n_launch - 1));
+    T.off[0] = 0;
+    for (int L = 0; L < T.n_launch; ++L)
+        T.off[L + 1] = T.off[L] + (sets[L] == kAll ? n : sets[L] == kCut ? n_cut : n_whole_rows);
+    const int64_t n_items = T.off[T.n_launch];
+    P->n_items = n_items;
+    if (T.lenbits + T.lbits > 64) return bail(pfail(SRG_ERR_INVALID, "row lengths too long to plan"));
+    if (n == 0) {
+        *plan = P;
+        srg_clear_error();
+        return SRG_OK;
+    }
+    // the two allocations: what the plan keeps, the build's scratch (sizes first, then carved)
+    const bool slots = B > 1 || compact;   // a one-launch CSR hop reads no slot spans
+    size_t cub_bytes = 0;
+    {
+        size_t tb = 0;
+        KeyLen op{(1ull << T.lenbits) - 1};
+        hipcub::TransformInputIterator<int64_t, KeyLen, const uint64_t*> lens((const uint64_t*)nullptr, op);
+        if (B > 1) {
+            SRG_PLAN_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (const int32_t*)nullptr, (int32_t*)nullptr, n, s));
+            cub_bytes = std::max(cub_bytes, tb);
+        }
+        SRG_PLAN_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                                                        (const int32_t*)nullptr, (int32_t*)nullptr, n_items, 0,
+                                                        T.lenbits + T.lbits, s));
+        cub_bytes = std::max(cub_bytes, tb);
+        SRG_PLAN_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, tb, lens, (int64_t*)nullptr, n_items, s));
+        cub_bytes = std::max(cub_bytes, tb);
+    }
+    int64_t *splits = nullptr, *slot_beg = nullptr, *slot_end = nullptr, *pos = nullptr, *dcounts = nullptr;
+    int32_t *cut = nullptr, *cutpos = nullptr, *vals = nullptr, *order = nullptr, *dhubs = nullptr, *oix = nullptr;
+    uint64_t *keys = nullptr, *skeys = nullptr;
+    float* ov = nullptr;
+    void* cub_tmp = nullptr;
+    for (int pass = 0; pass < 2; ++pass) {
+        Arena keep, tmp;
+        if (pass == 1) {
+            keep.base = (char*)P->owned;
+            tmp.base = (char*)scratch.p;
+        }
+        order = keep.take<int32_t>((size_t)n_items);
+        if (slots) {
+            slot_beg = keep.take<int64_t>((size_t)n_items);
+            slot_end = keep.take<int64_t>((size_t)n_items);
+        }
+        if (B > 1) splits = (compact ? tmp : keep).take<int64_t>((size_t)(B - 1) * n);
+        if (compact) {
+            oix = keep.take<int32_t>((size_t)nnz);
+            ov = keep.take<float>((size_t)nnz);
+            P->blk_beg = keep.take<int64_t>((size_t)B * n);
+            P->blk_end = keep.take<int64_t>((size_t)B * n);
+        }
+        if (B > 1) {
+            cut = tmp.take<int32_t>((size_t)n);
+            cutpos = tmp.take<int32_t>((size_t)n);
+        }
+        keys = tmp.take<uint64_t>((size_t)n_items);
+        skeys = tmp.take<uint64_t>((size_t)n_items);
+        vals = tmp.take<int32_t>((size_t)n_items);
+        pos = tmp.take<int64_t>((size_t)n_items + 1);
+        dcounts = tmp.take<int64_t>((size_t)4 * T.n_launch + 1);
+        dhubs = tmp.take<int32_t>((size_t)kHubPrefix * T.n_launch);
+        cub_tmp = tmp.take<char>(cub_bytes + 256);
+        if (pass == 0) {
+            if (hipMalloc(&P->owned, keep.used) != hipSuccess) {
+                (void)hipGetLastError();
+                P->owned = nullptr;
+                return bail(pfail(SRG_ERR_ALLOC, "plan: %zu bytes of device memory", keep.used));
+            }
+            P->bytes = (int64_t)keep.used;
+            if (hipMalloc(&scratch.p, tmp.used) != hipSuccess) {
+                (void)hipGetLastError();
+                scratch.p = nullptr;
+                return bail(pfail(SRG_ERR_ALLOC, "plan: %zu bytes of build scratch", tmp.used));
+            }
+        }
+    }
+    // split points and the cut rows' positions
+    if (B > 1) {
+        hipLaunchKernelGGL(k_plan_splits, dim3(grid_for(n * (B - 1), 256, 1u << 30)), dim3(256), 0, s, indptr, indices,
+                           n, B, splits, cut);
+        size_t tb = cub_bytes;
+        SRG_PLAN_HIP(hipcub::DeviceScan::ExclusiveSum(cub_tmp, tb, cut, cutpos, n, s));
+    }
+    // the sort items, sorted by (launch, decreasing span length)
+    SRG_PLAN_HIP(hipMemsetAsync(keys, 0xff, (size_t)n_items * sizeof(uint64_t), s));
+    hipLaunchKernelGGL(k_plan_items, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, indptr, splits, cutpos, n, B,
+                       split0 ? 1 : 0, T, keys, vals);
+    {
+        size_t tb = cub_bytes;
+        SRG_PLAN_HIP(hipcub::DeviceRadixSort::SortPairs(cub_tmp, tb, keys, skeys, vals, order, n_items, 0,
+                                                        T.lenbits + T.lbits, s));
+    }
+    {
+        // pos[i] = the entries of the items before i (launch-major): copy positions and launch nnz
+        KeyLen op{(1ull << T.lenbits) - 1};
+        hipcub::TransformInputIterator<int64_t, KeyLen, const uint64_t*> lens(skeys, op);
+        SRG_PLAN_HIP(hipMemsetAsync(pos, 0, sizeof(int64_t), s));
+        size_t tb = cub_bytes;
+        SRG_PLAN_HIP(hipcub::DeviceScan::InclusiveSum(cub_tmp, tb, lens, pos + 1, n_items, s));
+    }
+    // ---- 3: per-launch counts and the guard (host sync 2) ----
+    SRG_PLAN_HIP(hipMemsetAsync(dcounts + 4 * T.n_launch, 0, sizeof(int64_t), s));
+    hipLaunchKernelGGL(k_plan_check, dim3(grid_for(n_items, 256, 4096)), dim3(256), 0, s, skeys, n_items, T,
+                       (int32_t*)(dcounts + 4 * T.n_launch));
+    hipLaunchKernelGGL(k_plan_counts, dim3(1), dim3(128), 0, s, skeys, order, pos, T, dcounts, dhubs);
+    std::vector<int64_t> counts((size_t)4 * T.n_launch + 1);
+    std::vector<int32_t> hubs((size_t)kHubPrefix * T.n_launch);
+    SRG_PLAN_HIP(hipMemcpyAsync(counts.data(), dcounts, counts.size() * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    SRG_PLAN_HIP(hipMemcpyAsync(hubs.data(), dhubs, hubs.size() * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    {
+        hipError_t e = hipGetLastError();
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return bail(pfail(SRG_ERR_HIP, "plan build: %s", hipGetErrorString(e)));
+        int64_t total = 0;
+        for (int L = 0; L < T.n_launch; ++L) total += counts[4 * L];
+        if (counts[4 * T.n_launch] != 0 || total != nnz)
+            return bail(pfail(SRG_ERR_INVALID, "plan build: inconsistent layout (%lld of %lld entries placed%s)",
+                              (long long)total, (long long)nnz, counts[4 * T.n_launch] ? ", items outside their launch" : ""));
+    }
+    // ---- 4: the spans the launches read ----
+    // compact: row-indexed spans for the rows the packed-row width reads them for (hub and slice-wave
+    // rows), or every row for the other widths
+    P->rows_full = !compact || !packed_width(d);
+    for (int L = 0; L < T.n_launch; ++L)
+        T.rows_lim[L] = P->rows_full ? T.off[L + 1] - T.off[L] : counts[4 * L + 1] + counts[4 * L + 2];
+    if (slots)
+        hipLaunchKernelGGL(k_plan_spans, dim3(grid_for(n_items, 256, 1u << 20)), dim3(256), 0, s, indptr, splits, n, B,
+                           split0 ? 1 : 0, T, compact ? 1 : 0, skeys, order, pos, n_items, slot_beg, slot_end,
+                           P->blk_beg, P->blk_end);
+    if (compact)
+        hipLaunchKernelGGL(k_plan_copy, dim3(grid_for((nnz + kCopyChunk - 1) / kCopyChunk, 4, 1u << 16)), dim3(256), 0, s,
+                           indptr, splits, indices, values, n, B, split0 ? 1 : 0, T.lenbits, skeys, order, pos, n_items,
+                           nnz, oix, ov);
+    {
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return bail(pfail(SRG_ERR_HIP, "plan build: %s", hipGetErrorString(e)));
+    }
+    // ---- 5: the launch descriptors ----
+    for (int L = 0; L < T.n_launch; ++L) {
+        srg_plan::Launch D;
+        const int b = blocks[L];
+        D.block = b;
+        D.item0 = T.off[L];
+        D.order = order + T.off[L];
+        D.n_rows = T.off[L + 1] - T.off[L];
+        D.nnz = counts[4 * L + 0];
+        D.n_hub = counts[4 * L + 1];
+        D.n_heavy = counts[4 * L + 2];
+        D.n_narrow = counts[4 * L + 3];
+        D.whole_rows = sets[L] == kWhole;
+        if (compact) {
+            D.row_beg = P->blk_beg + (int64_t)b * n;
+            D.row_end = P->blk_end + (int64_t)b * n;
+            D.indices = oix;
+            D.values = ov;
+        } else {
+            D.row_beg = b == 0 ? indptr : splits + (int64_t)(b - 1) * n;
+            D.row_end = B == 1 ? nullptr : (b == B - 1 ? indptr + 1 : splits + (int64_t)b * n);
+            D.indices = indices;
+            D.values = values;
+        }
+        if (slots) {
+            D.slot_beg = slot_beg + T.off[L];
+            D.slot_end = slot_end + T.off[L];
+        }
+        P->launches.push_back(D);
+    }
+    // hub spans chain on the side stream when every launch over cut rows has the same hub rows
+    if (B > 1) {
+        bool same = true;
+        std::vector<int32_t> ref;
+        bool first = true;
+        for (int L = 0; L < T.n_launch && same; ++L) {
+            if (sets[L] == kWhole) continue;
+            const int64_t h = counts[4 * L + 1];
+            if (h > kHubPrefix) { same = false; break; }
+            std::vector<int32_t> set(hubs.begin() + (size_t)L * kHubPrefix, hubs.begin() + (size_t)L * kHubPrefix + h);
+            std::sort(set.begin(), set.end());
+            if (first) { ref = set; first = false; }
+            else same = set == ref;
+        }
+        P->same_hubs = same;
+    }
+    scratch.reset();   // after the build's kernels (one more wait on the stream: the copy)
+    *plan = P;
+    srg_clear_error();
+    return SRG_OK;
+}
+
+int srg_plan_destroy(srg_plan* plan, void* stream)
+{
+    if (!plan) return SRG_OK;
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    DevGuard g(s);
+    if (!s) (void)hipSetDevice(plan->device);
+    release(plan, s);
+    delete plan;
+    return SRG_OK;
+}
+
+int srg_plan_describe(const srg_plan* plan, srg_plan_desc* desc)
+{
+    if (!plan || !desc) return pfail(SRG_ERR_INVALID, "null plan / desc");
+    desc->n_rows = plan->n;
+    desc->nnz = plan->nnz;
+    desc->device_bytes = plan->bytes;
+    desc->d = plan->d;
+    desc->col_blocks = plan->B;
+    desc->n_launch = (int32_t)plan->launches.size();
+    desc->compact = plan->compact ? 1 : 0;
+    desc->split_block0 = plan->split0 ? 1 : 0;
+    desc->hub_chain = (plan->B > 1 && plan->same_hubs) ? 1 : 0;
+    desc->device = plan->device;
+    srg_clear_error();
+    return SRG_OK;
+}
+
+// the launches of one hop over a d-column panel (spmm._hop_plan's flags); returns whether the hub side
+// stream must be joined at the end of each hop
+static int plan_launches(const srg_plan* P, int32_t d, uint32_t flags, std::vector<srg_hop_launch>& out)
+{
+    const bool fast = (flags & SRG_SPMM_FAST) != 0;
+    const bool blocked = P->B > 1;
+    uint32_t base = flags & SRG_SPMM_NT_STORE;
+    if (blocked) {
+        base |= (d >= 128 ? SRG_SPMM_PACKED_U2 : 0u) |
+                (P->n * (int64_t)d * 4 >= kCapWavesMinPanel ? SRG_SPMM_CAP_WAVES : 0u);
+    }
+    const bool chain = blocked && !fast && P->same_hubs;
+    bool forked = false;
+    out.clear();
+    for (const srg_plan::Launch& D : P->launches) {
+        srg_hop_launch L{};
+        L.row_beg = D.row_beg;
+        L.row_end = D.row_end;
+        L.indices = D.indices;
+        L.values = D.values;
+        L.row_order = D.n_rows ? D.order : nullptr;
+        L.n_rows = D.n_rows;
+        L.n_hub = D.n_hub;
+        L.n_heavy = d <= 32 ? D.n_narrow : D.n_heavy;
+        L.slot_beg = D.slot_beg;
+        L.slot_end = D.slot_end;
+        uint32_t f = base | (D.block > 0 ? SRG_SPMM_ACCUMULATE : 0u);
+        if (chain && D.n_hub > 0) {
+            f |= SRG_SPMM_HUB_NOJOIN | (forked ? SRG_SPMM_HUB_CONTINUE : 0u);
+            forked = true;
+        } else if (fast) {
+            f |= SRG_SPMM_FAST;
+        }
+        L.flags = f;
+        out.push_back(L);
+    }
+    return forked ? 1 : 0;
+}
+
+int srg_plan_launch(const srg_plan* plan, int32_t i, int32_t d, srg_hop_launch* launch, int32_t* join_hub, void* stream)
+{
+    if (!plan || !launch) return pfail(SRG_ERR_INVALID, "null plan / launch");
+    if (i < 0 || i >= (int32_t)plan->launches.size() || d <= 0)
+        return pfail(SRG_ERR_INVALID, "launch %d of %zu, d=%d", i, plan->launches.size(), d);
+    if (!plan->rows_full) {
+        // a caller driving the launches may run any width: every row-indexed span, on `stream`
+        DevGuard g(static_cast<hipStream_t>(stream));
+        if (g.rc) return g.rc;
+        const int rc = complete_rows(const_cast<srg_plan*>(plan), static_cast<hipStream_t>(stream));
+        if (rc) return rc;
+    }
+    std::vector<srg_hop_launch> L;
+    const int join = plan_launches(plan, d, 0, L);
+    *launch = L[(size_t)i];
+    if (join_hub) *join_hub = join;
+    srg_clear_error();
+    return SRG_OK;
+}
+
+int srg_plan_propagate_f32(const srg_plan* plan, float* const* panels, int64_t ld, int32_t d, int32_t K, uint32_t flags,
+                           void* stream)
+{
+    if (!plan) return pfail(SRG_ERR_INVALID, "null plan");
+    if (flags & ~(SRG_SPMM_NT_STORE | SRG_SPMM_FAST))
+        return pfail(SRG_ERR_INVALID, "flags=0x%x: a plan's hops take NT_STORE and FAST only", flags);
+    if (d <= 0 || K < 0) return pfail(SRG_ERR_INVALID, "d=%d, K=%d", d, K);
+    if (K == 0 || plan->launches.empty()) { srg_clear_error(); return SRG_OK; }
+    DevGuard g(static_cast<hipStream_t>(stream));
+    if (g.rc) return g.rc;
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess || dev != plan->device)
+        return pfail(SRG_ERR_INVALID, "the plan lives on device %d, the stream on %d", plan->device, dev);
+    if (!plan->rows_full) {
+        // the packed light rows (spans by slot) run only at 64 / 128 / 256 columns on 16-byte rows
+        bool packed = packed_width(d) && ld % 4 == 0;
+        for (int k = 0; packed && panels && k <= K; ++k) packed = panels[k] && ((uintptr_t)panels[k] % 16) == 0;
+        if (!packed) {
+            const int rc = complete_rows(const_cast<srg_plan*>(plan), static_cast<hipStream_t>(stream));
+            if (rc) return rc;
+        }
+    }
+    std::vector<srg_hop_launch> L;
+    const int join = plan_launches(plan, d, flags, L);
+    return srg_propagate_plan_f32(L.data(), (int32_t)L.size(), join, panels, ld, d, K, stream);
+}
+
+}  // extern "C"

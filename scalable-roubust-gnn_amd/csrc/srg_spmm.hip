@@ -2131,6 +2131,16 @@ int srg_propagate_khop_f32(const int64_t* indptr, const int32_t* indices, const 
                              panels ? panels[0] : nullptr, ld, d);
     if (rc) return rc;
     const uint32_t f = flags & ~SRG_SPMM_ACCUMULATE;
+    if (!row_order && n_hub == 0 && n_heavy == 0 && K > 0 && n_rows > 0 && d > 0 &&
+        !(f & ~(SRG_SPMM_NT_STORE | SRG_SPMM_FAST))) {
+        // no schedule: the hops run through a plan made for them (srg_plan.hip), freed after them
+        srg_plan* P = nullptr;
+        rc = srg_plan_build(indptr, indices, values, n_rows, d, K, 0, 0, stream, &P);
+        if (rc) return rc;
+        rc = srg_plan_propagate_f32(P, panels, ld, d, K, f, stream);
+        const int rc2 = srg_plan_destroy(P, stream);
+        return rc ? rc : rc2;
+    }
     for (int k = 1; k <= K; ++k) {
         rc = launch_spmm<int64_t>(indptr, indices, values, n_rows, row_order, n_hub, n_heavy, panels[k - 1], ld,
                                   panels[k], ld, d, f, static_cast<hipStream_t>(stream));

@@ -42,6 +42,12 @@ SRG_TAIL_MAX = 32
 
 SRG_SPGEMM_SERIAL_B = 0x1
 
+SRG_PLAN_MIN_HOPS_TO_COMPACT = 6
+SRG_PLAN_COMPACT = 0x1
+SRG_PLAN_SPANS = 0x2
+SRG_PLAN_SPLIT_BLOCK0 = 0x4
+SRG_PLAN_WHOLE_BLOCK0 = 0x8
+
 SRG_HALO_AUTO = -1
 SRG_HALO_NONE = -2
 SRG_HALO_X_HALO_FILLED = 0x1
@@ -64,6 +70,11 @@ EXPORTED_SYMBOLS = (
     "srg_spmm_csr_f32",
     "srg_propagate_khop_f32",
     "srg_propagate_plan_f32",
+    "srg_plan_build",
+    "srg_plan_destroy",
+    "srg_plan_describe",
+    "srg_plan_launch",
+    "srg_plan_propagate_f32",
     "srg_cheby_step_f64",
     "srg_cheby_step_f32",
     "srg_cheby_epilogue_f32",
@@ -131,6 +142,13 @@ def _declare(lib):
     lib.srg_propagate_khop_f32.restype = ctypes.c_int
     lib.srg_propagate_plan_f32.argtypes = [_p, _i32, _i32, _p, _i64, _i32, _i32, _p]
     lib.srg_propagate_plan_f32.restype = ctypes.c_int
+    lib.srg_plan_build.argtypes = [_p, _p, _p, _i64, _i32, _i32, _i32, _u32, _p, ctypes.POINTER(_p)]
+    lib.srg_plan_destroy.argtypes = [_p, _p]
+    lib.srg_plan_describe.argtypes = [_p, _p]
+    lib.srg_plan_launch.argtypes = [_p, _i32, _i32, _p, _p, _p]
+    lib.srg_plan_propagate_f32.argtypes = [_p, _p, _i64, _i32, _i32, _u32, _p]
+    for name in ("srg_plan_build", "srg_plan_destroy", "srg_plan_describe", "srg_plan_launch", "srg_plan_propagate_f32"):
+        getattr(lib, name).restype = ctypes.c_int
     lib.srg_cheby_step_f64.argtypes = [_p, _p, _p, _i64, _p, _p, _p, _p, _i64, _i32, ctypes.c_int,
                                        _f64, _f64, _p, _p, _i32, _p, _i64, _p]
     lib.srg_cheby_step_f64.restype = ctypes.c_int

@@ -89,10 +89,13 @@ class DeviceCSR:
     values: torch.Tensor
     n_rows: int
     n_cols: int
-    order: torch.Tensor
-    n_heavy: int
-    n_hub: int = 0
-    n_heavy_narrow: int | None = None    # slice-wave rows for d <= 32 (None: n_heavy)
+    # the row schedule (order, n_heavy, n_hub, n_heavy_narrow below): None = not built yet -- built
+    # from the thresholds on first use (from_tensors leaves it to the first hop that reads it: a K-hop
+    # run through the native plan, srgnn.plan, never does)
+    _order: torch.Tensor | None
+    _n_heavy: int | None
+    _n_hub: int | None = 0
+    _n_heavy_narrow: int | None = None   # slice-wave rows for d <= 32 (None: n_heavy)
     # row spans (a column block, column_blocks()): row r's entries are [indptr[r], row_end[r]) of
     # indices / values, and indptr holds n_rows starts instead of n_rows + 1 pointers
     row_end: torch.Tensor | None = None
@@ -106,6 +109,51 @@ class DeviceCSR:
     # the thresholds the schedule was built with (None = automatic), reused by column blocks
     thresholds: tuple = (None, None)
     _blocks: dict = field(default_factory=dict, repr=False, compare=False)   # column_blocks() cache
+
+    def _schedule(self) -> None:
+        heavy_t, hub_t = self.thresholds
+        self._order, self._n_heavy, self._n_hub = make_schedule(self.indptr, heavy_t, hub_t)
+        self._n_heavy_narrow = narrow_heavy(self.indptr, self._n_hub) if _auto_heavy(heavy_t) else None
+
+    @property
+    def order(self) -> torch.Tensor:
+        if self._order is None:
+            self._schedule()
+        return self._order
+
+    @order.setter
+    def order(self, v):
+        self._order = v
+
+    @property
+    def n_heavy(self) -> int:
+        if self._order is None:
+            self._schedule()
+        return self._n_heavy
+
+    @n_heavy.setter
+    def n_heavy(self, v):
+        self._n_heavy = v
+
+    @property
+    def n_hub(self) -> int:
+        if self._order is None:
+            self._schedule()
+        return self._n_hub
+
+    @n_hub.setter
+    def n_hub(self, v):
+        self._n_hub = v
+
+    @property
+    def n_heavy_narrow(self):
+        if self._order is None:
+            self._schedule()
+        return self._n_heavy_narrow
+
+    @n_heavy_narrow.setter
+    def n_heavy_narrow(self, v):
+        self._n_heavy_narrow = v
 
     @property
     def out_rows(self) -> int:
@@ -165,9 +213,8 @@ class DeviceCSR:
         if validate:
             _lib.call(device, "srg_csr_validate", ip.data_ptr(), ix.data_ptr(), n_rows, ix.numel(), n_cols,
                       _lib.stream(device))
-        order, n_heavy, n_hub = make_schedule(ip, heavy_threshold, hub_threshold)
-        return cls(ip, ix, vv, n_rows, int(n_cols), order, n_heavy, n_hub,
-                   narrow_heavy(ip, n_hub) if _auto_heavy(heavy_threshold) else None,
+        # the schedule is built on first use (DeviceCSR.order)
+        return cls(ip, ix, vv, n_rows, int(n_cols), None, None, None, None,
                    thresholds=(heavy_threshold, hub_threshold))
 
     @classmethod

@@ -56,18 +56,40 @@ def _split_block0(A: DeviceCSR, d: int) -> bool:
 # tools/probes/colblock_build_time.py; 21 ms when the blocks were copies of the ids and values):
 # it is cut for a run of at least this many hops, or when its blocks already exist.
 MIN_HOPS_TO_CUT = 4
-# Runs of this many hops copy the blocks' spans into compact arrays (DeviceCSR.compact_column_blocks,
-# the srg_csr_copy_spans kernel), when the copy fits in a quarter of the free memory.  Products, K = 10
-# (profiles/r04h_one_shot_products.json): the layout costs 4.6 ms more and each hop 0.40 ms less
-# (6.09 against 6.49 ms), so the copy pays after ~12 hops.
-MIN_HOPS_TO_COMPACT = 16
+# Runs of this many hops copy the blocks' spans into compact arrays in launch order, when the copy fits in
+# a quarter of the free memory (= SRG_PLAN_MIN_HOPS_TO_COMPACT of the native planner).  Round 5, the
+# native planner (one device pass: profiles/r05_plan_products.json): the compact layout builds in
+# ~1.9 ms against ~1.2 ms for spans, and each products hop runs 5.48 instead of ~5.64 ms, so the copy
+# pays after ~4-5 hops.  (The torch formulation, DeviceCSR.compact_column_blocks, cost 4.6 ms more
+# than spans, round 4: profiles/r04h_one_shot_products.json.)
+MIN_HOPS_TO_COMPACT = 6
 _COMPACT = True                   # False: spans only (A/B of the round-2 / 3 layouts)
+
+
+# K-hop runs (prepare / propagate) lay the operator out with the native planner (srgnn.plan,
+# csrc/srg_plan.hip: one device pass) when every layout constant here and in srgnn.csr has its default
+# value and the operator's thresholds are automatic; otherwise (layout experiments, forced thresholds)
+# with the torch formulation below.  Both give the same layout.
+NATIVE_PLAN = True
+
+
+def _native_ok(A: DeviceCSR) -> bool:
+    from . import csr as C
+    return (NATIVE_PLAN and _COMPACT and _HUB_CHAIN and _SLOT_SPANS and _U2_BLOCKED and not A.is_span
+            and A.n_rows == A.n_cols and A.thresholds == (None, None) and C.BLOCK_WHOLE_MAX == 48
+            and C.BLOCK_HEAVY_PER == 30000 and C.NARROW_HEAVY_THRESHOLD == 32 and C.DEFAULT_HEAVY_THRESHOLD is None
+            and C.DEFAULT_HUB_THRESHOLD is None and SPLIT_BLOCK0_MAX_PANEL == 16 << 30
+            and CAP_WAVES_MIN_PANEL == 512 << 20 and MIN_HOPS_TO_CUT == 4
+            and MIN_HOPS_TO_COMPACT == _lib.SRG_PLAN_MIN_HOPS_TO_COMPACT)
 
 
 def prepare(A: DeviceCSR, d: int, hops: int) -> int:
     """Lays A out for a run of `hops` hops over d-column panels: column blocks (spans, or compact
     copies in launch order for long runs) or, for one launch per hop and a long run, a launch-ordered
     copy of the whole operator (DeviceCSR.schedule_ordered).  Returns the column blocks per hop."""
+    if _native_ok(A):
+        from .plan import plan_for
+        return plan_for(A, d, hops, int(FORCE_COL_BLOCKS or 0), SPLIT_BLOCK0).col_blocks
     B = auto_col_blocks(A, d, hops=hops)
     if B > 1 and column_blocks_for(A, B, hops=hops):
         return B
@@ -125,6 +147,10 @@ def launches_per_hop(A: DeviceCSR, B: int, d: int, agg: bool = False) -> int:
     """k_spmm launches of one hop of A over a d-column panel in B column blocks (hop()): B, plus
     one when block 0 runs as its cut spans and its whole rows (_split_block0, or the aggregation
     epilogue)."""
+    from .plan import cached
+    P = cached(A, d) if not agg else None
+    if P is not None and P.col_blocks == B:
+        return P.n_launch
     blocks = A.column_blocks(B) if B > 1 else None
     if not blocks:
         return 1
@@ -184,6 +210,14 @@ def hop(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, nt_store: bool = False
         _check_panel(agg[0], A.out_rows, "agg", d)
     if out.device != A.device or X.device != A.device:
         raise ValueError("A, X and out must be on the same device")
+    if agg is None and _native_ok(A) and X.stride(0) == out.stride(0) and X.data_ptr() != out.data_ptr():
+        # an operator prepared by the native planner: one hop of its plan
+        from .plan import cached
+        P = cached(A, d)
+        if P is not None and (col_blocks is None or int(col_blocks) == P.col_blocks):
+            P.propagate([X, out], X.stride(0), d, 1, (_lib.SRG_SPMM_NT_STORE if nt_store else 0) |
+                        (_lib.SRG_SPMM_FAST if fast else 0))
+            return out
     B = auto_col_blocks(A, d) if col_blocks is None else int(col_blocks)
     plan, join = _hop_plan(A, d, B, nt_store, fast, agg is not None)
     if agg is None and X.stride(0) == out.stride(0) and X.data_ptr() != out.data_ptr():
@@ -417,6 +451,15 @@ def propagate(A: DeviceCSR, X: torch.Tensor, K: int, panels: list | None = None,
         _check_panel(p, n, f"panels[{k}]", d)
         if p.stride(0) != ld:
             raise ValueError("all panels must share one leading dimension")
+    if K > 0 and _native_ok(A):
+        # the native plan (srgnn.plan): layout and hop loop in the library
+        from .plan import plan_for
+        cb = int(col_blocks) if col_blocks is not None else int(FORCE_COL_BLOCKS or 0)
+        flags = (_lib.SRG_SPMM_NT_STORE if nt_store else 0) | (_lib.SRG_SPMM_FAST if fast else 0)
+        plan_for(A, d, K, cb, SPLIT_BLOCK0).propagate(panels, ld, d, K, flags)
+        if panels[0] is not X0 and X is not X0:
+            panels = [X0] + list(panels[1:])
+        return panels
     B = auto_col_blocks(A, d, hops=K) if col_blocks is None else int(col_blocks)
     if K > 0 and B > 1 and column_blocks_for(A, B, hops=K):
         # the blocked hop loop runs natively: one call for the K hops (srg_propagate_plan_f32)

@@ -47,7 +47,7 @@ def _check_rows(oracle_mod, rows, sub, ucols, prev, got, what):
 @pytest.mark.timeout(600)
 def test_products_timed_layout_every_hop_bit_exact(oracle_mod):
     """The operator bench.py times on the headline config: products-shaped graph (126 M nonzeros),
-    K = 10, d = 128, default thresholds, eight COMPACT column blocks (>= 16 hops; block 0 in two
+    K = 10, d = 128, default thresholds, eight COMPACT column blocks (>= 6 hops; block 0 in two
     launches, its cut spans then its whole rows; compact copies in launch order, packed rows reading
     their spans by schedule slot), short rows (<= BLOCK_WHOLE_MAX = 48) whole in block 0, 2 gathers
     per packed row (PACKED_U2) -- EVERY row of every hop (2,449,029 x 128 per hop) checked bit for

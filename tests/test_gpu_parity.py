@@ -826,18 +826,25 @@ def test_propagate_plan_entry_rejects_bad_launches():
     c.check_hop(2, Z.cpu().numpy())
 
 
+@pytest.mark.parametrize("native", [True, False])
 @pytest.mark.parametrize("name", ["rand_d128_r05", "rand_d36_ppr", "cora_sym_k3"])
-def test_schedule_ordered_one_launch_bit_exact(name):
-    """A long-lived one-launch operator's launch-ordered copy (DeviceCSR.schedule_ordered, made by
-    spmm.prepare for runs of >= MIN_HOPS_TO_COMPACT hops): propagate and hop through it == the
-    reference, bit for bit."""
+def test_schedule_ordered_one_launch_bit_exact(monkeypatch, name, native):
+    """A long-lived one-launch operator's launch-ordered copy (made by spmm.prepare for runs of >=
+    MIN_HOPS_TO_COMPACT hops: the native plan's compact copy, or DeviceCSR.schedule_ordered in the
+    torch formulation): propagate and hop through it == the reference, bit for bit."""
     from srgnn import spmm as spmm_mod
+    from srgnn.plan import cached
+    monkeypatch.setattr(spmm_mod, "NATIVE_PLAN", native)
     c = G.Case(name)
     A = _csr(c, (None, None))
     X = torch.from_numpy(c.x()).cuda()
     assert spmm_mod.prepare(A, X.shape[1], hops=1000) == 1
-    S = A._blocks["sched"]
-    assert S.is_span and S.nnz == A.nnz and S.indices.data_ptr() != A.indices.data_ptr()
+    if native:
+        P = cached(A, X.shape[1])
+        assert P.compact and P.n_launch == 1 and P.col_blocks == 1
+    else:
+        S = A._blocks["sched"]
+        assert S.is_span and S.nnz == A.nnz and S.indices.data_ptr() != A.indices.data_ptr()
     hops = spmm_mod.propagate(A, X, c.k)
     torch.cuda.synchronize()
     for k in range(1, c.k + 1):
