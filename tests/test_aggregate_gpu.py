@@ -60,7 +60,7 @@ def test_propagate_aggregate_column_blocked_bit_exact(oracle_mod, monkeypatch, n
     """Column-blocked hops in the fused aggregation (spmm.hop: blocks with ACCUMULATE, the
     aggregation epilogue in the launch that finishes each row -- the last block's, or block 0's
     for the short rows it computes whole) == the reference's combine, bit for bit.  whole =
-    (SRGNN_BLOCK_WHOLE_MAX, compact copies)."""
+    (csr.BLOCK_WHOLE_MAX, compact copies)."""
     from srgnn import csr as csr_mod
     from srgnn.aggregate import combine_plan, combine_steps, propagate_aggregate
     from srgnn.csr import DeviceCSR

@@ -13,15 +13,16 @@ import json
 import os
 import sys
 
-os.environ.setdefault("SRGNN_BLOCK_WHOLE_MAX", "0")
 HERE = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(HERE, "scalable-roubust-gnn_amd"))
 
 import torch  # noqa: E402
 
-from srgnn import graphs, synth  # noqa: E402
+from srgnn import csr as _csr, graphs, synth  # noqa: E402
 from srgnn.csr import DeviceCSR  # noqa: E402
 from srgnn.spmm import hop  # noqa: E402
+
+_csr.BLOCK_WHOLE_MAX = 0      # every row cut (the probe's round-2 setting)
 
 B = 8
 LR = 4

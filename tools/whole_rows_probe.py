@@ -1,10 +1,10 @@
 #!/usr/bin/env python3
 """Probe: the launch of block 0's whole rows (the short rows a column-blocked hop computes in one
-piece, DeviceCSR.split_whole()[1]) timed alone, next to one cut-span launch of the same hop, under
-the process's packed-row settings (SRGNN_PACKED_ROWS / SRGNN_PACKED_U are read once per process:
-run it once per setting).  Prints one JSON line.
+piece, DeviceCSR.split_whole()[1]) timed alone, next to one cut-span launch of the same hop (the
+packed-row geometry is a compile-time constant of the library since round 5; round 3 swept it through
+environment knobs).  Prints one JSON line.
 
-    SRGNN_PACKED_U=4 python tools/whole_rows_probe.py [--config products] [--reps 20]
+    python tools/whole_rows_probe.py [--config products] [--reps 20]
 """
 import argparse
 import json
