@@ -102,7 +102,7 @@ int main(int argc, char** argv)
     void** streams = malloc(sizeof(void*) * P);
     srg_halo_info* info = malloc(sizeof(srg_halo_info) * P);
     for (int p = 0; p < P; ++p) {
-        CHECK(srg_halo_plan_build(ip, ix, n, P, p, 3, SRG_HALO_AUTO, SRG_HALO_AUTO, /*ghost_max_degree=*/4, &plan[p]));
+        CHECK(srg_halo_plan_build(ip, ix, n, P, p, 3, SRG_HALO_AUTO, SRG_HALO_AUTO, /*ghost_max_degree=*/4, 0.0, &plan[p]));
         CHECK(srg_halo_plan_info(plan[p], &info[p]));
         CHECK(srg_halo_share_create(plan[p], val, 0, d, &share[p]));
         panels[p] = malloc(sizeof(float*) * (K + 1));

@@ -479,9 +479,9 @@ int srg_dist_propagate_khop_f32(srg_comm* comm, const srg_shard_f32* shards, int
  * that pack), while the next chunks compute; the hub group's rows go last.  Low-degree halo rows
  * whose own columns are all local ("ghost rows") are computed locally instead of received.  Every
  * row keeps its entries in CSR order, so the hops are bitwise the one-GPU hops.  The same plan as
- * the Python package's srgnn/dist.py HaloPartitionedOperator (its automatic ghost cap, a link-rate
- * cost model, stays in Python: C hosts pass the cap).  Replaces the reference's single-process hop
- * loop, SSRG/operators/base_operator.py:32-35; SURVEY.md §8(b) item 5, §8(e). */
+ * the Python package's srgnn/dist.py HaloPartitionedOperator runs on (it builds its shares with this
+ * planner).  Replaces the reference's single-process hop loop, SSRG/operators/base_operator.py:32-35;
+ * SURVEY.md §8(b) item 5, §8(e). */
 #define SRG_HALO_AUTO (-1)     /* threshold chosen as the Python plan does (csr.auto_*_threshold) */
 #define SRG_HALO_NONE (-2)     /* hub_threshold: no hub rows */
 typedef struct srg_halo_plan srg_halo_plan;
@@ -495,11 +495,16 @@ typedef struct {
 } srg_halo_info;
 /* Rank `rank`'s share, from the GLOBAL CSR on the host (int64 indptr[n+1] from 0, int32 column ids;
  * the same arrays on every rank).  chunks in [1, 250]; hub_threshold / heavy_threshold a row length,
- * SRG_HALO_AUTO, or (hub) SRG_HALO_NONE; ghost_max_degree >= 0 (0: no ghost rows).  Host-only: needs
- * no device.  Validates the CSR (SRG_ERR_INVALID). */
+ * SRG_HALO_AUTO, or (hub) SRG_HALO_NONE; ghost_max_degree >= 0 (0: no ghost rows) or SRG_HALO_AUTO:
+ * the cap among 0, 1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64 that minimises the modelled hop, max over
+ * ranks of max(local SpMM bytes incl. ghost rows at 8.4e12 B/s, busiest peer link at link_bps per
+ * direction; a row is 4d bytes on both sides, so d cancels) -- deterministic from the global graph
+ * and link_bps, so every rank picks the same cap (pass every rank the same link_bps, e.g. the minimum
+ * over ranks of a measured rate; <= 0: 64e9).  srg_halo_plan_info reports the cap taken.  Host-only:
+ * needs no device; up to 16 host threads.  Validates the CSR (SRG_ERR_INVALID). */
 int srg_halo_plan_build(const int64_t* indptr, const int32_t* indices, int64_t n, int32_t nranks, int32_t rank,
                         int32_t chunks, int64_t hub_threshold, int64_t heavy_threshold, int32_t ghost_max_degree,
-                        srg_halo_plan** plan);
+                        double link_bps, srg_halo_plan** plan);
 int srg_halo_plan_destroy(srg_halo_plan* plan);
 int srg_halo_plan_info(const srg_halo_plan* plan, srg_halo_info* info);
 /* Read-only view of one of the plan's host arrays (diagnostics and tests): *data points into the plan

@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -85,6 +86,34 @@ void sort_by_degree(std::vector<int32_t>& rows, const std::vector<int64_t>& deg_
 
 // rows of at most this many entries run whole in block 0 (= srgnn.csr.BLOCK_WHOLE_MAX)
 constexpr int64_t kBlockWholeMax = 48;
+
+// the automatic ghost cap (ghost_max_degree = SRG_HALO_AUTO): candidates, the scan limit and the
+// modelled gather rate (products at P = 2: 63.1 M nonzeros x 512 B in 3.85 ms); DESIGN.md §7
+constexpr int kGhostScanMax = 64;
+constexpr int kGhostCaps[] = {0, 1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64};
+constexpr int kNumGhostCaps = (int)(sizeof(kGhostCaps) / sizeof(kGhostCaps[0]));
+constexpr double kGhostGatherBps = 8.4e12;
+constexpr double kGhostLinkBps = 64e9;
+
+// host threads for the planner's loops (the GPU boxes grant a job 16 CPUs)
+int plan_threads()
+{
+    return (int)std::max(1u, std::min<unsigned>(std::thread::hardware_concurrency(), 16u));
+}
+
+// f(lo, hi) over [0, count) in contiguous pieces, one per thread
+template <typename F>
+void parallel_ranges(int64_t count, F f)
+{
+    const int nt = count < (1 << 16) ? 1 : plan_threads();
+    if (nt == 1) { f((int64_t)0, count); return; }
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t) {
+        const int64_t lo = count * t / nt, hi = count * (t + 1) / nt;
+        th.emplace_back([=, &f]() { f(lo, hi); });
+    }
+    for (auto& x : th) x.join();
+}
 
 void free_blocks(SrgHaloBlocks& K)
 {
@@ -186,7 +215,7 @@ extern "C" {
 
 int srg_halo_plan_build(const int64_t* indptr, const int32_t* indices, int64_t n, int32_t nranks, int32_t rank,
                         int32_t chunks, int64_t hub_threshold, int64_t heavy_threshold, int32_t ghost_max_degree,
-                        srg_halo_plan** out)
+                        double link_bps, srg_halo_plan** out)
 {
     if (!out) return hfail(SRG_ERR_INVALID, "null output handle");
     *out = nullptr;
@@ -194,23 +223,46 @@ int srg_halo_plan_build(const int64_t* indptr, const int32_t* indices, int64_t n
     if (n < 0 || n > INT32_MAX - 1) return hfail(SRG_ERR_INVALID, "n=%lld out of range", (long long)n);
     if (nranks < 1 || rank < 0 || rank >= nranks) return hfail(SRG_ERR_INVALID, "rank %d of %d", rank, nranks);
     if (chunks < 1 || chunks > 250) return hfail(SRG_ERR_INVALID, "chunks=%d not in [1, 250]", chunks);
-    if (ghost_max_degree < 0) return hfail(SRG_ERR_INVALID, "ghost_max_degree=%d < 0", ghost_max_degree);
+    const bool auto_ghost = ghost_max_degree == SRG_HALO_AUTO;
+    if (ghost_max_degree < 0 && !auto_ghost)
+        return hfail(SRG_ERR_INVALID, "ghost_max_degree=%d < 0 (SRG_HALO_AUTO: the cost model)", ghost_max_degree);
     if (hub_threshold < SRG_HALO_NONE || heavy_threshold < SRG_HALO_AUTO)
         return hfail(SRG_ERR_INVALID, "thresholds: hub %lld, heavy %lld", (long long)hub_threshold, (long long)heavy_threshold);
     if (indptr[0] != 0) return hfail(SRG_ERR_INVALID, "indptr[0] = %lld != 0", (long long)indptr[0]);
-    for (int64_t r = 0; r < n; ++r)
-        if (indptr[r + 1] < indptr[r]) return hfail(SRG_ERR_INVALID, "indptr decreases at row %lld", (long long)r);
+    {
+        // the checks in parallel pieces; the first violation (lowest position) is reported
+        std::vector<int64_t> bad_row((size_t)plan_threads() + 1, INT64_MAX);
+        std::atomic<int> slot{0};
+        parallel_ranges(n, [&](int64_t lo, int64_t hi) {
+            int64_t b = INT64_MAX;
+            for (int64_t r = lo; r < hi && b == INT64_MAX; ++r)
+                if (indptr[r + 1] < indptr[r]) b = r;
+            bad_row[(size_t)slot++] = b;
+        });
+        const int64_t b = *std::min_element(bad_row.begin(), bad_row.end());
+        if (b != INT64_MAX) return hfail(SRG_ERR_INVALID, "indptr decreases at row %lld", (long long)b);
+    }
     const int64_t nnz = indptr[n];
-    for (int64_t e = 0; e < nnz; ++e)
-        if (indices[e] < 0 || indices[e] >= n)
+    {
+        std::vector<int64_t> bad_e((size_t)plan_threads() + 1, INT64_MAX);
+        std::atomic<int> slot{0};
+        parallel_ranges(nnz, [&](int64_t lo, int64_t hi) {
+            int64_t b = INT64_MAX;
+            for (int64_t e = lo; e < hi && b == INT64_MAX; ++e)
+                if (indices[e] < 0 || indices[e] >= n) b = e;
+            bad_e[(size_t)slot++] = b;
+        });
+        const int64_t e = *std::min_element(bad_e.begin(), bad_e.end());
+        if (e != INT64_MAX)
             return hfail(SRG_ERR_INVALID, "column id %d at entry %lld outside [0, %lld)", indices[e], (long long)e, (long long)n);
+    }
 
     srg_halo_plan* P_ = new (std::nothrow) srg_halo_plan();
     if (!P_) return hfail(SRG_ERR_ALLOC, "out of host memory");
     srg_halo_plan& pl = *P_;
     const int P = nranks, p = rank, C = chunks, G = C + 1;
     pl.P = P; pl.p = p; pl.C = C; pl.n = n; pl.nnz_total = nnz;
-    pl.ghost_max_degree = ghost_max_degree;
+    const int scan_cap = auto_ghost ? kGhostScanMax : ghost_max_degree;   // ghost candidates scanned up to
     pl.starts = balanced(indptr, n, P, 0);
     const std::vector<int64_t>& st = pl.starts;
     auto deg = [&](int64_t r) { return indptr[r + 1] - indptr[r]; };
@@ -234,9 +286,12 @@ int srg_halo_plan_build(const int64_t* indptr, const int32_t* indices, int64_t n
         if (q == p) pl.chunk_ranges = cb;
     }
 
-    // every rank's halo, sorted by (group, owner, id), and its ghost-eligible rows (one thread per rank)
+    // every rank's halo, sorted by (group, owner, id), its ghost-eligible rows (one thread per rank),
+    // and for the automatic cap each rank's modelled SpMM entries and busiest link per candidate cap
     std::vector<std::vector<int32_t>> halos(P);
     std::vector<std::vector<uint8_t>> ghost(P);
+    std::vector<std::vector<int64_t>> model_nnz(P, std::vector<int64_t>(kNumGhostCaps, 0));
+    std::vector<std::vector<int64_t>> model_link(P, std::vector<int64_t>(kNumGhostCaps, 0));
     auto halo_of = [&](int q) {
         const int64_t s0 = st[q], s1 = st[q + 1];
         std::vector<uint64_t> bits((size_t)(n + 63) / 64, 0);
@@ -262,10 +317,10 @@ int srg_halo_plan_build(const int64_t* indptr, const int32_t* indices, int64_t n
         // ghosts: degree <= cap and every column among q's own rows or halo rows
         std::vector<uint8_t>& g = ghost[q];
         g.assign(h.size(), 0);
-        if (ghost_max_degree > 0)
+        if (scan_cap > 0)
             for (size_t j = 0; j < h.size(); ++j) {
                 const int32_t r = h[j];
-                if (deg(r) > ghost_max_degree) continue;
+                if (deg(r) > scan_cap) continue;
                 bool ok = true;
                 for (int64_t e = indptr[r]; e < indptr[r + 1] && ok; ++e) {
                     const int32_t c = indices[e];
@@ -273,6 +328,23 @@ int srg_halo_plan_build(const int64_t* indptr, const int32_t* indices, int64_t n
                 }
                 g[j] = ok ? 1 : 0;
             }
+        if (auto_ghost) {
+            // per cap: q's SpMM entries (own + ghost rows) and its busiest inbound link (rows received
+            // from one owner) -- dist.ghost_plan's model
+            std::vector<int64_t> recv((size_t)kNumGhostCaps * P, 0);
+            std::vector<int64_t> gnnz(kNumGhostCaps, 0);
+            for (size_t j = 0; j < h.size(); ++j) {
+                const int64_t dr = deg(h[j]);
+                for (int k = 0; k < kNumGhostCaps; ++k) {
+                    if (g[j] && dr <= kGhostCaps[k]) gnnz[k] += dr;
+                    else ++recv[(size_t)k * P + owner[h[j]]];
+                }
+            }
+            for (int k = 0; k < kNumGhostCaps; ++k) {
+                model_nnz[q][k] = indptr[s1] - indptr[s0] + gnnz[k];
+                model_link[q][k] = *std::max_element(recv.begin() + (size_t)k * P, recv.begin() + (size_t)(k + 1) * P);
+            }
+        }
     };
     {
         const int nt = (int)std::max(1u, std::min<unsigned>(std::thread::hardware_concurrency(), 16u));
@@ -282,6 +354,23 @@ int srg_halo_plan_build(const int64_t* indptr, const int32_t* indices, int64_t n
             for (auto& t : th) t.join();
         }
     }
+
+    // the ghost cap: given, or the candidate with the least modelled hop (ties: the smaller cap)
+    int cap = ghost_max_degree;
+    if (auto_ghost) {
+        const double link = link_bps > 0 ? link_bps : kGhostLinkBps;
+        double best_t = 0;
+        for (int k = 0; k < kNumGhostCaps; ++k) {
+            double worst = 0.0;
+            for (int q = 0; q < P; ++q)
+                worst = std::max(worst, std::max((double)model_nnz[q][k] / kGhostGatherBps, (double)model_link[q][k] / link));
+            if (k == 0 || worst < best_t) { best_t = worst; cap = kGhostCaps[k]; }
+        }
+        for (int q = 0; q < P; ++q)
+            for (size_t j = 0; j < halos[q].size(); ++j)
+                if (ghost[q][j] && deg(halos[q][j]) > cap) ghost[q][j] = 0;
+    }
+    pl.ghost_max_degree = cap;
 
     const int64_t r0 = st[p], r1 = st[p + 1];
     pl.r0 = r0; pl.r1 = r1; pl.rows = r1 - r0;
@@ -337,18 +426,26 @@ int srg_halo_plan_build(const int64_t* indptr, const int32_t* indices, int64_t n
     for (int64_t j = 0; j < pl.n_recv; ++j) pl.lip[pl.rows + j + 1] = pl.lip[pl.rows + j];
     for (int64_t j = 0; j < pl.n_ghost; ++j) pl.lip[pl.rows + pl.n_recv + j + 1] = pl.lip[pl.rows + pl.n_recv + j] + deg(gh[j]);
     pl.lix.resize((size_t)pl.lip[nloc]);
-    for (int64_t e = pl.b0; e < pl.b1; ++e) pl.lix[e - pl.b0] = g2l[indices[e]];
+    parallel_ranges(pl.b1 - pl.b0, [&](int64_t lo, int64_t hi) {
+        for (int64_t e = lo; e < hi; ++e) pl.lix[(size_t)e] = g2l[indices[pl.b0 + e]];
+    });
     int64_t w = pl.b1 - pl.b0;
     for (int32_t r : gh)
         for (int64_t e = indptr[r]; e < indptr[r + 1]; ++e) {
             pl.ghost_pos.push_back(e);
             pl.lix[w++] = g2l[indices[e]];
         }
-    for (int32_t c : pl.lix)
-        if (c < 0) {
+    {
+        std::atomic<bool> miss{false};
+        parallel_ranges((int64_t)pl.lix.size(), [&](int64_t lo, int64_t hi) {
+            for (int64_t e = lo; e < hi; ++e)
+                if (pl.lix[(size_t)e] < 0) { miss = true; break; }
+        });
+        if (miss) {
             delete P_;
             return hfail(SRG_ERR_INVALID, "halo layout misses a referenced column");
         }
+    }
     pl.halo_ids.reserve(pl.halo);
     pl.halo_ids.insert(pl.halo_ids.end(), need.begin(), need.end());
     pl.halo_ids.insert(pl.halo_ids.end(), gh.begin(), gh.end());

@@ -212,7 +212,7 @@ def _declare(lib):
     lib.srg_dist_propagate_khop_f32.restype = ctypes.c_int
     lib.srg_csr_copy_spans.argtypes = [_p, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p]
     lib.srg_csr_copy_spans.restype = ctypes.c_int
-    lib.srg_halo_plan_build.argtypes = [_p, _p, _i64, _i32, _i32, _i32, _i64, _i64, _i32, ctypes.POINTER(_p)]
+    lib.srg_halo_plan_build.argtypes = [_p, _p, _i64, _i32, _i32, _i32, _i64, _i64, _i32, _f64, ctypes.POINTER(_p)]
     lib.srg_halo_plan_destroy.argtypes = [_p]
     lib.srg_halo_plan_info.argtypes = [_p, ctypes.POINTER(HaloInfo)]
     lib.srg_halo_plan_array.argtypes = [_p, _i32, _i32, ctypes.POINTER(_p), ctypes.POINTER(_i64)]

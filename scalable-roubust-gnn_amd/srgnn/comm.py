@@ -107,11 +107,12 @@ _HALO_DTYPES = {_lib.SRG_HALO_STARTS: ctypes.c_int64, _lib.SRG_HALO_LOCAL_INDPTR
 
 class HaloPlan:
     """srg_halo_plan: rank `rank`'s share of the halo partition, built by the library's host planner
-    from the global CSR (numpy / CPU arrays).  Needs no device."""
+    from the global CSR (numpy / CPU arrays).  Needs no device.  ghost_max_degree: a cap, or
+    SRG_HALO_AUTO for the link-rate cost model at `link_bps` (<= 0: 64e9)."""
 
     def __init__(self, indptr, indices, n: int, nranks: int, rank: int, chunks: int = 4,
                  hub_threshold: int = _lib.SRG_HALO_AUTO, heavy_threshold: int = _lib.SRG_HALO_AUTO,
-                 ghost_max_degree: int = 0):
+                 ghost_max_degree: int = 0, link_bps: float = 0.0):
         import numpy as np
         self._ip = np.ascontiguousarray(np.asarray(indptr), dtype=np.int64)
         self._ix = np.ascontiguousarray(np.asarray(indices), dtype=np.int32)
@@ -125,7 +126,7 @@ class HaloPlan:
         h = ctypes.c_void_p()
         _lib.call_host("srg_halo_plan_build", self._ip.ctypes.data, self._ix.ctypes.data if self._ix.size else None,
                        int(n), int(nranks), int(rank), int(chunks), int(hub_threshold), int(heavy_threshold),
-                       int(ghost_max_degree), ctypes.byref(h))
+                       int(ghost_max_degree), float(link_bps), ctypes.byref(h))
         self._h = h
         info = _lib.HaloInfo()
         _lib.call_host("srg_halo_plan_info", self._h, ctypes.byref(info))

@@ -152,56 +152,14 @@ def simulate_propagate(indptr, indices, values, n: int, x: torch.Tensor, K: int,
 # overlapped with the computation of the later groups.
 # ================================================================================================
 
-def _chunk_bounds(indptr_local: torch.Tensor, chunks: int):
-    """Contiguous local row ranges with about equal nonzeros (like balanced_row_starts)."""
-    return balanced_row_starts(indptr_local, chunks)
-
-
-# partition: rows longer than nnz / (1024 P) count (1 + GIANT_WEIGHT) times their length (0: plain
-# nnz balance)
-GIANT_WEIGHT = 0.0
-
-# ghost rows: candidates are scanned up to this degree; the automatic cap is chosen among these
-GHOST_SCAN_MAX = 64
-GHOST_CAPS = (0, 1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64)
-# cost model of ghost_plan(): gathered X-row bytes per second of one GPU's SpMM (products, P = 2:
-# 63.1 M nonzeros x 512 B in 3.85 ms) and one peer link's rate per direction (half of the
-# ~153 GB/s xGMI link figure, minus RCCL overhead); a row is 4d bytes on both sides, so d cancels
-GHOST_GATHER_BPS = 8.4e12
+# The plan of a rank's share (row blocks, chunks + hub group, halos, ghost rows, sends, local CSR,
+# schedules) is built by the library's planner, srg_halo_plan_build (csrc/srg_halo.hip), for this
+# package and for C hosts alike.  Its automatic ghost cap minimises the modelled hop: max over ranks
+# of max(SpMM bytes incl. ghost rows at 8.4e12 B/s -- products at P = 2: 63.1 M nonzeros x 512 B in
+# 3.85 ms --, busiest peer link at the link rate); a row is 4d bytes on both sides, so d cancels.
+# The rate: this group's all_to_all, measured (measure_link_bps), or, without a group, one peer
+# link's rate per direction assumed here (half of the ~153 GB/s xGMI link figure, minus RCCL overhead).
 GHOST_LINK_BPS = 64e9
-
-
-def _row_positions(gip: torch.Tensor, rows: torch.Tensor, lens: torch.Tensor) -> torch.Tensor:
-    """Global nonzero ids of `rows` (their CSR ranges, concatenated in the given row order)."""
-    total = int(lens.sum()) if lens.numel() else 0
-    if total == 0:
-        return torch.zeros(0, dtype=torch.int64, device=gip.device)
-    starts = torch.repeat_interleave(gip[rows], lens)
-    first = torch.repeat_interleave(torch.cumsum(lens, 0) - lens, lens)
-    return starts + (torch.arange(total, device=gip.device) - first)
-
-
-def _ghost_candidates(gip, gix, deg, halo, s0: int, s1: int, n: int, max_degree: int) -> torch.Tensor:
-    """Mask over `halo` (rank q's full halo; q owns rows [s0, s1)): rows with at most `max_degree`
-    nonzeros whose every column is one of q's own rows or halo rows -- q can compute them from its
-    own panel, so it need not receive them."""
-    ok = torch.zeros(halo.numel(), dtype=torch.bool, device=halo.device)
-    if max_degree <= 0 or halo.numel() == 0:
-        return ok
-    cand = torch.nonzero(deg[halo] <= max_degree).flatten()
-    if cand.numel() == 0:
-        return ok
-    rows = halo[cand]
-    lens = deg[rows]
-    mark = torch.zeros(n, dtype=torch.bool, device=halo.device)
-    mark[s0:s1] = True
-    mark[halo] = True
-    pos = _row_positions(gip, rows, lens)
-    seg = torch.repeat_interleave(torch.arange(rows.numel(), device=halo.device), lens)
-    bad = torch.zeros(rows.numel(), dtype=torch.int64, device=halo.device)
-    bad.index_add_(0, seg, (~mark[gix[pos].to(torch.int64)]).to(torch.int64))
-    ok[cand[bad == 0]] = True
-    return ok
 
 
 def measure_link_bps(group=None, device=None, mbytes_per_peer: int = 32, reps: int = 3) -> float:
@@ -228,34 +186,10 @@ def measure_link_bps(group=None, device=None, mbytes_per_peer: int = 32, reps: i
     return float(rate.item())
 
 
-def ghost_plan(halos, elig, deg, owner, gip, starts, caps=GHOST_CAPS, link_bps=None):
-    """The ghost degree cap minimising the modelled hop time max over ranks q of
-    max(q's SpMM incl. ghosts, q's busiest peer link), with the rates GHOST_GATHER_BPS and
-    `link_bps` (default GHOST_LINK_BPS).  Returns (cap, {cap: modelled seconds per byte of row}).
-    Deterministic from the global plan and the rates, so every rank picks the same cap."""
-    link_bps = GHOST_LINK_BPS if link_bps is None else float(link_bps)
-    P = len(halos)
-    model = {}
-    for c in caps:
-        worst = 0.0
-        for q in range(P):
-            h, e = halos[q], elig[q]
-            dh = deg[h]
-            gmask = e & (dh <= c)
-            nnz_q = int(gip[starts[q + 1]] - gip[starts[q]]) + int(dh[gmask].sum())
-            recv = torch.bincount(owner[h[~gmask]], minlength=P)
-            link = int(recv.max()) if recv.numel() else 0
-            worst = max(worst, nnz_q / GHOST_GATHER_BPS, link / link_bps)
-        model[c] = worst
-    best = min(caps, key=lambda c: (model[c], c))
-    return best, model
-
-
-# The row chunks' slice waves take rows above max(HALO_HEAVY_MIN, nnz_local / (100000 C)) entries.
-# Products at P = 8 (where the second term is below 96): per-rank hop 1.149-1.152 ms at 96, 1.123-1.129
-# at 128, 1.110-1.112 at 160-200, 1.131 at 256, 1.165 at 300 (round 4, with the slice waves' id
-# prefetch; profiles/r04ak_*, r04al_halo_heavy_ab.txt).  papers100M / RMAT-26 ranks are above it.
-HALO_HEAVY_MIN = 192
+# The row chunks' slice waves take rows above max(192, nnz_local / (100000 C)) entries (the planner's
+# kHaloHeavyMin).  Products at P = 8 (where the second term is below 96): per-rank hop 1.149-1.152 ms at
+# 96, 1.123-1.129 at 128, 1.110-1.112 at 160-200, 1.131 at 256, 1.165 at 300 (round 4, with the slice
+# waves' id prefetch; profiles/r04ak_*, r04al_halo_heavy_ab.txt).  papers100M / RMAT-26 ranks are above it.
 
 # column blocks per row-chunk launch of the halo path for large local panels (1 = off; the
 # operator's col_blocks argument forces a count).  Bitwise the same hops either way.  Default: 8 for
@@ -285,7 +219,7 @@ class HaloPartitionedOperator:
       * ghost rows: a halo row whose own neighbours all lie in this rank's rows or halo, with at
         most `ghost_max_degree` nonzeros, is computed here every hop (the same CSR row, the same
         fma chain, so the same bits) instead of received -- on a power-law graph most of the halo
-        is such low-degree rows, and a pair of GPUs shares one xGMI link (see ghost_plan());
+        is such low-degree rows, and a pair of GPUs shares one xGMI link (the planner's cost model, above);
       * local panel layout: [own rows | received halo rows by (group, source, id) | ghost rows by
         (source, id)], and the local operator (own rows and ghost rows) with its column ids
         remapped into it (each row's entries keep their CSR order, so every output element is the
@@ -299,10 +233,11 @@ class HaloPartitionedOperator:
 
     def __init__(self, indptr, indices, values, n: int, group=None, chunks: int = 4,
                  heavy_threshold=None, hub_threshold=None, device=None, rank=None, world=None,
-                 local_spmm=None, ghost_max_degree=None, hub_launches=None, giant_weight=None,
-                 calibrate_link: bool = True, fast: bool = False, col_blocks=None):
-        from .csr import (DEFAULT_HEAVY_THRESHOLD, DEFAULT_HUB_THRESHOLD, NARROW_HEAVY_THRESHOLD,
-                          auto_heavy_threshold, auto_hub_threshold)
+                 local_spmm=None, ghost_max_degree=None, calibrate_link: bool = True, fast: bool = False,
+                 col_blocks=None):
+        from . import _lib
+        from .comm import HaloPlan
+        from .csr import DEFAULT_HEAVY_THRESHOLD, DEFAULT_HUB_THRESHOLD, NARROW_HEAVY_THRESHOLD
         self._narrow_heavy = NARROW_HEAVY_THRESHOLD
         self.group = group
         # tolerance mode for the hub group (SRG_SPMM_FAST: each hub row as 64 exact segment chains
@@ -318,173 +253,103 @@ class HaloPartitionedOperator:
         dev = torch.device(device) if device is not None else indices.device
         self.device = dev
         self.n = n
-        gip = indptr.to(dev, torch.int64)
-        gix = indices.to(dev)
-        self.giant_weight = GIANT_WEIGHT if giant_weight is None else float(giant_weight)
-        self.starts = balanced_row_starts(gip, P, giant_weight=self.giant_weight if P > 1 else 0.0)
-        st = torch.tensor(self.starts, dtype=torch.int64, device=dev)
-        self.nnz_total = int(gip[-1])
-        deg = gip[1:] - gip[:-1]
-        owner = torch.bucketize(torch.arange(n, device=dev), st[1:], right=True)   # owner rank of each row
-        # hub flags: each owner's threshold (auto from its own nonzero count unless given)
-        if hub_threshold is None:
-            hub_threshold = DEFAULT_HUB_THRESHOLD
-        thr = torch.empty(P, dtype=torch.int64, device=dev)
-        for q in range(P):
-            nnz_q = int(gip[self.starts[q + 1]] - gip[self.starts[q]])
-            thr[q] = auto_hub_threshold(nnz_q, launches=max(1, int(hub_launches or chunks))) if hub_threshold is None else (
-                hub_threshold if hub_threshold >= 0 else (1 << 62))
-        is_hub = deg > thr[owner]
-        # chunk of every row (contiguous nnz-balanced ranges inside each owner's block)
         C = max(1, int(chunks))
         self.C = C
-        grp = torch.empty(n, dtype=torch.int64, device=dev)
-        for q in range(P):
-            s0, s1 = self.starts[q], self.starts[q + 1]
-            lip = gip[s0:s1 + 1] - gip[s0]
-            cb = _chunk_bounds(lip, C)
-            for c in range(C):
-                grp[s0 + cb[c]:s0 + cb[c + 1]] = c
-            if q == p:
-                # local row range of each chunk (its hub rows included: they belong to group C)
-                self.chunk_ranges = [(cb[c], cb[c + 1]) for c in range(C)]
-        grp[is_hub] = C
         self.n_groups = C + 1
         G = self.n_groups
-        r0, r1 = self.starts[p], self.starts[p + 1]
-        self.r0, self.r1, self.rows = r0, r1, r1 - r0
-        b0, b1 = int(gip[r0]), int(gip[r1])
-        self._b0, self._b1 = b0, b1
-        self.nnz_local = b1 - b0
-
-        def needs_of(q):
-            """q's full halo (distinct remote columns of its rows), sorted by (group, source, id)."""
-            q0, q1 = int(gip[self.starts[q]]), int(gip[self.starts[q + 1]])
-            cols = torch.unique(gix[q0:q1].to(torch.int64))
-            cols = cols[(cols < self.starts[q]) | (cols >= self.starts[q + 1])]
-            key = (grp[cols] * P + owner[cols]) * n + cols          # sort by (group, source, id)
-            return cols[torch.argsort(key)]
-
-        # --- every rank's halo and its ghost candidates (identical on all ranks: sends follow)
-        halos, elig = [], []
-        for q in range(P):
-            hq = needs_of(q)
-            halos.append(hq)
-            elig.append(_ghost_candidates(gip, gix, deg, hq, self.starts[q], self.starts[q + 1], n,
-                                          GHOST_SCAN_MAX if ghost_max_degree is None else ghost_max_degree))
+        # --- the plan: the library's planner (srg_halo_plan_build, csrc/srg_halo.hip) over the host
+        # copy of the global CSR, identical on every rank (no messages); the ghost cap from its link-rate
+        # model at the rate this group's all_to_all measures (the minimum over ranks, so every rank
+        # passes the same rate and gets the same cap), or the assumed GHOST_LINK_BPS
+        ip_h = indptr.detach().to("cpu", torch.int64).contiguous().numpy()
+        ix_h = indices.detach().to("cpu", torch.int32).contiguous().numpy()
         self.link_bps = GHOST_LINK_BPS
-        if ghost_max_degree is None:
-            # the link rate the model uses: measured on this group's all_to_all when there is one
-            # (every rank gets the same minimum, so the same cap), else the assumed constant
-            if calibrate_link and P > 1 and not self.virtual and dist.is_initialized():
-                self.link_bps = measure_link_bps(group, dev)
-            ghost_max_degree = ghost_plan(halos, elig, deg, owner, gip, self.starts, link_bps=self.link_bps)[0]
-        self.ghost_max_degree = int(ghost_max_degree)
-        ghosts = [e & (deg[h] <= self.ghost_max_degree) for h, e in zip(halos, elig)]
-        need = halos[p][~ghosts[p]]                                  # received: (group, source, id)
-        gh = halos[p][ghosts[p]]
-        gh = gh[torch.argsort(owner[gh] * n + gh)]                   # ghosts: (source, id)
-        ng, ns = grp[need], owner[need]
-        counts = torch.zeros((G, P), dtype=torch.int64, device=dev)
-        counts.index_put_((ng, ns), torch.ones_like(need), accumulate=True)
-        self.recv_counts = counts.cpu().tolist()                 # [group][source]
-        self.ghost_recv_counts = torch.bincount(owner[gh], minlength=P).cpu().tolist()
-        self.n_recv = int(need.numel())
-        self.n_ghost = int(gh.numel())
-        self.halo = self.n_recv + self.n_ghost
-        self.group_offsets = []                                  # start of each group's halo region
-        off = 0
-        for g in range(G):
-            self.group_offsets.append(off)
-            off += sum(self.recv_counts[g])
-        # --- my sends: for every peer q, my rows q receives, per group, in q's receive order, and
-        # (first exchange only) my rows q computes as ghosts, by id
-        self.send_idx = [[None] * P for _ in range(G)]
-        self.send_counts = [[0] * P for _ in range(G)]
-        self.ghost_send_idx = [None] * P
-        self.ghost_send_counts = [0] * P
-        for q in range(P):
-            if q == p:
-                continue
-            hq = halos[q]
-            from_me = owner[hq] == p
-            mine = hq[from_me & ~ghosts[q]]                      # already sorted by (group, id)
-            gm = grp[mine]
-            for g in range(G):
-                sel = mine[gm == g] - r0
-                self.send_idx[g][q] = sel
-                self.send_counts[g][q] = int(sel.numel())
-            gq = torch.sort(hq[from_me & ghosts[q]]).values - r0
-            self.ghost_send_idx[q] = gq
-            self.ghost_send_counts[q] = int(gq.numel())
-        del halos, elig, ghosts
-        self.send_cat = []
-        for g in range(G):
-            parts = [self.send_idx[g][q] for q in range(P) if q != p and self.send_counts[g][q] > 0]
-            self.send_cat.append(torch.cat(parts) if parts else torch.zeros(0, dtype=torch.int64, device=dev))
-        parts = [self.ghost_send_idx[q] for q in range(P) if q != p and self.ghost_send_counts[q] > 0]
-        self.ghost_send_cat = torch.cat(parts) if parts else torch.zeros(0, dtype=torch.int64, device=dev)
-        # --- local operator over the panel rows [own | received (empty rows) | ghosts], columns
-        # remapped into the same layout
-        self._halo_ids = torch.cat([need, gh]).contiguous()
-        g2l = torch.full((n,), -1, dtype=torch.int64, device=dev)
-        g2l[r0:r1] = torch.arange(self.rows, device=dev)
-        g2l[need] = self.rows + torch.arange(self.n_recv, device=dev)
-        g2l[gh] = self.rows + self.n_recv + torch.arange(self.n_ghost, device=dev)
-        gdeg = deg[gh]
-        self._ghost_pos = _row_positions(gip, gh, gdeg)              # global nnz ids of the ghost rows
-        glob = torch.cat([gix[b0:b1].to(torch.int64), gix[self._ghost_pos].to(torch.int64)])
-        lix = g2l[glob]
-        # the entries' GLOBAL column ids (sorted within each row, as Â's are): the column blocks
-        # of the chunks' launches split every row where these cross the global block bounds
-        self._lix_glob = glob.to(torch.int32).contiguous() if dev.type == "cuda" else None
-        del glob
-        if bool((lix < 0).any()):
-            raise RuntimeError("halo layout misses a referenced column")
-        lens = torch.cat([deg[r0:r1], torch.zeros(self.n_recv, dtype=torch.int64, device=dev), gdeg])
-        lip = torch.zeros(self.rows + self.halo + 1, dtype=torch.int64, device=dev)
-        torch.cumsum(lens, 0, out=lip[1:])
-        lix = lix.to(torch.int32).contiguous()
-        lvv = self._local_values(values)
-        self.ncols_local = self.rows + self.halo
-        # --- per-group row schedules (local row ids; long rows first)
-        lgrp = grp[r0:r1]
-        ldeg = deg[r0:r1]
+        if ghost_max_degree is None and calibrate_link and P > 1 and not self.virtual and dist.is_initialized():
+            self.link_bps = measure_link_bps(group, dev)
+        if hub_threshold is None:
+            hub_threshold = DEFAULT_HUB_THRESHOLD
+        hub_c = _lib.SRG_HALO_AUTO if hub_threshold is None else (int(hub_threshold) if hub_threshold >= 0
+                                                                 else _lib.SRG_HALO_NONE)
         if heavy_threshold is None:
             heavy_threshold = DEFAULT_HEAVY_THRESHOLD
-        # per launch: the rank's nonzeros split over its row chunks, as for the hub threshold
+        if heavy_threshold is not None and heavy_threshold < 0:
+            raise ValueError("heavy_threshold must be >= 0 (None: automatic)")
         auto_heavy = heavy_threshold is None
-        heavy_t = max(HALO_HEAVY_MIN, auto_heavy_threshold(int(lip[self.rows]), launches=C)) if auto_heavy \
-            else heavy_threshold
         self._auto_heavy = auto_heavy
         self._heavy_explicit = heavy_threshold
+        plan = HaloPlan(ip_h, ix_h, n, P, p, chunks=C, hub_threshold=hub_c,
+                        heavy_threshold=_lib.SRG_HALO_AUTO if auto_heavy else int(heavy_threshold),
+                        ghost_max_degree=_lib.SRG_HALO_AUTO if ghost_max_degree is None else int(ghost_max_degree),
+                        link_bps=self.link_bps)
+        info = plan.info
+        self.ghost_max_degree = int(info["ghost_max_degree"])
+        self.starts = [int(v) for v in plan.array(_lib.SRG_HALO_STARTS)]
+        cr = plan.array(_lib.SRG_HALO_CHUNK_RANGES)
+        self.chunk_ranges = [(int(cr[c]), int(cr[c + 1])) for c in range(C)]
+        self.nnz_total = int(ip_h[-1]) if ip_h.size else 0
+        r0, rows = int(info["row0"]), int(info["n_rows"])
+        r1 = r0 + rows
+        self.r0, self.r1, self.rows = r0, r1, rows
+        b0, b1 = int(ip_h[r0]), int(ip_h[r1])
+        self._b0, self._b1 = b0, b1
+        self.nnz_local = b1 - b0
+        self.n_recv, self.n_ghost, self.halo = int(info["n_recv"]), int(info["n_ghost"]), int(info["halo"])
+        self.recv_counts = [[int(v) for v in plan.array(_lib.SRG_HALO_RECV_COUNTS, g)] for g in range(G)]
+        self.ghost_recv_counts = [int(v) for v in plan.array(_lib.SRG_HALO_GHOST_RECV_COUNTS)]
+        self.group_offsets = [int(v) for v in plan.array(_lib.SRG_HALO_GROUP_OFFSETS)]
+
+        def dev64(a):
+            return torch.from_numpy(a.astype("int64", copy=False)).to(dev)
+
+        def split_peers(cat, counts):
+            """A concatenation over the peers q != p (ascending) -> per-peer pieces (None for p)."""
+            out, off = [None] * P, 0
+            for q in range(P):
+                if q == p:
+                    continue
+                out[q] = cat[off:off + counts[q]]
+                off += counts[q]
+            return out
+
+        # --- my sends: for every peer q, my rows q receives, per group, in q's receive order, and
+        # (first exchange only) my rows q computes as ghosts, by id
+        self.send_counts = [[int(v) for v in plan.array(_lib.SRG_HALO_SEND_COUNTS, g)] for g in range(G)]
+        self.send_cat = [dev64(plan.array(_lib.SRG_HALO_SEND_ROWS, g)) for g in range(G)]
+        self.send_idx = [split_peers(self.send_cat[g], self.send_counts[g]) for g in range(G)]
+        self.ghost_send_counts = [int(v) for v in plan.array(_lib.SRG_HALO_GHOST_SEND_COUNTS)]
+        self.ghost_send_cat = dev64(plan.array(_lib.SRG_HALO_GHOST_SEND))
+        self.ghost_send_idx = split_peers(self.ghost_send_cat, self.ghost_send_counts)
+        # --- local operator over the panel rows [own | received (empty rows) | ghosts], columns
+        # remapped into the same layout
+        self._halo_ids = dev64(plan.array(_lib.SRG_HALO_HALO_IDS))
+        self._ghost_pos = dev64(plan.array(_lib.SRG_HALO_GHOST_POSITIONS))
+        lip = dev64(plan.array(_lib.SRG_HALO_LOCAL_INDPTR))
+        lix = torch.from_numpy(plan.array(_lib.SRG_HALO_LOCAL_INDICES)).to(dev).contiguous()
+        # the entries' GLOBAL column ids (sorted within each row, as Â's are): the column blocks
+        # of the chunks' launches split every row where these cross the global block bounds
+        if dev.type == "cuda":
+            gix = indices.to(dev)
+            self._lix_glob = torch.cat([gix[b0:b1].to(torch.int32), gix[self._ghost_pos].to(torch.int32)]).contiguous()
+        else:
+            self._lix_glob = None
+        lvv = self._local_values(values)
+        self.ncols_local = self.rows + self.halo
+        # --- per-group row schedules (local row ids; long rows first), then the ghost rows' launch
         self.views = []
         narrow = []           # slice-wave rows of each view for narrow panels (d <= 32), automatic only
-        for g in range(G):
-            rows_g = torch.nonzero(lgrp == g).flatten()
-            rows_g = rows_g[torch.sort(ldeg[rows_g], descending=True, stable=True).indices]
-            n_g = int(rows_g.numel())
-            if g == C:
-                n_hub, n_heavy = n_g, 0
+        for v in range(G + 1):
+            order = torch.from_numpy(plan.array(_lib.SRG_HALO_VIEW_ORDER, v)).to(dev).contiguous()
+            n_g, n_hub, n_heavy, n_narrow = (int(x) for x in plan.array(_lib.SRG_HALO_VIEW_META, v))
+            if v < G:
+                self.views.append((order, n_g, n_heavy, n_hub))
             else:
-                n_hub = 0
-                n_heavy = int((ldeg[rows_g] > heavy_t).sum()) if heavy_t >= 0 else 0
-            self.views.append((rows_g.to(torch.int32).contiguous(), n_g, n_heavy, n_hub))
-            narrow.append(int((ldeg[rows_g] > NARROW_HEAVY_THRESHOLD).sum()) if auto_heavy and g != C else None)
-        # the ghost rows: one more launch (no exchange), panel rows rows + n_recv + i
-        gsort = torch.sort(gdeg, descending=True, stable=True)
-        g_rows = (self.rows + self.n_recv + gsort.indices).to(torch.int32).contiguous()
-        g_heavy = int((gsort.values > heavy_t).sum()) if heavy_t >= 0 else 0
-        self.ghost_view = (g_rows, self.n_ghost, g_heavy, 0)
-        narrow.append(int((gsort.values > NARROW_HEAVY_THRESHOLD).sum()) if auto_heavy else None)
+                self.ghost_view = (order, n_g, n_heavy, 0)
+            narrow.append(n_narrow if auto_heavy and v != C else None)
+        plan.destroy()
         self._lip, self._lix, self._lvv = lip, lix, lvv
         if local_spmm is None:
             from .csr import DeviceCSR
             from .spmm import spmm
-            if dev.type == "cuda":
-                from . import _lib
-                _lib.call(dev, "srg_csr_validate", lip.data_ptr(), lix.data_ptr(), self.rows + self.halo,
-                          lix.numel(), self.ncols_local, _lib.stream(dev))
             # the groups write own rows of the panel, the ghost launch the ghost slots of its halo
             spaces = [self.rows] * len(self.views) + [self.rows + self.halo]
             self._A = [DeviceCSR(lip, lix, lvv, n_g, self.ncols_local, order, n_heavy, n_hub, nn, row_space=rs)

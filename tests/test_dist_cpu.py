@@ -218,7 +218,7 @@ def test_ghost_plan_cost_model():
         D.GHOST_LINK_BPS = 1e3
         caps = {D.HaloPartitionedOperator(ip, ix, vals, n, chunks=2, device="cpu", rank=q, world=2,
                                           local_spmm=lambda *a: None).ghost_max_degree for q in range(2)}
-        assert len(caps) == 1 and caps.pop() in D.GHOST_CAPS[1:]
+        assert len(caps) == 1 and caps.pop() in (1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64)
     finally:
         D.GHOST_LINK_BPS = saved
 

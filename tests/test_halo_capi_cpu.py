@@ -1,8 +1,10 @@
-"""The C-ABI halo planner (srg_halo_plan_build, include/srgnn_hip.h) on the CPU: for a C / C++ host it
-builds rank p's share of the halo-exchange partition from the global CSR -- the same plan as the
-Python package's srgnn.dist.HaloPartitionedOperator.  Every array of the two plans is compared: row
-blocks, local CSR (remapped columns), schedules and their slice / hub counts, receive and send
-lists per group, ghost rows and their sends, halo ids.  Host-only entry: no device needed."""
+"""The halo planner (srg_halo_plan_build, include/srgnn_hip.h) on the CPU: it builds rank p's share of
+the halo-exchange partition from the global CSR, for C / C++ hosts and for the Python package's
+srgnn.dist.HaloPartitionedOperator alike.  Every array of its plan is compared with the torch
+restatement of the same plan (tests/halo_plan_ref.py, the planner the package ran before round 5): row
+blocks, local CSR (remapped columns), schedules and their slice / hub counts, receive and send lists
+per group, ghost rows and their sends, halo ids, and the automatic ghost cap of the link-rate cost
+model.  Host-only entry: no device needed."""
 import numpy as np
 import pytest
 import torch
@@ -17,22 +19,28 @@ def _graph(n=1500, e=9000, seed=12):
     return ip, ix, vals, n
 
 
-def _python_share(ip, ix, vals, n, world, rank, chunks, hub, ghost):
-    from srgnn.dist import HaloPartitionedOperator
-    return HaloPartitionedOperator(ip, ix, vals, n, chunks=chunks, hub_threshold=hub, device="cpu", rank=rank,
-                                   world=world, local_spmm=lambda *a: None, ghost_max_degree=ghost)
+def _python_share(ip, ix, vals, n, world, rank, chunks, hub, ghost, link_bps=64e9):
+    from halo_plan_ref import PyHaloPlan
+    return PyHaloPlan(ip, ix, n, world, rank, chunks=chunks, hub_threshold=hub, ghost_max_degree=ghost,
+                      link_bps=link_bps)
 
 
-@pytest.mark.parametrize("world,chunks,hub,ghost", [(2, 3, 60, 0), (3, 2, 60, 8), (8, 6, None, 2), (4, 4, 40, 16),
-                                                   (1, 2, None, 0)])
-def test_c_planner_equals_python_plan(world, chunks, hub, ghost):
+@pytest.mark.parametrize("world,chunks,hub,ghost,link", [(2, 3, 60, 0, 0), (3, 2, 60, 8, 0), (8, 6, None, 2, 0),
+                                                        (4, 4, 40, 16, 0), (1, 2, None, 0, 0),
+                                                        (4, 3, 60, None, 64e9), (4, 3, 60, None, 1e3),
+                                                        (8, 6, None, None, 2e4), (3, 2, None, None, 1e30)])
+def test_c_planner_equals_python_plan(world, chunks, hub, ghost, link):
     from srgnn import _lib
     from srgnn.comm import HaloPlan
     ip, ix, vals, n = _graph()
+    caps = set()
     for rank in range(world):
-        op = _python_share(ip, ix, vals, n, world, rank, chunks, hub, ghost)
+        op = _python_share(ip, ix, vals, n, world, rank, chunks, hub, ghost, link_bps=link or 64e9)
         pl = HaloPlan(ip.numpy(), ix.numpy(), n, world, rank, chunks=chunks,
-                      hub_threshold=_lib.SRG_HALO_AUTO if hub is None else hub, ghost_max_degree=ghost)
+                      hub_threshold=_lib.SRG_HALO_AUTO if hub is None else hub,
+                      ghost_max_degree=_lib.SRG_HALO_AUTO if ghost is None else ghost, link_bps=link)
+        assert pl.info["ghost_max_degree"] == op.ghost_max_degree
+        caps.add(op.ghost_max_degree)
         info = pl.info
         assert (info["row0"], info["n_rows"], info["n_recv"], info["n_ghost"], info["halo"]) == \
             (op.r0, op.rows, op.n_recv, op.n_ghost, op.halo)
@@ -56,7 +64,14 @@ def test_c_planner_equals_python_plan(world, chunks, hub, ghost):
             np.testing.assert_array_equal(pl.array(_lib.SRG_HALO_VIEW_ORDER, v), order.numpy(), err_msg=f"view {v}")
             meta = pl.array(_lib.SRG_HALO_VIEW_META, v)
             assert (meta[0], meta[1], meta[2]) == (n_g, n_hub, n_heavy), f"view {v}"
+            if op.narrow[v] is not None:
+                assert meta[3] == op.narrow[v], f"view {v}"
         pl.destroy()
+    assert len(caps) == 1                    # every rank derives the same cap
+    if ghost is None and link >= 1e30:
+        assert caps == {0}                   # free links: nothing is worth computing twice
+    if ghost is None and link <= 1e3:
+        assert caps.pop() > 0                # slow links: ghosts
 
 
 def test_c_planner_argument_checks():

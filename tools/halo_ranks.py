@@ -32,10 +32,6 @@ def main():
     ap.add_argument("--chunks", type=int, default=4)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--d", type=int, default=None, help="feature width (default: the config's)")
-    ap.add_argument("--hub-launches", type=int, default=None,
-                    help="launch count the hub threshold assumes (default: the chunk count)")
-    ap.add_argument("--giant-weight", type=float, default=None,
-                    help="partition weight of giant rows (default: srgnn.dist.GIANT_WEIGHT)")
     ap.add_argument("--fast", action="store_true", help="the hub group in tolerance mode (SRG_SPMM_FAST)")
     ap.add_argument("--col-blocks", default=None,
                     help="column blocks of the row chunks' launches: one value or a comma list (default: auto)")
@@ -55,9 +51,12 @@ def main():
     for P, ghost, cb in [(int(w), gc, cb) for w in a.worlds.split(",") for gc in ghosts for cb in cbs]:
         ranks = []
         for q in range(P):
+            import time
+            t_plan = time.perf_counter()
             op = HaloPartitionedOperator(ip, ix, vals, n, chunks=a.chunks, device=dev, rank=q, world=P,
-                                         ghost_max_degree=ghost, hub_launches=a.hub_launches,
-                                         giant_weight=a.giant_weight, fast=a.fast, col_blocks=cb)
+                                         ghost_max_degree=ghost, fast=a.fast, col_blocks=cb)
+            torch.cuda.synchronize()
+            t_plan = time.perf_counter() - t_plan
             src = op.new_panel(d)
             src[: op.rows].copy_(x[op.r0:op.r1])
             src[op.rows:].uniform_(-1, 1)
@@ -75,6 +74,7 @@ def main():
                 torch.cuda.synchronize()
                 ms = sorted(ev[2 * r].elapsed_time(ev[2 * r + 1]) for r in range(a.reps))
                 ranks.append({"rank": q, "rows": op.rows, "nnz": op.nnz_local, "hub_rows": op.views[op.C][1],
+                              "ghost_max_degree": op.ghost_max_degree, "s_operator_build": round(t_plan, 3),
                               "ms_compute": ms[len(ms) // 2]})
                 print(f"  P={P} rank {q}: compute {ms[len(ms) // 2]:.3f} ms", file=sys.stderr, flush=True)
                 del op, src, dst
