@@ -98,3 +98,60 @@ def test_plain_c_host_runs_the_halo_path():
         r = subprocess.run([exe] + args, capture_output=True, timeout=120)
         out = r.stdout.decode() + r.stderr.decode()
         assert r.returncode == 0 and out.startswith("ok:"), out
+
+
+def test_planner_rejects_bad_arguments_before_the_device():
+    """srg_plan_build / _describe / _propagate_f32 argument checks (csrc/srg_plan.hip): every one fails
+    with SRG_ERR_INVALID and a message before any HIP call, so they run without a GPU."""
+    L = _lib.lib()
+    out = ctypes.c_void_p()
+    ip = (ctypes.c_int64 * 3)(0, 1, 2)
+    cases = [
+        ((ip, None, None, 2, 8, 4, 0, 0, None, None), "null plan"),
+        ((None, None, None, 2, 8, 4, 0, 0, None, ctypes.byref(out)), "indptr"),
+        ((ip, None, None, -1, 8, 4, 0, 0, None, ctypes.byref(out)), "n_rows"),
+        ((ip, None, None, 2, 0, 4, 0, 0, None, ctypes.byref(out)), "d=0"),
+        ((ip, None, None, 2, 8, -1, 0, 0, None, ctypes.byref(out)), "hops=-1"),
+        ((ip, None, None, 2, 8, 4, 65, 0, None, ctypes.byref(out)), "col_blocks=65"),
+        ((ip, None, None, 2, 8, 4, 0, _lib.SRG_PLAN_COMPACT | _lib.SRG_PLAN_SPANS, None, ctypes.byref(out)), "opts"),
+        ((ip, None, None, 2, 8, 4, 0, 0x100, None, ctypes.byref(out)), "opts"),
+    ]
+    for args, msg in cases:
+        assert L.srg_plan_build(*args) == _lib.SRG_ERR_INVALID, msg
+        assert msg in _lib.last_error(), (msg, _lib.last_error())
+    assert L.srg_plan_describe(None, None) == _lib.SRG_ERR_INVALID
+    assert L.srg_plan_propagate_f32(None, None, 8, 8, 1, 0, None) == _lib.SRG_ERR_INVALID
+    assert L.srg_plan_launch(None, 0, 8, None, None, None) == _lib.SRG_ERR_INVALID
+    assert L.srg_plan_destroy(None, None) == 0
+
+
+@pytest.mark.gpu
+def test_plain_c_host_runs_the_planner(tmp_path):
+    """examples/plan_propagate.c: a plain C program reads a CSR file, plans its hops on the device
+    (srg_plan_build), checks the plans' launches on the host, times the one-shot and long-lived runs
+    and compares hops 1, 2 and K bit for bit with the unscheduled one-launch hops."""
+    import json
+    import subprocess
+
+    import numpy as np
+    exe = os.path.join(REPO, "examples", "plan_propagate")
+    assert os.path.exists(exe), "build it with `make -C examples` (__graft_entry__.build() does)"
+    rng = np.random.default_rng(4)
+    n = 30000
+    deg = np.minimum(rng.zipf(1.8, n), 3000).astype(np.int64)
+    deg[7] = 20000
+    ip = np.concatenate([[0], np.cumsum(deg)]).astype(np.int64)
+    ix = np.concatenate([np.sort(rng.choice(n, k, replace=False)) for k in deg]).astype(np.int32)
+    v = rng.standard_normal(ix.size).astype(np.float32)
+    path = tmp_path / "g.csr"
+    with open(path, "wb") as f:
+        f.write(b"SRGCSR1\0")
+        f.write(np.array([n, ix.size], dtype=np.int64).tobytes())
+        f.write(ip.tobytes())
+        f.write(ix.tobytes())
+        f.write(v.tobytes())
+    for d, K in (("64", "7"), ("128", "3")):
+        r = subprocess.run([exe, str(path), d, K, "2"], capture_output=True, timeout=120)
+        assert r.returncode == 0, r.stdout.decode() + r.stderr.decode()
+        res = json.loads(r.stdout.decode())
+        assert res["bitwise_vs_one_launch"] is True and res["n"] == n
