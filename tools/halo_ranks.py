@@ -33,6 +33,9 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--d", type=int, default=None, help="feature width (default: the config's)")
     ap.add_argument("--fast", action="store_true", help="the hub group in tolerance mode (SRG_SPMM_FAST)")
+    ap.add_argument("--hub-threshold", default="auto",
+                    help="hub row length(s): 'auto' (nnz_rank / (1024 chunks), floor 2048) or a comma list")
+    ap.add_argument("--heavy-threshold", type=int, default=None, help="chunk slice-wave row length (default: auto)")
     ap.add_argument("--col-blocks", default=None,
                     help="column blocks of the row chunks' launches: one value or a comma list (default: auto)")
     ap.add_argument("--quick", action="store_true",
@@ -48,13 +51,16 @@ def main():
     ghosts = [None] if a.ghost == "auto" else [int(c) for c in a.ghost.split(",")]
     cbs = [None] if a.col_blocks is None else [int(c) for c in a.col_blocks.split(",")]
     hcb = None
-    for P, ghost, cb in [(int(w), gc, cb) for w in a.worlds.split(",") for gc in ghosts for cb in cbs]:
+    hubs = [None] if a.hub_threshold == "auto" else [int(h) for h in a.hub_threshold.split(",")]
+    for P, ghost, cb, hub in [(int(w), gc, cb, h) for w in a.worlds.split(",") for gc in ghosts for cb in cbs
+                              for h in hubs]:
         ranks = []
         for q in range(P):
             import time
             t_plan = time.perf_counter()
             op = HaloPartitionedOperator(ip, ix, vals, n, chunks=a.chunks, device=dev, rank=q, world=P,
-                                         ghost_max_degree=ghost, fast=a.fast, col_blocks=cb)
+                                         ghost_max_degree=ghost, fast=a.fast, col_blocks=cb, hub_threshold=hub,
+                                         heavy_threshold=a.heavy_threshold)
             torch.cuda.synchronize()
             t_plan = time.perf_counter() - t_plan
             src = op.new_panel(d)
@@ -168,10 +174,10 @@ def main():
             del op, src, dst
             torch.cuda.empty_cache()
         if a.quick:
-            key = f"{P}" + ("" if cb is None else f"/cb{cb}") + ("" if hcb is None else f"/hcb{hcb}")
+            key = f"{P}" + ("" if cb is None else f"/cb{cb}") + ("" if hub is None else f"/hub{hub}")
             out["worlds"][key] = {"ranks": ranks, "max_hop_compute_ms": max(r["ms_compute"] for r in ranks)}
-            print(f"P={P} col blocks {cb} hub blocks {hcb}: hop compute {out['worlds'][key]['max_hop_compute_ms']:.3f} ms (max over ranks)",
-                  file=sys.stderr, flush=True)
+            print(f"P={P} col blocks {cb} hub threshold {hub or 'auto'}: hop compute "
+                  f"{out['worlds'][key]['max_hop_compute_ms']:.3f} ms (max over ranks)", file=sys.stderr, flush=True)
             continue
         worst = max(ranks, key=lambda r: max(r["ms_hub"], r["ms_chunks"]))
         key = (f"{P}" if a.ghost == "auto" else f"{P}/ghost{ghost}") + ("" if cb is None else f"/cb{cb}") + \
