@@ -26,18 +26,12 @@ import torch
 import torch.distributed as dist
 
 
-def balanced_row_starts(indptr: torch.Tensor, parts: int, giant_weight: float = 0.0, giant_threshold=None):
-    """Row boundaries [0 = s_0 <= ... <= s_P = n] splitting the nonzeros as evenly as rows allow.
-    giant_weight > 0: rows longer than giant_threshold count (1 + giant_weight) times their length,
-    so the rank holding a giant row (a latency-bound chain beside its other rows) gets fewer of
-    the others."""
+def balanced_row_starts(indptr: torch.Tensor, parts: int):
+    """Row boundaries [0 = s_0 <= ... <= s_P = n] splitting the nonzeros as evenly as rows allow (the
+    halo planner's rule too: srg_halo.hip balanced()).  Weighting long rows more (so the rank holding a
+    giant row gets fewer others) was measured and dropped."""
     ip = indptr.to(torch.int64).cpu()
     n = ip.numel() - 1
-    if giant_weight > 0 and n > 0:
-        deg = ip[1:] - ip[:-1]
-        thr = int(giant_threshold) if giant_threshold is not None else max(2048, int(ip[-1]) // (1024 * parts))
-        extra = torch.where(deg > thr, (deg.double() * giant_weight).round().to(torch.int64), torch.zeros_like(deg))
-        ip = ip + torch.cat([torch.zeros(1, dtype=torch.int64), torch.cumsum(extra, 0)])
     nnz = int(ip[-1])
     targets = torch.tensor([(nnz * p) // parts for p in range(parts + 1)], dtype=torch.int64)
     starts = torch.searchsorted(ip, targets, right=False).clamp_(0, n)

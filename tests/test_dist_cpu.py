@@ -84,19 +84,6 @@ def test_balanced_row_starts_and_remap():
     assert bool((m[1:] > m[:-1]).all())          # monotone: CSR order (and fma chains) preserved
 
 
-def test_balanced_row_starts_giant_weight():
-    """giant_weight: a row longer than the threshold counts (1 + w) times, so its block holds fewer
-    other rows; w = 0 is the plain nnz balance."""
-    from srgnn.dist import balanced_row_starts
-    deg = torch.tensor([400] + [10] * 99)
-    ip = torch.cat([torch.zeros(1, dtype=torch.int64), torch.cumsum(deg, 0)])
-    plain = balanced_row_starts(ip, 2)
-    heavy = balanced_row_starts(ip, 2, giant_weight=3.0, giant_threshold=100)
-    assert plain == [0, 31, 100]                  # 700 of the 1390 nonzeros in block 0
-    assert heavy == [0, 1, 100]                   # the giant weighs 1600 of 2590: alone in block 0
-    assert balanced_row_starts(ip, 2, giant_weight=0.0, giant_threshold=100) == plain
-
-
 def _halo_worker(rank, world, port, out_path, chunks, ghost=None, full_x=False):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
