@@ -217,8 +217,10 @@ typedef struct {
 } srg_plan_desc;
 int srg_plan_build(const int64_t* indptr, const int32_t* indices, const float* values, int64_t n_rows,
                    int32_t d, int32_t hops, int32_t col_blocks, uint32_t opts, void* stream, srg_plan** plan);
-/* Releases the plan's device memory in stream order on `stream`: every hop that uses the plan must
- * be ordered before that point of `stream` (enqueued on it, or joined into it). */
+/* Releases the plan's device memory after the work enqueued on `stream` (it synchronises `stream`):
+ * every hop that uses the plan must be ordered before that point (enqueued on it, or joined into it).
+ * A plan is used by one host thread at a time (a propagate over a width other than 64 / 128 / 256
+ * completes its row-indexed spans in place; srg_plan_launch does so up front). */
 int srg_plan_destroy(srg_plan* plan, void* stream);
 int srg_plan_describe(const srg_plan* plan, srg_plan_desc* desc);
 /* Launch i of one hop over a d-column panel, as srg_plan_propagate_f32 runs it (flags included), and

@@ -29,7 +29,7 @@ import torch.distributed as dist
 def balanced_row_starts(indptr: torch.Tensor, parts: int):
     """Row boundaries [0 = s_0 <= ... <= s_P = n] splitting the nonzeros as evenly as rows allow (the
     halo planner's rule too: srg_halo.hip balanced()).  Weighting long rows more (so the rank holding a
-    giant row gets fewer others) was measured and dropped."""
+    giant row gets fewer others) was measured and dropped (profiles/r01_giant_weight_sweep.json)."""
     ip = indptr.to(torch.int64).cpu()
     n = ip.numel() - 1
     nnz = int(ip[-1])
