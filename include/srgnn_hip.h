@@ -233,7 +233,9 @@ int srg_plan_launch(const srg_plan* plan, int32_t i, int32_t d, srg_hop_launch* 
                     void* stream);
 /* K hops through the plan: panels[k] = A * panels[k-1], k = 1..K (HOST array of K+1 device pointers
  * of leading dimension ld, d columns; any d, the layout was chosen for the build's d).  flags:
- * SRG_SPMM_NT_STORE, SRG_SPMM_FAST.  Bitwise srg_propagate_khop_f32's hops (FAST: its tolerance). */
+ * SRG_SPMM_NT_STORE, SRG_SPMM_FAST.  Bitwise srg_propagate_khop_f32's hops (FAST: its tolerance).
+ * Repeated with the same panels, d, K, flags and a non-null stream, the call replays the K hops as a
+ * HIP graph captured on its second occurrence (the same launches and arguments: the same bits). */
 int srg_plan_propagate_f32(const srg_plan* plan, float* const* panels, int64_t ld, int32_t d, int32_t K,
                            uint32_t flags, void* stream);
 

@@ -298,3 +298,31 @@ def test_native_plan_automatic_choices_match_prepare(monkeypatch):
     ref = S.spmm(A, X)
     assert torch.equal(out[1].view(torch.int32), ref.view(torch.int32))
     assert isinstance(P, NativePlan) and P.device_bytes > A.indices.numel() * 8
+
+
+def test_repeated_plan_calls_replay_a_graph_bitwise():
+    """srg_plan_propagate_f32 repeated with the same arguments on a non-null stream replays the K hops
+    as a HIP graph from the second call on: every call's hops stay the one-launch hops, bit for bit,
+    for one launch per hop and for column blocks with the hub chain; a changed panel list re-plans."""
+    from srgnn.plan import NativePlan
+    from srgnn.spmm import spmm
+    ip, ix, v, n = _power_law(seed=9)
+    A = _csr(ip, ix, v, n)
+    st = torch.cuda.Stream()
+    with torch.cuda.stream(st):
+        for B in (1, 3):
+            P = NativePlan(A, 64, hops=4, col_blocks=B)
+            X = torch.randn(n, 64, device="cuda")
+            ref = [X]
+            for _ in range(4):
+                ref.append(spmm(A, ref[-1]))
+            for trial in range(2):
+                panels = [X] + [torch.empty_like(X) for _ in range(4)]
+                for _ in range(4):
+                    for p in panels[1:]:
+                        p.fill_(float("nan"))
+                    P.propagate(panels, 64, 64, 4)
+                    st.synchronize()
+                    for k in range(1, 5):
+                        assert torch.equal(panels[k].view(torch.int32), ref[k].view(torch.int32)), (B, trial, k)
+            P.close()
