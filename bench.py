@@ -408,7 +408,7 @@ def one_shot(ip, ix, vals, n, X, K, dev, heavy_threshold=None):
     allocated inside the bracket; HIP events on the launch stream plus the host wall clock around it.
     Â and X already resident (GraphOp.propagate's construct_adj and H2D / D2H are tools/e2e_api.py's)."""
     from srgnn.csr import DeviceCSR
-    from srgnn.spmm import auto_col_blocks, propagate
+    from srgnn.spmm import col_blocks_of, propagate
     stream = torch.cuda.current_stream(dev)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
     torch.cuda.synchronize()
@@ -420,7 +420,7 @@ def one_shot(ip, ix, vals, n, X, K, dev, heavy_threshold=None):
     ev[2].record(stream)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    B = auto_col_blocks(A1, X.shape[1], hops=K)
+    B = col_blocks_of(A1, X.shape[1])
     nnz = int(ix.numel())
     res = {"what": ("one GraphOp.propagate(K) hop loop as the reference calls it (once per run, "
                     "node_classification.py:62): fresh operator + column cut + K hops + output panels, "
@@ -591,7 +591,7 @@ def run_wavelet(a, dev, world=1, rank=0, pmc=None):
     from srgnn import wavelet as W
     from srgnn.csr import DeviceCSR
     from srgnn import _lib
-    from srgnn.spmm import auto_col_blocks, hop, launches_per_hop, spmm_cheby
+    from srgnn.spmm import col_blocks_of, hop, launches_per_hop, spmm_cheby
     t_build = time.perf_counter()
     ip, ix, lv, n, d, lmax = graphs.build_laplacian(a.config, dev, d=a.d)
     nnz = int(ix.numel())
@@ -629,8 +629,7 @@ def run_wavelet(a, dev, world=1, rank=0, pmc=None):
     # SpMM launch of the split path
     stream = torch.cuda.current_stream(dev)
     Fm = filt._csr(filt.fvals)
-    B = auto_col_blocks(Fm, cb)
-    B = 1 if fused or B < 2 or not Fm.column_blocks(B) else B
+    B = 1 if fused else col_blocks_of(Fm, cb)
     LB = launches_per_hop(Fm, B, cb)
     tb = torch.zeros((n, cb), dtype=torch.float32, device=dev)
     ns = len(filt.taus)
@@ -787,7 +786,7 @@ def main():
         log(f"rank {rank}: backend {backend}, {devices['distinct_gpus']} distinct GPUs over {world} ranks")
 
     from srgnn.csr import DeviceCSR
-    from srgnn.spmm import column_blocks_for, hop, launches_per_hop, prepare, propagate, spmm
+    from srgnn.spmm import hop, launches_per_hop, prepare, propagate, spmm
 
     t_build = time.perf_counter()
     ip, ix, vals, n, d, K = graphs.build(a.config, dev, d=a.d)
@@ -807,12 +806,7 @@ def main():
             mode = "panels" if K * n * d * 4 < 0.9 * free else "last"
             log(f"mode {mode}: {K} panels need {K * n * d * 4 / 1e9:.1f} GB, {free / 1e9:.1f} GB free")
         # the operator serves every warm-up and timed step: cut it once here when that amortises
-        if a.col_blocks is None:
-            col_blocks = prepare(A, d, hops=K * (a.steps + a.warmup))
-        else:
-            col_blocks = a.col_blocks
-            if col_blocks > 1 and not column_blocks_for(A, col_blocks, hops=K * (a.steps + a.warmup)):
-                col_blocks = 1
+        col_blocks = prepare(A, d, K * (a.steps + a.warmup), a.col_blocks)
         launches = launches_per_hop(A, col_blocks, d, agg=bool(a.aggregate))
         log(f"schedule: n_hub={A.n_hub} n_heavy={A.n_heavy} column blocks per hop={col_blocks} ({launches} launches)")
         if a.aggregate:

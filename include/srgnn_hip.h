@@ -195,9 +195,9 @@ int srg_propagate_plan_f32(const srg_hop_launch* launches, int32_t n_launch, int
  * srgnn package builds its K-hop runs with this planner).  Replaces the reference's per-hop
  * csr_sparse_dense_matmul setup inside GraphOp.propagate (SSRG/operators/base_operator.py:32-35,
  * utils.py:17-47), which re-reads the scipy CSR every hop.
- * Unlike the other (B) entries the plan allocates device memory (stream-ordered, hipMallocAsync on
- * `stream`: the schedules, the spans by slot, the copies -- srg_plan_describe's device_bytes) and
- * synchronises `stream` twice while it builds.  The plan BORROWS indptr / indices / values (span
+ * Unlike the other (B) entries the plan allocates device memory (hipMalloc: the schedules, the spans
+ * by slot, the copies -- srg_plan_describe's device_bytes -- and a scratch arena freed before it
+ * returns) and synchronises `stream` while it builds.  The plan BORROWS indptr / indices / values (span
  * layouts read them every hop): they must outlive it.  indptr[n_rows + 1], indices / values
  * [indptr[n_rows] - indptr[0]], column ids in [0, n_rows) (not validated here: srg_csr_validate). */
 typedef struct srg_plan srg_plan;
@@ -238,6 +238,16 @@ int srg_plan_launch(const srg_plan* plan, int32_t i, int32_t d, srg_hop_launch* 
  * HIP graph captured on its second occurrence (the same launches and arguments: the same bits). */
 int srg_plan_propagate_f32(const srg_plan* plan, float* const* panels, int64_t ld, int32_t d, int32_t K,
                            uint32_t flags, void* stream);
+/* One hop through the plan between panels of their own leading dimensions: Y = A * X (X: ldx, Y: ldy,
+ * d columns; Y must not alias X) and, when agg is not NULL, the aggregation step fused into the
+ * epilogue of the launch where each row's chain ends: agg = (agg_init ? 0 : agg) + w * Y (lda),
+ * srg_hop_accumulate_f32's arithmetic, so bitwise the hop followed by that step.  A plan whose block 0
+ * is one launch (panels >= 16 GiB) runs the hop, then that step.  flags: SRG_SPMM_NT_STORE,
+ * SRG_SPMM_FAST (not with agg).  The aggregating hop of srgnn.aggregate's hop loop: the reference's
+ * MessageOp.aggregate -> combine over the hop list (SSRG/operators/base_operator.py:49-59) folded
+ * into the hops as they are produced. */
+int srg_plan_hop_f32(const srg_plan* plan, const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t d,
+                     uint32_t flags, float* agg, int64_t lda, float w, int32_t agg_init, void* stream);
 
 /* Chebyshev heat-kernel filter bank (wavelet basis), SSRG/models/base_scalable/base_model.py:
  * 184-191, 236-265 via pygsp cheby_op.  One fused launch per Chebyshev order:

@@ -34,6 +34,9 @@
 
 extern "C" void srg_set_error(int code, const char* msg);   // srg_spmm.hip: thread-local srg_last_error
 extern "C" void srg_clear_error(void);
+extern "C" int srg_run_plan_hop(const srg_hop_launch* launches, int32_t n_launch, int32_t join_hub, const float* X,
+                                int64_t ldx, float* Y, int64_t ldy, int32_t d, const uint8_t* agg_on, float* agg,
+                                int64_t lda, float w, int32_t agg_init, void* stream);   // srg_spmm.hip
 
 struct srg_plan {
     struct Launch {
@@ -906,6 +909,62 @@ int srg_plan_propagate_f32(const srg_plan* plan, float* const* panels, int64_t l
     }
 #endif
     return srg_propagate_plan_f32(L.data(), (int32_t)L.size(), join, panels, ld, d, K, stream);
+}
+
+int srg_plan_hop_f32(const srg_plan* plan, const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t d,
+                     uint32_t flags, float* agg, int64_t lda, float w, int32_t agg_init, void* stream)
+{
+    if (!plan) return pfail(SRG_ERR_INVALID, "null plan");
+    if (flags & ~(SRG_SPMM_NT_STORE | SRG_SPMM_FAST))
+        return pfail(SRG_ERR_INVALID, "flags=0x%x: a plan's hops take NT_STORE and FAST only", flags);
+    if ((flags & SRG_SPMM_FAST) && agg)
+        return pfail(SRG_ERR_INVALID, "FAST takes no aggregation epilogue");
+    if (d <= 0 || ldx < d || ldy < d) return pfail(SRG_ERR_INVALID, "d=%d, ldx=%lld, ldy=%lld", d, (long long)ldx, (long long)ldy);
+    if (plan->launches.empty()) {
+        // no rows: nothing to write
+        srg_clear_error();
+        return SRG_OK;
+    }
+    if (!X || !Y) return pfail(SRG_ERR_INVALID, "null X / Y");
+    if (agg && lda < d) return pfail(SRG_ERR_INVALID, "lda=%lld < d=%d", (long long)lda, d);
+    DevGuard g(static_cast<hipStream_t>(stream));
+    if (g.rc) return g.rc;
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess || dev != plan->device)
+        return pfail(SRG_ERR_INVALID, "the plan lives on device %d, the stream on %d", plan->device, dev);
+    if (!plan->rows_full) {
+        // the packed light rows run only at 64 / 128 / 256 columns on 16-byte rows (agg's too)
+        const bool packed = packed_width(d) && ldx % 4 == 0 && ldy % 4 == 0 && (uintptr_t)X % 16 == 0 &&
+                            (uintptr_t)Y % 16 == 0 && (!agg || (lda % 4 == 0 && (uintptr_t)agg % 16 == 0));
+        if (!packed) {
+            const int rc = complete_rows(const_cast<srg_plan*>(plan), static_cast<hipStream_t>(stream));
+            if (rc) return rc;
+        }
+    }
+    std::vector<srg_hop_launch> L;
+    const int join = plan_launches(plan, d, flags, L);
+    // the epilogue runs where the rows' chains end: the one launch; with block 0 split, its whole rows'
+    // launch and the last block's (every cut row is in it).  Block 0 as one launch ends some chains
+    // (its whole rows) and continues others: the hop runs plain, then one accumulation pass over Y
+    // (the same two roundings, srg_hop_accumulate_f32)
+    std::vector<uint8_t> on(L.size(), 0);
+    bool fused = agg != nullptr;
+    if (agg) {
+        if (plan->B == 1) on[0] = 1;
+        else if (plan->split0) {
+            for (size_t i = 0; i < L.size(); ++i) on[i] = plan->launches[i].whole_rows ? 1 : 0;
+            on.back() = 1;
+        } else fused = false;
+    }
+    int rc = srg_run_plan_hop(L.data(), (int32_t)L.size(), join, X, ldx, Y, ldy, d, fused ? on.data() : nullptr,
+                              fused ? agg : nullptr, lda, w, agg_init, stream);
+    if (rc) return rc;
+    if (agg && !fused) {
+        rc = srg_hop_accumulate_f32(agg, lda, Y, ldy, plan->n, d, w, agg_init ? SRG_ACC_INIT : SRG_ACC_ADD, stream);
+        if (rc) return rc;
+    }
+    srg_clear_error();
+    return SRG_OK;
 }
 
 }  // extern "C"

@@ -2149,6 +2149,62 @@ int srg_propagate_khop_f32(const int64_t* indptr, const int32_t* indices, const 
     return ok();
 }
 
+// one hop of a launch list: X (ldx) -> Y (ldy); launch i carries the aggregation epilogue (agg = (init ?
+// 0 : agg) + w * Y, at the end of each of its rows' chains) when agg && agg_on[i]; with join_hub the
+// hub side stream is joined into `s` after the hop
+static int run_hop_launches(const srg_hop_launch* launches, int32_t n_launch, bool join_hub, const float* X,
+                            int64_t ldx, float* Y, int64_t ldy, int32_t d, const uint8_t* agg_on, float* agg,
+                            int64_t lda, float w, int agg_init, hipStream_t s, int dev)
+{
+    for (int i = 0; i < n_launch; ++i) {
+        const srg_hop_launch& L = launches[i];
+        Epi e{};
+        if (agg && agg_on && agg_on[i]) {
+            e.agg = agg;
+            e.lda = lda;
+            e.w = w;
+            e.init = agg_init ? 1 : 0;
+        }
+        int rc;
+        if (L.row_end) {
+            e.row_end = L.row_end;
+            // the light rows' slots count from the first non-hub row of the schedule
+            e.slot_beg = L.slot_beg ? L.slot_beg + L.n_hub : nullptr;
+            e.slot_end = L.slot_beg ? L.slot_end + L.n_hub : nullptr;
+            rc = launch_spmm<int64_t, kEpiSpan>(L.row_beg, L.indices, L.values, L.n_rows, L.row_order, L.n_hub,
+                                                L.n_heavy, X, ldx, Y, ldy, d, L.flags, s, e);
+        } else {
+            rc = launch_spmm<int64_t>(L.row_beg, L.indices, L.values, L.n_rows, L.row_order, L.n_hub, L.n_heavy,
+                                      X, ldx, Y, ldy, d, L.flags, s, e);
+        }
+        if (rc) return rc;
+    }
+    if (join_hub) {
+        std::lock_guard<std::mutex> lock(g_side_mu);
+        auto it = g_side.find(std::make_pair(dev, s));
+        if (it != g_side.end() && it->second.pending) {
+            SRG_HIP_CHECK(hipStreamWaitEvent(s, it->second.join, 0));
+            it->second.pending = false;
+        }
+    }
+    return SRG_OK;
+}
+
+static int check_launches(const srg_hop_launch* launches, int32_t n_launch, const float* X, int64_t ldx,
+                          const float* Y, int64_t ldy, int32_t d)
+{
+    for (int i = 0; i < n_launch; ++i) {
+        const srg_hop_launch& L = launches[i];
+        int rc = check_spmm_args(L.row_beg, L.indices, L.values, L.n_rows, X, ldx, Y, ldy, d);
+        if (rc) return rc;
+        if (L.n_rows > 0 && L.n_hub + L.n_heavy > 0 && !L.row_order)
+            return fail(SRG_ERR_INVALID, "launch %d: hub / heavy rows need a row_order", i);
+        if ((L.slot_beg != nullptr) != (L.slot_end != nullptr) || (L.slot_beg && !L.row_end))
+            return fail(SRG_ERR_INVALID, "launch %d: slot_beg / slot_end come together, with row_end", i);
+    }
+    return SRG_OK;
+}
+
 int srg_propagate_plan_f32(const srg_hop_launch* launches, int32_t n_launch, int32_t join_hub,
                            float* const* panels, int64_t ld, int32_t d, int32_t K, void* stream)
 {
@@ -2158,48 +2214,41 @@ int srg_propagate_plan_f32(const srg_hop_launch* launches, int32_t n_launch, int
     if (!launches || !panels) return fail(SRG_ERR_INVALID, "null launches or panels");
     for (int k = 0; k <= K; ++k)
         if (!panels[k] && d > 0) return fail(SRG_ERR_INVALID, "panels[%d] is null", k);
+    int rc = check_launches(launches, n_launch, panels[0], ld, panels[0], ld, d);
+    if (rc) return rc;
     for (int i = 0; i < n_launch; ++i) {
-        const srg_hop_launch& L = launches[i];
-        int rc = check_spmm_args(L.row_beg, L.indices, L.values, L.n_rows, panels[0], ld, panels[0], ld, d);
-        if (rc) return rc;
-        if (L.n_rows > 0 && L.n_hub + L.n_heavy > 0 && !L.row_order)
-            return fail(SRG_ERR_INVALID, "launch %d: hub / heavy rows need a row_order", i);
-        if ((L.slot_beg != nullptr) != (L.slot_end != nullptr) || (L.slot_beg && !L.row_end))
-            return fail(SRG_ERR_INVALID, "launch %d: slot_beg / slot_end come together, with row_end", i);
         // without the per-hop join, hop k's hub rows would still run on the side stream while hop
         // k+1's launches on `stream` read panels[k]: a data race
+        const srg_hop_launch& L = launches[i];
         if (!join_hub && K > 1 && L.n_hub > 0 && (L.flags & SRG_SPMM_HUB_NOJOIN))
             return fail(SRG_ERR_INVALID, "launch %d: HUB_NOJOIN hub rows over K=%d hops need join_hub", i, K);
     }
     const hipStream_t s = static_cast<hipStream_t>(stream);
     for (int k = 1; k <= K; ++k) {
-        for (int i = 0; i < n_launch; ++i) {
-            const srg_hop_launch& L = launches[i];
-            int rc;
-            if (L.row_end) {
-                Epi e{};
-                e.row_end = L.row_end;
-                // the light rows' slots count from the first non-hub row of the schedule
-                e.slot_beg = L.slot_beg ? L.slot_beg + L.n_hub : nullptr;
-                e.slot_end = L.slot_beg ? L.slot_end + L.n_hub : nullptr;
-                rc = launch_spmm<int64_t, kEpiSpan>(L.row_beg, L.indices, L.values, L.n_rows, L.row_order, L.n_hub,
-                                                    L.n_heavy, panels[k - 1], ld, panels[k], ld, d, L.flags, s, e);
-            } else {
-                rc = launch_spmm<int64_t>(L.row_beg, L.indices, L.values, L.n_rows, L.row_order, L.n_hub, L.n_heavy,
-                                          panels[k - 1], ld, panels[k], ld, d, L.flags, s);
-            }
-            if (rc) return rc;
-        }
-        if (join_hub) {
-            std::lock_guard<std::mutex> lock(g_side_mu);
-            auto it = g_side.find(std::make_pair(guard_.dev, s));
-            if (it != g_side.end() && it->second.pending) {
-                SRG_HIP_CHECK(hipStreamWaitEvent(s, it->second.join, 0));
-                it->second.pending = false;
-            }
-        }
+        rc = run_hop_launches(launches, n_launch, join_hub != 0, panels[k - 1], ld, panels[k], ld, d, nullptr, nullptr,
+                              0, 0.0f, 0, s, guard_.dev);
+        if (rc) return rc;
     }
     return ok();
+}
+
+// srg_plan.hip's single hop (srg_plan_hop_f32): the launches of one hop between panels of their own
+// leading dimensions, the aggregation epilogue on the launches agg_on names (checked here)
+__attribute__((visibility("hidden"))) int srg_run_plan_hop(const srg_hop_launch* launches, int32_t n_launch,
+                                                           int32_t join_hub, const float* X, int64_t ldx, float* Y,
+                                                           int64_t ldy, int32_t d, const uint8_t* agg_on, float* agg,
+                                                           int64_t lda, float w, int32_t agg_init, void* stream)
+{
+    SRG_DEVICE_GUARD(stream);
+    if (n_launch <= 0) return ok();
+    int rc = check_launches(launches, n_launch, X, ldx, Y, ldy, d);
+    if (rc) return rc;
+    if (X == Y) return fail(SRG_ERR_INVALID, "Y must not alias X (its rows are gathered)");
+    if (agg && (lda < d || agg == Y || agg == X))
+        return fail(SRG_ERR_INVALID, "aggregation panel: lda=%lld < d=%d or agg aliases X / Y", (long long)lda, d);
+    rc = run_hop_launches(launches, n_launch, join_hub != 0, X, ldx, Y, ldy, d, agg_on, agg, lda, w, agg_init,
+                          static_cast<hipStream_t>(stream), guard_.dev);
+    return rc ? rc : ok();
 }
 
 int srg_cheby_step_f64(const int64_t* indptr, const int32_t* indices, const double* values,

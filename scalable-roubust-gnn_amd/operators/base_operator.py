@@ -33,11 +33,9 @@ def _hops_to_host(A, X, K, ring=3):
     while the next hop runs (the D2H of the reference-shaped list overlaps the kernels); device
     memory holds a ring of `ring` hop panels.  Returns the K host tensors.  The hops are
     column-blocked where srgnn.spmm.auto_col_blocks says so (bitwise the one-launch hop)."""
-    from srgnn.spmm import auto_col_blocks, column_blocks_for, hop
+    from srgnn.spmm import hop, prepare
     dev = A.device
-    B = auto_col_blocks(A, X.shape[1], hops=K)
-    if B > 1 and not column_blocks_for(A, B, hops=K):
-        B = 1
+    B = prepare(A, X.shape[1], K)
     main = torch.cuda.current_stream(dev)
     copy_s = torch.cuda.Stream(dev)
     R = max(1, min(K, ring))

@@ -75,6 +75,7 @@ EXPORTED_SYMBOLS = (
     "srg_plan_describe",
     "srg_plan_launch",
     "srg_plan_propagate_f32",
+    "srg_plan_hop_f32",
     "srg_cheby_step_f64",
     "srg_cheby_step_f32",
     "srg_cheby_epilogue_f32",
@@ -147,7 +148,9 @@ def _declare(lib):
     lib.srg_plan_describe.argtypes = [_p, _p]
     lib.srg_plan_launch.argtypes = [_p, _i32, _i32, _p, _p, _p]
     lib.srg_plan_propagate_f32.argtypes = [_p, _p, _i64, _i32, _i32, _u32, _p]
-    for name in ("srg_plan_build", "srg_plan_destroy", "srg_plan_describe", "srg_plan_launch", "srg_plan_propagate_f32"):
+    lib.srg_plan_hop_f32.argtypes = [_p, _p, _i64, _p, _i64, _i32, _u32, _p, _i64, _f32, _i32, _p]
+    for name in ("srg_plan_build", "srg_plan_destroy", "srg_plan_describe", "srg_plan_launch", "srg_plan_propagate_f32",
+                 "srg_plan_hop_f32"):
         getattr(lib, name).restype = ctypes.c_int
     lib.srg_cheby_step_f64.argtypes = [_p, _p, _p, _i64, _p, _p, _p, _p, _i64, _i32, ctypes.c_int,
                                        _f64, _f64, _p, _p, _i32, _p, _i64, _p]

@@ -238,11 +238,9 @@ def propagate_aggregate(A: DeviceCSR, X: torch.Tensor, K: int, steps=None, last_
         raise ValueError("propagate_aggregate needs a square operator matching X")
     if X.dim() != 2 or X.dtype != torch.float32 or X.stride(1) != 1 or X.stride(0) < d:
         raise ValueError("X must be a row-major float32 [n, d] device panel")
-    from .spmm import auto_col_blocks, column_blocks_for
-    if col_blocks is None:
-        col_blocks = auto_col_blocks(A, d, hops=K)
-    if col_blocks > 1 and K > 0 and not column_blocks_for(A, col_blocks, hops=K):
-        col_blocks = 1
+    from .spmm import prepare
+    # the layout for the K hops (the native plan, srgnn.plan: its single hops take the epilogue)
+    col_blocks = prepare(A, d, K, col_blocks) if K > 0 else 1
     groups, trailing = schedule(steps or [])
     if len(groups) > K + 1:
         raise ValueError("hop index out of range")

@@ -1,11 +1,13 @@
 """The native one-GPU planner (srg_plan_build / srg_plan_propagate_f32, csrc/srg_plan.hip) for a DeviceCSR.
 
-srgnn.spmm.prepare / propagate run their K-hop loops through it: the column blocks, block 0's split,
-the per-launch schedules, the hub chain, the spans by slot and the compact launch-ordered copies are
-built on the device in one pass (a radix sort of (launch, span length) keys, one scan, one copy), the
-layout DeviceCSR.column_blocks / compact_column_blocks / split_whole + spmm._hop_plan build with torch
-(which stay for the aggregation, wavelet and halo paths and for layout experiments with other
-constants).  C / C++ hosts call the same entry points (examples/plan_propagate.c).
+srgnn.spmm.prepare / propagate run their K-hop loops through it, and spmm.hop (the aggregation and
+wavelet hop loops, the host-copy loop of GraphOp.propagate) its single hops, with the aggregation
+epilogue where asked (srg_plan_hop_f32): the column blocks, block 0's split, the per-launch schedules,
+the hub chain, the spans by slot and the compact launch-ordered copies are built on the device in one
+pass (a radix sort of (launch, span length) keys, one scan, one copy) -- the layout
+DeviceCSR.column_blocks / compact_column_blocks / split_whole + spmm._hop_plan build with torch (kept
+for layout experiments with other constants, and as the layout tests' reference).  C / C++ hosts call
+the same entry points (examples/plan_propagate.c).
 """
 from __future__ import annotations
 
@@ -85,6 +87,15 @@ class NativePlan:
         arr = (ctypes.c_void_p * (K + 1))(*[p.data_ptr() for p in panels])
         _lib.call(self.device, "srg_plan_propagate_f32", self._p, arr, int(ld), int(d), int(K), int(flags),
                   _lib.stream(self.device))
+
+    def hop(self, X, Y, d: int, flags: int = 0, agg=None, w: float = 0.0, init: bool = False) -> None:
+        """One hop Y = A @ X (device tensors with their own row strides, checked by the caller); agg: a
+        panel that gets (0 if init else agg) + w * Y in the epilogue where each row's chain ends."""
+        if self._p is None:
+            raise ValueError("the plan is closed")
+        _lib.call(self.device, "srg_plan_hop_f32", self._p, X.data_ptr(), X.stride(0), Y.data_ptr(), Y.stride(0),
+                  int(d), int(flags), agg.data_ptr() if agg is not None else None,
+                  agg.stride(0) if agg is not None else 0, float(w), 1 if init else 0, _lib.stream(self.device))
 
     def close(self) -> None:
         """Releases the plan's memory in stream order on the device's current stream."""

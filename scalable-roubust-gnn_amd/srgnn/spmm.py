@@ -83,14 +83,16 @@ def _native_ok(A: DeviceCSR) -> bool:
             and MIN_HOPS_TO_COMPACT == _lib.SRG_PLAN_MIN_HOPS_TO_COMPACT)
 
 
-def prepare(A: DeviceCSR, d: int, hops: int) -> int:
+def prepare(A: DeviceCSR, d: int, hops: int, col_blocks=None) -> int:
     """Lays A out for a run of `hops` hops over d-column panels: column blocks (spans, or compact
     copies in launch order for long runs) or, for one launch per hop and a long run, a launch-ordered
-    copy of the whole operator (DeviceCSR.schedule_ordered).  Returns the column blocks per hop."""
+    copy of the whole operator (DeviceCSR.schedule_ordered).  col_blocks: None = automatic, else the
+    blocks per hop asked for.  Returns the column blocks per hop that hop() / propagate() then run."""
     if _native_ok(A):
         from .plan import plan_for
-        return plan_for(A, d, hops, int(FORCE_COL_BLOCKS or 0), SPLIT_BLOCK0).col_blocks
-    B = auto_col_blocks(A, d, hops=hops)
+        cb = int(col_blocks) if col_blocks is not None else int(FORCE_COL_BLOCKS or 0)
+        return plan_for(A, d, hops, cb, SPLIT_BLOCK0).col_blocks
+    B = auto_col_blocks(A, d, hops=hops) if col_blocks is None else int(col_blocks)
     if B > 1 and column_blocks_for(A, B, hops=hops):
         return B
     if _COMPACT and hops >= MIN_HOPS_TO_COMPACT and not A.is_span and A.n_rows == A.n_cols:
@@ -138,6 +140,16 @@ def auto_col_blocks(A: DeviceCSR, d: int, hops: int | None = None) -> int:
     return B
 
 
+def col_blocks_of(A: DeviceCSR, d: int) -> int:
+    """The column blocks per hop hop() runs A in over a d-column panel as A is laid out now (its native
+    plan for d, or its torch-formulated blocks); 1 = the one-launch hop."""
+    if _native_ok(A):
+        from .plan import cached
+        P = cached(A, d)
+        return P.col_blocks if P is not None else 1
+    return auto_col_blocks(A, d)
+
+
 # Hops over panels of at least this many bytes cap the row kernel's occupancy (SRG_SPMM_CAP_WAVES):
 # products 5.84 -> 5.81 ms per hop, arxiv (87 MB) 3 % slower capped (profiles/r04x_waves_ab.txt)
 CAP_WAVES_MIN_PANEL = 512 << 20
@@ -148,7 +160,7 @@ def launches_per_hop(A: DeviceCSR, B: int, d: int, agg: bool = False) -> int:
     one when block 0 runs as its cut spans and its whole rows (_split_block0, or the aggregation
     epilogue)."""
     from .plan import cached
-    P = cached(A, d) if not agg else None
+    P = cached(A, d) if _native_ok(A) else None
     if P is not None and P.col_blocks == B:
         return P.n_launch
     blocks = A.column_blocks(B) if B > 1 else None
@@ -210,13 +222,17 @@ def hop(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, nt_store: bool = False
         _check_panel(agg[0], A.out_rows, "agg", d)
     if out.device != A.device or X.device != A.device:
         raise ValueError("A, X and out must be on the same device")
-    if agg is None and _native_ok(A) and X.stride(0) == out.stride(0) and X.data_ptr() != out.data_ptr():
-        # an operator prepared by the native planner: one hop of its plan
+    if _native_ok(A) and X.data_ptr() != out.data_ptr() and not (fast and agg is not None):
+        # an operator prepared by the native planner: one hop of its plan (srg_plan_hop_f32), the
+        # aggregation step in the epilogue of the launches where the rows' chains end
         from .plan import cached
         P = cached(A, d)
         if P is not None and (col_blocks is None or int(col_blocks) == P.col_blocks):
-            P.propagate([X, out], X.stride(0), d, 1, (_lib.SRG_SPMM_NT_STORE if nt_store else 0) |
-                        (_lib.SRG_SPMM_FAST if fast else 0))
+            flags = (_lib.SRG_SPMM_NT_STORE if nt_store else 0) | (_lib.SRG_SPMM_FAST if fast else 0)
+            if agg is None:
+                P.hop(X, out, d, flags)
+            else:
+                P.hop(X, out, d, flags, agg[0], agg[1], agg[2])
             return out
     B = auto_col_blocks(A, d) if col_blocks is None else int(col_blocks)
     plan, join = _hop_plan(A, d, B, nt_store, fast, agg is not None)

@@ -171,6 +171,7 @@ class HeatWaveletFilter:
         # INIT + STEP epilogues (same bits; set the attribute for A/B runs)
         self.lean_epilogue = True
         self.order, self.n_heavy, self.n_hub = make_schedule(self.indptr, heavy_threshold, hub_threshold)
+        self.thresholds = (heavy_threshold, hub_threshold)
         self.n_heavy_narrow = narrow_heavy(self.indptr, self.n_hub) if _auto_heavy(heavy_threshold) else None
 
     def _coef(self, ct, vals):
@@ -245,19 +246,16 @@ class HeatWaveletFilter:
         cache = self.__dict__.setdefault("_csr_cache", {})
         if id(vals) not in cache:
             cache[id(vals)] = DeviceCSR(self.indptr, self.indices, vals, self.n, self.n, self.order, self.n_heavy,
-                                        self.n_hub, self.n_heavy_narrow)
+                                        self.n_hub, self.n_heavy_narrow, thresholds=self.thresholds)
         return cache[id(vals)]
 
     def prepare_column_blocks(self, width: int, hops: int) -> int:
-        """Cut L and F into column blocks (spmm.hop) when `hops` SpMMs over panels `width` columns
-        wide amortise it (spmm.auto_col_blocks); returns the blocks per SpMM."""
-        from .spmm import auto_col_blocks, column_blocks_for
+        """Lay L and F out (spmm.prepare: the native plan, column blocks when `hops` SpMMs over panels
+        `width` columns wide amortise them) for the split path's hops; returns the blocks per SpMM."""
+        from .spmm import prepare
         B = 1
         for vals in (self.lvals, self.fvals):
-            A = self._csr(vals)
-            B = auto_col_blocks(A, width, hops=hops)
-            if B > 1 and not column_blocks_for(A, B, hops=hops):
-                B = 1
+            B = prepare(self._csr(vals), width, hops)
         return B
 
     def work_panels(self, fused_epilogue: bool = False) -> int:

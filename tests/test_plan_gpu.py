@@ -230,6 +230,22 @@ def test_native_plan_edge_cases():
     Y = torch.full_like(X, 7.0)
     P.propagate([X, Y], 8, 8, 1)
     assert torch.equal(Y, torch.zeros_like(Y))
+    # no rows at all: a plan with no launches, every call a no-op
+    A0 = _csr(np.zeros(1, np.int64), np.zeros(0, np.int32), np.zeros(0, np.float32), 0)
+    P0 = NativePlan(A0, 16, hops=20, col_blocks=3)
+    assert P0.n_launch == 0 and P0.device_bytes == 0
+    E = torch.zeros(0, 16, device="cuda")
+    P0.propagate([E, torch.zeros(0, 16, device="cuda")], 16, 16, 1)
+    # more blocks than rows and columns: empty spans everywhere but the hops are exact
+    ipt = np.array([0, 2, 3, 3, 6], np.int64)
+    ixt = np.array([0, 3, 1, 0, 1, 2], np.int32)
+    At = _csr(ipt, ixt, np.arange(1, 7, dtype=np.float32), 4)
+    Xt = torch.randn(4, 64, device="cuda")
+    for compact in (False, True):
+        Pt = NativePlan(At, 64, hops=3, col_blocks=9, compact=compact, split_block0=True)
+        pt = [Xt, torch.empty_like(Xt), torch.empty_like(Xt)]
+        Pt.propagate(pt, 64, 64, 2)
+        assert torch.equal(pt[2].view(torch.int32), spmm(At, spmm(At, Xt)).view(torch.int32))
     # every row short: block 0 computes all of them, the later launches schedule no row
     rng = np.random.default_rng(1)
     n = 3000
@@ -326,3 +342,83 @@ def test_repeated_plan_calls_replay_a_graph_bitwise():
                     for k in range(1, 5):
                         assert torch.equal(panels[k].view(torch.int32), ref[k].view(torch.int32)), (B, trial, k)
             P.close()
+
+
+AGG_LAYOUTS = [(1, False, None), (1, True, None), (3, True, True), (3, False, True), (3, True, False),
+               (6, True, True)]
+
+
+@pytest.mark.parametrize("B,compact,split", AGG_LAYOUTS)
+@pytest.mark.parametrize("d", [64, 128, 36])
+def test_plan_hop_strided_and_aggregating(B, compact, split, d):
+    """srg_plan_hop_f32: one hop between panels of different leading dimensions (X a column slice of
+    a wider panel), bitwise the one-launch hop; with the aggregation epilogue (INIT, then ADD) bitwise
+    the hop followed by srg_hop_accumulate_f32 -- fused where block 0 is split or the hop is one launch,
+    a separate pass where block 0 is one launch (split False)."""
+    from srgnn import _lib
+    from srgnn.plan import NativePlan
+    from srgnn.spmm import spmm
+    ip, ix, v, n = _power_law(seed=13, unsorted_rows=2)
+    A = _csr(ip, ix, v, n)
+    P = NativePlan(A, d, hops=8, col_blocks=B, compact=compact, split_block0=split)
+    wide = torch.randn(n, d + 40, device="cuda")
+    X = wide[:, 8:8 + d]                       # ld d + 40, 32-byte offset
+    ref = spmm(A, X.contiguous())
+    Y = torch.full((n, d), float("nan"), device="cuda")
+    P.hop(X, Y, d)
+    assert torch.equal(Y.view(torch.int32), ref.view(torch.int32))
+    # the aggregation epilogue: agg = 0 + w * Y, then agg += w2 * Y2
+    agg = torch.full((n, d + 4), float("nan"), device="cuda")[:, :d]
+    ref_agg = torch.empty((n, d), device="cuda")
+    st = _lib.stream(X.device)
+    Y1 = torch.empty((n, d), device="cuda")
+    P.hop(X, Y1, d, 0, agg, 0.375, True)
+    _lib.call(X.device, "srg_hop_accumulate_f32", ref_agg.data_ptr(), d, ref.data_ptr(), d, n, d, 0.375,
+              _lib.SRG_ACC_INIT, st)
+    assert torch.equal(Y1.view(torch.int32), ref.view(torch.int32))
+    assert torch.equal(agg.view(torch.int32), ref_agg.view(torch.int32))
+    Y2 = torch.empty((n, d), device="cuda")
+    P.hop(Y1, Y2, d, _lib.SRG_SPMM_NT_STORE, agg, -1.25, False)
+    ref2 = spmm(A, ref)
+    _lib.call(X.device, "srg_hop_accumulate_f32", ref_agg.data_ptr(), d, ref2.data_ptr(), d, n, d, -1.25,
+              _lib.SRG_ACC_ADD, st)
+    assert torch.equal(Y2.view(torch.int32), ref2.view(torch.int32))
+    assert torch.equal(agg.view(torch.int32), ref_agg.view(torch.int32))
+    # argument checks before any launch
+    for bad in (dict(flags=_lib.SRG_SPMM_ACCUMULATE), dict(flags=_lib.SRG_SPMM_FAST, agg=agg)):
+        with pytest.raises(_lib.SrgError):
+            P.hop(X, Y, d, bad.get("flags", 0), bad.get("agg"), 1.0, True)
+    with pytest.raises(_lib.SrgError):
+        P.hop(Y, Y, d)
+
+
+def test_aggregation_loop_runs_the_native_plan(monkeypatch):
+    """spmm.prepare lays the operator out with the native plan; propagate_aggregate's fused hops then
+    run through it (srg_plan_hop_f32), with the same bits as the torch-formulated layout (NATIVE_PLAN
+    off)."""
+    from srgnn import spmm as S
+    from srgnn.aggregate import combine_plan, combine_steps, propagate_aggregate
+    from srgnn.plan import cached
+    ip, ix, v, n = _power_law(seed=17)
+    d, K = 128, 6
+
+    class _Msg:
+        aggr_type, start, end, combination_type, alpha, weight_list = "simple_weighted", 0, K + 1, "alpha", 0.15, None
+    steps = combine_steps(*combine_plan(_Msg(), K + 1))
+    X = torch.randn(n, d, device="cuda")
+    outs = []
+    calls = []
+    from srgnn import plan as PL
+    orig = PL.NativePlan.hop
+
+    def spy(self, *a, **k):
+        calls.append(a[4] if len(a) > 4 else k.get("agg"))
+        return orig(self, *a, **k)
+    monkeypatch.setattr(PL.NativePlan, "hop", spy)
+    for native in (True, False):
+        monkeypatch.setattr(S, "NATIVE_PLAN", native)
+        A = _csr(ip, ix, v, n)
+        outs.append(propagate_aggregate(A, X, K, steps, col_blocks=3))
+        assert (cached(A, d) is not None) == native
+    assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
+    assert len(calls) == K and any(c is not None for c in calls)

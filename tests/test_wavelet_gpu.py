@@ -162,6 +162,22 @@ def test_split_path_column_blocked_bit_identical(monkeypatch, B):
     assert torch.equal(f.apply(S, split=False), f.apply(S, split=True, col_block=64))
 
 
+def test_split_path_runs_the_native_plan(monkeypatch):
+    """Automatic thresholds: prepare_column_blocks lays L and F out with the native plan (srgnn.plan)
+    and the split path's hops -- over column slices of the panel, a leading dimension other than the
+    work panels' -- run through srg_plan_hop_f32: bit for bit the fused kernel."""
+    from srgnn import spmm as S_, wavelet as W
+    from srgnn.plan import cached
+    monkeypatch.setattr(S_, "FORCE_COL_BLOCKS", 3)
+    a = graphs()["rmat3000"]
+    L = W.laplacian_from_adj(a)
+    f = W.HeatWaveletFilter(L, [-0.5, 0.5], order=4, lmax=None, dtype=torch.float32, device="cuda")
+    assert f.prepare_column_blocks(64, hops=8) == 3
+    assert cached(f._csr(f.fvals), 64) is not None and cached(f._csr(f.lvals), 64) is not None
+    S = torch.from_numpy(np.random.default_rng(5).standard_normal((a.shape[0], 128)).astype(np.float32)).cuda()
+    assert torch.equal(f.apply(S, split=False), f.apply(S, split=True, col_block=64))
+
+
 def test_spmm_cheby_in_place_and_argument_checks():
     """srg_spmm_cheby_f32 directly: a step written over T_{k-1} equals the step into a fresh panel
     and the two-launch form; aliasing and flag misuse are rejected before any launch."""

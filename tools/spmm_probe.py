@@ -24,7 +24,7 @@ import torch  # noqa: E402
 
 from srgnn import graphs, roofline, synth  # noqa: E402
 from srgnn.csr import DeviceCSR  # noqa: E402
-from srgnn.spmm import column_blocks_for, hop, launches_per_hop, prepare  # noqa: E402
+from srgnn.spmm import hop, launches_per_hop, prepare  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="products")
@@ -92,10 +92,8 @@ Y = torch.empty_like(X)
 # the probe stands for a long run of hops (bench.py's operator serves every step): the panel rule alone
 if a.identity or a.permutation:
     B = 1
-elif a.col_blocks is None:
-    B = prepare(A, d, hops=a.hops)          # as bench.py: blocks, or a launch-ordered copy for long runs
 else:
-    B = a.col_blocks if a.col_blocks > 1 and column_blocks_for(A, a.col_blocks, hops=a.hops) else 1
+    B = prepare(A, d, a.hops, a.col_blocks)   # as bench.py: blocks, or a launch-ordered copy for long runs
 torch.cuda.synchronize()
 for _ in range(a.reps):
     hop(A, X, Y, col_blocks=B)      # one hop = B k_spmm launches (column blocks), same bits
