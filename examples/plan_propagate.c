@@ -160,7 +160,7 @@ int main(int argc, char** argv)
     /* 0. two plans for K hops checked on the host and run, with a synchronisation after each step */
     for (int t = 0; t < 2; ++t) {
         srg_plan* P0 = NULL;
-        CHECK(srg_plan_build(d_ip, d_ix, d_v, n, d, K, 0, 0, s, &P0));
+        CHECK(srg_plan_build(d_ip, d_ix, d_v, n, d, K, 0, SRG_PLAN_AUTO, SRG_PLAN_AUTO, 0, s, &P0));
         HCHECK(hipStreamSynchronize(s));
         const long bad = validate(P0, n, nnz, d);
         if (bad) { fprintf(stderr, "plan layout invalid (%ld)\n", bad); return 4; }
@@ -182,7 +182,7 @@ int main(int argc, char** argv)
         HCHECK(hipStreamSynchronize(s));
         const double t0 = now_ms();
         srg_plan* P1 = NULL;
-        CHECK(srg_plan_build(d_ip, d_ix, d_v, n, d, K, 0, 0, s, &P1));
+        CHECK(srg_plan_build(d_ip, d_ix, d_v, n, d, K, 0, SRG_PLAN_AUTO, SRG_PLAN_AUTO, 0, s, &P1));
         stage("one-shot plan built");
         CHECK(srg_plan_propagate_f32(P1, panels, d, d, K, 0, s));
         CHECK(srg_plan_destroy(P1, s));
@@ -195,7 +195,7 @@ int main(int argc, char** argv)
     HCHECK(hipStreamSynchronize(s));
     double t0 = now_ms();
     srg_plan* P = NULL;
-    CHECK(srg_plan_build(d_ip, d_ix, d_v, n, d, K * (reps + 1), 0, 0, s, &P));
+    CHECK(srg_plan_build(d_ip, d_ix, d_v, n, d, K * (reps + 1), 0, SRG_PLAN_AUTO, SRG_PLAN_AUTO, 0, s, &P));
     HCHECK(hipStreamSynchronize(s));
     const double build_ms = now_ms() - t0;
     stage("long-lived plan built");

@@ -199,13 +199,19 @@ int srg_propagate_plan_f32(const srg_hop_launch* launches, int32_t n_launch, int
  * by slot, the copies -- srg_plan_describe's device_bytes -- and a scratch arena freed before it
  * returns) and synchronises `stream` while it builds.  The plan BORROWS indptr / indices / values (span
  * layouts read them every hop): they must outlive it.  indptr[n_rows + 1], indices / values
- * [indptr[n_rows] - indptr[0]], column ids in [0, n_rows) (not validated here: srg_csr_validate). */
+ * [indptr[n_rows] - indptr[0]], column ids in [0, n_rows) (not validated here: srg_csr_validate).
+ * hub_threshold / heavy_threshold: SRG_PLAN_AUTO (per launch, from its nnz: hub rows > max(2048,
+ * nnz / 1024) entries, slice-wave rows > max(96, nnz / 100000) for the one-launch hop, nnz / 30000 for
+ * a column block's), SRG_PLAN_NONE (no such rows) or a row length that holds for every launch, as a
+ * DeviceCSR built with explicit thresholds schedules its blocks (srgnn.csr.make_schedule). */
 typedef struct srg_plan srg_plan;
 #define SRG_PLAN_MIN_HOPS_TO_COMPACT 6
 #define SRG_PLAN_COMPACT 0x1u        /* copy the entries in launch order whatever the run length */
 #define SRG_PLAN_SPANS 0x2u          /* never copy: spans of the caller's arrays */
 #define SRG_PLAN_SPLIT_BLOCK0 0x4u   /* block 0 as two launches (default: panels < 16 GiB) */
 #define SRG_PLAN_WHOLE_BLOCK0 0x8u   /* block 0 as one launch */
+#define SRG_PLAN_AUTO (-1)
+#define SRG_PLAN_NONE (-2)
 typedef struct {
     int64_t n_rows, nnz;
     int64_t device_bytes;            /* device memory the plan holds */
@@ -216,7 +222,8 @@ typedef struct {
     int32_t device;
 } srg_plan_desc;
 int srg_plan_build(const int64_t* indptr, const int32_t* indices, const float* values, int64_t n_rows,
-                   int32_t d, int32_t hops, int32_t col_blocks, uint32_t opts, void* stream, srg_plan** plan);
+                   int32_t d, int32_t hops, int32_t col_blocks, int64_t hub_threshold, int64_t heavy_threshold,
+                   uint32_t opts, void* stream, srg_plan** plan);
 /* Releases the plan's device memory after the work enqueued on `stream` (it synchronises `stream`):
  * every hop that uses the plan must be ordered before that point (enqueued on it, or joined into it).
  * A plan is used by one host thread at a time (a propagate over a width other than 64 / 128 / 256

@@ -118,6 +118,7 @@ struct LaunchTable {
     int lbits;                                 // launch id bits above the length bits
     int lenbits;
     int whole_rule;                            // 1: the one-launch hop's heavy threshold (nnz / 100000)
+    int64_t hub_t, heavy_t;                    // row lengths, or SRG_PLAN_AUTO / SRG_PLAN_NONE
     int64_t off[kMaxLaunch + 1];               // item offsets of the launches
     int64_t rows_lim[kMaxLaunch];              // compact: items of launch L below off[L] + rows_lim[L] get row-indexed spans
 };
@@ -269,13 +270,17 @@ __global__ void k_plan_counts(const uint64_t* __restrict__ keys, const int32_t* 
         }
         return lo;
     };
-    const int64_t hub_t = max<int64_t>(2048, nnz / 1024);
-    const int64_t heavy_t = max<int64_t>(96, nnz / (T.whole_rule ? 100000 : kBlockHeavyPer));
-    const int64_t n_hub = above(hub_t);
+    // automatic thresholds from the launch's nnz; a caller's thresholds hold for every launch (the
+    // narrow panels' slice waves then follow the heavy threshold too: DeviceCSR.heavy)
+    const int64_t hub_t = T.hub_t == SRG_PLAN_AUTO ? max<int64_t>(2048, nnz / 1024) : T.hub_t;
+    const int64_t heavy_t = T.heavy_t == SRG_PLAN_AUTO ? max<int64_t>(96, nnz / (T.whole_rule ? 100000 : kBlockHeavyPer))
+                                                       : T.heavy_t;
+    const int64_t n_hub = T.hub_t == SRG_PLAN_NONE ? 0 : above(hub_t);
+    const int64_t n_heavy = max<int64_t>(0, (T.heavy_t == SRG_PLAN_NONE ? 0 : above(heavy_t)) - n_hub);
     counts[4 * L + 0] = nnz;
     counts[4 * L + 1] = n_hub;
-    counts[4 * L + 2] = max<int64_t>(0, above(heavy_t) - n_hub);
-    counts[4 * L + 3] = max<int64_t>(0, above(kNarrowHeavy) - n_hub);
+    counts[4 * L + 2] = n_heavy;
+    counts[4 * L + 3] = T.heavy_t == SRG_PLAN_AUTO ? max<int64_t>(0, above(kNarrowHeavy) - n_hub) : n_heavy;
     for (int64_t j = 0; j < min<int64_t>(n_hub, kHubPrefix); ++j) hubs[(int64_t)L * kHubPrefix + j] = vals[o + j];
 }
 
@@ -478,7 +483,8 @@ bool packed_width(int d) { return d == 64 || d == 128 || d == 256; }
 extern "C" {
 
 int srg_plan_build(const int64_t* indptr, const int32_t* indices, const float* values, int64_t n_rows, int32_t d,
-                   int32_t hops, int32_t col_blocks, uint32_t opts, void* stream, srg_plan** plan)
+                   int32_t hops, int32_t col_blocks, int64_t hub_threshold, int64_t heavy_threshold, uint32_t opts,
+                   void* stream, srg_plan** plan)
 {
     if (!plan) return pfail(SRG_ERR_INVALID, "null plan");
     *plan = nullptr;
@@ -486,6 +492,9 @@ int srg_plan_build(const int64_t* indptr, const int32_t* indices, const float* v
     if (n_rows < 0 || n_rows >= (1ll << 31)) return pfail(SRG_ERR_INVALID, "n_rows=%lld outside [0, 2^31)", (long long)n_rows);
     if (d <= 0 || hops < 0 || col_blocks < 0 || col_blocks > kMaxBlocks)
         return pfail(SRG_ERR_INVALID, "d=%d, hops=%d, col_blocks=%d (0 = automatic, at most %d)", d, hops, col_blocks, kMaxBlocks);
+    if (hub_threshold < SRG_PLAN_NONE || heavy_threshold < SRG_PLAN_NONE)
+        return pfail(SRG_ERR_INVALID, "hub_threshold=%lld, heavy_threshold=%lld: a row length, SRG_PLAN_AUTO or SRG_PLAN_NONE",
+                     (long long)hub_threshold, (long long)heavy_threshold);
     const uint32_t known = SRG_PLAN_COMPACT | SRG_PLAN_SPANS | SRG_PLAN_SPLIT_BLOCK0 | SRG_PLAN_WHOLE_BLOCK0;
     if ((opts & ~known) || ((opts & SRG_PLAN_COMPACT) && (opts & SRG_PLAN_SPANS)) ||
         ((opts & SRG_PLAN_SPLIT_BLOCK0) && (opts & SRG_PLAN_WHOLE_BLOCK0)))
@@ -555,6 +564,8 @@ int srg_plan_build(const int64_t* indptr, const int32_t* indices, const float* v
     LaunchTable T{};
     T.n_launch = (int)sets.size();
     T.whole_rule = B == 1 ? 1 : 0;
+    T.hub_t = hub_threshold;
+    T.heavy_t = heavy_threshold;
     T.lenbits = bits_for((uint64_t)max_deg);
     T.lbits = bits_for((uint64_t)std::max(0, T.n_launch - 1));
     T.off[0] = 0;

@@ -2135,7 +2135,7 @@ int srg_propagate_khop_f32(const int64_t* indptr, const int32_t* indices, const 
         !(f & ~(SRG_SPMM_NT_STORE | SRG_SPMM_FAST))) {
         // no schedule: the hops run through a plan made for them (srg_plan.hip), freed after them
         srg_plan* P = nullptr;
-        rc = srg_plan_build(indptr, indices, values, n_rows, d, K, 0, 0, stream, &P);
+        rc = srg_plan_build(indptr, indices, values, n_rows, d, K, 0, SRG_PLAN_AUTO, SRG_PLAN_AUTO, 0, stream, &P);
         if (rc) return rc;
         rc = srg_plan_propagate_f32(P, panels, ld, d, K, f, stream);
         const int rc2 = srg_plan_destroy(P, stream);

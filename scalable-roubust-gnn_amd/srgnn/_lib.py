@@ -47,6 +47,8 @@ SRG_PLAN_COMPACT = 0x1
 SRG_PLAN_SPANS = 0x2
 SRG_PLAN_SPLIT_BLOCK0 = 0x4
 SRG_PLAN_WHOLE_BLOCK0 = 0x8
+SRG_PLAN_AUTO = -1
+SRG_PLAN_NONE = -2
 
 SRG_HALO_AUTO = -1
 SRG_HALO_NONE = -2
@@ -143,7 +145,7 @@ def _declare(lib):
     lib.srg_propagate_khop_f32.restype = ctypes.c_int
     lib.srg_propagate_plan_f32.argtypes = [_p, _i32, _i32, _p, _i64, _i32, _i32, _p]
     lib.srg_propagate_plan_f32.restype = ctypes.c_int
-    lib.srg_plan_build.argtypes = [_p, _p, _p, _i64, _i32, _i32, _i32, _u32, _p, ctypes.POINTER(_p)]
+    lib.srg_plan_build.argtypes = [_p, _p, _p, _i64, _i32, _i32, _i32, _i64, _i64, _u32, _p, ctypes.POINTER(_p)]
     lib.srg_plan_destroy.argtypes = [_p, _p]
     lib.srg_plan_describe.argtypes = [_p, _p]
     lib.srg_plan_launch.argtypes = [_p, _i32, _i32, _p, _p, _p]

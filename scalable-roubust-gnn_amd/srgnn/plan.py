@@ -53,9 +53,12 @@ class NativePlan:
         self._p = None
         p = ctypes.c_void_p()
         n = A.n_rows
+        # A's thresholds (None: automatic per launch; negative: no such rows), for every launch
+        hub_t, heavy_t = (_lib.SRG_PLAN_AUTO if t is None else _lib.SRG_PLAN_NONE if int(t) < 0 else int(t)
+                          for t in (A.thresholds[1], A.thresholds[0]))
         _lib.call(self.device, "srg_plan_build", A.indptr.data_ptr(), A.indices.data_ptr() if A.indices.numel() else None,
-                  A.values.data_ptr() if A.values.numel() else None, n, int(d), int(hops), int(col_blocks), opts,
-                  _lib.stream(self.device), ctypes.byref(p))
+                  A.values.data_ptr() if A.values.numel() else None, n, int(d), int(hops), int(col_blocks), hub_t,
+                  heavy_t, opts, _lib.stream(self.device), ctypes.byref(p))
         self._p = p.value
         self.hops = int(hops)
         self.forced = int(col_blocks) != 0

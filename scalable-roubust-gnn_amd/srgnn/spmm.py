@@ -67,16 +67,16 @@ _COMPACT = True                   # False: spans only (A/B of the round-2 / 3 la
 
 
 # K-hop runs (prepare / propagate) lay the operator out with the native planner (srgnn.plan,
-# csrc/srg_plan.hip: one device pass) when every layout constant here and in srgnn.csr has its default
-# value and the operator's thresholds are automatic; otherwise (layout experiments, forced thresholds)
-# with the torch formulation below.  Both give the same layout.
+# csrc/srg_plan.hip: one device pass, the operator's thresholds passed on) when every layout constant
+# here and in srgnn.csr has its default value; otherwise (layout experiments) with the torch
+# formulation below.  Both give the same layout.
 NATIVE_PLAN = True
 
 
 def _native_ok(A: DeviceCSR) -> bool:
     from . import csr as C
     return (NATIVE_PLAN and _COMPACT and _HUB_CHAIN and _SLOT_SPANS and _U2_BLOCKED and not A.is_span
-            and A.n_rows == A.n_cols and A.thresholds == (None, None) and C.BLOCK_WHOLE_MAX == 48
+            and A.n_rows == A.n_cols and C.BLOCK_WHOLE_MAX == 48
             and C.BLOCK_HEAVY_PER == 30000 and C.NARROW_HEAVY_THRESHOLD == 32 and C.DEFAULT_HEAVY_THRESHOLD is None
             and C.DEFAULT_HUB_THRESHOLD is None and SPLIT_BLOCK0_MAX_PANEL == 16 << 30
             and CAP_WAVES_MIN_PANEL == 512 << 20 and MIN_HOPS_TO_CUT == 4
@@ -286,12 +286,17 @@ def _plan_array(plan, d):
     return arr
 
 
+HUB_CHAIN_MAX = 256     # = kHubPrefix (csrc/srg_plan.hip)
+
+
 def _same_hub_rows(A: DeviceCSR, B: int, blocks, agg: bool = False) -> bool:
     """Whether every column block schedules the same set of hub rows (cached per B on A)."""
     key = ("same_hubs", B, agg)
     if key not in A._blocks:
         sets = [torch.sort(b.order[: b.n_hub].to(torch.int64)).values for b in blocks]
-        A._blocks[key] = all(s.numel() == sets[0].numel() and bool(torch.equal(s, sets[0])) for s in sets)
+        # more than HUB_CHAIN_MAX hub rows in a launch: no chain (the native planner compares that many)
+        A._blocks[key] = all(s.numel() <= HUB_CHAIN_MAX for s in sets) and \
+            all(s.numel() == sets[0].numel() and bool(torch.equal(s, sets[0])) for s in sets)
     return A._blocks[key]
 
 

@@ -106,15 +106,19 @@ def test_planner_rejects_bad_arguments_before_the_device():
     L = _lib.lib()
     out = ctypes.c_void_p()
     ip = (ctypes.c_int64 * 3)(0, 1, 2)
+    A, N = _lib.SRG_PLAN_AUTO, _lib.SRG_PLAN_NONE
     cases = [
-        ((ip, None, None, 2, 8, 4, 0, 0, None, None), "null plan"),
-        ((None, None, None, 2, 8, 4, 0, 0, None, ctypes.byref(out)), "indptr"),
-        ((ip, None, None, -1, 8, 4, 0, 0, None, ctypes.byref(out)), "n_rows"),
-        ((ip, None, None, 2, 0, 4, 0, 0, None, ctypes.byref(out)), "d=0"),
-        ((ip, None, None, 2, 8, -1, 0, 0, None, ctypes.byref(out)), "hops=-1"),
-        ((ip, None, None, 2, 8, 4, 65, 0, None, ctypes.byref(out)), "col_blocks=65"),
-        ((ip, None, None, 2, 8, 4, 0, _lib.SRG_PLAN_COMPACT | _lib.SRG_PLAN_SPANS, None, ctypes.byref(out)), "opts"),
-        ((ip, None, None, 2, 8, 4, 0, 0x100, None, ctypes.byref(out)), "opts"),
+        ((ip, None, None, 2, 8, 4, 0, A, A, 0, None, None), "null plan"),
+        ((None, None, None, 2, 8, 4, 0, A, A, 0, None, ctypes.byref(out)), "indptr"),
+        ((ip, None, None, -1, 8, 4, 0, A, A, 0, None, ctypes.byref(out)), "n_rows"),
+        ((ip, None, None, 2, 0, 4, 0, A, A, 0, None, ctypes.byref(out)), "d=0"),
+        ((ip, None, None, 2, 8, -1, 0, A, A, 0, None, ctypes.byref(out)), "hops=-1"),
+        ((ip, None, None, 2, 8, 4, 65, A, A, 0, None, ctypes.byref(out)), "col_blocks=65"),
+        ((ip, None, None, 2, 8, 4, 0, N - 1, A, 0, None, ctypes.byref(out)), "hub_threshold=-3"),
+        ((ip, None, None, 2, 8, 4, 0, A, -7, 0, None, ctypes.byref(out)), "heavy_threshold=-7"),
+        ((ip, None, None, 2, 8, 4, 0, A, A, _lib.SRG_PLAN_COMPACT | _lib.SRG_PLAN_SPANS, None, ctypes.byref(out)),
+         "opts"),
+        ((ip, None, None, 2, 8, 4, 0, A, A, 0x100, None, ctypes.byref(out)), "opts"),
     ]
     for args, msg in cases:
         assert L.srg_plan_build(*args) == _lib.SRG_ERR_INVALID, msg
@@ -122,6 +126,7 @@ def test_planner_rejects_bad_arguments_before_the_device():
     assert L.srg_plan_describe(None, None) == _lib.SRG_ERR_INVALID
     assert L.srg_plan_propagate_f32(None, None, 8, 8, 1, 0, None) == _lib.SRG_ERR_INVALID
     assert L.srg_plan_launch(None, 0, 8, None, None, None) == _lib.SRG_ERR_INVALID
+    assert L.srg_plan_hop_f32(None, None, 8, None, 8, 8, 0, None, 0, 0.0, 0, None) == _lib.SRG_ERR_INVALID
     assert L.srg_plan_destroy(None, None) == 0
 
 

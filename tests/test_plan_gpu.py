@@ -142,6 +142,28 @@ def test_native_layout_matches_torch_formulation(monkeypatch, B, compact, split,
     P.close()
 
 
+@pytest.mark.parametrize("thresholds", [(40, 400), (-1, 3000), (200, -1), (0, 0)])
+@pytest.mark.parametrize("B,compact,split", [(1, False, None), (1, True, None), (3, True, True), (3, False, False)])
+def test_native_layout_with_explicit_thresholds(monkeypatch, B, compact, split, thresholds):
+    """An operator built with its own heavy / hub thresholds (negative: no such rows): the native plan
+    schedules every launch with them, as the torch formulation's blocks do; the hops bit for bit."""
+    from srgnn.csr import DeviceCSR
+    from srgnn.plan import NativePlan
+    from srgnn.spmm import spmm
+    ip, ix, v, n = _power_law(seed=21, unsorted_rows=2)
+    heavy_t, hub_t = thresholds
+    A = DeviceCSR.from_tensors(ip, ix, v, n_cols=n, heavy_threshold=heavy_t, hub_threshold=hub_t, device="cuda")
+    for d in (16, 64):
+        P = NativePlan(A, d, hops=3, col_blocks=B, compact=compact, split_block0=split)
+        X = torch.randn(n, d, device="cuda")
+        panels = [X] + [torch.empty_like(X) for _ in range(2)]
+        P.propagate(panels, d, d, 2)
+        assert torch.equal(panels[2].view(torch.int32), spmm(A, spmm(A, X)).view(torch.int32))
+        py, join = _python_layout(A, d, B, compact, split, monkeypatch)
+        _check_layout(A, P, d, py, join)
+        P.close()
+
+
 @pytest.mark.parametrize("d_run", [8, 36, 64, 256])
 def test_compact_plan_other_widths(d_run):
     """A compact plan built for 128 columns keeps row-indexed spans for its hub and slice-wave rows
