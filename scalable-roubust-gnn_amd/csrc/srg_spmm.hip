@@ -778,7 +778,8 @@ struct HubGeom {
     static constexpr int TILE = kSliceCols * LD;             // floats per tile
     static constexpr size_t LDS_BYTES = (size_t)(2 * TILE + 2 * W) * sizeof(float);
 };
-constexpr int kHubWideLaunch = 256;   // more hub workgroups than this (the CU count) -> W = 256
+constexpr int kHubWideLaunch = 256;   // more hub workgroups than this (the CU count) -> W = kHubWideW
+constexpr int kHubWideW = 256;
 __device__ __forceinline__ int hub_swz(int c) { return (c >> 2) & 7; }
 // Full windows take their link values by DPP quad broadcast (hub_links16; the value-read-per-4-links
 // loop it replaced in round 3 was removed in round 5)
@@ -1517,10 +1518,10 @@ int hub_attrs()
                            (const void*)k_spmm_hub<true, IP, kEpiCheby>, (const void*)k_spmm_hub<false, IP, kEpiCheby>,
                            (const void*)k_spmm_hub<true, IP, kEpiSpan>, (const void*)k_spmm_hub<false, IP, kEpiSpan>})
         SRG_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kHubLdsBytes));
-    for (const void* fn : {(const void*)k_spmm_hub<true, IP, kEpiPlain, 256>, (const void*)k_spmm_hub<false, IP, kEpiPlain, 256>,
-                           (const void*)k_spmm_hub<true, IP, kEpiCheby, 256>, (const void*)k_spmm_hub<false, IP, kEpiCheby, 256>,
-                           (const void*)k_spmm_hub<true, IP, kEpiSpan, 256>, (const void*)k_spmm_hub<false, IP, kEpiSpan, 256>})
-        SRG_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)HubGeom<256>::LDS_BYTES));
+    for (const void* fn : {(const void*)k_spmm_hub<true, IP, kEpiPlain, kHubWideW>, (const void*)k_spmm_hub<false, IP, kEpiPlain, kHubWideW>,
+                           (const void*)k_spmm_hub<true, IP, kEpiCheby, kHubWideW>, (const void*)k_spmm_hub<false, IP, kEpiCheby, kHubWideW>,
+                           (const void*)k_spmm_hub<true, IP, kEpiSpan, kHubWideW>, (const void*)k_spmm_hub<false, IP, kEpiSpan, kHubWideW>})
+        SRG_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)HubGeom<kHubWideW>::LDS_BYTES));
     return SRG_OK;
 }
 
@@ -1724,10 +1725,10 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
     hipLaunchKernelGGL((k_spmm_hub<SF, IP, EX, WW>), hgrid, dim3(kHubThreads), (HubGeom<WW>::LDS_BYTES), ss->stream, \
                        indptr, indices, vals, order, n_slices, X, ldx, Y, ldy, d, acc, nt, epi)
         if (sfull) {
-            if (w256) SRG_LAUNCH_HUB(true, 256);
+            if (w256) SRG_LAUNCH_HUB(true, kHubWideW);
             else SRG_LAUNCH_HUB(true, 512);
         } else {
-            if (w256) SRG_LAUNCH_HUB(false, 256);
+            if (w256) SRG_LAUNCH_HUB(false, kHubWideW);
             else SRG_LAUNCH_HUB(false, 512);
         }
 #undef SRG_LAUNCH_HUB
