@@ -31,6 +31,9 @@ def main():
     ap.add_argument("--worlds", default="2,4,8")
     ap.add_argument("--chunks", type=int, default=4)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=20,
+                    help="untimed op.compute calls before the timed ones (--quick): the GPU's clocks ramp up "
+                         "after the host-side plan build left it idle")
     ap.add_argument("--d", type=int, default=None, help="feature width (default: the config's)")
     ap.add_argument("--fast", action="store_true", help="the hub group in tolerance mode (SRG_SPMM_FAST)")
     ap.add_argument("--hub-threshold", default="auto",
@@ -70,7 +73,7 @@ def main():
             times = {}
             G = op.n_groups            # op._A[G] is the ghost rows' launch (into dst's halo)
             if a.quick:
-                for _ in range(2):
+                for _ in range(a.warmup):
                     op.compute(src, dst)
                 ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * a.reps)]
                 for r in range(a.reps):
