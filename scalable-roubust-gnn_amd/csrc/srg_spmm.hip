@@ -262,15 +262,13 @@ constexpr int kSliceCols = 32;
 // Two (the round-1 layout) cost 8 KB per k_spmm block, which beside the hub group's 72 KB workgroups
 // (halo exchange) left room for only two row blocks per CU.
 constexpr int kSliceLdsBufs = 1;
-// The row waves' (column id, value) loads for the next group of entries are issued right after the
+// The slice waves' (column id, value) loads for the next group of entries are issued right after the
 // current group's gathers, so their latency overlaps the gathers and the fma links instead of
-// preceding the next gathers.  SRG_PREFETCH_IDS bit 0: packed_rows, bit 1: slice_wave.  Products
-// (one box, profiles/r04u_prefetch_ab.txt): none 6.02 ms per hop, slice waves 5.82, packed rows 6.06,
-// both 6.01 -- the packed rows' prefetch, like their LDS-staged ids, raises the traffic (+2.3 GB per
-// hop).  The slice waves' prefetch costs 2 UH registers (73 instead of 54-70: 6 waves per SIMD).
-// Same entries in the same order: same bits.  The packed rows' variant (and the LDS-staged entries
-// of round 4, profiles/r04h_stage_entries_negative.txt) measured slower and were removed in round 5.
-constexpr bool kPrefetchIds = false;
+// preceding the next gathers.  Products (one box, profiles/r04u_prefetch_ab.txt): none 6.02 ms per
+// hop, slice waves 5.82.  It costs 2 UH registers (73 instead of 54-70: 6 waves per SIMD).  Same
+// entries in the same order: same bits.  (The packed light rows stage their ids across their lanes
+// instead, packed_rows; their round-4 per-group prefetch and LDS-staged entries measured slower,
+// profiles/r04h_stage_entries_negative.txt.)
 constexpr bool kPrefetchSliceIds = true;
 
 // Epilogues of the SpMM kernels (every output element y a kernel stores may also go to):
@@ -556,9 +554,9 @@ __device__ __forceinline__ void narrow_rows(const IP* __restrict__ indptr, const
 // lanes of a row read 16*S contiguous bytes per gather).  A one-row wave walks its row's short
 // stream through a chain of dependent loads (schedule slot -> row pointers -> column ids -> X) and
 // the phase is bound by how many rows are in flight, not by bytes; LR rows per wave multiply that.
-// Each lane loads its own row's (column id, value) entries (the S lanes of a row share the address),
-// then U gathers per row in flight, then the fma links in CSR order.  Entries past a row's end are
-// skipped (never folded in as 0*x).  Still one sequential fma chain per output element.
+// The S lanes of a row load S consecutive (column id, value) entries of it at once and hand them
+// out by ds_bpermute, U gathers per row in flight, then the fma links in CSR order.  Entries past a
+// row's end are skipped (never folded in as 0*x).  Still one sequential fma chain per output element.
 template <int LR, int LQ, int U, typename IP, int EX>
 __device__ __forceinline__ void packed_rows(const IP* __restrict__ indptr, const int32_t* __restrict__ indices,
                                             const float* __restrict__ vals, const int32_t* __restrict__ order,
@@ -568,6 +566,7 @@ __device__ __forceinline__ void packed_rows(const IP* __restrict__ indptr, const
 {
     typedef typename Vec<float, 4>::type V4;
     constexpr int S = 64 / LR;
+    static_assert(S % U == 0, "a row's id chunk holds whole groups of U entries");
     const int lane = threadIdx.x & 63;
     const int g = lane / S, l = lane % S;
     const int slot = first + g;
@@ -610,45 +609,48 @@ __device__ __forceinline__ void packed_rows(const IP* __restrict__ indptr, const
         if constexpr (EX == kEpiCheby)
             if (rv) cheby_load<4>(epi, row, col, X, ldx, cop[q]);
     }
-    int cv[U];
-    float av[U];
-    auto load_ids = [&](int j0, int* c, float* a) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const bool ok = j0 + u < len;
-            const int64_t p = beg + (ok ? j0 + u : 0);
-            c[u] = ok ? indices[p] : 0;
-            a[u] = ok ? vals[p] : 0.0f;
-        }
+    // The row's entries S at a time: lane l of the row loads the (column id, value) of entry j0 + l, and
+    // each group of U gathers takes its ids from the row's S lanes by ds_bpermute, so the dependent
+    // chain per U entries is the gather alone (one id load per S entries instead of one per U); the
+    // next S entries' ids load behind the current chunk's gathers.  Products 5.52 -> 5.33 ms per hop,
+    // arxiv 0.157 -> 0.154 (round 5, profiles/r05ab_shfl_ids_ab.txt; before, every U entries began
+    // with their id loads).  Entries past a row's end load nothing and are skipped.
+    const int base = g * S;
+    auto load_ids = [&](int j0, int& c, float& a) {
+        const bool ok = j0 + l < len;
+        const int64_t p = beg + (ok ? j0 + l : 0);
+        c = ok ? indices[p] : 0;
+        a = ok ? vals[p] : 0.0f;
     };
-    if (kPrefetchIds && maxlen > 0) load_ids(0, cv, av);
-    for (int j = 0; j < maxlen; j += U) {
-        if constexpr (!kPrefetchIds) load_ids(j, cv, av);
-        __builtin_amdgcn_sched_barrier(0);   // every id load ahead of the first gather
-        V4 x[U][LQ];
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-#pragma unroll
-            for (int q = 0; q < LQ; ++q)
-                x[u][q] = (j + u < len) ? gload<float, 4>(X + (int64_t)cv[u] * ldx + q * 4 * S + 4 * l)
-                                        : vzero<float, 4>();
-        [[maybe_unused]] int ncv[U];
-        [[maybe_unused]] float nav[U];
-        if constexpr (kPrefetchIds) {        // the next entries' ids behind the gathers
-            if (j + U < maxlen) load_ids(j + U, ncv, nav);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (j + u < len)
-#pragma unroll
-                for (int q = 0; q < LQ; ++q) chain<float, 4>(acc[q], av[u], x[u][q]);
-        if constexpr (kPrefetchIds) {
+    int nid = 0;
+    float nva = 0.0f;
+    if (maxlen > 0) load_ids(0, nid, nva);
+    for (int j0 = 0; j0 < maxlen; j0 += S) {
+        const int cid = nid;
+        const float cva = nva;
+        if (j0 + S < maxlen) load_ids(j0 + S, nid, nva);
+        const int nstep = (maxlen - j0) < S ? (maxlen - j0) : S;   // wave-uniform; S is a multiple of U
+        for (int jj = 0; jj < nstep; jj += U) {
+            int cv[U];
+            float av[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                cv[u] = ncv[u];
-                av[u] = nav[u];
+                cv[u] = __shfl(cid, base + jj + u);
+                av[u] = __shfl(cva, base + jj + u);
             }
+            const int j = j0 + jj;
+            V4 x[U][LQ];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int q = 0; q < LQ; ++q)
+                    x[u][q] = (j + u < len) ? gload<float, 4>(X + (int64_t)cv[u] * ldx + q * 4 * S + 4 * l)
+                                            : vzero<float, 4>();
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (j + u < len)
+#pragma unroll
+                    for (int q = 0; q < LQ; ++q) chain<float, 4>(acc[q], av[u], x[u][q]);
         }
     }
     if (!rv) return;
