@@ -622,6 +622,53 @@ __device__ __forceinline__ void packed_rows(const IP* __restrict__ indptr, const
         c = ok ? indices[p] : 0;
         a = ok ? vals[p] : 0.0f;
     };
+    if constexpr (U <= 2) {
+    // U = 2 (the column blocks' launches): two chunks of ids (A: entries [ca, ca + S), B: the next S)
+    // and two gather buffers, so step j + U's gathers are issued before step j's fma links -- 2U
+    // gathers in flight across the steps.  Products 5.33 -> 5.27 ms per hop; with U = 4 (the one-launch
+    // hop) the same pipeline costs arxiv 6 % (0.154 -> 0.163 ms: 8 gathers in flight per row, like
+    // U = 8), so that keeps one U-group in flight (profiles/r05af_pipe_gathers_ab.txt)
+    int ida = 0, idb = 0;
+    float vaa = 0.0f, vab = 0.0f;
+    int ca = 0;
+    if (maxlen > 0) load_ids(0, ida, vaa);
+    if (S < maxlen) load_ids(S, idb, vab);
+    auto issue = [&](int j, V4 (&x)[U][LQ], float (&av)[U]) {
+        const bool in_a = j < ca + S;            // wave-uniform
+        const int off = base + (j & (S - 1));
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int c = __shfl(in_a ? ida : idb, off + u);
+            av[u] = __shfl(in_a ? vaa : vab, off + u);
+#pragma unroll
+            for (int q = 0; q < LQ; ++q)
+                x[u][q] = (j + u < len) ? gload<float, 4>(X + (int64_t)c * ldx + q * 4 * S + 4 * l) : vzero<float, 4>();
+        }
+    };
+    auto links = [&](int j, const V4 (&x)[U][LQ], const float (&av)[U]) {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (j + u < len)
+#pragma unroll
+                for (int q = 0; q < LQ; ++q) chain<float, 4>(acc[q], av[u], x[u][q]);
+        if (j + U == ca + S) {                   // chunk A done: B becomes A, B loads the next S
+            ida = idb;
+            vaa = vab;
+            ca += S;
+            if (ca + S < maxlen) load_ids(ca + S, idb, vab);
+        }
+    };
+    V4 xa[U][LQ], xb[U][LQ];
+    float fa[U], fb[U];
+    if (maxlen > 0) issue(0, xa, fa);
+    for (int j = 0; j < maxlen; j += 2 * U) {
+        if (j + U < maxlen) issue(j + U, xb, fb);
+        links(j, xa, fa);
+        if (j + U >= maxlen) break;
+        if (j + 2 * U < maxlen) issue(j + 2 * U, xa, fa);
+        links(j + U, xb, fb);
+    }
+    } else {
     int nid = 0;
     float nva = 0.0f;
     if (maxlen > 0) load_ids(0, nid, nva);
@@ -652,6 +699,7 @@ __device__ __forceinline__ void packed_rows(const IP* __restrict__ indptr, const
 #pragma unroll
                     for (int q = 0; q < LQ; ++q) chain<float, 4>(acc[q], av[u], x[u][q]);
         }
+    }
     }
     if (!rv) return;
 #pragma unroll
