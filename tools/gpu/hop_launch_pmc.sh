@@ -14,4 +14,4 @@ for C in FETCH_SIZE WRITE_SIZE; do
   rm -rf $O/hl_$C
 done
 timeout -s KILL 300 rocprofv3 --kernel-trace -d $O/hl_tr -o t --output-format csv -- python3 $R/tools/spmm_probe.py --reps 5 "$@" > /dev/null 2> $O/hl_tr.err || exit 1
-python3 $R/tools/trace_timeline.py $O/hl_tr --last 40 > $O/hop_launch_trace.txt && rm -rf $O/hl_tr
+python3 $R/tools/trace_timeline.py $O/hl_tr --last 40 --only spmm,hub,delay > $O/hop_launch_trace.txt && rm -rf $O/hl_tr
