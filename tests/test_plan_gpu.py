@@ -444,3 +444,34 @@ def test_aggregation_loop_runs_the_native_plan(monkeypatch):
         assert (cached(A, d) is not None) == native
     assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
     assert len(calls) == K and any(c is not None for c in calls)
+
+
+@pytest.mark.parametrize("d", [64, 128, 256])
+@pytest.mark.parametrize("B,compact", [(1, True), (1, False), (3, True), (4, False)])
+def test_packed_row_id_chunks_at_every_length(oracle_mod, d, B, compact):
+    """The packed light rows take their (id, value) entries S at a time (S = 8 / 16 / 32 lanes per row at
+    d = 64 / 128 / 256) and, in column blocks, pipeline their gathers one step ahead:
+    rows of every length 0..3S+1 (chunk and step boundaries on both sides), in waves that mix lengths,
+    plus a few long rows, against the CPU oracle bit for bit -- one launch (U = 4) and column blocks
+    (U = 2), spans and compact copies."""
+    from srgnn.plan import NativePlan
+    rng = np.random.default_rng(d + 7 * B)
+    n = 3000
+    S = {64: 8, 128: 16, 256: 32}[d]
+    lens = np.concatenate([np.arange(0, 3 * S + 2), rng.integers(0, 3 * S + 2, n - 3 * S - 2 - 6),
+                           [400, 700, 1200, 1600, 2500, 2999]])[:n]
+    rng.shuffle(lens)
+    ip = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    ix = np.concatenate([np.sort(rng.choice(n, k, replace=False)) if k else np.zeros(0, np.int64)
+                         for k in lens]).astype(np.int32)
+    v = (rng.standard_normal(ix.size) * 0.5).astype(np.float32)
+    A = _csr(ip, ix, v, n)
+    x = rng.standard_normal((n, d)).astype(np.float32)
+    X = torch.from_numpy(x).cuda()
+    P = NativePlan(A, d, hops=8, col_blocks=B, compact=compact, split_block0=True if B > 1 else None)
+    panels = [X, torch.full_like(X, float("nan")), torch.full_like(X, float("nan"))]
+    P.propagate(panels, d, d, 2)
+    torch.cuda.synchronize()
+    h1 = oracle_mod.spmm(ip, ix, v, x)
+    np.testing.assert_array_equal(panels[1].cpu().numpy(), h1)
+    np.testing.assert_array_equal(panels[2].cpu().numpy(), oracle_mod.spmm(ip, ix, v, h1))
