@@ -619,8 +619,25 @@ def run_wavelet(a, dev, world=1, rank=0, pmc=None):
     # gather more bytes per nonzero (RMAT-26: 64 columns 1.37 s per step, 32 columns 1.87 s)
     while not a.col_block and cb > 8 and n_work * n * cb * 4 > free - 2 ** 30:
         cb //= 2
-    filt.prepare_column_blocks(cb, hops=order * (d // cb) * (a.steps + a.warmup))
-    log(f"wavelet {a.config}: n={n} nnz(L)={nnz} d={d} lmax={lmax} col_block={cb} "
+    layout = "native plan"
+    while True:
+        # the layout of L and F for cb-column panels: the native plans hold device memory of their own,
+        # so where the work panels no longer fit beside them, the torch formulation of the same blocks
+        # (its arrays in torch's cache, which the graph build left fragmented), then narrower blocks
+        native = layout == "native plan"
+        filt.prepare_column_blocks(cb, hops=order * (d // cb) * (a.steps + a.warmup), native=native)
+        torch.cuda.synchronize()
+        free, _ = torch.cuda.mem_get_info(dev)
+        if a.col_block or cb <= 8 or n_work * n * cb * 4 <= free - 2 ** 30:
+            break
+        filt.drop_layouts()
+        torch.cuda.synchronize()
+        if native:
+            layout = "torch blocks"
+        else:
+            layout = "native plan"
+            cb //= 2
+    log(f"wavelet {a.config}: n={n} nnz(L)={nnz} d={d} lmax={lmax} col_block={cb} layout={layout} "
         f"hub={filt.n_hub} heavy={filt.n_heavy} built in {time.perf_counter() - t_build:.1f}s")
 
     def step():

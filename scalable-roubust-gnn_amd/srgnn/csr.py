@@ -166,8 +166,11 @@ class DeviceCSR:
         return self.out_rows != self.n_rows
 
     def drop_blocks(self) -> None:
-        """Frees the cached column blocks (compact copies hold one more copy of the ids and
-        values)."""
+        """Frees the cached layouts: column blocks (compact copies hold one more copy of the ids and
+        values) and native plans (srgnn.plan; released in stream order)."""
+        for v in list(self._blocks.values()):
+            if hasattr(v, "close"):
+                v.close()
         self._blocks.clear()
 
     def heavy(self, d: int) -> int:

@@ -146,7 +146,8 @@ def col_blocks_of(A: DeviceCSR, d: int) -> int:
     if _native_ok(A):
         from .plan import cached
         P = cached(A, d)
-        return P.col_blocks if P is not None else 1
+        if P is not None:
+            return P.col_blocks
     return auto_col_blocks(A, d)
 
 

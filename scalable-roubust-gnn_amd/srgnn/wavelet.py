@@ -249,14 +249,28 @@ class HeatWaveletFilter:
                                         self.n_hub, self.n_heavy_narrow, thresholds=self.thresholds)
         return cache[id(vals)]
 
-    def prepare_column_blocks(self, width: int, hops: int) -> int:
+    def prepare_column_blocks(self, width: int, hops: int, native: bool = True) -> int:
         """Lay L and F out (spmm.prepare: the native plan, column blocks when `hops` SpMMs over panels
-        `width` columns wide amortise them) for the split path's hops; returns the blocks per SpMM."""
-        from .spmm import prepare
+        `width` columns wide amortise them) for the split path's hops; returns the blocks per SpMM.
+        native=False: the torch formulation of the same blocks (spmm.column_blocks_for), whose arrays
+        come from torch's caching allocator instead of the plan's own device memory -- for panels that
+        fill the GPU (bench.py's RMAT-26 filter bank); the same bits either way."""
+        from .spmm import auto_col_blocks, column_blocks_for, prepare
         B = 1
         for vals in (self.lvals, self.fvals):
-            B = prepare(self._csr(vals), width, hops)
+            A = self._csr(vals)
+            if native:
+                B = prepare(A, width, hops)
+            else:
+                B = auto_col_blocks(A, width, hops=hops)
+                if B > 1 and not column_blocks_for(A, B, hops=hops):
+                    B = 1
         return B
+
+    def drop_layouts(self) -> None:
+        """Frees L's and F's cached layouts (native plans, column blocks)."""
+        for vals in (self.lvals, self.fvals):
+            self._csr(vals).drop_blocks()
 
     def work_panels(self, fused_epilogue: bool = False) -> int:
         """[n, column block] work panels the split path needs: T_1 alone for order 1; T_{k-1} and
