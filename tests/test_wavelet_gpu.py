@@ -178,6 +178,26 @@ def test_split_path_runs_the_native_plan(monkeypatch):
     assert torch.equal(f.apply(S, split=False), f.apply(S, split=True, col_block=64))
 
 
+def test_split_path_torch_blocks_fallback(monkeypatch):
+    """prepare_column_blocks(native=False) (bench.py's fallback when the plans crowd out the work
+    panels): the torch formulation of the same blocks, no native plan, bit for bit the fused kernel;
+    drop_layouts frees every cached layout, plans included."""
+    from srgnn import spmm as S_, wavelet as W
+    from srgnn.plan import cached, plan_for
+    monkeypatch.setattr(S_, "FORCE_COL_BLOCKS", 3)
+    a = graphs()["rmat3000"]
+    L = W.laplacian_from_adj(a)
+    f = W.HeatWaveletFilter(L, [-0.5, 0.5], order=4, lmax=None, dtype=torch.float32, device="cuda")
+    assert f.prepare_column_blocks(64, hops=8, native=False) == 3
+    Fm = f._csr(f.fvals)
+    assert cached(Fm, 64) is None and 3 in Fm._blocks
+    S = torch.from_numpy(np.random.default_rng(6).standard_normal((a.shape[0], 128)).astype(np.float32)).cuda()
+    assert torch.equal(f.apply(S, split=False), f.apply(S, split=True, col_block=64))
+    P = plan_for(Fm, 64, 8)
+    f.drop_layouts()
+    assert not Fm._blocks and P._p is None
+
+
 def test_spmm_cheby_in_place_and_argument_checks():
     """srg_spmm_cheby_f32 directly: a step written over T_{k-1} equals the step into a fresh panel
     and the two-launch form; aliasing and flag misuse are rejected before any launch."""
