@@ -1501,10 +1501,13 @@ int pick_vec(int d, int64_t ldx, int64_t ldy, const void* X, const void* Y, size
     return 1;
 }
 
+// slice-wave groups of 8 entries in flight.  Round 5, with the packed rows' id staging: 4 groups take
+// the products hop from 5.26 to 5.22 ms (8 and 6 measure the same, 2 is 4 % slower, 12 and 16 do not
+// unroll: 9.9 / 11.7 ms); arxiv flat (profiles/r05bf_slice_unroll_ab.txt)
 #ifndef SRG_UNROLL_HEAVY
-#define SRG_UNROLL_HEAVY 8
+#define SRG_UNROLL_HEAVY 4
 #endif
-constexpr int kUnrollHeavy = SRG_UNROLL_HEAVY;   // slice-wave groups of 8 entries in flight
+constexpr int kUnrollHeavy = SRG_UNROLL_HEAVY;
 
 // One wave that sleeps ~`us` microseconds (s_memrealtime ticks at 100 MHz).  Enqueued on the main
 // stream right after the hub workgroups are forked onto the side stream, so they are dispatched
