@@ -1501,13 +1501,16 @@ int pick_vec(int d, int64_t ldx, int64_t ldy, const void* X, const void* Y, size
     return 1;
 }
 
-// slice-wave groups of 8 entries in flight.  Round 5, with the packed rows' id staging: 4 groups take
-// the products hop from 5.26 to 5.22 ms (8 and 6 measure the same, 2 is 4 % slower, 12 and 16 do not
-// unroll: 9.9 / 11.7 ms); arxiv flat (profiles/r05bf_slice_unroll_ab.txt)
+// slice-wave groups of 8 entries in flight.  Round 5, with the packed rows' id staging: for the
+// 128- / 256-column packed launches 4 groups take the products hop from 5.26 to 5.22 ms (8 and 6
+// measure the same, 2 is 4 % slower, 12 and 16 do not unroll: 9.9 / 11.7 ms; arxiv flat), but the
+// RMAT-26 filter bank's 64-column blocks lose 3 % with 4 (1.243 against 1.202 s per step), so the
+// 64-column packed launches and the other row paths keep 8 (profiles/r05bf_slice_unroll_ab.txt)
 #ifndef SRG_UNROLL_HEAVY
-#define SRG_UNROLL_HEAVY 4
+#define SRG_UNROLL_HEAVY 8
 #endif
 constexpr int kUnrollHeavy = SRG_UNROLL_HEAVY;
+constexpr int kUnrollHeavyWide = 4;           // the packed launches with 4 or 2 rows per wave (d = 128 / 256)
 
 // One wave that sleeps ~`us` microseconds (s_memrealtime ticks at 100 MHz).  Enqueued on the main
 // stream right after the hub workgroups are forked onto the side stream, so they are dispatched
@@ -1849,11 +1852,11 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
 #define SRG_LAUNCH_PACKED(LRV, LQV, UV)                                                              \
     do {                                                                                              \
         if (xh)                                                                                       \
-            hipLaunchKernelGGL((k_spmm<1, UV, kUnrollHeavy, false, true, IP, 0, EX, LRV, LQV, true>), grid, dim3(kBlock), \
+            hipLaunchKernelGGL((k_spmm<1, UV, (LRV < 8 ? kUnrollHeavyWide : kUnrollHeavy), false, true, IP, 0, EX, LRV, LQV, true>), grid, dim3(kBlock), \
                                shm, s, indptr, indices, vals, morder, nr, nh, n_slices, nb_heavy_launch, X, ldx, Y, ldy, \
                                d, acc, nt, bb, epi);                                                  \
         else                                                                                          \
-            hipLaunchKernelGGL((k_spmm<1, UV, kUnrollHeavy, false, true, IP, 0, EX, LRV, LQV>), grid, dim3(kBlock), shm, s, \
+            hipLaunchKernelGGL((k_spmm<1, UV, (LRV < 8 ? kUnrollHeavyWide : kUnrollHeavy), false, true, IP, 0, EX, LRV, LQV>), grid, dim3(kBlock), shm, s, \
                                indptr, indices, vals, morder, nr, nh, n_slices, nb_heavy, X, ldx, Y, ldy, \
                                d, acc, nt, bb, epi);                                                  \
     } while (0)
