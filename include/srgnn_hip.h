@@ -186,8 +186,8 @@ int srg_propagate_plan_f32(const srg_hop_launch* launches, int32_t n_launch, int
 
 /* ---- the one-GPU planner (csrc/srg_plan.hip) ------------------------------------------------------
  * The layout of a square operator for a run of `hops` hops over d-column panels, built on the device:
- * column blocks as row spans (col_blocks: 0 = automatic -- 4..8 blocks for panels of >= 512 MiB at
- * d >= 64 and runs of >= 4 hops, else 1), block 0 as its cut rows' spans and its whole rows (rows of
+ * column blocks as row spans (col_blocks: 0 = automatic -- 12..16 blocks, one per ~100 MiB, for panels
+ * of 512 MiB .. 16 GiB at d >= 64 and runs of >= 4 hops, 4 for larger panels, else 1), block 0 as its cut rows' spans and its whole rows (rows of
  * <= 48 entries), per-launch schedules by decreasing span length with their hub / slice-wave counts,
  * the hub spans chained on the side stream, spans by schedule slot and, for runs of at least
  * SRG_PLAN_MIN_HOPS_TO_COMPACT hops when it fits in a quarter of the free memory, compact copies of

@@ -6,7 +6,7 @@
 // The layout:
 //   * column blocks: block b of row r is the span of its entries whose column ids lie in
 //     [ceil(b n / B), ceil((b+1) n / B)) (one binary search per row and boundary); rows of <= 48 entries
-//     run whole in block 0; B from the panel size (4..8 for panels of >= 512 MiB at d >= 64);
+//     run whole in block 0; B from the panel size (12..16 for panels of 512 MiB .. 16 GiB at d >= 64, 4 above);
 //   * launches: block 0 as its cut rows' first spans and its whole rows (panels < 16 GiB), then blocks
 //     1..B-1 with ACCUMULATE -- every output element is the one-launch fma chain, continued;
 //   * schedules: each launch's rows by decreasing span length (stable: ties in row order), the first
@@ -106,6 +106,12 @@ constexpr int kMinHopsToCut = 4;               // spmm.MIN_HOPS_TO_CUT
 constexpr int64_t kSplitBlock0MaxPanel = 16ll << 30;   // spmm.SPLIT_BLOCK0_MAX_PANEL
 constexpr int64_t kCapWavesMinPanel = 512ll << 20;     // spmm.CAP_WAVES_MIN_PANEL
 constexpr int kMaxBlocks = 64;
+// automatic blocks for panels of 512 MiB .. 16 GiB at d >= 64: one per ~100 MiB, 12 to 16 (spmm.auto_col_blocks).
+// Round 5, with the packed rows' id staging and gather pipeline (profiles/r05bn_col_blocks_final_kernels.txt):
+// products d = 64 (0.63 GB) 3.37 / 3.13 / 3.08 ms per hop at 4 / 8 / 12 blocks, d = 128 (1.25 GB)
+// 5.23 / 5.16 / 5.15 / 5.19 / 5.25 at 8 / 10 / 12 / 14 / 16, d = 256 (2.5 GB) 11.73 / 11.18 / 11.00 / 11.20
+// at 8 / 12 / 16 / 20 (round 4: 4..8 blocks, one per ~150 MiB)
+constexpr int64_t kAutoBlocksMin = 12, kAutoBlocksMax = 16;
 constexpr int kMaxLaunch = kMaxBlocks + 1;
 constexpr int kHubPrefix = 256;                // hub rows compared for the chain (more: no chain)
 constexpr int64_t kCopyChunk = 4096;           // entries of the copy per wave task
@@ -536,7 +542,7 @@ int srg_plan_build(const int64_t* indptr, const int32_t* indices, const float* v
     if (B == 0) {
         if (d < 64 || panel < (512ll << 20)) B = 1;
         else if (panel >= kSplitBlock0MaxPanel) B = 4;
-        else B = (int)std::min<int64_t>(8, std::max<int64_t>(4, (int64_t)std::nearbyint((double)panel / (150 << 20))));
+        else B = (int)std::min<int64_t>(kAutoBlocksMax, std::max<int64_t>(kAutoBlocksMin, (int64_t)std::nearbyint((double)panel / (100 << 20))));
         if (hops < kMinHopsToCut) B = 1;
     }
     if (n == 0 || nnz == 0) B = 1;

@@ -20,8 +20,8 @@ _stream = _lib.stream
 # of <= csr.BLOCK_WHOLE_MAX nonzeros are not cut (block 0 computes them whole).  Measured
 # (profiles/r02t-v_*): products d = 128 7.05 (one launch 7.31) -> 6.67 (B = 2) -> 6.30 ms (B = 4),
 # flat over B = 4..6, 6.47 at 8; d = 256 +9 % and papers100M / RMAT-26 +3 / +2 % for B = 4 over 2 / 1;
-# arxiv (X 87 MB, already cache-resident) 0.224 vs 0.163 ms at B = 2.  auto_col_blocks: 4 to 8 blocks
-# for panels of >= 512 MiB at d >= 64 (callers pass col_blocks to force a count; FORCE_COL_BLOCKS
+# arxiv (X 87 MB, already cache-resident) 0.224 vs 0.163 ms at B = 2.  auto_col_blocks: 12 to 16 blocks
+# for panels of 512 MiB .. 16 GiB at d >= 64 (4 to 8 before round 5's packed-row kernels) (callers pass col_blocks to force a count; FORCE_COL_BLOCKS
 # forces one for every automatic choice, a test hook).
 FORCE_COL_BLOCKS = None
 # column blocks' launches keep 2 gathers per packed light row in flight (SRG_SPMM_PACKED_U2) for
@@ -118,8 +118,10 @@ def column_blocks_for(A: DeviceCSR, B: int, hops: int | None = None):
 def auto_col_blocks(A: DeviceCSR, d: int, hops: int | None = None) -> int:
     """Column blocks per hop for a panel of d columns (1 = the one-launch hop), if A's blocks exist
     or `hops` hops will amortise cutting it: for panels of >= 512 MiB at d >= 64, one block per
-    ~150 MiB of panel (a slice well inside the 256 MiB Infinity Cache), 4 to 8; 4 for panels of
-    >= 16 GiB.  Round 4 (slice waves from ~1000-entry spans, rows of <= 48 entries whole): products
+    ~100 MiB of panel, 12 to 16 (round 5, profiles/r05bn_col_blocks_final_kernels.txt: products d = 64
+    3.37 -> 3.08 ms per hop at 4 -> 12 blocks, d = 128 5.23 -> 5.15 at 8 -> 12, d = 256 11.73 -> 11.00
+    at 8 -> 16); 4 for panels of >= 16 GiB.  Before round 5's packed-row kernels: one per ~150 MiB, 4
+    to 8.  Round 4 (slice waves from ~1000-entry spans, rows of <= 48 entries whole): products
     d = 128 5.63 ms at B = 6, 5.60-5.61 at 7 and 8; with 48-entry whole rows 5.58 / 5.53 / 5.51-5.52 at
     6 / 7 / 8 (profiles/r04af_*, r04ag_*, r04ah_*).  Round 3, block 0 in two launches, compact blocks in launch order
     (profiles/r03_ab_col_blocks_round3.txt): products d = 128 (1.25 GB) 5.98 ms at B = 6 against
@@ -134,7 +136,8 @@ def auto_col_blocks(A: DeviceCSR, d: int, hops: int | None = None) -> int:
     elif panel >= SPLIT_BLOCK0_MAX_PANEL:
         B = 4
     else:
-        B = min(8, max(4, int(round(panel / (150 << 20)))))
+        # round 5 (= kAutoBlocksMin / Max of srg_plan.hip): one per ~100 MiB, 12 to 16 blocks
+        B = min(16, max(12, int(round(panel / (100 << 20)))))
     if B > 1 and B not in A._blocks and (hops is None or hops < MIN_HOPS_TO_CUT):
         return 1
     return B

@@ -47,7 +47,7 @@ def _check_rows(oracle_mod, rows, sub, ucols, prev, got, what):
 @pytest.mark.timeout(600)
 def test_products_timed_layout_every_hop_bit_exact(oracle_mod):
     """The operator bench.py times on the headline config: products-shaped graph (126 M nonzeros),
-    K = 10, d = 128, default thresholds, eight COMPACT column blocks (>= 6 hops; block 0 in two
+    K = 10, d = 128, default thresholds, twelve COMPACT column blocks (>= 6 hops; block 0 in two
     launches, its cut spans then its whole rows; compact copies in launch order, packed rows reading
     their spans by schedule slot), short rows (<= BLOCK_WHOLE_MAX = 48) whole in block 0, 2 gathers
     per packed row (PACKED_U2) -- EVERY row of every hop (2,449,029 x 128 per hop) checked bit for
@@ -61,13 +61,13 @@ def test_products_timed_layout_every_hop_bit_exact(oracle_mod):
     A = DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, device="cuda")
     hops = K * 25                                   # the driver's 20 steps + 5 warm-up
     B = auto_col_blocks(A, d, hops=hops)
-    assert B == 8
+    assert B == 12
     blocks = column_blocks_for(A, B, hops=hops)
-    assert len(blocks) == 8 and A._blocks.get(("compact", 8)) and blocks[0].whole_rows is not None
+    assert len(blocks) == 12 and A._blocks.get(("compact", 12)) and blocks[0].whole_rows is not None
     assert sum(b.nnz for b in blocks) == A.nnz and A.n_hub >= 1
-    assert spmm_mod.launches_per_hop(A, B, d) == 9
+    assert spmm_mod.launches_per_hop(A, B, d) == 13
     x = synth.uniform_features_t(n, d, seed=synth.FEATURE_SEED, device="cuda")
-    panels = propagate(A, x, K)                     # col_blocks from auto_col_blocks: the cached 8
+    panels = propagate(A, x, K)                     # col_blocks from auto_col_blocks: the cached 12
     torch.cuda.synchronize()
     ipn, ixn, vn = ip.cpu().numpy(), ix.cpu().numpy(), vals.cpu().numpy()
     del ip, ix, vals

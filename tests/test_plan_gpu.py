@@ -321,7 +321,7 @@ def test_native_plan_automatic_choices_match_prepare(monkeypatch):
     d = 128
     B = S.prepare(A, d, hops=40)
     P = cached(A, d)
-    assert P is not None and B == P.col_blocks == 4 and P.split_block0 and P.compact
+    assert P is not None and B == P.col_blocks == 12 and P.split_block0 and P.compact
     assert S.launches_per_hop(A, B, d) == B + 1
     # the torch formulation of the same layout on a second operator over the same arrays
     from srgnn.csr import DeviceCSR
