@@ -224,10 +224,31 @@ typedef struct {
 int srg_plan_build(const int64_t* indptr, const int32_t* indices, const float* values, int64_t n_rows,
                    int32_t d, int32_t hops, int32_t col_blocks, int64_t hub_threshold, int64_t heavy_threshold,
                    uint32_t opts, void* stream, srg_plan** plan);
-/* Releases the plan's device memory after the work enqueued on `stream` (it synchronises `stream`):
- * every hop that uses the plan must be ordered before that point (enqueued on it, or joined into it).
- * A plan is used by one host thread at a time (a propagate over a width other than 64 / 128 / 256
- * completes its row-indexed spans in place; srg_plan_launch does so up front). */
+/* The device memory srg_plan_build would take for these arguments -- keep_bytes for the plan's life,
+ * scratch_bytes during the build -- and the choices it would make (resolved_opts: SRG_PLAN_COMPACT or
+ * SPANS | SPLIT_BLOCK0 or WHOLE_BLOCK0; resolved_col_blocks).  One pass over indptr (synchronises
+ * `stream`); nothing is allocated.  With srg_plan_build_in, a host puts the plan in memory of its own
+ * allocator (srgnn: torch's caching allocator, so a plan competes for the same cached blocks as the
+ * panels instead of beside them). */
+int srg_plan_query(const int64_t* indptr, int64_t n_rows, int32_t d, int32_t hops, int32_t col_blocks,
+                   uint32_t opts, void* stream, size_t* keep_bytes, size_t* scratch_bytes, uint32_t* resolved_opts,
+                   int32_t* resolved_col_blocks);
+/* srg_plan_build into the caller's memory: `keep` (>= keep_bytes of srg_plan_query for the same
+ * arguments and the resolved opts / col_blocks, 256-byte aligned) holds the plan until srg_plan_destroy
+ * returns; `scratch` (>= scratch_bytes) only until this call returns.  The plan never frees either. */
+int srg_plan_build_in(const int64_t* indptr, const int32_t* indices, const float* values, int64_t n_rows, int32_t d,
+                      int32_t hops, int32_t col_blocks, int64_t hub_threshold, int64_t heavy_threshold, uint32_t opts,
+                      void* keep, size_t keep_bytes, void* scratch, size_t scratch_bytes, void* stream,
+                      srg_plan** plan);
+/* Releases the plan after every reader of its memory.  The plan records, per stream its work was
+ * enqueued on (its build, propagates, hops, graph replays, the row-span completion), an event after
+ * that work with the hub side stream already joined; destroy makes `stream` wait for all of them,
+ * joins the hub side stream of `stream`, drains `stream` (a host synchronisation), destroys the
+ * executable graphs and only then frees the memory (srg_plan_build's; srg_plan_build_in's memory may
+ * be reused by its owner once destroy returns).  Launches a caller ran itself from srg_plan_launch's
+ * descriptors must be ordered before `stream` by the caller.  A plan is used by one host thread at a
+ * time (a propagate over a width other than 64 / 128 / 256 completes its row-indexed spans in place;
+ * srg_plan_launch does so up front). */
 int srg_plan_destroy(srg_plan* plan, void* stream);
 int srg_plan_describe(const srg_plan* plan, srg_plan_desc* desc);
 /* Launch i of one hop over a d-column panel, as srg_plan_propagate_f32 runs it (flags included), and

@@ -419,10 +419,16 @@ int srg_dist_propagate_khop_f32(srg_comm* comm, const srg_shard_f32* shards, int
     // block q must read only rows rank q owns, which have arrived when it runs)
     std::vector<int64_t*> splits(n_shards, nullptr);
     int* bad = nullptr;
+    // The split points are read by the span launches on the shard's stream and by their hub rows on
+    // the library's side stream.  Every span launch here forks and joins its own hub rows (no
+    // HUB_NOJOIN), so the free, enqueued on the shard's stream after the last launch, is already
+    // ordered after both; srg_hub_join makes that explicit (a no-op when nothing is pending), so the
+    // stream-ordered free never depends on how the launches chained their hub rows.
     auto release = [&]() {
         for (int i = 0; i < n_shards; ++i)
             if (splits[i]) {
                 (void)hipSetDevice(shards[i].device);
+                (void)srg_hub_join(shards[i].stream);
                 (void)hipFreeAsync(splits[i], st(i));
             }
     };
@@ -600,14 +606,54 @@ int halo_transport(const Rccl* r, srg_comm* comm, srg_halo_share* const* shares,
 // rows of every group and of X's ghost rows, plus (n, nnz) of the plan's graph -- and checks that
 // against what it expects to receive.  Plans built with different arguments (chunks, thresholds, ghost
 // caps, graphs) then fail with SRG_ERR_INVALID instead of hanging in ncclGroupEnd or filling the halo
-// with the wrong rows.  One small grouped exchange and a host sync per share, once.
+// with the wrong rows.  Two small grouped exchanges and two host syncs per share, once: first a
+// fixed-size header (groups C, n, nnz, ranks P) -- its length never depends on the plan, so ranks whose
+// plans have different chunk counts still exchange matching messages and all fail on the mismatch
+// (every rank that differs from any rank sees a difference: a != b means no rank equals both) -- then,
+// only when every header agrees, the C + 2 per-group counts.
+constexpr int kCountHeader = 4;
+
+// one grouped exchange of `len` int64 per peer: buf[i] holds [P][len] to send, then [P][len] received
+int exchange_words(const Rccl* r, srg_comm* comm, srg_halo_share* const* shares, int n, const std::vector<int64_t*>& buf,
+                   const std::vector<std::vector<int64_t>>& mine, int len, std::vector<std::vector<int64_t>>& theirs)
+{
+    const int P = comm->nranks;
+    for (int i = 0; i < n; ++i)
+        if (hipSetDevice(shares[i]->device) != hipSuccess ||
+            hipMemcpy(buf[i], mine[i].data(), (size_t)P * len * sizeof(int64_t), hipMemcpyHostToDevice) != hipSuccess)
+            return comm_fail(SRG_ERR_HIP, "share %d: count upload failed", i);
+    if (r->GroupStart() != ncclSuccess) return comm_fail(SRG_ERR_HIP, "ncclGroupStart failed");
+    int rc = SRG_OK;
+    for (int i = 0; i < n && !rc; ++i) {
+        const int me = comm->ranks[i];
+        for (int q = 0; q < P && !rc; ++q) {
+            if (q == me) continue;
+            ncclResult_t e = r->Send(buf[i] + (size_t)q * len, len, ncclInt64, q, comm->comms[i], shares[i]->comm_stream);
+            if (e == ncclSuccess)
+                e = r->Recv(buf[i] + (size_t)(P + q) * len, len, ncclInt64, q, comm->comms[i], shares[i]->comm_stream);
+            if (e != ncclSuccess) rc = comm_fail(SRG_ERR_HIP, "count exchange failed: %s", r->GetErrorString(e));
+        }
+    }
+    const ncclResult_t ge = r->GroupEnd();
+    if (!rc && ge != ncclSuccess) rc = comm_fail(SRG_ERR_HIP, "count exchange: ncclGroupEnd failed: %s", r->GetErrorString(ge));
+    theirs.assign(n, std::vector<int64_t>((size_t)P * len, 0));
+    for (int i = 0; i < n && !rc; ++i)
+        if (hipSetDevice(shares[i]->device) != hipSuccess || hipStreamSynchronize(shares[i]->comm_stream) != hipSuccess ||
+            hipMemcpy(theirs[i].data(), buf[i] + (size_t)P * len, (size_t)P * len * sizeof(int64_t), hipMemcpyDeviceToHost) !=
+                hipSuccess)
+            rc = comm_fail(SRG_ERR_HIP, "share %d: count exchange readback failed", i);
+    return rc;
+}
+
 int verify_counts(const Rccl* r, srg_comm* comm, srg_halo_share* const* shares, int n)
 {
     bool all = true;
     for (int i = 0; i < n; ++i) all &= shares[i]->counts_verified;
     if (all) return SRG_OK;
     const int P = comm->nranks;
-    const int NG = shares[0]->plan->C + 4;        // groups 0..C, ghosts (C + 1), then n and nnz
+    int cmax = 0;
+    for (int i = 0; i < n; ++i) cmax = std::max(cmax, shares[i]->plan->C);
+    const int NG = std::max(cmax + 2, kCountHeader);   // words per peer: the buffers fit either exchange
     std::vector<int64_t*> buf(n, nullptr);
     auto release = [&]() {
         for (int i = 0; i < n; ++i)
@@ -616,59 +662,62 @@ int verify_counts(const Rccl* r, srg_comm* comm, srg_halo_share* const* shares, 
                 (void)hipFree(buf[i]);
             }
     };
-    std::vector<std::vector<int64_t>> mine(n, std::vector<int64_t>((size_t)P * NG, 0));
-    for (int i = 0; i < n; ++i) {
-        const srg_halo_plan& pl = *shares[i]->plan;
-        for (int q = 0; q < P; ++q) {
-            for (int g = 0; g <= pl.C + 1; ++g) mine[i][(size_t)q * NG + g] = send_count(pl, g, q);
-            mine[i][(size_t)q * NG + pl.C + 2] = pl.n;
-            mine[i][(size_t)q * NG + pl.C + 3] = pl.nnz_total;
-        }
+    for (int i = 0; i < n; ++i)
         if (hipSetDevice(shares[i]->device) != hipSuccess ||
-            hipMalloc(reinterpret_cast<void**>(&buf[i]), (size_t)2 * P * NG * sizeof(int64_t)) != hipSuccess ||
-            hipMemcpy(buf[i], mine[i].data(), (size_t)P * NG * sizeof(int64_t), hipMemcpyHostToDevice) != hipSuccess) {
+            hipMalloc(reinterpret_cast<void**>(&buf[i]), (size_t)2 * P * NG * sizeof(int64_t)) != hipSuccess) {
             release();
             return comm_fail(SRG_ERR_HIP, "share %d: count buffers failed", i);
         }
-    }
-    int rc = SRG_OK;
-    if (r->GroupStart() != ncclSuccess) {
-        release();
-        return comm_fail(SRG_ERR_HIP, "ncclGroupStart failed");
-    }
-    for (int i = 0; i < n && !rc; ++i) {
-        const int me = comm->ranks[i];
-        for (int q = 0; q < P && !rc; ++q) {
-            if (q == me) continue;
-            ncclResult_t e = r->Send(buf[i] + (size_t)q * NG, NG, ncclInt64, q, comm->comms[i], shares[i]->comm_stream);
-            if (e == ncclSuccess)
-                e = r->Recv(buf[i] + (size_t)(P + q) * NG, NG, ncclInt64, q, comm->comms[i], shares[i]->comm_stream);
-            if (e != ncclSuccess) rc = comm_fail(SRG_ERR_HIP, "count exchange failed: %s", r->GetErrorString(e));
+    // 1: the header, kCountHeader words per peer whatever the plan
+    std::vector<std::vector<int64_t>> mine(n), theirs;
+    for (int i = 0; i < n; ++i) {
+        const srg_halo_plan& pl = *shares[i]->plan;
+        mine[i].assign((size_t)P * kCountHeader, 0);
+        for (int q = 0; q < P; ++q) {
+            int64_t* h = mine[i].data() + (size_t)q * kCountHeader;
+            h[0] = pl.C;
+            h[1] = pl.n;
+            h[2] = pl.nnz_total;
+            h[3] = P;
         }
     }
-    const ncclResult_t ge = r->GroupEnd();
-    if (!rc && ge != ncclSuccess) rc = comm_fail(SRG_ERR_HIP, "count exchange: ncclGroupEnd failed: %s", r->GetErrorString(ge));
+    int rc = exchange_words(r, comm, shares, n, buf, mine, kCountHeader, theirs);
     for (int i = 0; i < n && !rc; ++i) {
-        std::vector<int64_t> theirs((size_t)P * NG, 0);
-        if (hipSetDevice(shares[i]->device) != hipSuccess || hipStreamSynchronize(shares[i]->comm_stream) != hipSuccess ||
-            hipMemcpy(theirs.data(), buf[i] + (size_t)P * NG, (size_t)P * NG * sizeof(int64_t), hipMemcpyDeviceToHost) !=
-                hipSuccess) {
-            rc = comm_fail(SRG_ERR_HIP, "share %d: count exchange readback failed", i);
-            break;
-        }
         const srg_halo_plan& pl = *shares[i]->plan;
         for (int q = 0; q < P && !rc; ++q) {
             if (q == comm->ranks[i]) continue;
-            const int64_t* t = theirs.data() + (size_t)q * NG;
-            if (t[pl.C + 2] != pl.n || t[pl.C + 3] != pl.nnz_total)
+            const int64_t* t = theirs[i].data() + (size_t)q * kCountHeader;
+            if (t[1] != pl.n || t[2] != pl.nnz_total)
                 rc = comm_fail(SRG_ERR_INVALID, "rank %d's plan is of a graph with n=%lld nnz=%lld, rank %d's of n=%lld "
-                               "nnz=%lld", q, (long long)t[pl.C + 2], (long long)t[pl.C + 3], comm->ranks[i],
-                               (long long)pl.n, (long long)pl.nnz_total);
-            for (int g = 0; g <= pl.C + 1 && !rc; ++g)
-                if (t[g] != recv_count(pl, g, q))
-                    rc = comm_fail(SRG_ERR_INVALID, "plans disagree: rank %d sends %lld rows of group %d to rank %d, which "
-                                   "expects %lld (build every rank's plan with the same arguments)", q, (long long)t[g],
-                                   g, comm->ranks[i], (long long)recv_count(pl, g, q));
+                               "nnz=%lld", q, (long long)t[1], (long long)t[2], comm->ranks[i], (long long)pl.n,
+                               (long long)pl.nnz_total);
+            else if (t[0] != pl.C || t[3] != P)
+                rc = comm_fail(SRG_ERR_INVALID, "plans disagree: rank %d's plan has %lld row chunks over %lld ranks, rank "
+                               "%d's %d over %d (build every rank's plan with the same arguments)", q, (long long)t[0],
+                               (long long)t[3], comm->ranks[i], pl.C, P);
+        }
+    }
+    // 2: the per-group counts (every plan has the same C now)
+    if (!rc) {
+        const int C = shares[0]->plan->C, len = C + 2;
+        for (int i = 0; i < n; ++i) {
+            const srg_halo_plan& pl = *shares[i]->plan;
+            mine[i].assign((size_t)P * len, 0);
+            for (int q = 0; q < P; ++q)
+                for (int g = 0; g <= C + 1; ++g) mine[i][(size_t)q * len + g] = send_count(pl, g, q);
+        }
+        rc = exchange_words(r, comm, shares, n, buf, mine, len, theirs);
+        for (int i = 0; i < n && !rc; ++i) {
+            const srg_halo_plan& pl = *shares[i]->plan;
+            for (int q = 0; q < P && !rc; ++q) {
+                if (q == comm->ranks[i]) continue;
+                const int64_t* t = theirs[i].data() + (size_t)q * len;
+                for (int g = 0; g <= C + 1 && !rc; ++g)
+                    if (t[g] != recv_count(pl, g, q))
+                        rc = comm_fail(SRG_ERR_INVALID, "plans disagree: rank %d sends %lld rows of group %d to rank %d, "
+                                       "which expects %lld (build every rank's plan with the same arguments)", q,
+                                       (long long)t[g], g, comm->ranks[i], (long long)recv_count(pl, g, q));
+            }
         }
     }
     release();

@@ -64,7 +64,16 @@ struct srg_plan {
     int64_t* blk_end = nullptr;
     std::vector<Launch> launches;
     void* owned = nullptr;                   // one device allocation holds every array of the plan
+    bool owns = true;                        // false: the caller's memory (srg_plan_build_in)
     int64_t bytes = 0;
+    // Every stream that work reading the plan's memory was enqueued on, with an event recorded after
+    // that work (the hub side stream already joined into it): srg_plan_destroy joins them all into
+    // its stream and drains that before the memory goes
+    struct Use {
+        hipStream_t stream = nullptr;
+        hipEvent_t done = nullptr;
+    };
+    std::vector<Use> uses;
     // the K-hop loop captured as a HIP graph, replayed while the caller repeats a call (SRG_PLAN_GRAPHS)
     struct Graph {
         std::vector<float*> panels;
@@ -75,7 +84,15 @@ struct srg_plan {
         int calls = 0;                       // eager calls with this key so far
         bool off = false;                    // capture failed once: eager from then on
         hipGraphExec_t exec = nullptr;
+        hipEvent_t done = nullptr;           // recorded after the exec's last launch
     } graph;
+    // executable graphs of earlier keys, destroyed once their last launch has completed (never while
+    // a launch of theirs may still run)
+    struct Retired {
+        hipGraphExec_t exec = nullptr;
+        hipEvent_t done = nullptr;
+    };
+    std::vector<Retired> retired;
 };
 
 namespace {
@@ -180,24 +197,27 @@ __global__ void __launch_bounds__(256) k_plan_splits(const int64_t* __restrict__
                                                      int64_t n, int B, int64_t* __restrict__ splits,
                                                      int32_t* __restrict__ cut)
 {
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n * (B - 1)) return;
-    const int b = (int)(t / n) + 1;
-    const int64_t r = t % n;
-    const int64_t beg = ip[r], end = ip[r + 1];
-    const bool whole = end - beg <= kWholeMax;
-    if (b == 1) cut[r] = whole ? 0 : 1;
-    if (whole) {
-        if (b == 1) splits[t] = end;
-        return;
+    // grid-stride over the n (B - 1) (row, boundary) pairs: the grid is capped, so an operator of any
+    // size (n (B - 1) past 2^32 work-items: 1.4e9 rows at B = 4) launches
+    const int64_t total = n * (B - 1), stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
+        const int b = (int)(t / n) + 1;
+        const int64_t r = t % n;
+        const int64_t beg = ip[r], end = ip[r + 1];
+        const bool whole = end - beg <= kWholeMax;
+        if (b == 1) cut[r] = whole ? 0 : 1;
+        if (whole) {
+            if (b == 1) splits[t] = end;
+            continue;
+        }
+        const int64_t bound = ((int64_t)b * n + B - 1) / B;
+        int64_t lo = beg, hi = end;
+        while (lo < hi) {
+            const int64_t mid = lo + (hi - lo) / 2;
+            if ((int64_t)ix[mid] < bound) lo = mid + 1; else hi = mid;
+        }
+        splits[t] = lo;
     }
-    const int64_t bound = ((int64_t)b * n + B - 1) / B;
-    int64_t lo = beg, hi = end;
-    while (lo < hi) {
-        const int64_t mid = lo + (hi - lo) / 2;
-        if ((int64_t)ix[mid] < bound) lo = mid + 1; else hi = mid;
-    }
-    splits[t] = lo;
 }
 
 __device__ __forceinline__ int64_t bound_of(const int64_t* __restrict__ ip, const int64_t* __restrict__ splits,
@@ -430,8 +450,7 @@ struct DevGuard {
     }
 };
 
-// device memory released after the work enqueued on `s` so far (hipMalloc'd: the stream-ordered pool
-// lost track of plan memory reused across builds with the hub side stream in flight -- DESIGN.md §3)
+// build temporaries: released after the work enqueued on `s` so far
 struct DevBuf {
     void* p = nullptr;
     hipStream_t s = nullptr;
@@ -445,18 +464,90 @@ struct DevBuf {
     }
 };
 
-void drop_graph(srg_plan* P)
+bool capturing(hipStream_t s)
 {
-    if (P->graph.exec) (void)hipGraphExecDestroy(P->graph.exec);
-    P->graph.exec = nullptr;
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &st) != hipSuccess) { (void)hipGetLastError(); return false; }
+    return st != hipStreamCaptureStatusNone;
 }
 
+constexpr size_t kMaxUses = 16;              // streams remembered per plan (older ones are drained)
+
+// Work reading the plan's memory has been enqueued on `s` (hub side stream joined into it): remember
+// it.  A stream the caller is capturing into its own graph is not recorded (an event recorded there
+// would be a graph node); such a caller orders its graph's launches before srg_plan_destroy itself.
+void note_use(srg_plan* P, hipStream_t s)
+{
+    if (capturing(s)) return;
+    srg_plan::Use* u = nullptr;
+    for (auto& x : P->uses)
+        if (x.stream == s) u = &x;
+    if (!u) {
+        if (P->uses.size() >= kMaxUses) {
+            (void)hipEventSynchronize(P->uses.front().done);
+            (void)hipEventDestroy(P->uses.front().done);
+            P->uses.erase(P->uses.begin());
+        }
+        srg_plan::Use nu;
+        nu.stream = s;
+        if (hipEventCreateWithFlags(&nu.done, hipEventDisableTiming) != hipSuccess) {
+            (void)hipGetLastError();
+            (void)hipStreamSynchronize(s);   // no event: make the work complete instead
+            return;
+        }
+        P->uses.push_back(nu);
+        u = &P->uses.back();
+    }
+    if (hipEventRecord(u->done, s) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipStreamSynchronize(s);
+    }
+}
+
+// executable graphs of earlier keys whose last launch has completed
+void reap_retired(srg_plan* P, bool wait)
+{
+    for (size_t i = 0; i < P->retired.size();) {
+        srg_plan::Retired& r = P->retired[i];
+        const hipError_t q = wait ? hipEventSynchronize(r.done) : hipEventQuery(r.done);
+        if (q == hipErrorNotReady) { ++i; continue; }
+        (void)hipGetLastError();
+        (void)hipGraphExecDestroy(r.exec);
+        (void)hipEventDestroy(r.done);
+        P->retired.erase(P->retired.begin() + (long)i);
+    }
+}
+
+// the current key's graph goes: retired until its last launch has completed
+void drop_graph(srg_plan* P)
+{
+    srg_plan::Graph& G = P->graph;
+    if (G.exec) P->retired.push_back({G.exec, G.done});
+    else if (G.done) (void)hipEventDestroy(G.done);
+    G.exec = nullptr;
+    G.done = nullptr;
+}
+
+// Releases the plan's memory after every reader: each stream the plan's work went to is joined into
+// `s` (its last recorded event), then `s` is drained -- so the hub side stream (joined into those
+// streams by the hops), replayed graphs and complete_rows' kernels have all finished -- and only then
+// are the executable graphs destroyed and the memory freed.  Before round 6 the graph exec was
+// destroyed first and only `s` was drained: a graph launch or a hop on another stream could still be
+// reading the plan (hipFree's implicit device synchronisation hid it).
 void release(srg_plan* P, hipStream_t s)
 {
-    drop_graph(P);
-    if (!P->owned) return;
+    for (const auto& u : P->uses)
+        if (u.done && hipStreamWaitEvent(s, u.done, 0) != hipSuccess) {
+            (void)hipGetLastError();
+            (void)hipEventSynchronize(u.done);
+        }
     (void)hipStreamSynchronize(s);
-    (void)hipFree(P->owned);
+    for (const auto& u : P->uses) (void)hipEventSynchronize(u.done);   // already complete: cheap
+    drop_graph(P);
+    reap_retired(P, true);
+    for (auto& u : P->uses) (void)hipEventDestroy(u.done);
+    P->uses.clear();
+    if (P->owned && P->owns) (void)hipFree(P->owned);
     P->owned = nullptr;
 }
 
@@ -479,6 +570,7 @@ int complete_rows(srg_plan* P, hipStream_t s)
     hipLaunchKernelGGL(k_plan_rows, dim3(grid_for(P->n_items, 256, 1u << 20)), dim3(256), 0, s, P->n, L0.order, (const int64_t*)t.p, nl, L0.slot_beg, L0.slot_end, P->n_items, P->blk_beg, P->blk_end);
     SRG_PLAN_HIP(hipGetLastError());
     P->rows_full = true;
+    note_use(P, s);
     return SRG_OK;
 }
 
@@ -486,14 +578,30 @@ bool packed_width(int d) { return d == 64 || d == 128 || d == 256; }
 
 }  // namespace
 
-extern "C" {
+// Where a build's memory comes from: the library (hipMalloc: srg_plan_build), the caller
+// (srg_plan_build_in: `keep` for the plan's lifetime, `scratch` for the call), or nowhere -- a size
+// query (srg_plan_query: the sizes and the resolved choices are returned, nothing is built).
+namespace {
+struct BuildMem {
+    void* keep = nullptr;
+    size_t keep_bytes = 0;
+    void* scratch = nullptr;
+    size_t scratch_bytes = 0;
+    size_t* q_keep = nullptr;                // non-null: query only
+    size_t* q_scratch = nullptr;
+    uint32_t* q_opts = nullptr;
+    int32_t* q_blocks = nullptr;
+    bool query() const { return q_keep != nullptr; }
+    bool caller() const { return keep != nullptr; }
+};
+}  // namespace
 
-int srg_plan_build(const int64_t* indptr, const int32_t* indices, const float* values, int64_t n_rows, int32_t d,
-                   int32_t hops, int32_t col_blocks, int64_t hub_threshold, int64_t heavy_threshold, uint32_t opts,
-                   void* stream, srg_plan** plan)
+static int build_impl(const int64_t* indptr, const int32_t* indices, const float* values, int64_t n_rows, int32_t d,
+               int32_t hops, int32_t col_blocks, int64_t hub_threshold, int64_t heavy_threshold, uint32_t opts,
+               void* stream, srg_plan** plan, const BuildMem& mem)
 {
-    if (!plan) return pfail(SRG_ERR_INVALID, "null plan");
-    *plan = nullptr;
+    if (!plan && !mem.query()) return pfail(SRG_ERR_INVALID, "null plan");
+    if (plan) *plan = nullptr;
     if (!indptr) return pfail(SRG_ERR_INVALID, "null indptr");
     if (n_rows < 0 || n_rows >= (1ll << 31)) return pfail(SRG_ERR_INVALID, "n_rows=%lld outside [0, 2^31)", (long long)n_rows);
     if (d <= 0 || hops < 0 || col_blocks < 0 || col_blocks > kMaxBlocks)
@@ -517,8 +625,9 @@ int srg_plan_build(const int64_t* indptr, const int32_t* indices, const float* v
     P->d = d;
     auto bail = [&](int rc) { release(P, s); delete P; return rc; };
     const int64_t n = n_rows;
-    DevBuf scratch;
+    DevBuf scratch;                          // the library's scratch (srg_plan_build)
     scratch.s = s;
+    char* scratch_base = nullptr;
     // ---- 1: degree statistics (host sync 1) ----
     unsigned long long hs[4] = {0, 0, 0, 0};
     {
@@ -534,7 +643,7 @@ int srg_plan_build(const int64_t* indptr, const int32_t* indices, const float* v
     const int64_t max_deg = (int64_t)hs[0], n_whole_rows = (int64_t)hs[1];
     const int64_t nnz = (int64_t)hs[3] - (int64_t)hs[2];
     if (nnz < 0) return bail(pfail(SRG_ERR_INVALID, "indptr[n] < indptr[0]"));
-    if (nnz > 0 && (!indices || !values)) return bail(pfail(SRG_ERR_INVALID, "null indices / values"));
+    if (nnz > 0 && !mem.query() && (!indices || !values)) return bail(pfail(SRG_ERR_INVALID, "null indices / values"));
     P->nnz = nnz;
     // ---- 2: the layout: blocks, launches, copies ----
     const int64_t panel = n * (int64_t)d * 4;
@@ -580,6 +689,17 @@ int srg_plan_build(const int64_t* indptr, const int32_t* indices, const float* v
     const int64_t n_items = T.off[T.n_launch];
     P->n_items = n_items;
     if (T.lenbits + T.lbits > 64) return bail(pfail(SRG_ERR_INVALID, "row lengths too long to plan"));
+    if (mem.query()) {
+        *mem.q_opts = (compact ? SRG_PLAN_COMPACT : SRG_PLAN_SPANS) | (split0 ? SRG_PLAN_SPLIT_BLOCK0 : SRG_PLAN_WHOLE_BLOCK0);
+        *mem.q_blocks = B;
+        if (n == 0) {
+            *mem.q_keep = 0;
+            *mem.q_scratch = 0;
+            delete P;
+            srg_clear_error();
+            return SRG_OK;
+        }
+    }
     if (n == 0) {
         *plan = P;
         srg_clear_error();
@@ -612,7 +732,7 @@ int srg_plan_build(const int64_t* indptr, const int32_t* indices, const float* v
         Arena keep, tmp;
         if (pass == 1) {
             keep.base = (char*)P->owned;
-            tmp.base = (char*)scratch.p;
+            tmp.base = scratch_base;
         }
         order = keep.take<int32_t>((size_t)n_items);
         if (slots) {
@@ -638,22 +758,42 @@ int srg_plan_build(const int64_t* indptr, const int32_t* indices, const float* v
         dhubs = tmp.take<int32_t>((size_t)kHubPrefix * T.n_launch);
         cub_tmp = tmp.take<char>(cub_bytes + 256);
         if (pass == 0) {
+            if (mem.query()) {
+                *mem.q_keep = keep.used;
+                *mem.q_scratch = tmp.used;
+                delete P;
+                srg_clear_error();
+                return SRG_OK;
+            }
+            P->bytes = (int64_t)keep.used;
+            if (mem.caller()) {
+                // the caller's memory: 256-byte aligned (the arena's pieces are), large enough
+                if (((uintptr_t)mem.keep & 255) || ((uintptr_t)mem.scratch & 255) || !mem.scratch ||
+                    mem.keep_bytes < keep.used || mem.scratch_bytes < tmp.used)
+                    return bail(pfail(SRG_ERR_INVALID, "plan: caller memory keep %zu of %zu bytes, scratch %zu of %zu "
+                                      "(srg_plan_query's sizes, 256-byte aligned)", mem.keep_bytes, keep.used,
+                                      mem.scratch_bytes, tmp.used));
+                P->owned = mem.keep;
+                P->owns = false;
+                scratch_base = (char*)mem.scratch;
+                continue;
+            }
             if (hipMalloc(&P->owned, keep.used) != hipSuccess) {
                 (void)hipGetLastError();
                 P->owned = nullptr;
                 return bail(pfail(SRG_ERR_ALLOC, "plan: %zu bytes of device memory", keep.used));
             }
-            P->bytes = (int64_t)keep.used;
             if (hipMalloc(&scratch.p, tmp.used) != hipSuccess) {
                 (void)hipGetLastError();
                 scratch.p = nullptr;
                 return bail(pfail(SRG_ERR_ALLOC, "plan: %zu bytes of build scratch", tmp.used));
             }
+            scratch_base = (char*)scratch.p;
         }
     }
     // split points and the cut rows' positions
     if (B > 1) {
-        hipLaunchKernelGGL(k_plan_splits, dim3(grid_for(n * (B - 1), 256, 1u << 30)), dim3(256), 0, s, indptr, indices,
+        hipLaunchKernelGGL(k_plan_splits, dim3(grid_for(n * (B - 1), 256, 1u << 20)), dim3(256), 0, s, indptr, indices,
                            n, B, splits, cut);
         size_t tb = cub_bytes;
         SRG_PLAN_HIP(hipcub::DeviceScan::ExclusiveSum(cub_tmp, tb, cut, cutpos, n, s));
@@ -758,10 +898,59 @@ int srg_plan_build(const int64_t* indptr, const int32_t* indices, const float* v
         }
         P->same_hubs = same;
     }
-    scratch.reset();   // after the build's kernels (one more wait on the stream: the copy)
+    // after the build's kernels (one more wait on the stream: the copy); the caller's scratch may go
+    // once the call returns
+    scratch.reset();
+    if (mem.caller()) {
+        const hipError_t e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return bail(pfail(SRG_ERR_HIP, "plan build: %s", hipGetErrorString(e)));
+    }
+    note_use(P, s);
     *plan = P;
     srg_clear_error();
     return SRG_OK;
+}
+
+extern "C" {
+
+int srg_plan_build(const int64_t* indptr, const int32_t* indices, const float* values, int64_t n_rows, int32_t d,
+                   int32_t hops, int32_t col_blocks, int64_t hub_threshold, int64_t heavy_threshold, uint32_t opts,
+                   void* stream, srg_plan** plan)
+{
+    return build_impl(indptr, indices, values, n_rows, d, hops, col_blocks, hub_threshold, heavy_threshold, opts,
+                      stream, plan, BuildMem{});
+}
+
+int srg_plan_query(const int64_t* indptr, int64_t n_rows, int32_t d, int32_t hops, int32_t col_blocks,
+                   uint32_t opts, void* stream, size_t* keep_bytes, size_t* scratch_bytes, uint32_t* resolved_opts,
+                   int32_t* resolved_col_blocks)
+{
+    if (!keep_bytes || !scratch_bytes || !resolved_opts || !resolved_col_blocks)
+        return pfail(SRG_ERR_INVALID, "null output");
+    BuildMem m;
+    m.q_keep = keep_bytes;
+    m.q_scratch = scratch_bytes;
+    m.q_opts = resolved_opts;
+    m.q_blocks = resolved_col_blocks;
+    // the sizes do not depend on the ids / values, only on indptr (lengths and split counts) and the
+    // thresholds (which only pick rows inside the sized arrays)
+    return build_impl(indptr, nullptr, nullptr, n_rows, d, hops, col_blocks, SRG_PLAN_AUTO, SRG_PLAN_AUTO, opts,
+                      stream, nullptr, m);
+}
+
+int srg_plan_build_in(const int64_t* indptr, const int32_t* indices, const float* values, int64_t n_rows, int32_t d,
+                      int32_t hops, int32_t col_blocks, int64_t hub_threshold, int64_t heavy_threshold, uint32_t opts,
+                      void* keep, size_t keep_bytes, void* scratch, size_t scratch_bytes, void* stream,
+                      srg_plan** plan)
+{
+    if (!keep) return pfail(SRG_ERR_INVALID, "null keep memory (srg_plan_build allocates its own)");
+    BuildMem m;
+    m.keep = keep;
+    m.keep_bytes = keep_bytes;
+    m.scratch = scratch;
+    m.scratch_bytes = scratch_bytes;
+    return build_impl(indptr, indices, values, n_rows, d, hops, col_blocks, hub_threshold, heavy_threshold, opts,
+                      stream, plan, m);
 }
 
 int srg_plan_destroy(srg_plan* plan, void* stream)
@@ -770,6 +959,8 @@ int srg_plan_destroy(srg_plan* plan, void* stream)
     const hipStream_t s = static_cast<hipStream_t>(stream);
     DevGuard g(s);
     if (!s) (void)hipSetDevice(plan->device);
+    // hub rows a caller driving the launches itself (srg_plan_launch) left on the side stream of `s`
+    (void)srg_hub_join(stream);
     release(plan, s);
     delete plan;
     return SRG_OK;
@@ -883,13 +1074,16 @@ int srg_plan_propagate_f32(const srg_plan* plan, float* const* panels, int64_t l
     }
     std::vector<srg_hop_launch> L;
     const int join = plan_launches(plan, d, flags, L);
+    srg_plan* P = const_cast<srg_plan*>(plan);
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    reap_retired(P, false);
 #if SRG_PLAN_GRAPHS
     // A repeated call (same panels, widths, hops, flags and stream) replays the K hops as one HIP graph,
     // captured from the second call on: the same launches with the same arguments, so the same bits.
     // Not for FAST (its scratch is stream-ordered allocation) nor the null stream (not capturable).
-    srg_plan* P = const_cast<srg_plan*>(plan);
+    // A graph of an earlier key is retired, not destroyed: its last launch may still be running.
     srg_plan::Graph& G = P->graph;
-    if (stream && !(flags & SRG_SPMM_FAST) && panels) {
+    if (stream && !(flags & SRG_SPMM_FAST) && panels && !capturing(s)) {
         const std::vector<float*> key(panels, panels + K + 1);
         if (G.panels != key || G.ld != ld || G.d != d || G.K != K || G.flags != flags || G.stream != stream) {
             drop_graph(P);
@@ -898,26 +1092,30 @@ int srg_plan_propagate_f32(const srg_plan* plan, float* const* panels, int64_t l
             G.calls = 0;
             G.off = false;
         }
-        const hipStream_t s = static_cast<hipStream_t>(stream);
-        if (G.exec) {
+        auto replay = [&]() {
             SRG_PLAN_HIP(hipGraphLaunch(G.exec, s));
+            SRG_PLAN_HIP(hipEventRecord(G.done, s));
+            note_use(P, s);
             srg_clear_error();
             return SRG_OK;
-        }
+        };
+        if (G.exec) return replay();
         if (G.calls >= 1 && !G.off) {
             if (hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed) == hipSuccess) {
                 const int rc = srg_propagate_plan_f32(L.data(), (int32_t)L.size(), join, panels, ld, d, K, stream);
-                hipGraph_t g = nullptr;
-                const hipError_t e = hipStreamEndCapture(s, &g);
+                hipGraph_t gr = nullptr;
+                const hipError_t e = hipStreamEndCapture(s, &gr);
                 hipGraphExec_t x = nullptr;
-                if (!rc && e == hipSuccess && g && hipGraphInstantiate(&x, g, nullptr, nullptr, 0) == hipSuccess) {
-                    (void)hipGraphDestroy(g);
+                hipEvent_t done = nullptr;
+                if (!rc && e == hipSuccess && gr && hipGraphInstantiate(&x, gr, nullptr, nullptr, 0) == hipSuccess &&
+                    hipEventCreateWithFlags(&done, hipEventDisableTiming) == hipSuccess) {
+                    (void)hipGraphDestroy(gr);
                     G.exec = x;
-                    SRG_PLAN_HIP(hipGraphLaunch(G.exec, s));
-                    srg_clear_error();
-                    return SRG_OK;
+                    G.done = done;
+                    return replay();
                 }
-                if (g) (void)hipGraphDestroy(g);
+                if (x) (void)hipGraphExecDestroy(x);
+                if (gr) (void)hipGraphDestroy(gr);
             }
             (void)hipGetLastError();
             G.off = true;                    // nothing ran: the eager loop below does the hops
@@ -925,7 +1123,9 @@ int srg_plan_propagate_f32(const srg_plan* plan, float* const* panels, int64_t l
         ++G.calls;
     }
 #endif
-    return srg_propagate_plan_f32(L.data(), (int32_t)L.size(), join, panels, ld, d, K, stream);
+    const int rc = srg_propagate_plan_f32(L.data(), (int32_t)L.size(), join, panels, ld, d, K, stream);
+    if (!rc) note_use(P, s);
+    return rc;
 }
 
 int srg_plan_hop_f32(const srg_plan* plan, const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t d,
@@ -976,6 +1176,7 @@ int srg_plan_hop_f32(const srg_plan* plan, const float* X, int64_t ldx, float* Y
     int rc = srg_run_plan_hop(L.data(), (int32_t)L.size(), join, X, ldx, Y, ldy, d, fused ? on.data() : nullptr,
                               fused ? agg : nullptr, lda, w, agg_init, stream);
     if (rc) return rc;
+    note_use(const_cast<srg_plan*>(plan), static_cast<hipStream_t>(stream));
     if (agg && !fused) {
         rc = srg_hop_accumulate_f32(agg, lda, Y, ldy, plan->n, d, w, agg_init ? SRG_ACC_INIT : SRG_ACC_ADD, stream);
         if (rc) return rc;

@@ -73,6 +73,8 @@ EXPORTED_SYMBOLS = (
     "srg_propagate_khop_f32",
     "srg_propagate_plan_f32",
     "srg_plan_build",
+    "srg_plan_query",
+    "srg_plan_build_in",
     "srg_plan_destroy",
     "srg_plan_describe",
     "srg_plan_launch",
@@ -146,12 +148,16 @@ def _declare(lib):
     lib.srg_propagate_plan_f32.argtypes = [_p, _i32, _i32, _p, _i64, _i32, _i32, _p]
     lib.srg_propagate_plan_f32.restype = ctypes.c_int
     lib.srg_plan_build.argtypes = [_p, _p, _p, _i64, _i32, _i32, _i32, _i64, _i64, _u32, _p, ctypes.POINTER(_p)]
+    lib.srg_plan_query.argtypes = [_p, _i64, _i32, _i32, _i32, _u32, _p, ctypes.POINTER(ctypes.c_size_t),
+                                   ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(_u32), ctypes.POINTER(_i32)]
+    lib.srg_plan_build_in.argtypes = [_p, _p, _p, _i64, _i32, _i32, _i32, _i64, _i64, _u32, _p, ctypes.c_size_t, _p,
+                                      ctypes.c_size_t, _p, ctypes.POINTER(_p)]
     lib.srg_plan_destroy.argtypes = [_p, _p]
     lib.srg_plan_describe.argtypes = [_p, _p]
     lib.srg_plan_launch.argtypes = [_p, _i32, _i32, _p, _p, _p]
     lib.srg_plan_propagate_f32.argtypes = [_p, _p, _i64, _i32, _i32, _u32, _p]
     lib.srg_plan_hop_f32.argtypes = [_p, _p, _i64, _p, _i64, _i32, _u32, _p, _i64, _f32, _i32, _p]
-    for name in ("srg_plan_build", "srg_plan_destroy", "srg_plan_describe", "srg_plan_launch", "srg_plan_propagate_f32",
+    for name in ("srg_plan_build", "srg_plan_query", "srg_plan_build_in", "srg_plan_destroy", "srg_plan_describe", "srg_plan_launch", "srg_plan_propagate_f32",
                  "srg_plan_hop_f32"):
         getattr(lib, name).restype = ctypes.c_int
     lib.srg_cheby_step_f64.argtypes = [_p, _p, _p, _i64, _p, _p, _p, _p, _i64, _i32, ctypes.c_int,

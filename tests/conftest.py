@@ -18,6 +18,17 @@ for p in (PKG, REPO):
 GOLDEN = os.path.join(REPO, "tests", "golden")
 
 
+def progress(msg: str) -> None:
+    """A progress line for long GPU tests, appended to gpurun_out/test_progress.log on the GPU box
+    (pytest captures stdout / stderr; a run that writes nothing for minutes is taken to be hung)."""
+    root = os.environ.get("GRAFT_REPO_ROOT")
+    if not root:
+        return
+    os.makedirs(os.path.join(root, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(root, "gpurun_out", "test_progress.log"), "a") as f:
+        f.write(msg + "\n")
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a HIP (MI355X) device")
     config.addinivalue_line("markers", "slow: long-running")

@@ -79,26 +79,33 @@ def main():
                 comm.destroy()
                 for s in shares:
                     s.destroy()
-    # plans that disagree across ranks (different ghost caps): the exchange must fail, not hang
-    P = 3
-    plans = [HaloPlan(ipn, ixn, n, P, r, chunks=3, ghost_max_degree=(4 if r == 1 else 0), hub_threshold=256)
-             for r in range(P)]
-    shares = [HaloShare(p, vn, 0, d) for p in plans]
-    panels = [[s.new_panel(d) for _ in range(3)] for s in shares]
-    comm = Comm.init_all([0] * P)
-    try:
-        halo_propagate(comm, shares, panels, 2)
-        torch.cuda.synchronize()
-        mismatch = "not detected"
-    except _lib.SrgError as e:
-        mismatch = str(e)
-    finally:
-        comm.destroy()
-        for s in shares:
-            s.destroy()
-    cases.append({"path": "mismatched plans", "error": mismatch})
+    # plans that disagree across ranks: the exchange must fail with the library's own check, not hang.
+    # Different ghost caps (same chunk count: the per-group counts differ) and different chunk counts
+    # (the count messages would differ in length: real RCCL would block, so the fixed-size header
+    # exchanged first must catch it -- ADVICE r5)
+    mismatches = []
+    for what, chunk_of, ghost_of, want in (("ghost caps", lambda r: 3, lambda r: 4 if r == 1 else 0, "plans disagree"),
+                                           ("chunk counts", lambda r: 4 if r == 1 else 3, lambda r: 0, "row chunks")):
+        P = 3
+        plans = [HaloPlan(ipn, ixn, n, P, r, chunks=chunk_of(r), ghost_max_degree=ghost_of(r), hub_threshold=256)
+                 for r in range(P)]
+        shares = [HaloShare(p, vn, 0, d) for p in plans]
+        panels = [[s.new_panel(d) for _ in range(3)] for s in shares]
+        comm = Comm.init_all([0] * P)
+        try:
+            halo_propagate(comm, shares, panels, 2)
+            torch.cuda.synchronize()
+            msg = "not detected"
+        except _lib.SrgError as e:
+            msg = str(e)
+        finally:
+            comm.destroy()
+            for s in shares:
+                s.destroy()
+        cases.append({"path": f"mismatched plans ({what})", "error": msg, "detected_by_library_check": want in msg})
+        mismatches.append(want in msg)
     ok = all(c.get("bitwise_equal_one_gpu", True) and c.get("halo_rows_equal_owners", True) for c in cases) and \
-        mismatch != "not detected"
+        all(mismatches)
     print(json.dumps({"cases": cases, "ok": ok}))
 
 
