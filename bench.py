@@ -37,6 +37,7 @@ Extra objects on the JSON line:
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import shutil
@@ -89,6 +90,10 @@ def parse():
                     help="khop: the K-hop propagate (GraphOp.propagate); wavelet: the heat-wavelet "
                          "Chebyshev filter bank (order 3, scales -0.5/+0.5) applied to the feature panel")
     ap.add_argument("--col-block", type=int, default=None, help="wavelet: column block width")
+    ap.add_argument("--dtype", default="f32", choices=["f32", "f64"],
+                    help="wavelet: f64 = the reference's precision (pygsp cheby_op in fp64, base_model.py:236-265): "
+                         "one srg_cheby_step_f64 launch per order, bit-exact vs the oracle; f32 = the reduced-"
+                         "precision variant (load-balanced SpMM + epilogue)")
     ap.add_argument("--fused-epilogue", action="store_true",
                     help="wavelet: one srg_spmm_cheby_f32 launch per order (two work panels) instead of the "
                          "SpMM + epilogue launches (three work panels); same bits, measured slower")
@@ -301,6 +306,8 @@ def measure_pmc(a):
     env = dict(os.environ, TMPDIR="/tmp")
     probe = None
     sums = {}
+    # the kernel whose traffic is the roofline's: the hop's k_spmm launches, or the fp64 Chebyshev step
+    kern = "k_cheby<double" if (a.op == "wavelet" and a.dtype == "f64") else "k_spmm<"
     try:
         for counter in ("FETCH_SIZE", "WRITE_SIZE"):
             d = os.path.join(out, counter)
@@ -315,7 +322,8 @@ def measure_pmc(a):
             if a.d is not None:
                 cmd += ["--d", str(a.d)]
             if a.op == "wavelet":
-                cmd += ["--op", "wavelet"] + (["--col-block", str(a.col_block)] if a.col_block else [])
+                cmd += ["--op", "wavelet64" if a.dtype == "f64" else "wavelet"] + \
+                    (["--col-block", str(a.col_block)] if a.col_block else [])
             elif a.col_blocks is not None:
                 cmd += ["--col-blocks", str(a.col_blocks)]
             if a.heavy_threshold is not None:
@@ -331,11 +339,11 @@ def measure_pmc(a):
                 with open(f) as fh:
                     for row in csv.DictReader(fh):
                         name = row.get("Kernel_Name", "")
-                        if "k_spmm<" in name and "k_spmm_hub" not in name and row.get("Counter_Name") == counter:
+                        if kern in name and "k_spmm_hub" not in name and row.get("Counter_Name") == counter:
                             total += float(row["Counter_Value"])
                             launches += 1
             if not launches:
-                log(f"pmc pass {counter}: no k_spmm rows")
+                log(f"pmc pass {counter}: no {kern} rows")
                 return None
             sums[counter] = total / probe["reps"]           # KiB per hop (all of a hop's launches)
     except Exception as e:  # noqa: BLE001
@@ -597,6 +605,8 @@ def run_wavelet(a, dev, world=1, rank=0, pmc=None):
     partition, one halo exchange per order, bitwise equal to one GPU)."""
     if world > 1:
         return run_wavelet_dist(a, dev, world, rank)
+    if a.dtype == "f64":
+        return run_wavelet_f64(a, dev, pmc)
     from srgnn import wavelet as W
     from srgnn.csr import DeviceCSR
     from srgnn import _lib
@@ -713,6 +723,141 @@ def run_wavelet(a, dev, world=1, rank=0, pmc=None):
         cb_res["sample"] = "the SpMM part of each Chebyshev order: " + cb_res["sample"]
         res["cpu_baseline"] = cb_res
     print(json.dumps(res), flush=True)
+
+
+def run_wavelet_f64(a, dev, pmc=None):
+    """The filter bank at the reference's precision: pygsp cheby_op is fp64 (SSRG/models/base_scalable/
+    base_model.py:236-265, :243), R_s = sum_k c_{s,k} T_k(L~) S for tau = -0.5, +0.5, order 3.  Each order
+    is one srg_cheby_step_f64 launch (the row-wave gather with the recurrence and every scale's output
+    fused, scipy's operation order: bit-exact vs the oracle's restatement of cheby_op).  The panel is the
+    config's d columns, or -- where five fp64 panels of that width (S, two T work panels, the two scales'
+    R) do not fit -- the widest power-of-two column block that does (RMAT-26): a step then filters that
+    block, and `config.col_block` says so.  value = order * nnz(L) * steps / time.  Parity after the
+    timed steps: every row of two columns of R against oracle.cheby_op (fp64, whole graph) bit for bit.
+    cpu_baseline: the reference's CPU path for one order, scipy's fp64 csr @ dense (pygsp's L.dot), on
+    a row block."""
+    from srgnn import wavelet as W
+    t_build = time.perf_counter()
+    ip, ix, lv, n, d, lmax = graphs.build_laplacian(a.config, dev, d=a.d)
+    nnz = int(ix.numel())
+    order, taus = 3, [-0.5, 0.5]
+    ns = len(taus)
+    filt = W.HeatWaveletFilter.from_device(ip, ix, lv, n, taus, order=order, lmax=lmax, dtype=torch.float64,
+                                           heavy_threshold=a.heavy_threshold)
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    free, _ = torch.cuda.mem_get_info(dev)
+    cb = a.col_block or d
+    while not a.col_block and cb > 1 and (3 + ns) * n * cb * 8 > free - 4 * 2 ** 30:
+        cb //= 2
+    S = synth.uniform_features_t(n, cb, seed=synth.FEATURE_SEED, device=dev).to(torch.float64)
+    R = torch.empty((ns, n, cb), dtype=torch.float64, device=dev)
+    torch.cuda.synchronize()
+    log(f"wavelet f64 {a.config}: n={n} nnz(L)={nnz} d={d} col_block={cb} lmax={lmax} hub={filt.n_hub} "
+        f"heavy={filt.n_heavy} built in {time.perf_counter() - t_build:.1f}s")
+
+    def step():
+        filt.apply(S, split=False, out=R)
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    # roofline: one Chebyshev STEP launch (F T_k - T_{k-1}, both scales' R updated), HIP events on the
+    # launch stream, over work panels of the block's width
+    from srgnn import _lib
+    stream = torch.cuda.current_stream(dev)
+    t_cur, t_old = torch.empty_like(S), torch.empty_like(S)
+    t_cur.copy_(S)
+    t_old.zero_()
+    coef = (ctypes.c_double * ns)(*[float(c) for c in filt.coeffs[:, 2]])
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * a.roofline_reps)]
+    for r in range(a.roofline_reps):
+        ev[2 * r].record(stream)
+        _lib.call(dev, "srg_cheby_step_f64", filt.indptr.data_ptr(), filt.indices.data_ptr(), filt.fvals.data_ptr(), n,
+                  filt.order.data_ptr(), S.data_ptr(), t_old.data_ptr(), t_cur.data_ptr(), cb, cb,
+                  _lib.SRG_CHEBY_STEP, filt.a1, filt.a2, None, coef, ns, R.data_ptr(), n * cb, _lib.stream(dev))
+        ev[2 * r + 1].record(stream)
+    torch.cuda.synchronize()
+    kern_s = float(np.mean([ev[2 * r].elapsed_time(ev[2 * r + 1]) * 1e-3 for r in range(a.roofline_reps)]))
+    del t_cur, t_old
+    b_alg = roofline.cheby_step_bytes_no_reuse_f64(n, nnz, cb, ns)
+    b_comp = roofline.cheby_step_bytes_compulsory_f64(n, nnz, cb, ns)
+    peak = roofline.MI355X_HBM_PEAK_GBS
+    traffic = float(pmc["hbm_bytes_per_hop"]) if pmc is not None else None
+    achieved = (traffic if traffic else b_comp) / kern_s / 1e9
+    # parity: the whole recurrence on two columns, every row, against the oracle's fp64 cheby_op
+    filt.apply(S, split=False, out=R)
+    torch.cuda.synchronize()
+    from oracle import oracle as O
+    cols = [0, cb - 1] if cb > 1 else [0]
+    host = (ip.cpu().numpy(), ix.cpu().numpy(), lv.to(torch.float64).cpu().numpy())
+    want = O.cheby_op(host, filt.coeffs, S[:, cols].cpu().numpy(), lmax)
+    got = R[:, :, cols].cpu().numpy()
+    parity = {"checked": f"every row of R (both scales) in columns {cols}, after the timed steps",
+              "bit_exact": bool(np.array_equal(got.view(np.uint64), want.view(np.uint64))),
+              "checker": "oracle.cheby_op: oracle/srg_oracle.c's fp64 restatement of pygsp cheby_op (scipy's "
+                         "csr_matvecs order), the whole graph"}
+    log(f"parity vs oracle fp64: {parity['bit_exact']}")
+    res = {
+        "metric": "propagated edges/sec (wavelet-basis Chebyshev propagation)",
+        "value": a.steps * order * nnz / dt,
+        "unit": "propagated edges/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "f64",
+        "data": f"synthetic (R-MAT power-law graph with the {a.config} node/edge counts, U[-1,1) features)",
+        "config": {"workload": f"{a.config}-shaped heat-wavelet filter bank, fp64 (the reference's precision)",
+                   "n_nodes": n, "nnz_L": nnz, "d": d, "col_block": cb,
+                   "columns_per_step": cb, "chebyshev_order": order, "scales": taus, "lmax": lmax,
+                   "parallelism": "x1",
+                   "mode": "fp64, one srg_cheby_step_f64 launch per order (SpMM + recurrence + both scales fused)"
+                           + ("" if cb == d else f"; a step filters one {cb}-column block of the {d}-column "
+                                                 "panel (the widest whose five fp64 panels fit)")},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
+                     "frac": achieved / peak, "traffic": traffic,
+                     "achieved_basis": ("L2 -> fabric bytes of one Chebyshev STEP launch (PMC 2 * FETCH_SIZE + "
+                                        "WRITE_SIZE = traffic) / its time" if traffic
+                                        else "compulsory bytes / the launch's time (no counter run: a lower bound)"),
+                     "traffic_source": pmc["source"] if traffic else None,
+                     "unit_of_work": f"one Chebyshev STEP order over a {cb}-column fp64 panel",
+                     "kernel": "k_cheby<double> (srg_cheby_step_f64, SRG_CHEBY_STEP)",
+                     "kernel_ms": kern_s * 1e3,
+                     "frac_no_reuse": b_alg / kern_s / 1e9 / peak, "frac_compulsory": b_comp / kern_s / 1e9 / peak,
+                     "algorithmic_bytes_per_launch": b_alg, "compulsory_bytes_per_launch": b_comp,
+                     "traffic_over_compulsory": (traffic / b_comp) if traffic else None},
+        "parity_vs_oracle": parity,
+        "cpu_baseline": None,
+    }
+    if not a.no_cpu_baseline:
+        log("cpu baseline ...")
+        res["cpu_baseline"] = cpu_baseline_cheby64(host[0], host[1], filt.fvals.cpu().numpy(),
+                                                   S.cpu().numpy(), n, cb, a.cpu_seconds)
+    print(json.dumps(res), flush=True)
+
+
+def cpu_baseline_cheby64(ip, ix, fv, S, n, d, budget_s):
+    """The reference's CPU path for one Chebyshev order at its precision: pygsp cheby_op's
+    `L.dot(T)` is scipy's fp64 csr @ dense (one thread: scipy's csr_matvecs), timed on row blocks of
+    F = (2/a1)(L - a2 I) for ~budget_s."""
+    import scipy.sparse as sp
+    nnz = int(ip[-1])
+    block = max(1, int(n * min(1.0, 5e7 / max(nnz, 1))))
+    edges, t0, r0 = 0, time.perf_counter(), 0
+    while time.perf_counter() - t0 < budget_s:
+        r1 = min(n, r0 + block)
+        e0, e1 = int(ip[r0]), int(ip[r1])
+        A = sp.csr_matrix((fv[e0:e1], ix[e0:e1], ip[r0:r1 + 1] - e0), shape=(r1 - r0, n))
+        _ = A @ S
+        edges += e1 - e0
+        r0 = 0 if r1 == n else r1
+    dt = time.perf_counter() - t0
+    return {"value": edges / dt, "unit": "propagated edges/s", "cores": 1, "kind": "reference",
+            "cpu_model": _cpu_model(),
+            "sample": f"scipy {sp.__name__} fp64 csr @ dense [n, {d}] (pygsp cheby_op's L.dot, base_model.py:243) on "
+                      f"row blocks of ~{block} rows of F for {dt:.1f} s, one thread"}
 
 
 def run_wavelet_dist(a, dev, world, rank):

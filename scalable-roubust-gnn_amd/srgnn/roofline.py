@@ -25,3 +25,15 @@ def bytes_no_reuse(n_rows: int, nnz: int, d: int) -> int:
 def bytes_compulsory(n_rows: int, nnz: int, d: int, n_cols: int | None = None) -> int:
     n_cols = n_rows if n_cols is None else n_cols
     return nnz * 8 + (n_rows + 1) * s_ptr(nnz) + n_rows * 4 * d + n_cols * 4 * d
+
+
+def cheby_step_bytes_no_reuse_f64(n_rows: int, nnz: int, d: int, n_scales: int) -> int:
+    """One fp64 Chebyshev STEP launch (srg_cheby_step_f64: T_{k+1} = F T_k - T_{k-1}, R_s += c_s T_{k+1}),
+    pygsp cheby_op's precision: the SpMM with fp64 values and gathered rows (8 B) plus the epilogue's
+    panel passes -- T_{k-1} read, T_{k+1} written, every scale's R read and written."""
+    return nnz * (4 + 8 + 8 * d) + (n_rows + 1) * 8 + n_rows * 8 * d * (2 + 2 * n_scales)
+
+
+def cheby_step_bytes_compulsory_f64(n_rows: int, nnz: int, d: int, n_scales: int) -> int:
+    """cheby_step_bytes_no_reuse_f64 with T_k read once."""
+    return nnz * (4 + 8) + (n_rows + 1) * 8 + n_rows * 8 * d * (3 + 2 * n_scales)

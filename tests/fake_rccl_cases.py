@@ -80,16 +80,26 @@ def main():
                 for s in shares:
                     s.destroy()
     # plans that disagree across ranks: the exchange must fail with the library's own check, not hang.
-    # Different ghost caps (same chunk count: the per-group counts differ) and different chunk counts
-    # (the count messages would differ in length: real RCCL would block, so the fixed-size header
-    # exchanged first must catch it -- ADVICE r5)
+    #  * ghost caps (same chunk count): the per-group counts differ -> verify_counts' second exchange;
+    #  * graphs (rank 1 planned another graph, same n and chunks): n / nnz differ -> the fixed-size header
+    #    verify_counts exchanges FIRST (its length never depends on the plan, so ranks whose
+    #    plans have different chunk counts -- count messages of different lengths, which real RCCL would
+    #    block on -- still exchange matching messages and fail);
+    #  * chunk counts: in ONE process the shares are side by side and srg_halo_propagate_f32's host check
+    #    sees them first; across processes (one share each) it is the header above that catches them.
+    ip2, ix2, vals2, _ = graph(20000, 200000, 64, 6)
+    ip2n, ix2n, v2n = ip2.cpu().numpy(), ix2.cpu().numpy(), vals2.cpu().numpy()
+    assert ix2n.size != ixn.size
     mismatches = []
-    for what, chunk_of, ghost_of, want in (("ghost caps", lambda r: 3, lambda r: 4 if r == 1 else 0, "plans disagree"),
-                                           ("chunk counts", lambda r: 4 if r == 1 else 3, lambda r: 0, "row chunks")):
+    for what, chunk_of, ghost_of, graph_of, want in (
+            ("ghost caps", lambda r: 3, lambda r: 4 if r == 1 else 0, lambda r: 0, "plans disagree"),
+            ("graphs", lambda r: 3, lambda r: 0, lambda r: 1 if r == 1 else 0, "plan is of a graph"),
+            ("chunk counts", lambda r: 4 if r == 1 else 3, lambda r: 0, lambda r: 0, "different chunk counts")):
         P = 3
-        plans = [HaloPlan(ipn, ixn, n, P, r, chunks=chunk_of(r), ghost_max_degree=ghost_of(r), hub_threshold=256)
-                 for r in range(P)]
-        shares = [HaloShare(p, vn, 0, d) for p in plans]
+        g_of = [(ipn, ixn, vn), (ip2n, ix2n, v2n)]
+        plans = [HaloPlan(g_of[graph_of(r)][0], g_of[graph_of(r)][1], n, P, r, chunks=chunk_of(r),
+                          ghost_max_degree=ghost_of(r), hub_threshold=256) for r in range(P)]
+        shares = [HaloShare(p, g_of[graph_of(r)][2], 0, d) for r, p in enumerate(plans)]
         panels = [[s.new_panel(d) for _ in range(3)] for s in shares]
         comm = Comm.init_all([0] * P)
         try:

@@ -6,8 +6,9 @@ per process, so the fake cannot share a process with the real one) and runs test
     P = 2, 3, 8, uneven and empty row blocks;
   * srg_halo_propagate_f32 through its RCCL branch (grouped ncclSend / ncclRecv per group, the
     offsets a real node uses) at P = 2, 3, 8, with and without ghost rows, X's halo exchanged or filled;
-  * plans built with different arguments on different ranks (ghost caps; chunk counts, whose count
-    messages would differ in length -- ADVICE r5): the library's own check fails them, not a hang.
+  * plans built with different arguments on different ranks (ghost caps; graphs, caught by the
+    fixed-size header exchanged before the per-group counts -- ADVICE r5; chunk counts): the library's
+    own checks fail them, not a hang.
 Every rank's rows of every hop are bitwise the one-GPU hops."""
 import json
 import os
@@ -33,7 +34,7 @@ def test_rccl_paths_with_several_ranks_on_one_gpu():
         assert c.get("bitwise_equal_one_gpu", True), c
         assert c.get("halo_rows_equal_owners", True), c
     mism = [c for c in res["cases"] if c["path"].startswith("mismatched plans")]
-    assert len(mism) == 2, mism
+    assert len(mism) == 3, mism
     for c in mism:
         # SRG_ERR_INVALID from verify_counts, not the stand-in's ncclInvalidUsage
         assert c["detected_by_library_check"] and "fake_rccl" not in c["error"], c

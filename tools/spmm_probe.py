@@ -36,13 +36,44 @@ ap.add_argument("--col-blocks", type=int, default=None, help="column blocks per 
 ap.add_argument("--d", type=int, default=None, help="panel width (default: the config's)")
 ap.add_argument("--hops", type=int, default=1 << 30,
                 help="hops the operator serves (bench.py: K x (steps + warmup)); picks spans or compact blocks")
-ap.add_argument("--op", default="khop", choices=["khop", "wavelet"],
+ap.add_argument("--op", default="khop", choices=["khop", "wavelet", "wavelet64"],
                 help="wavelet: the Chebyshev STEP operator F = (2/a1)(L - a2 I) of the config's Laplacian "
                      "on a --col-block wide panel (bench.py --op wavelet's SpMM launches)")
 ap.add_argument("--col-block", type=int, default=None,
                 help="wavelet: column block width (default: bench.py's rule, the widest whose work panels fit)")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
+if a.op == "wavelet64":
+    # bench.py --op wavelet --dtype f64's roofline launch: one fp64 Chebyshev STEP (srg_cheby_step_f64)
+    # over the block width bench.py picks (the widest whose five fp64 panels fit), `reps` times
+    import ctypes
+    from srgnn import _lib
+    from srgnn import wavelet as W
+    ip, ix, lv, n, d, lmax = graphs.build_laplacian(a.config, dev, d=a.d)
+    filt = W.HeatWaveletFilter.from_device(ip, ix, lv, n, [-0.5, 0.5], order=3, lmax=lmax, dtype=torch.float64,
+                                           heavy_threshold=a.heavy_threshold)
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    free, _ = torch.cuda.mem_get_info(dev)
+    cb = a.col_block or d
+    while not a.col_block and cb > 1 and 5 * n * cb * 8 > free - 4 * 2 ** 30:
+        cb //= 2
+    S = synth.uniform_features_t(n, cb, device=dev).to(torch.float64)
+    R = torch.zeros((2, n, cb), dtype=torch.float64, device=dev)
+    To, Tn = torch.zeros_like(S), torch.empty_like(S)
+    coef = (ctypes.c_double * 2)(*[float(c) for c in filt.coeffs[:, 2]])
+    torch.cuda.synchronize()
+    for _ in range(a.reps):
+        _lib.call(dev, "srg_cheby_step_f64", filt.indptr.data_ptr(), filt.indices.data_ptr(), filt.fvals.data_ptr(), n,
+                  filt.order.data_ptr(), S.data_ptr(), To.data_ptr(), Tn.data_ptr(), cb, cb, _lib.SRG_CHEBY_STEP,
+                  filt.a1, filt.a2, None, coef, 2, R.data_ptr(), n * cb, _lib.stream(dev))
+    torch.cuda.synchronize()
+    nnz = int(ix.numel())
+    print(json.dumps({"config": a.config, "op": "wavelet64", "n": n, "nnz": nnz, "d": cb, "reps": a.reps,
+                      "launches_per_hop": 1, "column_blocks": 1, "n_heavy": filt.n_heavy, "n_hub": filt.n_hub,
+                      "algorithmic_bytes": roofline.cheby_step_bytes_no_reuse_f64(n, nnz, cb, 2),
+                      "compulsory_bytes": roofline.cheby_step_bytes_compulsory_f64(n, nnz, cb, 2)}))
+    sys.exit(0)
 if a.op == "wavelet":
     from srgnn import wavelet as W
     ip, ix, lv, n, d, lmax = graphs.build_laplacian(a.config, dev, d=a.d)
