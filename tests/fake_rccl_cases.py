@@ -87,7 +87,7 @@ def main():
     #    block on -- still exchange matching messages and fail);
     #  * chunk counts: in ONE process the shares are side by side and srg_halo_propagate_f32's host check
     #    sees them first; across processes (one share each) it is the header above that catches them.
-    ip2, ix2, vals2, _ = graph(20000, 200000, 64, 6)
+    ip2, ix2, vals2, _ = graph(20000, 199000, 64, 6)
     ip2n, ix2n, v2n = ip2.cpu().numpy(), ix2.cpu().numpy(), vals2.cpu().numpy()
     assert ix2n.size != ixn.size
     mismatches = []
