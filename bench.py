@@ -412,7 +412,7 @@ def one_shot(ip, ix, vals, n, X, K, dev, heavy_threshold=None):
     (SSRG/tasks/node_classification.py:62), i.e. ONE propagate(K) on a freshly built operator.  Here:
     a fresh DeviceCSR from the device arrays (validated; its row schedule is left to first use),
     srgnn.spmm.propagate laying it out for a K-hop run with the native planner (srg_plan_build: column
-    blocks, compact launch-ordered copies from spmm.MIN_HOPS_TO_COMPACT hops) and the K output panels
+    blocks, compact launch-ordered copies from SRG_PLAN_MIN_HOPS_TO_COMPACT hops) and the K output panels
     allocated inside the bracket; HIP events on the launch stream plus the host wall clock around it.
     Â and X already resident (GraphOp.propagate's construct_adj and H2D / D2H are tools/e2e_api.py's)."""
     from srgnn.csr import DeviceCSR
@@ -629,24 +629,19 @@ def run_wavelet(a, dev, world=1, rank=0, pmc=None):
     # gather more bytes per nonzero (RMAT-26: 64 columns 1.37 s per step, 32 columns 1.87 s)
     while not a.col_block and cb > 8 and n_work * n * cb * 4 > free - 2 ** 30:
         cb //= 2
-    layout = "native plan"
+    from srgnn.plan import _torch_free
     while True:
-        # the layout of L and F for cb-column panels: the native plans hold device memory of their own,
-        # so where the work panels no longer fit beside them, the torch formulation of the same blocks
-        # (its arrays in torch's cache, which the graph build left fragmented), then narrower blocks
-        native = layout == "native plan"
-        filt.prepare_column_blocks(cb, hops=order * (d // cb) * (a.steps + a.warmup), native=native)
+        # the native plans of L and F for cb-column panels; their memory comes from torch's cache (which
+        # the graph build left fragmented), so what must still fit is the work panels: narrower blocks
+        # until they do
+        filt.prepare_column_blocks(cb, hops=order * (d // cb) * (a.steps + a.warmup))
         torch.cuda.synchronize()
-        free, _ = torch.cuda.mem_get_info(dev)
-        if a.col_block or cb <= 8 or n_work * n * cb * 4 <= free - 2 ** 30:
+        if a.col_block or cb <= 8 or n_work * n * cb * 4 <= _torch_free(dev) - 2 ** 30:
             break
         filt.drop_layouts()
         torch.cuda.synchronize()
-        if native:
-            layout = "torch blocks"
-        else:
-            layout = "native plan"
-            cb //= 2
+        cb //= 2
+    layout = "native plan (in torch's caching allocator)"
     log(f"wavelet {a.config}: n={n} nnz(L)={nnz} d={d} lmax={lmax} col_block={cb} layout={layout} "
         f"hub={filt.n_hub} heavy={filt.n_heavy} built in {time.perf_counter() - t_build:.1f}s")
 

@@ -205,7 +205,8 @@ int srg_propagate_plan_f32(const srg_hop_launch* launches, int32_t n_launch, int
  * a column block's), SRG_PLAN_NONE (no such rows) or a row length that holds for every launch, as a
  * DeviceCSR built with explicit thresholds schedules its blocks (srgnn.csr.make_schedule). */
 typedef struct srg_plan srg_plan;
-#define SRG_PLAN_MIN_HOPS_TO_COMPACT 6
+#define SRG_PLAN_MIN_HOPS_TO_CUT 4       /* automatic column blocks for runs of at least this many hops */
+#define SRG_PLAN_MIN_HOPS_TO_COMPACT 6   /* automatic compact copies (when they fit) from this many */
 #define SRG_PLAN_COMPACT 0x1u        /* copy the entries in launch order whatever the run length */
 #define SRG_PLAN_SPANS 0x2u          /* never copy: spans of the caller's arrays */
 #define SRG_PLAN_SPLIT_BLOCK0 0x4u   /* block 0 as two launches (default: panels < 16 GiB) */

@@ -16,10 +16,11 @@
 //     launch's rows in its schedule order, so no cache line of the streams is read by two launches;
 //   * spans by schedule slot (the packed light rows read consecutive slots);
 //   * hub spans chained on the side stream when every launch over cut rows has the same hub rows.
-// This is srgnn/spmm.py prepare + _hop_plan (the torch formulation kept for the aggregation and
-// wavelet paths), restated as one radix sort of (launch, span length) keys over every launch's rows,
-// one scan of the lengths (the copy positions and each launch's nnz) and one copy pass; two host
-// synchronisations (the degree statistics; the per-launch counts, checked before any span is derived).
+// The package's only layout code (round 6: srgnn.spmm / srgnn.plan call this; the torch formulation that
+// used to be built beside it is a test restatement now, tests/plan_layout_ref.py): one radix sort of
+// (launch, span length) keys over every launch's rows, one scan of the lengths (the copy positions and
+// each launch's nnz) and one copy pass; two host synchronisations (the degree statistics; the per-launch
+// counts, checked before any span is derived).
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -115,15 +116,15 @@ int pfail(int code, const char* fmt, ...)
             return pfail(SRG_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(e_));            \
     } while (0)
 
-// the constants of srgnn/csr.py and srgnn/spmm.py (DESIGN.md §3 has the measurements)
-constexpr int64_t kWholeMax = 48;              // csr.BLOCK_WHOLE_MAX
-constexpr int64_t kBlockHeavyPer = 30000;      // csr.BLOCK_HEAVY_PER
-constexpr int64_t kNarrowHeavy = 32;           // csr.NARROW_HEAVY_THRESHOLD
-constexpr int kMinHopsToCut = 4;               // spmm.MIN_HOPS_TO_CUT
-constexpr int64_t kSplitBlock0MaxPanel = 16ll << 30;   // spmm.SPLIT_BLOCK0_MAX_PANEL
-constexpr int64_t kCapWavesMinPanel = 512ll << 20;     // spmm.CAP_WAVES_MIN_PANEL
+// The layout's constants (DESIGN.md §5.1 has the measurements behind each; srgnn.csr keeps kWholeMax and
+// the narrow threshold for the halo planner's chunks and the one-launch schedule of a DeviceCSR)
+constexpr int64_t kWholeMax = 48;              // rows this short run whole in block 0
+constexpr int64_t kBlockHeavyPer = 30000;      // a column block's slice-wave rows: > nnz_b / this entries
+constexpr int64_t kNarrowHeavy = 32;           // slice-wave rows of narrow panels (d <= 32)
+constexpr int64_t kSplitBlock0MaxPanel = 16ll << 30;   // block 0 as two launches below this panel size
+constexpr int64_t kCapWavesMinPanel = 512ll << 20;     // the row kernel's occupancy cap from this panel size
 constexpr int kMaxBlocks = 64;
-// automatic blocks for panels of 512 MiB .. 16 GiB at d >= 64: one per ~100 MiB, 12 to 16 (spmm.auto_col_blocks).
+// automatic blocks for panels of 512 MiB .. 16 GiB at d >= 64: one per ~100 MiB, 12 to 16.
 // Round 5, with the packed rows' id staging and gather pipeline (profiles/r05bn_col_blocks_final_kernels.txt):
 // products d = 64 (0.63 GB) 3.37 / 3.13 / 3.08 ms per hop at 4 / 8 / 12 blocks, d = 128 (1.25 GB)
 // 5.23 / 5.16 / 5.15 / 5.19 / 5.25 at 8 / 10 / 12 / 14 / 16, d = 256 (2.5 GB) 11.73 / 11.18 / 11.00 / 11.20
@@ -652,7 +653,7 @@ static int build_impl(const int64_t* indptr, const int32_t* indices, const float
         if (d < 64 || panel < (512ll << 20)) B = 1;
         else if (panel >= kSplitBlock0MaxPanel) B = 4;
         else B = (int)std::min<int64_t>(kAutoBlocksMax, std::max<int64_t>(kAutoBlocksMin, (int64_t)std::nearbyint((double)panel / (100 << 20))));
-        if (hops < kMinHopsToCut) B = 1;
+        if (hops < SRG_PLAN_MIN_HOPS_TO_CUT) B = 1;
     }
     if (n == 0 || nnz == 0) B = 1;
     P->B = B;
@@ -991,7 +992,7 @@ int srg_plan_describe(const srg_plan* plan, srg_plan_desc* desc)
 #define SRG_PLAN_GRAPHS 1
 #endif
 
-// the launches of one hop over a d-column panel (spmm._hop_plan's flags); returns whether the hub side
+// the launches of one hop over a d-column panel with their flags; returns whether the hub side
 // stream must be joined at the end of each hop
 static int plan_launches(const srg_plan* P, int32_t d, uint32_t flags, std::vector<srg_hop_launch>& out)
 {

@@ -42,6 +42,7 @@ SRG_TAIL_MAX = 32
 
 SRG_SPGEMM_SERIAL_B = 0x1
 
+SRG_PLAN_MIN_HOPS_TO_CUT = 4
 SRG_PLAN_MIN_HOPS_TO_COMPACT = 6
 SRG_PLAN_COMPACT = 0x1
 SRG_PLAN_SPANS = 0x2

@@ -35,11 +35,12 @@ DEFAULT_HEAVY_THRESHOLD = None
 # r02_ab_auto.txt: d = 8 hop 3.34 ms at 32 vs 3.76 at the wide auto threshold; the RMAT-26 wavelet
 # in 32-column blocks 63.8 vs 98.9 ms per block).  Used when the wide threshold is automatic.
 NARROW_HEAVY_THRESHOLD = 32
-# Column blocks: rows of at most this many nonzeros are not cut but computed whole in block 0
-# (DeviceCSR.column_blocks); 0 cuts every row.
-# Round 4: 48 (products 5.63 -> 5.58 ms per hop at six blocks, 5.53 at seven; 64: the same, 96: 5.62;
-# papers100M 236.7 -> 236.1 ms, RMAT-26 307.6 -> 307.1; profiles/r04ag_*, r04ah_*).  Round 2: 32.
-BLOCK_WHOLE_MAX = 48             # = kBlockWholeMax of the C halo planner (srg_halo.hip)
+# Column blocks of the halo partition's row chunks (srgnn.dist.HaloPartitionedOperator.chunk_blocks):
+# rows of at most this many nonzeros are not cut but computed whole in block 0; 0 cuts every row.  The
+# one-GPU plan's rule (kWholeMax, csrc/srg_plan.hip) and the C halo planner's (kBlockWholeMax,
+# srg_halo.hip) are the same 48 (round 4: products 5.63 -> 5.58 ms per hop at six blocks, 5.53 at seven;
+# 64: the same, 96: 5.62; profiles/r04ag_*, r04ah_*).
+BLOCK_WHOLE_MAX = 48
 # "auto": rows whose slice-wave time (~40 ns per nonzero, measured) would exceed about half of the
 # expected hop time (~nnz / 13.5e9 s at the measured hop rate) go to the hub path:
 # threshold = nnz // 1024, at least 8192.  Products on 1 GPU -> only the top hub; 1/8 of it -> ~15 K.
@@ -96,19 +97,17 @@ class DeviceCSR:
     _n_heavy: int | None
     _n_hub: int | None = 0
     _n_heavy_narrow: int | None = None   # slice-wave rows for d <= 32 (None: n_heavy)
-    # row spans (a column block, column_blocks()): row r's entries are [indptr[r], row_end[r]) of
-    # indices / values, and indptr holds n_rows starts instead of n_rows + 1 pointers
+    # row spans (a column block of the halo partition's row chunks, srgnn.dist): row r's entries are
+    # [indptr[r], row_end[r]) of indices / values, and indptr holds n_rows starts instead of n_rows + 1
+    # pointers
     row_end: torch.Tensor | None = None
-    # column block 0 only: rows this block computes whole (short rows are not cut: the later blocks
-    # do not schedule them, so their Y is written once instead of written, read and written again)
-    whole_rows: torch.Tensor | None = None
     # rows of the output panel a launch may write: the schedule (`order`) names row ids of the whole
     # operator, so a column block or a row group that schedules a subset of the rows still writes
     # rows up to row_space - 1 (None: n_rows, a schedule that is a permutation of the rows)
     row_space: int | None = None
     # the thresholds the schedule was built with (None = automatic), reused by column blocks
     thresholds: tuple = (None, None)
-    _blocks: dict = field(default_factory=dict, repr=False, compare=False)   # column_blocks() cache
+    _blocks: dict = field(default_factory=dict, repr=False, compare=False)   # cached plans (srgnn.plan)
 
     def _schedule(self) -> None:
         heavy_t, hub_t = self.thresholds
@@ -166,8 +165,8 @@ class DeviceCSR:
         return self.out_rows != self.n_rows
 
     def drop_blocks(self) -> None:
-        """Frees the cached layouts: column blocks (compact copies hold one more copy of the ids and
-        values) and native plans (srgnn.plan; released in stream order)."""
+        """Frees the cached layouts: the native plans (srgnn.plan; compact ones hold one more copy of
+        the ids and values), released after every stream their work went to."""
         for v in list(self._blocks.values()):
             if hasattr(v, "close"):
                 v.close()
@@ -228,163 +227,6 @@ class DeviceCSR:
                                 np.asarray(adj.data),   # cast to fp32 on the device (round to nearest, as astype)
                                 n_cols=adj.shape[1], heavy_threshold=heavy_threshold, device=device)
 
-    def column_blocks(self, B: int):
-        """B operators over the same rows: block b holds, as a span of each row, the row's entries
-        whose column ids lie in [ceil(b * n_cols / B), ceil((b + 1) * n_cols / B)), each block with
-        its own schedule (or None for an empty operator or B < 2).
-
-        A hop is then block 0 from +0.0f and blocks 1..B-1 with ACCUMULATE: each output element is
-        the same fma chain over the same entries in the same order, continued from the fp32 value
-        the previous block stored, so the result is bitwise the one-launch hop.  Â from
-        construct_adj has sorted column ids (utils.py:81-93 builds a canonical transpose), so a
-        block is one span of every row: the blocks share indices / values and hold only their
-        split points (srg_csr_col_splits, one binary search per row and boundary; an n_rows int64
-        array per boundary).  Rows with unsorted ids still split into spans that partition them in
-        CSR order -- exact, only without the locality.  Cached per B (compact blocks, once made by
-        compact_column_blocks, are returned instead)."""
-        B = int(B)
-        if B in self._blocks:
-            return self._blocks[B]
-        if self.is_span:
-            raise ValueError("column_blocks of a column block")
-        if B < 2 or self.n_rows == 0 or self.nnz == 0:
-            self._blocks[B] = None
-            return None
-        ip, n = self.indptr, self.n_cols
-        dev = ip.device
-        splits = torch.empty((B - 1, self.n_rows), dtype=torch.int64, device=dev)
-        _lib.call(dev, "srg_csr_col_splits", ip.data_ptr(), self.indices.data_ptr(), self.n_rows, n, B,
-                  splits.data_ptr(), _lib.stream(dev))
-        whole = (ip[1:] - ip[:-1]) <= BLOCK_WHOLE_MAX if BLOCK_WHOLE_MAX > 0 else None
-        if whole is not None:
-            # short rows run whole in block 0: their later spans are empty and not scheduled
-            splits = torch.where(whole.unsqueeze(0), ip[1:].unsqueeze(0), splits)
-            later = torch.nonzero(~whole).squeeze(1)
-        bounds = [ip[:-1]] + [splits[b] for b in range(B - 1)] + [ip[1:]]
-        heavy_t, hub_t = self.thresholds
-        auto_narrow = self.n_heavy_narrow is not None      # the parent's narrow split is automatic
-        out = []
-        for b in range(B):
-            beg, end = bounds[b], bounds[b + 1]
-            deg = end - beg
-            nnz_b = int(deg.sum().item())
-            sel = deg[later] if (b > 0 and whole is not None) else deg
-            order, n_heavy, n_hub = schedule_from_degrees(sel, nnz_b, heavy_t, hub_t, block=True)
-            if b > 0 and whole is not None:
-                order = later[order.to(torch.int64)].to(torch.int32)
-            narrow = narrow_heavy_degrees(sel, n_hub) if auto_narrow else None
-            out.append(DeviceCSR(beg, self.indices, self.values, int(sel.numel()), n, order, n_heavy, n_hub, narrow,
-                                 row_end=end, whole_rows=whole if b == 0 else None, row_space=self.n_rows,
-                                 thresholds=self.thresholds))
-        self._blocks[B] = out
-        return out
-
-    def split_whole(self):
-        """Column block 0 as two schedules over the same arrays: (the cut rows' first spans, the
-        rows it computes whole) -- for a hop whose aggregation epilogue must run in the launch
-        that finishes each row (srgnn.spmm.hop with agg).  Cached."""
-        if self.whole_rows is None:
-            return None
-        if "split" not in self._blocks:
-            parts = []
-            for sel in (~self.whole_rows, self.whole_rows):
-                rows = torch.nonzero(sel).squeeze(1)
-                ip = self.indptr
-                deg = ((self.row_end - ip) if self.is_span else (ip[1:] - ip[:-1]))[rows]
-                heavy_t, hub_t = self.thresholds
-                order, n_heavy, n_hub = schedule_from_degrees(deg, int(deg.sum().item()), heavy_t, hub_t,
-                                                              block=True)
-                order = rows[order.to(torch.int64)].to(torch.int32)
-                narrow = narrow_heavy_degrees(deg, n_hub) if self.n_heavy_narrow is not None else None
-                parts.append(DeviceCSR(self.indptr, self.indices, self.values, int(rows.numel()), self.n_cols, order,
-                                       n_heavy, n_hub, narrow, row_end=self.row_end, row_space=self.out_rows,
-                                       thresholds=self.thresholds))
-            self._blocks["split"] = tuple(parts)
-        return self._blocks["split"]
-
-    def slot_spans(self):
-        """(beg, end) int64 [n_rows]: the span of the row in each schedule slot (span operators).
-        Cached."""
-        if "slots" not in self._blocks:
-            o = self.order.to(torch.int64)
-            self._blocks["slots"] = (self.indptr[o].contiguous(), self.row_end[o].contiguous())
-        return self._blocks["slots"]
-
-    def _copy_in_order(self, rows: torch.Tensor):
-        """(beg, end, indices, values): the entries of `rows` (int64 row ids) copied out one row after
-        the other in that order, row r's at [beg[r], end[r]) of the copies (rows not listed: empty)."""
-        ip = self.indptr
-        dev = ip.device
-        b0 = ip[rows]
-        deg = (self.row_end[rows] if self.is_span else ip[rows + 1]) - b0
-        pos = torch.zeros(rows.numel() + 1, dtype=torch.int64, device=dev)
-        torch.cumsum(deg, 0, out=pos[1:])
-        nnz = int(pos[-1].item())
-        beg = torch.zeros(self.out_rows, dtype=torch.int64, device=dev)
-        end = torch.zeros(self.out_rows, dtype=torch.int64, device=dev)
-        if self.indices.dtype != torch.int32 or self.values.dtype != torch.float32:
-            # entry e of the copy is entry b0[i] + (e - pos[i]) of row i of the list
-            idx = torch.repeat_interleave(b0 - pos[:-1], deg, output_size=nnz)
-            idx += torch.arange(nnz, dtype=torch.int64, device=dev)
-            beg[rows] = pos[:-1]
-            end[rows] = pos[1:]
-            return beg, end, self.indices[idx], self.values[idx]
-        ix = torch.empty(nnz, dtype=self.indices.dtype, device=dev)
-        v = torch.empty(nnz, dtype=self.values.dtype, device=dev)
-        # srg_csr_copy_spans: one pass over the spans (the torch formulation, an int64 gather index of
-        # nnz entries built with repeat_interleave, took 4.6 ms more on products' six blocks)
-        order = rows.to(torch.int32).contiguous()
-        row_end = self.row_end if self.is_span else ip[1:]
-        _lib.call(dev, "srg_csr_copy_spans", order.data_ptr(), order.numel(), ip.data_ptr(), row_end.data_ptr(),
-                  self.indices.data_ptr(), self.values.data_ptr(), pos.data_ptr(), ix.data_ptr(), v.data_ptr(),
-                  beg.data_ptr(), end.data_ptr(), _lib.stream(dev))
-        return beg, end, ix, v
-
-    def schedule_ordered(self) -> "DeviceCSR":
-        """This operator with its entries copied out in the order its launch takes the rows (its
-        schedule): a span operator over the copy, the same entries in the same order per row, so the
-        same bits.  For a long-lived one-launch operator (spmm.propagate), as compact_column_blocks
-        is for blocked ones.  Cached."""
-        if "sched" not in self._blocks:
-            beg, end, ix, v = self._copy_in_order(self.order.to(torch.int64))
-            self._blocks["sched"] = DeviceCSR(beg, ix, v, self.n_rows, self.n_cols, self.order, self.n_heavy, self.n_hub,
-                                              self.n_heavy_narrow, row_end=end, row_space=self.out_rows,
-                                              thresholds=self.thresholds)
-        return self._blocks["sched"]
-
-    def compact_column_blocks(self, B: int):
-        """column_blocks(B) with each block's entries copied into arrays of its own, laid out in the
-        order its launches take the rows: block b's schedule, and for block 0 the schedule of its
-        cut rows' spans followed by that of its whole rows (its two launches, split_whole()).  One
-        more copy of the ids and values (1 GB on products), for operators that serve many hops
-        (spmm.MIN_HOPS_TO_COMPACT): no cache line of the id / value streams is read by two launches
-        (45.4 -> 44.9 GB per hop on products, round 2), and the consecutive rows a wave takes read
-        consecutive entries (round 3, tools/whole_rows_probe.py --sched: the whole-row launch 0.898
-        -> 0.862 ms, block 0's cut spans 1.339 -> 1.301, a later block 1.399 -> 1.384).  Each block
-        is a span operator over its copy; the same entries in the same order per row, so the same
-        bits as the spans."""
-        B = int(B)
-        key = ("compact", B)
-        blocks = self.column_blocks(B)
-        if not blocks or self._blocks.get(key):
-            return blocks
-        out = []
-        for blk in blocks:
-            parts = blk.split_whole() if blk.whole_rows is not None else None
-            rows = torch.cat([parts[0].order, parts[1].order]) if parts else blk.order
-            beg, end, ix, v = blk._copy_in_order(rows.to(torch.int64))
-            nb = DeviceCSR(beg, ix, v, blk.n_rows, self.n_cols, blk.order, blk.n_heavy, blk.n_hub, blk.n_heavy_narrow,
-                           row_end=end, whole_rows=blk.whole_rows, row_space=blk.row_space, thresholds=blk.thresholds)
-            if parts:
-                nb._blocks["split"] = tuple(
-                    DeviceCSR(beg, ix, v, p.n_rows, self.n_cols, p.order, p.n_heavy, p.n_hub, p.n_heavy_narrow,
-                              row_end=end, row_space=p.row_space, thresholds=p.thresholds) for p in parts)
-            out.append(nb)
-            del beg, end, ix, v
-        self._blocks[B] = out
-        self._blocks[key] = True
-        return out
-
     def rows(self, r0: int, r1: int, heavy_threshold=None, hub_threshold=None) -> "DeviceCSR":
         """Row block [r0, r1) with rebased row pointers (global column ids kept)."""
         if self.is_span:
@@ -424,25 +266,12 @@ def make_schedule(indptr: torch.Tensor, heavy_threshold=None, hub_threshold=None
                                  heavy_threshold, hub_threshold)
 
 
-# Column blocks' spans take the slice waves above nnz_b / BLOCK_HEAVY_PER entries.  Round 3 (five
-# blocks): 300-500 best, 6.13 ms per hop; 160: 6.43, 600: 6.19 (profiles/r03_ab_heavy_threshold_B5.txt).
-# Round 4, with the slice waves' id prefetch and the occupancy cap, longer packed spans pay: products
-# (six blocks, nnz_b ~ 19 M) 5.79 ms at 60000 (~320 entries), 5.62-5.64 at 30000 / 20000 / 15000
-# (650-1300; 2000+ entries: 6.84); papers100M 239.0 -> 237.4 ms, RMAT-26 307.7 -> 306.2
-# (profiles/r04ab_*, r04ac_*, r04ad_*).  At eight blocks (nnz_b ~ 14.5 M, shorter launches) the cliff
-# comes sooner: 5.51 ms at 30000 and 20000 (~485 / ~730 entries), 7.04 at 12000 (~1200;
-# r04ap_*), so 30000 keeps the margin.
-BLOCK_HEAVY_PER = 30000
-
-
-def schedule_from_degrees(deg: torch.Tensor, nnz: int, heavy_threshold=None, hub_threshold=None,
-                          block: bool = False):
-    """make_schedule from the row lengths `deg` (nnz = their sum, for the automatic thresholds);
-    block: the lengths are a column block's spans (BLOCK_HEAVY_PER for the automatic heavy split)."""
+def schedule_from_degrees(deg: torch.Tensor, nnz: int, heavy_threshold=None, hub_threshold=None):
+    """make_schedule from the row lengths `deg` (nnz = their sum, for the automatic thresholds)."""
     if heavy_threshold is None:
         heavy_threshold = DEFAULT_HEAVY_THRESHOLD
     if heavy_threshold is None:
-        heavy_threshold = max(96, int(nnz) // BLOCK_HEAVY_PER) if block else auto_heavy_threshold(nnz)
+        heavy_threshold = auto_heavy_threshold(nnz)
     if hub_threshold is None:
         hub_threshold = DEFAULT_HUB_THRESHOLD
     if hub_threshold is None:

@@ -395,7 +395,7 @@ class HaloPartitionedOperator:
         ACCUMULATE, so each row is the same fma chain in the same order: bitwise the unblocked
         chunk.  Rows of <= csr.BLOCK_WHOLE_MAX entries are computed whole in block 0.  Each launch
         gathers from 1 / B of the global columns, so the caches hold B times as many of the rows
-        it reads (one GPU: csr.DeviceCSR.column_blocks).  Cached per B."""
+        it reads (one GPU: the plan's column blocks, srg_plan_build).  Cached per B."""
         B = self._col_blocks_for(d)
         if B < 2:
             return None

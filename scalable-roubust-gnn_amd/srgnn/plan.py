@@ -1,17 +1,21 @@
-"""The native one-GPU planner (srg_plan_build / srg_plan_propagate_f32, csrc/srg_plan.hip) for a DeviceCSR.
+"""The one-GPU planner (srg_plan_query / srg_plan_build_in / srg_plan_propagate_f32, csrc/srg_plan.hip) for a
+DeviceCSR -- the only layout code of the package (round 6: the torch formulation of the same layout
+lives on as a test restatement, tests/plan_layout_ref.py).
 
-srgnn.spmm.prepare / propagate run their K-hop loops through it, and spmm.hop (the aggregation and
-wavelet hop loops, the host-copy loop of GraphOp.propagate) its single hops, with the aggregation
-epilogue where asked (srg_plan_hop_f32): the column blocks, block 0's split, the per-launch schedules,
-the hub chain, the spans by slot and the compact launch-ordered copies are built on the device in one
-pass (a radix sort of (launch, span length) keys, one scan, one copy) -- the layout
-DeviceCSR.column_blocks / compact_column_blocks / split_whole + spmm._hop_plan build with torch (kept
-for layout experiments with other constants, and as the layout tests' reference).  C / C++ hosts call
-the same entry points (examples/plan_propagate.c).
+srgnn.spmm.prepare / propagate / hop and everything above them (the aggregation and wavelet hop loops,
+GraphOp.propagate) run through it: the column blocks, block 0's split, the per-launch schedules, the
+hub chain, the spans by slot and the compact launch-ordered copies are built on the device in one pass
+(a radix sort of (launch, span length) keys, one scan, one copy).  The plan's memory comes from torch's
+caching allocator (srg_plan_query sizes it, srg_plan_build_in builds into it), so a plan competes for
+the same cached blocks as the panels instead of sitting beside them; when that memory is short the
+layout steps down (compact copies -> spans -> one launch) rather than failing.  C / C++ hosts call the
+same entry points (srg_plan_build allocates for them; examples/plan_propagate.c).
 """
 from __future__ import annotations
 
 import ctypes
+
+import torch
 
 from . import _lib
 
@@ -32,34 +36,82 @@ class HopLaunch(ctypes.Structure):
                 ("slot_beg", ctypes.c_void_p), ("slot_end", ctypes.c_void_p)]
 
 
+def _opts(compact, split_block0) -> int:
+    opts = 0
+    if compact is not None:
+        opts |= _lib.SRG_PLAN_COMPACT if compact else _lib.SRG_PLAN_SPANS
+    if split_block0 is not None:
+        opts |= _lib.SRG_PLAN_SPLIT_BLOCK0 if split_block0 else _lib.SRG_PLAN_WHOLE_BLOCK0
+    return opts
+
+
+def query(A, d: int, hops: int, col_blocks: int = 0, compact=None, split_block0=None):
+    """(keep_bytes, scratch_bytes, resolved opts, resolved column blocks) of a plan for these arguments
+    (srg_plan_query: one pass over indptr, nothing allocated)."""
+    kb, sb = ctypes.c_size_t(), ctypes.c_size_t()
+    ro, rb = ctypes.c_uint32(), ctypes.c_int32()
+    _lib.call(A.device, "srg_plan_query", A.indptr.data_ptr(), A.n_rows, int(d), int(hops), int(col_blocks),
+              _opts(compact, split_block0), _lib.stream(A.device), ctypes.byref(kb), ctypes.byref(sb), ctypes.byref(ro),
+              ctypes.byref(rb))
+    return int(kb.value), int(sb.value), int(ro.value), int(rb.value)
+
+
+def _torch_free(device) -> int:
+    """Device memory a new allocation can get: free on the device plus what torch holds cached."""
+    free, _ = torch.cuda.mem_get_info(device)
+    return int(free) + int(torch.cuda.memory_reserved(device) - torch.cuda.memory_allocated(device))
+
+
 class NativePlan:
     """A srg_plan over the arrays of square DeviceCSR `A` for a run of `hops` hops of d-column panels.
 
-    col_blocks: 0 = automatic (spmm.auto_col_blocks' rule), else forced; compact: None = automatic
-    (runs of >= SRG_PLAN_MIN_HOPS_TO_COMPACT hops, if it fits), True / False = always / never;
-    split_block0: None = automatic (panels < 16 GiB), True / False.  The plan borrows A's arrays (it
-    keeps references to them) and holds device memory until it is closed or collected."""
+    col_blocks: 0 = automatic (srg_plan_build's rule), else forced; compact: None = automatic (runs of
+    >= SRG_PLAN_MIN_HOPS_TO_COMPACT hops, when the copies and the build's temporaries fit in a quarter
+    of the memory torch can still hand out), True / False = always / never; split_block0: None =
+    automatic (panels < 16 GiB), True / False.  The plan borrows A's arrays (it keeps references to
+    them) and holds its memory -- a torch tensor -- until it is closed or collected.  When torch cannot
+    give it that memory (after emptying its cache once), an automatic layout steps down: compact copies
+    -> spans of A's arrays -> one launch per hop (the same bits every time)."""
 
     def __init__(self, A, d: int, hops: int, col_blocks: int = 0, compact=None, split_block0=None):
         if A.is_span or A.n_rows != A.n_cols:
             raise ValueError("a plan takes a whole square operator")
-        opts = 0
-        if compact is not None:
-            opts |= _lib.SRG_PLAN_COMPACT if compact else _lib.SRG_PLAN_SPANS
-        if split_block0 is not None:
-            opts |= _lib.SRG_PLAN_SPLIT_BLOCK0 if split_block0 else _lib.SRG_PLAN_WHOLE_BLOCK0
         self.device = A.device
         self._arrays = (A.indptr, A.indices, A.values)       # borrowed by the plan
         self._p = None
-        p = ctypes.c_void_p()
+        self._keep = None
         n = A.n_rows
         # A's thresholds (None: automatic per launch; negative: no such rows), for every launch
         hub_t, heavy_t = (_lib.SRG_PLAN_AUTO if t is None else _lib.SRG_PLAN_NONE if int(t) < 0 else int(t)
                           for t in (A.thresholds[1], A.thresholds[0]))
-        _lib.call(self.device, "srg_plan_build", A.indptr.data_ptr(), A.indices.data_ptr() if A.indices.numel() else None,
-                  A.values.data_ptr() if A.values.numel() else None, n, int(d), int(hops), int(col_blocks), hub_t,
-                  heavy_t, opts, _lib.stream(self.device), ctypes.byref(p))
-        self._p = p.value
+        if compact is None and hops >= _lib.SRG_PLAN_MIN_HOPS_TO_COMPACT:
+            # the library's rule (the copies and the build's keys / ids / positions, < 32 B per entry, in a
+            # quarter of the free memory) over the memory torch can hand out, cached blocks included
+            compact = A.nnz * 32 <= _torch_free(self.device) // 4
+        tries = [(int(col_blocks), compact)]
+        if compact is not False:
+            tries.append((int(col_blocks), False))
+        if int(col_blocks) == 0:
+            tries.append((1, False))
+        last = None
+        for cb, cp in tries:
+            kb, sb, ro, rb = query(A, d, hops, cb, cp, split_block0)
+            try:
+                keep, scratch = self._alloc(kb, sb)
+            except torch.cuda.OutOfMemoryError as e:     # a smaller layout, the same bits
+                last = e
+                continue
+            p = ctypes.c_void_p()
+            _lib.call(self.device, "srg_plan_build_in", A.indptr.data_ptr(),
+                      A.indices.data_ptr() if A.indices.numel() else None,
+                      A.values.data_ptr() if A.values.numel() else None, n, int(d), int(hops), rb, hub_t, heavy_t,
+                      ro, keep.data_ptr() if kb else _dummy(self.device), kb,
+                      scratch.data_ptr() if sb else _dummy(self.device), sb, _lib.stream(self.device), ctypes.byref(p))
+            del scratch                 # the build has returned (and synchronised): the scratch goes back
+            self._p, self._keep = p.value, keep
+            break
+        else:
+            raise last
         self.hops = int(hops)
         self.forced = int(col_blocks) != 0
         desc = PlanDesc()
@@ -71,6 +123,20 @@ class NativePlan:
         self.split_block0 = bool(desc.split_block0)
         self.hub_chain = bool(desc.hub_chain)
         self.device_bytes = int(desc.device_bytes)
+
+    def _alloc(self, keep_bytes: int, scratch_bytes: int):
+        """The plan's memory and the build's scratch from torch's allocator (one retry after emptying
+        its cache)."""
+        for attempt in range(2):
+            try:
+                keep = torch.empty(max(keep_bytes, 1), dtype=torch.uint8, device=self.device)
+                scratch = torch.empty(max(scratch_bytes, 1), dtype=torch.uint8, device=self.device)
+                return keep, scratch
+            except torch.cuda.OutOfMemoryError:
+                keep = scratch = None
+                if attempt:
+                    raise
+                torch.cuda.empty_cache()
 
     def launches(self, d: int):
         """[(srg_hop_launch, join_hub)] of one hop over a d-column panel, as the hops run them."""
@@ -101,10 +167,12 @@ class NativePlan:
                   agg.stride(0) if agg is not None else 0, float(w), 1 if init else 0, _lib.stream(self.device))
 
     def close(self) -> None:
-        """Releases the plan's memory in stream order on the device's current stream."""
+        """Releases the plan: srg_plan_destroy orders itself after every stream the plan's work went to
+        and drains the current stream, so its memory returns to torch's cache with nothing reading it."""
         p, self._p = self._p, None
         if p is not None:
             _lib.call(self.device, "srg_plan_destroy", p, _lib.stream(self.device))
+        self._keep = None
 
     def __del__(self):
         try:
@@ -113,10 +181,21 @@ class NativePlan:
             pass
 
 
+_DUMMIES = {}
+
+
+def _dummy(device):
+    """A valid 256-byte aligned device address for an empty arena (nothing is written to it)."""
+    key = str(device)
+    if key not in _DUMMIES:
+        _DUMMIES[key] = torch.empty(256, dtype=torch.uint8, device=device)
+    return _DUMMIES[key].data_ptr()
+
+
 def hop_class(hops: int) -> int:
-    """0: one launch per hop, 1: column blocks, 2: compact copies -- what a run of `hops` hops buys."""
-    from .spmm import MIN_HOPS_TO_CUT
-    return (1 if hops >= MIN_HOPS_TO_CUT else 0) + (1 if hops >= _lib.SRG_PLAN_MIN_HOPS_TO_COMPACT else 0)
+    """0: one launch per hop, 1: column blocks, 2: compact copies -- what a run of `hops` hops buys
+    (srg_plan_build's SRG_PLAN_MIN_HOPS_TO_CUT / SRG_PLAN_MIN_HOPS_TO_COMPACT)."""
+    return (1 if hops >= _lib.SRG_PLAN_MIN_HOPS_TO_CUT else 0) + (1 if hops >= _lib.SRG_PLAN_MIN_HOPS_TO_COMPACT else 0)
 
 
 def plan_for(A, d: int, hops: int, col_blocks: int = 0, split_block0=None) -> NativePlan:
@@ -140,4 +219,4 @@ def cached(A, d: int):
     return A._blocks.get(("native", int(d)))
 
 
-__all__ = ["NativePlan", "PlanDesc", "HopLaunch", "plan_for", "cached", "hop_class"]
+__all__ = ["NativePlan", "PlanDesc", "HopLaunch", "plan_for", "cached", "hop_class", "query"]

@@ -15,293 +15,109 @@ from .csr import DeviceCSR
 
 _stream = _lib.stream
 
-# Column-blocked hops (DeviceCSR.column_blocks): B launches per hop, each gathering from one
-# contiguous slice of X's rows, so the caches hold a larger share of the rows a launch reads; rows
-# of <= csr.BLOCK_WHOLE_MAX nonzeros are not cut (block 0 computes them whole).  Measured
-# (profiles/r02t-v_*): products d = 128 7.05 (one launch 7.31) -> 6.67 (B = 2) -> 6.30 ms (B = 4),
-# flat over B = 4..6, 6.47 at 8; d = 256 +9 % and papers100M / RMAT-26 +3 / +2 % for B = 4 over 2 / 1;
-# arxiv (X 87 MB, already cache-resident) 0.224 vs 0.163 ms at B = 2.  auto_col_blocks: 12 to 16 blocks
-# for panels of 512 MiB .. 16 GiB at d >= 64 (4 to 8 before round 5's packed-row kernels) (callers pass col_blocks to force a count; FORCE_COL_BLOCKS
-# forces one for every automatic choice, a test hook).
+# K-hop runs and single hops run through the one-GPU planner (srgnn.plan -> srg_plan_build, csrc/
+# srg_plan.hip): column blocks for runs of >= SRG_PLAN_MIN_HOPS_TO_CUT hops over panels of >= 512 MiB at
+# d >= 64 (one block per ~100 MiB, 12 to 16; 4 from 16 GiB), block 0 as its cut rows' spans and its
+# whole rows below 16 GiB, compact launch-ordered copies from SRG_PLAN_MIN_HOPS_TO_COMPACT hops when they
+# fit.  The measurements behind every rule are in DESIGN.md §5.1; the rules themselves live in the
+# planner only (round 6: the torch formulation of the layout is a test restatement,
+# tests/plan_layout_ref.py).
+# Test hooks: FORCE_COL_BLOCKS forces a block count for every automatic choice; SPLIT_BLOCK0 forces
+# block 0's split on / off (None: the planner's rule).  The same bits whatever they are.
 FORCE_COL_BLOCKS = None
-# column blocks' launches keep 2 gathers per packed light row in flight (SRG_SPMM_PACKED_U2) for
-# d >= 128: products 7.15 -> 7.03 ms per hop, d = 256 +1.3 %, d = 64 -3 % (so not there;
-# profiles/r02_ab_col_blocks.txt)
-_U2_BLOCKED = True
-# column-blocked hops: block b's hub rows continue block b-1's side-stream fork (SRG_SPMM_HUB_CONTINUE)
-# instead of a fork, dispatch delay and join per block (profiles/r03_ab_hub_chain_products.txt)
-_HUB_CHAIN = True
-# span launches of the native plan loop hand the packed light rows their spans by schedule slot
-# (DeviceCSR.slot_spans; profiles/r03_ab_slot_spans.txt)
-_SLOT_SPANS = True
-# block 0 of a column-blocked hop as two launches over the same arrays (DeviceCSR.split_whole): the
-# cut rows' first spans, then the rows it computes whole.  Products (1.25 GB panel): 6.21 vs 6.24 ms
-# per hop, six alternations; the whole rows first, last or after the cut spans measure the same, and
-# beside the blocks on a second stream 6.80 ms.  The HBM-bound giants lose: papers100M (57 GB panel)
-# 245.6-246.1 vs 244.1-244.2 ms, RMAT-26 (68 GB) 314.3-315.8 vs 311.5-313.1 ms
-# (profiles/r03_ab_split_block0*.txt): split for panels below SPLIT_BLOCK0_MAX_PANEL
-SPLIT_BLOCK0_MAX_PANEL = 16 << 30
-# None: automatic (tests force it on / off to check both layouts give the same bits)
 SPLIT_BLOCK0 = None
 
 
-def _split_block0(A: DeviceCSR, d: int) -> bool:
-    if SPLIT_BLOCK0 is not None:
-        return bool(SPLIT_BLOCK0)
-    return A.n_cols * d * 4 < SPLIT_BLOCK0_MAX_PANEL
-
-
-# Cutting an operator into column blocks (row spans: one binary search per row and boundary, plus
-# each block's schedule) costs about 3 hops' gain (products: 1.1 ms against 0.42 ms per hop,
-# tools/probes/colblock_build_time.py; 21 ms when the blocks were copies of the ids and values):
-# it is cut for a run of at least this many hops, or when its blocks already exist.
-MIN_HOPS_TO_CUT = 4
-# Runs of this many hops copy the blocks' spans into compact arrays in launch order, when the copy fits in
-# a quarter of the free memory (= SRG_PLAN_MIN_HOPS_TO_COMPACT of the native planner).  Round 5, the
-# native planner (one device pass: profiles/r05_plan_products.json): the compact layout builds in
-# ~1.9 ms against ~1.2 ms for spans, and each products hop runs 5.48 instead of ~5.64 ms, so the copy
-# pays after ~4-5 hops.  (The torch formulation, DeviceCSR.compact_column_blocks, cost 4.6 ms more
-# than spans, round 4: profiles/r04h_one_shot_products.json.)
-MIN_HOPS_TO_COMPACT = 6
-_COMPACT = True                   # False: spans only (A/B of the round-2 / 3 layouts)
-
-
-# K-hop runs (prepare / propagate) lay the operator out with the native planner (srgnn.plan,
-# csrc/srg_plan.hip: one device pass, the operator's thresholds passed on) when every layout constant
-# here and in srgnn.csr has its default value; otherwise (layout experiments) with the torch
-# formulation below.  Both give the same layout.
-NATIVE_PLAN = True
-
-
-def _native_ok(A: DeviceCSR) -> bool:
-    from . import csr as C
-    return (NATIVE_PLAN and _COMPACT and _HUB_CHAIN and _SLOT_SPANS and _U2_BLOCKED and not A.is_span
-            and A.n_rows == A.n_cols and C.BLOCK_WHOLE_MAX == 48
-            and C.BLOCK_HEAVY_PER == 30000 and C.NARROW_HEAVY_THRESHOLD == 32 and C.DEFAULT_HEAVY_THRESHOLD is None
-            and C.DEFAULT_HUB_THRESHOLD is None and SPLIT_BLOCK0_MAX_PANEL == 16 << 30
-            and CAP_WAVES_MIN_PANEL == 512 << 20 and MIN_HOPS_TO_CUT == 4
-            and MIN_HOPS_TO_COMPACT == _lib.SRG_PLAN_MIN_HOPS_TO_COMPACT)
+def _forced(col_blocks) -> int:
+    return int(col_blocks) if col_blocks is not None else int(FORCE_COL_BLOCKS or 0)
 
 
 def prepare(A: DeviceCSR, d: int, hops: int, col_blocks=None) -> int:
-    """Lays A out for a run of `hops` hops over d-column panels: column blocks (spans, or compact
-    copies in launch order for long runs) or, for one launch per hop and a long run, a launch-ordered
-    copy of the whole operator (DeviceCSR.schedule_ordered).  col_blocks: None = automatic, else the
+    """Lays A out for a run of `hops` hops over d-column panels with the native planner (cached on A;
+    rebuilt only when a longer run buys a richer layout).  col_blocks: None = automatic, else the
     blocks per hop asked for.  Returns the column blocks per hop that hop() / propagate() then run."""
-    if _native_ok(A):
-        from .plan import plan_for
-        cb = int(col_blocks) if col_blocks is not None else int(FORCE_COL_BLOCKS or 0)
-        return plan_for(A, d, hops, cb, SPLIT_BLOCK0).col_blocks
-    B = auto_col_blocks(A, d, hops=hops) if col_blocks is None else int(col_blocks)
-    if B > 1 and column_blocks_for(A, B, hops=hops):
-        return B
-    if _COMPACT and hops >= MIN_HOPS_TO_COMPACT and not A.is_span and A.n_rows == A.n_cols:
-        free, _ = torch.cuda.mem_get_info(A.device)
-        if A.nnz * (A.indices.element_size() + A.values.element_size()) + 24 * A.nnz <= free // 4:
-            A.schedule_ordered()
-    return 1
-
-
-def column_blocks_for(A: DeviceCSR, B: int, hops: int | None = None):
-    """A's column blocks for a run of `hops` hops: spans, or compact copies for long runs."""
-    if _COMPACT and hops is not None and hops >= MIN_HOPS_TO_COMPACT and not A.is_span:
-        free, _ = torch.cuda.mem_get_info(A.device)
-        # the copies (ids + values of every block: nnz entries) stay; while a block is copied its
-        # int64 gather index, the arange added to it and repeat_interleave's output (<= nnz
-        # entries each) are alive too
-        copies = A.nnz * (A.indices.element_size() + A.values.element_size())
-        if copies + 24 * A.nnz <= free // 4:
-            return A.compact_column_blocks(B)
-    return A.column_blocks(B)
+    from .plan import plan_for
+    return plan_for(A, d, hops, _forced(col_blocks), SPLIT_BLOCK0).col_blocks
 
 
 def auto_col_blocks(A: DeviceCSR, d: int, hops: int | None = None) -> int:
-    """Column blocks per hop for a panel of d columns (1 = the one-launch hop), if A's blocks exist
-    or `hops` hops will amortise cutting it: for panels of >= 512 MiB at d >= 64, one block per
-    ~100 MiB of panel, 12 to 16 (round 5, profiles/r05bn_col_blocks_final_kernels.txt: products d = 64
-    3.37 -> 3.08 ms per hop at 4 -> 12 blocks, d = 128 5.23 -> 5.15 at 8 -> 12, d = 256 11.73 -> 11.00
-    at 8 -> 16); 4 for panels of >= 16 GiB.  Before round 5's packed-row kernels: one per ~150 MiB, 4
-    to 8.  Round 4 (slice waves from ~1000-entry spans, rows of <= 48 entries whole): products
-    d = 128 5.63 ms at B = 6, 5.60-5.61 at 7 and 8; with 48-entry whole rows 5.58 / 5.53 / 5.51-5.52 at
-    6 / 7 / 8 (profiles/r04af_*, r04ag_*, r04ah_*).  Round 3, block 0 in two launches, compact blocks in launch order
-    (profiles/r03_ab_col_blocks_round3.txt): products d = 128 (1.25 GB) 5.98 ms at B = 6 against
-    6.00-6.01 at 5 and 7, 6.03 at 8, 6.10 at 4; d = 256 (2.5 GB) 12.35 ms at 7-8 against 12.40 at 6
-    (before the launch order: 12.55 at 6, 12.67 at 5, 12.70 at 10, 12.91 at 4); d = 64 (0.63 GB) flat
-    over 4-5; RMAT-26 (68 GB) 312.8 at 4 against 315.6 at 5, papers100M (57 GB) 242.9 against 242.0."""
+    """Column blocks per hop the planner gives a run of `hops` hops over d-column panels (None: A's
+    cached plan for d, or one launch) -- srg_plan_query's resolved choice, nothing built."""
+    from .plan import cached, query
     if FORCE_COL_BLOCKS is not None:
         return max(1, int(FORCE_COL_BLOCKS))
-    panel = A.n_cols * d * 4
-    if d < 64 or panel < (512 << 20):
-        B = 1
-    elif panel >= SPLIT_BLOCK0_MAX_PANEL:
-        B = 4
-    else:
-        # round 5 (= kAutoBlocksMin / Max of srg_plan.hip): one per ~100 MiB, 12 to 16 blocks
-        B = min(16, max(12, int(round(panel / (100 << 20)))))
-    if B > 1 and B not in A._blocks and (hops is None or hops < MIN_HOPS_TO_CUT):
-        return 1
-    return B
+    if hops is None:
+        P = cached(A, d)
+        return P.col_blocks if P is not None else 1
+    return query(A, d, hops, 0, None, SPLIT_BLOCK0)[3]
 
 
 def col_blocks_of(A: DeviceCSR, d: int) -> int:
-    """The column blocks per hop hop() runs A in over a d-column panel as A is laid out now (its native
-    plan for d, or its torch-formulated blocks); 1 = the one-launch hop."""
-    if _native_ok(A):
-        from .plan import cached
-        P = cached(A, d)
-        if P is not None:
-            return P.col_blocks
-    return auto_col_blocks(A, d)
-
-
-# Hops over panels of at least this many bytes cap the row kernel's occupancy (SRG_SPMM_CAP_WAVES):
-# products 5.84 -> 5.81 ms per hop, arxiv (87 MB) 3 % slower capped (profiles/r04x_waves_ab.txt)
-CAP_WAVES_MIN_PANEL = 512 << 20
+    """The column blocks per hop hop() runs A in over a d-column panel as A is laid out now (its
+    cached plan for d); 1 = the one-launch hop."""
+    from .plan import cached
+    P = cached(A, d)
+    return P.col_blocks if P is not None else 1
 
 
 def launches_per_hop(A: DeviceCSR, B: int, d: int, agg: bool = False) -> int:
-    """k_spmm launches of one hop of A over a d-column panel in B column blocks (hop()): B, plus
-    one when block 0 runs as its cut spans and its whole rows (_split_block0, or the aggregation
-    epilogue)."""
-    from .plan import cached
-    P = cached(A, d) if _native_ok(A) else None
+    """k_spmm launches of one hop of A over a d-column panel in B column blocks: the cached plan's,
+    else what a plan with B blocks would run (B, plus one when block 0 runs as its cut spans and its
+    whole rows).  agg: the aggregation epilogue needs no launch of its own where block 0 is split, and
+    a separate accumulation pass (not a k_spmm launch) where it is not."""
+    from .plan import cached, query
+    P = cached(A, d)
     if P is not None and P.col_blocks == B:
         return P.n_launch
-    blocks = A.column_blocks(B) if B > 1 else None
-    if not blocks:
+    if B <= 1:
         return 1
-    return len(blocks) + (1 if (agg or _split_block0(A, d)) and blocks[0].whole_rows is not None else 0)
-
-
-def _hop_plan(A: DeviceCSR, d: int, B: int, nt_store: bool = False, fast: bool = False, agg: bool = False):
-    """The launches of one hop of A over a d-column panel in B column blocks: ([(operator, flags,
-    kind)], join) with kind "plain" or "agg" (the launch that carries the aggregation epilogue), and
-    join = whether the hub side stream must be joined at the end of the hop."""
-    # one launch: a long-lived operator's launch-ordered copy when prepare() made one
-    blocks = (A.column_blocks(B) if B > 1 else None) or [A._blocks.get("sched", A) if _COMPACT else A]
-    # a block's rows are short: 2 gathers per packed row in flight (d >= 128: 4 or 2 rows per wave;
-    # at d = 64, 8 rows per wave, it is 3 % slower)
-    u2 = len(blocks) > 1 and d >= 128 and _U2_BLOCKED
-    split = blocks[0].split_whole() if (agg or _split_block0(A, d)) and len(blocks) > 1 else None
-    # the blocks' hub spans chained on the side stream: one fork (the first block with hub rows),
-    # one join at the end of the hop.  X is not written during the hop, and when every block has
-    # the same hub rows only the side stream touches them, so nothing else orders them (a row that
-    # is a hub in one block only would have spans on both streams: then every block forks and joins)
-    # (with block 0 split, the launches over cut rows are split[0] and blocks 1..; split[1]'s rows --
-    # whole rows -- are in no other launch, so its hub rows never matter)
-    chain = len(blocks) > 1 and not fast and _HUB_CHAIN and \
-        _same_hub_rows(A, B, ([split[0]] + blocks[1:]) if split is not None else blocks, agg=split is not None)
-    base = (_lib.SRG_SPMM_NT_STORE if nt_store else 0) | (_lib.SRG_SPMM_PACKED_U2 if u2 else 0) | \
-        (_lib.SRG_SPMM_CAP_WAVES if A.n_cols * d * 4 >= CAP_WAVES_MIN_PANEL else 0)
-    seq = []     # (operator, accumulate, kind)
-    for b, Ab in enumerate(blocks):
-        if split is not None and b == 0:
-            # rows block 0 computes whole finish there: their aggregation runs in that launch
-            seq += [(split[0], False, "plain"), (split[1], False, "agg" if agg else "plain")]
-        else:
-            seq.append((Ab, b > 0, "agg" if agg and b == len(blocks) - 1 else "plain"))
-    plan, forked = [], False
-    for Ab, acc, kind in seq:
-        f = base | (_lib.SRG_SPMM_ACCUMULATE if acc else 0)
-        if chain and Ab.n_hub > 0:
-            f |= _lib.SRG_SPMM_HUB_NOJOIN | (_lib.SRG_SPMM_HUB_CONTINUE if forked else 0)
-            forked = True
-        elif fast and kind == "plain":
-            f |= _lib.SRG_SPMM_FAST
-        plan.append((Ab, f, kind))
-    return plan, forked
+    _, _, ro, rb = query(A, d, _lib.SRG_PLAN_MIN_HOPS_TO_CUT, B, None, SPLIT_BLOCK0)
+    return rb + (1 if (ro & _lib.SRG_PLAN_SPLIT_BLOCK0) and rb > 1 else 0)
 
 
 def hop(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, nt_store: bool = False, col_blocks=None,
         agg=None, fast: bool = False) -> torch.Tensor:
-    """out = A @ X (one hop, exact), column-blocked when auto_col_blocks (or `col_blocks`) says so
-    and A's rows allow it; bitwise the same either way.  agg = (panel, w, init): the aggregation
-    step fused into the (last) launch's epilogue, as spmm_agg.  fast: SRG_SPMM_FAST for the hub
-    rows of every launch (tolerance mode, see spmm)."""
+    """out = A @ X (one hop, exact) through A's plan for X's width (srg_plan_hop_f32): the cached one
+    (prepare / propagate laid A out), or a one-launch plan made here; col_blocks forces another block
+    count.  Bitwise the same in every layout.  agg = (panel, w, init): the aggregation step
+    (0 if init else panel) + w * out fused into the epilogue of the launches where the rows' chains
+    end.  fast: SRG_SPMM_FAST for the hub rows (tolerance mode, see spmm); with agg, the step then runs
+    as its own accumulation pass."""
+    from .plan import cached, plan_for
     d = X.shape[1]
-    # every launch below writes rows of A's whole row space (the blocks' schedules name them)
     _check_panel(X, A.n_cols, "X")
     _check_panel(out, A.out_rows, "out", d)
     if agg is not None:
         _check_panel(agg[0], A.out_rows, "agg", d)
     if out.device != A.device or X.device != A.device:
         raise ValueError("A, X and out must be on the same device")
-    if _native_ok(A) and X.data_ptr() != out.data_ptr() and not (fast and agg is not None):
-        # an operator prepared by the native planner: one hop of its plan (srg_plan_hop_f32), the
-        # aggregation step in the epilogue of the launches where the rows' chains end
-        from .plan import cached
-        P = cached(A, d)
-        if P is not None and (col_blocks is None or int(col_blocks) == P.col_blocks):
-            flags = (_lib.SRG_SPMM_NT_STORE if nt_store else 0) | (_lib.SRG_SPMM_FAST if fast else 0)
-            if agg is None:
-                P.hop(X, out, d, flags)
-            else:
-                P.hop(X, out, d, flags, agg[0], agg[1], agg[2])
-            return out
-    B = auto_col_blocks(A, d) if col_blocks is None else int(col_blocks)
-    plan, join = _hop_plan(A, d, B, nt_store, fast, agg is not None)
-    if agg is None and X.stride(0) == out.stride(0) and X.data_ptr() != out.data_ptr():
-        # one hop through the native plan loop (the packed rows get their spans by slot there)
-        arr = (ctypes.c_void_p * 2)(X.data_ptr(), out.data_ptr())
-        _lib.call(X.device, "srg_propagate_plan_f32", _plan_array(plan, d), len(plan), 1 if join else 0, arr,
-                  X.stride(0), d, 1, _stream(X.device))
-        return out
-    for Ab, f, kind in plan:
-        if kind == "agg":
-            _launch(Ab, X, out, d, f, agg[0], agg[1], agg[2])
-        else:
-            _launch(Ab, X, out, d, f)
-    if join:
-        _lib.call(X.device, "srg_hub_join", _stream(X.device))
-    return out
-
-
-def _launch(A: DeviceCSR, X, out, d, flags, agg=None, w=0.0, init=False):
-    """One k_spmm launch of a planned hop (operands checked by the caller)."""
-    if A.is_span:
-        _span_call(A, X, out, d, flags, agg, agg.stride(0) if agg is not None else 0, w, init)
-    elif agg is not None:
-        _lib.call(X.device, "srg_spmm_agg_f32", A.indptr.data_ptr(), A.indices.data_ptr(), A.values.data_ptr(),
-                  A.n_rows, A.order.data_ptr() if A.n_rows else None, A.n_hub, A.heavy(d), X.data_ptr(),
-                  X.stride(0), out.data_ptr(), out.stride(0), d, flags, agg.data_ptr(), agg.stride(0), float(w),
-                  1 if init else 0, _stream(X.device))
+    if X.data_ptr() == out.data_ptr():
+        raise ValueError("out must not alias X (its rows are gathered)")
+    _no_spans(A, "hop")
+    if A.n_rows != A.n_cols:
+        # a rectangular operator (a row block): one launch with its own schedule
+        if col_blocks not in (None, 1):
+            raise ValueError("column blocks take a square operator")
+        if agg is None:
+            return spmm(A, X, out=out, nt_store=nt_store, fast=fast)
+        if fast:
+            raise ValueError("fast with agg takes a square operator")
+        return spmm_agg(A, X, out, agg[0], agg[1], agg[2], nt_store=nt_store)
+    P = cached(A, d)
+    if P is None or (col_blocks is not None and int(col_blocks) != P.col_blocks):
+        cb = _forced(col_blocks)
+        P = plan_for(A, d, _lib.SRG_PLAN_MIN_HOPS_TO_CUT if cb > 1 else 1, cb, SPLIT_BLOCK0)
+    flags = (_lib.SRG_SPMM_NT_STORE if nt_store else 0) | (_lib.SRG_SPMM_FAST if fast else 0)
+    if agg is None:
+        P.hop(X, out, d, flags)
+    elif not fast:
+        P.hop(X, out, d, flags, agg[0], agg[1], agg[2])
     else:
-        _lib.call(X.device, "srg_spmm_csr_f32", A.indptr.data_ptr(), A.indices.data_ptr(), A.values.data_ptr(),
-                  A.n_rows, A.order.data_ptr() if A.n_rows else None, A.n_hub, A.heavy(d), X.data_ptr(),
-                  X.stride(0), out.data_ptr(), out.stride(0), d, flags, _stream(X.device))
-
-
-class _HopLaunch(ctypes.Structure):
-    """srg_hop_launch (include/srgnn_hip.h)."""
-    _fields_ = [("row_beg", ctypes.c_void_p), ("row_end", ctypes.c_void_p), ("indices", ctypes.c_void_p),
-                ("values", ctypes.c_void_p), ("row_order", ctypes.c_void_p), ("n_rows", ctypes.c_int64),
-                ("n_hub", ctypes.c_int64), ("n_heavy", ctypes.c_int64), ("flags", ctypes.c_uint32),
-                ("slot_beg", ctypes.c_void_p), ("slot_end", ctypes.c_void_p)]
-
-
-def _plan_array(plan, d):
-    arr = (_HopLaunch * len(plan))()
-    for i, (Ab, f, _) in enumerate(plan):
-        sb, se = Ab.slot_spans() if (Ab.is_span and Ab.n_rows and _SLOT_SPANS) else (None, None)
-        arr[i] = _HopLaunch(Ab.indptr.data_ptr(), Ab.row_end.data_ptr() if Ab.is_span else None,
-                            Ab.indices.data_ptr(), Ab.values.data_ptr(), Ab.order.data_ptr() if Ab.n_rows else None,
-                            Ab.n_rows, Ab.n_hub, Ab.heavy(d), f, sb.data_ptr() if sb is not None else None,
-                            se.data_ptr() if se is not None else None)
-    return arr
-
-
-HUB_CHAIN_MAX = 256     # = kHubPrefix (csrc/srg_plan.hip)
-
-
-def _same_hub_rows(A: DeviceCSR, B: int, blocks, agg: bool = False) -> bool:
-    """Whether every column block schedules the same set of hub rows (cached per B on A)."""
-    key = ("same_hubs", B, agg)
-    if key not in A._blocks:
-        sets = [torch.sort(b.order[: b.n_hub].to(torch.int64)).values for b in blocks]
-        # more than HUB_CHAIN_MAX hub rows in a launch: no chain (the native planner compares that many)
-        A._blocks[key] = all(s.numel() <= HUB_CHAIN_MAX for s in sets) and \
-            all(s.numel() == sets[0].numel() and bool(torch.equal(s, sets[0])) for s in sets)
-    return A._blocks[key]
+        P.hop(X, out, d, flags)
+        _lib.call(X.device, "srg_hop_accumulate_f32", agg[0].data_ptr(), agg[0].stride(0), out.data_ptr(),
+                  out.stride(0), A.out_rows, d, float(agg[1]), _lib.SRG_ACC_INIT if agg[2] else _lib.SRG_ACC_ADD,
+                  _stream(X.device))
+    return out
 
 
 def _check_panel(X: torch.Tensor, rows: int, name: str, d=None):
@@ -454,8 +270,8 @@ def propagate(A: DeviceCSR, X: torch.Tensor, K: int, panels: list | None = None,
     """[X, ÂX, …, Â^K X] as device tensors (panels[0] is X itself, like the reference's list).
 
     Device-resident form of GraphOp.propagate's hop loop (SSRG/operators/base_operator.py:32-35):
-    the K hops run back to back on the GPU with no host round trips (srg_propagate_khop_f32, or
-    hop() per hop when the hops are column-blocked).  fast: tolerance mode for the hub rows (spmm)."""
+    the K hops run back to back on the GPU with no host round trips, through A's plan for a K-hop run
+    (srg_plan_propagate_f32).  fast: tolerance mode for the hub rows (spmm)."""
     _no_spans(A, "propagate")
     if A.n_rows != A.n_cols:
         raise ValueError("propagate needs a square operator")
@@ -476,36 +292,11 @@ def propagate(A: DeviceCSR, X: torch.Tensor, K: int, panels: list | None = None,
         _check_panel(p, n, f"panels[{k}]", d)
         if p.stride(0) != ld:
             raise ValueError("all panels must share one leading dimension")
-    if K > 0 and _native_ok(A):
+    if K > 0:
         # the native plan (srgnn.plan): layout and hop loop in the library
         from .plan import plan_for
-        cb = int(col_blocks) if col_blocks is not None else int(FORCE_COL_BLOCKS or 0)
         flags = (_lib.SRG_SPMM_NT_STORE if nt_store else 0) | (_lib.SRG_SPMM_FAST if fast else 0)
-        plan_for(A, d, K, cb, SPLIT_BLOCK0).propagate(panels, ld, d, K, flags)
-        if panels[0] is not X0 and X is not X0:
-            panels = [X0] + list(panels[1:])
-        return panels
-    B = auto_col_blocks(A, d, hops=K) if col_blocks is None else int(col_blocks)
-    if K > 0 and B > 1 and column_blocks_for(A, B, hops=K):
-        # the blocked hop loop runs natively: one call for the K hops (srg_propagate_plan_f32)
-        plan, join = _hop_plan(A, d, B, nt_store, fast)
-        arr = (ctypes.c_void_p * (K + 1))(*[p.data_ptr() for p in panels])
-        _lib.call(X.device, "srg_propagate_plan_f32", _plan_array(plan, d), len(plan), 1 if join else 0, arr,
-                  ld, d, K, _stream(X.device))
-    elif K > 0 and _COMPACT and "sched" in A._blocks:
-        # a long-lived operator's launch-ordered copy (DeviceCSR.schedule_ordered): the one launch
-        # per hop as a span operator, through the native plan loop
-        S = A._blocks["sched"]
-        flags = (_lib.SRG_SPMM_NT_STORE if nt_store else 0) | (_lib.SRG_SPMM_FAST if fast else 0)
-        arr = (ctypes.c_void_p * (K + 1))(*[p.data_ptr() for p in panels])
-        _lib.call(X.device, "srg_propagate_plan_f32", _plan_array([(S, flags, "plain")], d), 1, 0, arr, ld, d, K,
-                  _stream(X.device))
-    else:
-        arr = (ctypes.c_void_p * (K + 1))(*[p.data_ptr() for p in panels])
-        flags = (_lib.SRG_SPMM_NT_STORE if nt_store else 0) | (_lib.SRG_SPMM_FAST if fast else 0)
-        _lib.call(X.device, "srg_propagate_khop_f32", A.indptr.data_ptr(), A.indices.data_ptr(),
-                  A.values.data_ptr(), n, A.order.data_ptr() if n else None, A.n_hub, A.heavy(d), arr, ld, d,
-                  K, flags, _stream(X.device))
+        plan_for(A, d, K, _forced(col_blocks), SPLIT_BLOCK0).propagate(panels, ld, d, K, flags)
     if panels[0] is not X0 and X is not X0:
         panels = [X0] + list(panels[1:])
     return panels

@@ -249,22 +249,15 @@ class HeatWaveletFilter:
                                         self.n_hub, self.n_heavy_narrow, thresholds=self.thresholds)
         return cache[id(vals)]
 
-    def prepare_column_blocks(self, width: int, hops: int, native: bool = True) -> int:
+    def prepare_column_blocks(self, width: int, hops: int) -> int:
         """Lay L and F out (spmm.prepare: the native plan, column blocks when `hops` SpMMs over panels
         `width` columns wide amortise them) for the split path's hops; returns the blocks per SpMM.
-        native=False: the torch formulation of the same blocks (spmm.column_blocks_for), whose arrays
-        come from torch's caching allocator instead of the plan's own device memory -- for panels that
-        fill the GPU (bench.py's RMAT-26 filter bank); the same bits either way."""
-        from .spmm import auto_col_blocks, column_blocks_for, prepare
+        The plans' memory comes from torch's caching allocator (srgnn.plan), so where the panels fill
+        the GPU (the RMAT-26 filter bank) the plans reuse the blocks the graph build left cached."""
+        from .spmm import prepare
         B = 1
         for vals in (self.lvals, self.fvals):
-            A = self._csr(vals)
-            if native:
-                B = prepare(A, width, hops)
-            else:
-                B = auto_col_blocks(A, width, hops=hops)
-                if B > 1 and not column_blocks_for(A, B, hops=hops):
-                    B = 1
+            B = prepare(self._csr(vals), width, hops)
         return B
 
     def drop_layouts(self) -> None:

@@ -250,3 +250,33 @@ def propagate(A: DeviceCSR, X: torch.Tensor, K: int, B: int, compact: bool = Fal
     _lib.call(X.device, "srg_propagate_plan_f32", launch_array(plan, d), len(plan), 1 if join else 0, arr,
               X.stride(0), d, K, _lib.stream(X.device))
     return panels
+
+
+def hop(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, B: int, compact: bool = False, split: bool = True,
+        whole_max: int = WHOLE_MAX, agg=None):
+    """One hop over this layout, launch by launch (srg_spmm_span_f32 / srg_spmm_csr_f32 / srg_spmm_agg_f32),
+    agg = (panel, w, init) fused into the launches that finish the rows' chains; the hub side stream
+    joined at the end."""
+    d = X.shape[1]
+    plan, join = hop_plan(A, d, B, compact, split, whole_max, agg=agg is not None)
+    st = _lib.stream(X.device)
+    for Ab, f, kind in plan:
+        ag = agg if kind == "agg" else None
+        if Ab.is_span:
+            _lib.call(X.device, "srg_spmm_span_f32", Ab.indptr.data_ptr(), Ab.row_end.data_ptr(), Ab.indices.data_ptr(),
+                      Ab.values.data_ptr(), Ab.n_rows, Ab.order.data_ptr() if Ab.n_rows else None, Ab.n_hub,
+                      Ab.heavy(d), X.data_ptr(), X.stride(0), out.data_ptr(), out.stride(0), d, f,
+                      ag[0].data_ptr() if ag else None, ag[0].stride(0) if ag else 0, float(ag[1]) if ag else 0.0,
+                      (1 if ag[2] else 0) if ag else 0, st)
+        elif ag is not None:
+            _lib.call(X.device, "srg_spmm_agg_f32", Ab.indptr.data_ptr(), Ab.indices.data_ptr(), Ab.values.data_ptr(),
+                      Ab.n_rows, Ab.order.data_ptr() if Ab.n_rows else None, Ab.n_hub, Ab.heavy(d), X.data_ptr(),
+                      X.stride(0), out.data_ptr(), out.stride(0), d, f, ag[0].data_ptr(), ag[0].stride(0),
+                      float(ag[1]), 1 if ag[2] else 0, st)
+        else:
+            _lib.call(X.device, "srg_spmm_csr_f32", Ab.indptr.data_ptr(), Ab.indices.data_ptr(), Ab.values.data_ptr(),
+                      Ab.n_rows, Ab.order.data_ptr() if Ab.n_rows else None, Ab.n_hub, Ab.heavy(d), X.data_ptr(),
+                      X.stride(0), out.data_ptr(), out.stride(0), d, f, st)
+    if join:
+        _lib.call(X.device, "srg_hub_join", st)
+    return out

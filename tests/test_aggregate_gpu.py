@@ -53,28 +53,20 @@ def test_fused_combine_bit_exact(oracle_mod, name, K):
         np.testing.assert_array_equal(got, want, err_msg=f"{name} K={K} {msg.aggr_type} {msg.start}:{msg.end}")
 
 
-@pytest.mark.parametrize("whole", [(0, False), (4, False), (16, True), (1 << 30, False)])
 @pytest.mark.parametrize("B", [2, 3])
 @pytest.mark.parametrize("name", ["cora_sym_k3", "rand_d130_r1", "rand_d36_ppr"])
-def test_propagate_aggregate_column_blocked_bit_exact(oracle_mod, monkeypatch, name, B, whole):
-    """Column-blocked hops in the fused aggregation (spmm.hop: blocks with ACCUMULATE, the
-    aggregation epilogue in the launch that finishes each row -- the last block's, or block 0's
-    for the short rows it computes whole) == the reference's combine, bit for bit.  whole =
-    (csr.BLOCK_WHOLE_MAX, compact copies)."""
-    from srgnn import csr as csr_mod
+def test_propagate_aggregate_column_blocked_bit_exact(oracle_mod, name, B):
+    """Column-blocked hops in the fused aggregation (the plan's hops, srg_plan_hop_f32: blocks with
+    ACCUMULATE, the aggregation epilogue in the launch that finishes each row -- the last block's, or
+    block 0's whole-row launch for the short rows) == the reference's combine, bit for bit."""
     from srgnn.aggregate import combine_plan, combine_steps, propagate_aggregate
     from srgnn.csr import DeviceCSR
-    monkeypatch.setattr(csr_mod, "BLOCK_WHOLE_MAX", whole[0])
     c = G.Case(name)
     ip, ix, v = c.ahat()
     x = c.x()
     K = 5
     hops = oracle_mod.propagate(ip, ix, v, x, K)
     A = DeviceCSR.from_tensors(ip, ix, v, n_cols=c.n, device="cuda")
-    blocks = A.compact_column_blocks(B) if whole[1] else A.column_blocks(B)
-    assert blocks is not None and sum(b.nnz for b in blocks) == A.nnz
-    if whole[0]:
-        assert blocks[0].whole_rows is not None and blocks[0].split_whole() is not None
     X = torch.from_numpy(x).cuda()
     for msg in _ops(K):
         mode, terms, div = combine_plan(msg, K + 1)
@@ -84,6 +76,34 @@ def test_propagate_aggregate_column_blocked_bit_exact(oracle_mod, monkeypatch, n
             got = propagate_aggregate(A, X, K, combine_steps(mode, terms, div), col_blocks=B)
         np.testing.assert_array_equal(got.cpu().numpy(), _expected(oracle_mod, msg, hops),
                                       err_msg=f"{name} B={B} {msg.aggr_type} {msg.start}:{msg.end}")
+
+
+@pytest.mark.parametrize("whole", [(0, False), (4, False), (16, True), (1 << 30, False)])
+@pytest.mark.parametrize("B", [2, 3])
+@pytest.mark.parametrize("name", ["cora_sym_k3", "rand_d130_r1", "rand_d36_ppr"])
+def test_aggregation_epilogue_over_restated_layouts(name, B, whole):
+    """The aggregation epilogue in layouts the planner does not pick (tests/plan_layout_ref.py: every
+    row cut, short rows whole up to 4 / 16 entries or every row whole, spans or compact copies):
+    out and agg == the one-launch srg_spmm_agg_f32, bit for bit."""
+    import plan_layout_ref as R
+    from srgnn.csr import DeviceCSR
+    from srgnn.spmm import spmm_agg
+    c = G.Case(name)
+    ip, ix, v = c.ahat()
+    A = DeviceCSR.from_tensors(ip, ix, v, n_cols=c.n, device="cuda")
+    blocks = (R.compact_column_blocks if whole[1] else R.column_blocks)(A, B, whole[0])
+    assert blocks is not None and sum(b.nnz for b in blocks) == A.nnz
+    if whole[0]:
+        assert blocks[0].whole_rows is not None and R.split_whole(blocks[0]) is not None
+    X = torch.from_numpy(c.x()).cuda()
+    prev = torch.from_numpy(np.random.default_rng(3).standard_normal(X.shape).astype(np.float32)).cuda()
+    y_ref, agg_ref = torch.empty_like(X), prev.clone()
+    spmm_agg(A, X, y_ref, agg_ref, 0.37, False)
+    y, agg = torch.empty_like(X), prev.clone()
+    R.hop(A, X, y, B, compact=whole[1], split=True, whole_max=whole[0], agg=(agg, 0.37, False))
+    torch.cuda.synchronize()
+    assert torch.equal(y.view(torch.int32), y_ref.view(torch.int32))
+    assert torch.equal(agg.view(torch.int32), agg_ref.view(torch.int32))
 
 
 def test_graphop_propagate_aggregate_matches_aggregate_of_propagate():
@@ -230,8 +250,9 @@ def test_span_blocks_every_path(thr, d):
     y_ref = spmm(A, X)
     agg_ref = prev.clone()
     spmm_agg(A, X, torch.empty_like(y_ref), agg_ref, 0.37, False)
+    import plan_layout_ref as R
     for B in (2, 3):
-        spans = A.column_blocks(B)
+        spans = R.column_blocks(A, B)
         blocks = []
         for s in spans:        # the same spans, scheduled with the test's thresholds
             deg = s.row_end - s.indptr

@@ -83,7 +83,8 @@ def test_fast_blocked_hops_and_khop(oracle_mod):
     B = 3
     ye = hop(A, x, torch.empty_like(x), col_blocks=B)
     yf = hop(A, x, torch.empty_like(x), col_blocks=B, fast=True)
-    blocks = A.column_blocks(B)
+    import plan_layout_ref as R
+    blocks = R.column_blocks(A, B)        # the plan's blocks, restated: their hub rows run FAST
     hubs = set()
     for blk in blocks:
         hubs |= set(blk.order[: blk.n_hub].tolist())

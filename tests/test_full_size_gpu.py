@@ -47,27 +47,29 @@ def _check_rows(oracle_mod, rows, sub, ucols, prev, got, what):
 @pytest.mark.timeout(600)
 def test_products_timed_layout_every_hop_bit_exact(oracle_mod):
     """The operator bench.py times on the headline config: products-shaped graph (126 M nonzeros),
-    K = 10, d = 128, default thresholds, twelve COMPACT column blocks (>= 6 hops; block 0 in two
+    K = 10, d = 128, default thresholds, the native plan's twelve COMPACT column blocks (>= 6 hops; block 0 in two
     launches, its cut spans then its whole rows; compact copies in launch order, packed rows reading
     their spans by schedule slot), short rows (<= BLOCK_WHOLE_MAX = 48) whole in block 0, 2 gathers
     per packed row (PACKED_U2) -- EVERY row of every hop (2,449,029 x 128 per hop) checked bit for
     bit against the oracle fed with the GPU's previous hop (~1-3 s of host time per hop)."""
     from srgnn import csr as csr_mod, graphs, spmm as spmm_mod, synth
     from srgnn.csr import DeviceCSR
-    from srgnn.spmm import auto_col_blocks, column_blocks_for, propagate
-    assert csr_mod.BLOCK_WHOLE_MAX == 48 and spmm_mod._U2_BLOCKED and csr_mod.DEFAULT_HEAVY_THRESHOLD is None
+    from srgnn.plan import cached
+    from srgnn.spmm import auto_col_blocks, prepare, propagate
+    assert csr_mod.DEFAULT_HEAVY_THRESHOLD is None and csr_mod.DEFAULT_HUB_THRESHOLD is None
     ip, ix, vals, n, d, K = graphs.build("products", "cuda")
     assert K == 10 and d == 128
     A = DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, device="cuda")
     hops = K * 25                                   # the driver's 20 steps + 5 warm-up
-    B = auto_col_blocks(A, d, hops=hops)
-    assert B == 12
-    blocks = column_blocks_for(A, B, hops=hops)
-    assert len(blocks) == 12 and A._blocks.get(("compact", 12)) and blocks[0].whole_rows is not None
-    assert sum(b.nnz for b in blocks) == A.nnz and A.n_hub >= 1
-    assert spmm_mod.launches_per_hop(A, B, d) == 13
+    assert auto_col_blocks(A, d, hops=hops) == 12
+    assert prepare(A, d, hops) == 12                # bench.py's call: the native plan
+    P = cached(A, d)
+    assert P.compact and P.split_block0 and P.hub_chain and P.n_launch == 13
+    assert spmm_mod.launches_per_hop(A, 12, d) == 13
+    launches = P.launches(d)
+    assert sum(L.n_hub for L, _ in launches) >= 12  # the top row is a hub row of every cut launch
     x = synth.uniform_features_t(n, d, seed=synth.FEATURE_SEED, device="cuda")
-    panels = propagate(A, x, K)                     # col_blocks from auto_col_blocks: the cached 12
+    panels = propagate(A, x, K)                     # through the cached plan
     torch.cuda.synchronize()
     ipn, ixn, vn = ip.cpu().numpy(), ix.cpu().numpy(), vals.cpu().numpy()
     del ip, ix, vals

@@ -178,65 +178,63 @@ def test_column_blocked_chain_continuation(name, thr):
 @pytest.mark.parametrize("compact", [False, True])
 @pytest.mark.parametrize("B,whole_max", [(2, 0), (2, 8), (3, 0), (3, 8), (5, 0), (5, 8), (4, 0), (4, 32)])
 @pytest.mark.parametrize("name", G.names("norm"))
-def test_propagate_column_blocked_bit_exact(monkeypatch, name, B, compact, whole_max):
-    """The product path's column-blocked hops (DeviceCSR.column_blocks -- row spans of the shared
-    arrays -- or compact_column_blocks -- the spans copied out -- + propagate(col_blocks=B): B
-    launches per hop, each block with its own schedule) == the reference's hops, bit for bit."""
-    from srgnn import csr as csr_mod
+def test_propagate_column_blocked_bit_exact(name, B, compact, whole_max):
+    """Column-blocked hops through the library's plan loop (srg_propagate_plan_f32: span launches,
+    ACCUMULATE, slot spans, the hub chain) over layouts the planner itself does not pick -- every row
+    cut (whole_max 0) or short rows whole up to 8 / 32 entries, spans or compact copies; built by the
+    test restatement tests/plan_layout_ref.py -- and the product path's own plan for B blocks
+    (propagate(col_blocks=B), hop(col_blocks=B)): the reference's hops, bit for bit."""
+    import plan_layout_ref as R
     from srgnn.spmm import hop, propagate
-    monkeypatch.setattr(csr_mod, "BLOCK_WHOLE_MAX", whole_max)   # rows this short run whole in block 0
     c = G.Case(name)
     A = _csr(c, (None, None))
-    blocks = A.compact_column_blocks(B) if compact else A.column_blocks(B)
+    blocks = (R.compact_column_blocks if compact else R.column_blocks)(A, B, whole_max)
     assert blocks is not None and len(blocks) == B and sum(b.nnz for b in blocks) == A.nnz
     assert all(b.is_span for b in blocks)
     # compact blocks hold copies of their entries (laid out in launch order), spans share A's arrays
     assert all((b.indices.data_ptr() != A.indices.data_ptr()) == compact for b in blocks)
     X = torch.from_numpy(c.x()).cuda()
-    hops = propagate(A, X, c.k, col_blocks=B)
-    torch.cuda.synchronize()
-    for k in range(1, c.k + 1):
-        c.check_hop(k, hops[k].cpu().numpy())
+    for hops in (R.propagate(A, X, c.k, B, compact=compact, split=True, whole_max=whole_max),
+                 R.propagate(A, X, c.k, B, compact=compact, split=False, whole_max=whole_max),
+                 propagate(A, X, c.k, col_blocks=B)):
+        torch.cuda.synchronize()
+        for k in range(1, c.k + 1):
+            c.check_hop(k, hops[k].cpu().numpy())
     one = hop(A, X, torch.empty_like(X), col_blocks=B)
     c.check_hop(1, one.cpu().numpy())
 
 
 @pytest.mark.parametrize("name", ["rand_d128_r05", "rand_d36_ppr", "cora_sym_k3"])
-@pytest.mark.parametrize("compact", [False, True])
-def test_block0_split_launches_bit_exact(monkeypatch, name, compact):
+def test_block0_split_launches_bit_exact(monkeypatch, name):
     """Block 0 of a column-blocked hop as two launches (its cut spans, then its whole rows; the
-    default) or one (spmm.SPLIT_BLOCK0 = False): the same bits as the reference either way, and
-    launches_per_hop counts B + 1 or B launches."""
-    from srgnn import csr as csr_mod
+    default below 16 GiB panels) or one (spmm.SPLIT_BLOCK0 = False): the same bits as the reference
+    either way, and launches_per_hop counts B + 1 or B launches."""
     from srgnn import spmm as spmm_mod
-    monkeypatch.setattr(csr_mod, "BLOCK_WHOLE_MAX", 8)
     c = G.Case(name)
-    A = _csr(c, (None, None))
-    blocks = A.compact_column_blocks(4) if compact else A.column_blocks(4)
-    assert blocks[0].whole_rows is not None and bool(blocks[0].whole_rows.any())
     X = torch.from_numpy(c.x()).cuda()
     d = X.shape[1]
-    assert spmm_mod._split_block0(A, d)            # "auto": a small panel is split
     for split in (True, False):
         monkeypatch.setattr(spmm_mod, "SPLIT_BLOCK0", split)
+        A = _csr(c, (None, None))
         assert spmm_mod.launches_per_hop(A, 4, d) == (5 if split else 4)
-        assert spmm_mod.launches_per_hop(A, 4, d, agg=True) == 5
         hops = spmm_mod.propagate(A, X, c.k, col_blocks=4)
         torch.cuda.synchronize()
+        assert spmm_mod.launches_per_hop(A, 4, d) == (5 if split else 4)
         for k in range(1, c.k + 1):
             c.check_hop(k, hops[k].cpu().numpy())
-    assert spmm_mod.launches_per_hop(A, 1, d) == 1
     monkeypatch.setattr(spmm_mod, "SPLIT_BLOCK0", None)
-    monkeypatch.setattr(spmm_mod, "SPLIT_BLOCK0_MAX_PANEL", 1)   # a "giant" panel: one launch
-    assert spmm_mod.launches_per_hop(A, 4, d) == 4
+    A = _csr(c, (None, None))
+    assert spmm_mod.launches_per_hop(A, 1, d) == 1
+    assert spmm_mod.launches_per_hop(A, 4, d) == 5        # "auto": a small panel is split
 
 
 @pytest.mark.parametrize("name", G.names("raw"))
 def test_column_blocks_exact_for_unordered_rows(name):
-    """Column blocks are spans of each row (srg_csr_col_splits: one binary search per row and
-    boundary), and the split points of any row -- sorted or not -- lie in the row and never
-    decrease, so the spans partition it in CSR order: the blocked hop is the one-launch hop bit
-    for bit even where the ids are unsorted (those rows only lose the blocks' locality)."""
+    """Column blocks are spans of each row (one binary search per row and boundary), and the split
+    points of any row -- sorted or not -- lie in the row and never decrease, so the spans partition it
+    in CSR order: the blocked hop is the one-launch hop bit for bit even where the ids are unsorted
+    (those rows only lose the blocks' locality)."""
+    import plan_layout_ref as R
     from srgnn.csr import DeviceCSR
     from srgnn.spmm import hop
     c = G.Case(name)
@@ -245,22 +243,23 @@ def test_column_blocks_exact_for_unordered_rows(name):
     A = DeviceCSR.from_tensors(ip, ix, a.data.astype(np.float32), n_cols=c.n, device="cuda")
     X = torch.from_numpy(c.x()).cuda()
     want = hop(A, X, torch.empty((c.n, X.shape[1]), device="cuda"), col_blocks=1).cpu().numpy()
+    assert A.n_rows == A.n_cols
     for B in (2, 3):
-        blocks = A.column_blocks(B)
+        blocks = R.column_blocks(A, B)
         assert blocks is not None and sum(b.nnz for b in blocks) == A.nnz
-        Y = hop(A, X, torch.empty((c.n, X.shape[1]), device="cuda"), col_blocks=B)
-        np.testing.assert_array_equal(Y.cpu().numpy(), want)
+        for Y in (hop(A, X, torch.empty((c.n, X.shape[1]), device="cuda"), col_blocks=B),
+                  R.propagate(A, X, 1, B, split=True)[1], R.propagate(A, X, 1, B, compact=True)[1]):
+            np.testing.assert_array_equal(Y.cpu().numpy(), want)
     c.check_hop(1, want)
 
 
 @pytest.mark.parametrize("whole_max", [0, 16])
-def test_column_block_spans_are_lower_bounds(monkeypatch, whole_max):
+def test_column_block_spans_are_lower_bounds(whole_max):
     """srg_csr_col_splits on a host-checkable CSR: for sorted rows each split is the first entry
     whose id reaches ceil(b n / B); every split lies in its row and is monotone in b (any row).
     Rows of <= whole_max entries end in block 0 (every later split at the row's end)."""
-    from srgnn import csr as csr_mod
+    import plan_layout_ref as R
     from srgnn.csr import DeviceCSR
-    monkeypatch.setattr(csr_mod, "BLOCK_WHOLE_MAX", whole_max)
     rng = np.random.default_rng(5)
     n, deg = 997, rng.integers(0, 40, 997)
     deg[3], deg[10] = 3000, 0
@@ -271,7 +270,7 @@ def test_column_block_spans_are_lower_bounds(monkeypatch, whole_max):
     for ids, sorted_rows in ((ix, True), (shuffled, False)):
         A = DeviceCSR.from_tensors(ip, ids, np.ones(ids.size, np.float32), n_cols=n, device="cuda")
         for B in (2, 3, 7):
-            blocks = A.column_blocks(B)
+            blocks = R.column_blocks(A, B, whole_max)
             starts = [b.indptr.cpu().numpy() for b in blocks] + [blocks[-1].row_end.cpu().numpy()]
             assert np.array_equal(starts[0], ip[:-1]) and np.array_equal(starts[-1], ip[1:])
             for b in range(1, B):
@@ -676,11 +675,12 @@ def test_blocked_hop_rejects_undersized_out_and_agg():
     """Column blocks 1.. and the split parts of block 0 schedule a subset of the rows but write rows
     of the whole operator: hop / spmm / spmm_agg check out and agg against the full row count
     (ValueError, nothing launched), and a block refuses to allocate its own out."""
+    import plan_layout_ref as R
     from srgnn.spmm import hop, spmm, spmm_agg
     c = G.Case("rand_d128_r05")
     A = _csr(c, (None, None))
     X = torch.from_numpy(c.x()).cuda()
-    blocks = A.column_blocks(4)
+    blocks = R.column_blocks(A, 4)
     assert any(b.schedules_subset for b in blocks[1:])
     small = torch.empty((c.n - 1, X.shape[1]), device="cuda")
     full = torch.empty_like(X)
@@ -721,22 +721,30 @@ def test_hub_side_streams_bounded():
 
 
 def test_column_blocks_keep_explicit_thresholds():
-    """An operator built with explicit thresholds schedules its column blocks (and block 0's split
-    parts) with the same thresholds and no automatic narrow split; the automatic operator's blocks
-    keep the narrow split.  Same bits either way."""
+    """An operator built with explicit thresholds has its column blocks (and block 0's split parts)
+    scheduled with the same thresholds and no automatic narrow split -- in the native plan, launch by
+    launch, as in the test restatement; the automatic operator's blocks keep the narrow split.  Same
+    bits either way."""
+    import plan_layout_ref as R
+    from srgnn.plan import NativePlan
     from srgnn.spmm import hop
     c = G.Case("rand_d128_r05")
     A = _csr(c, (5, 60))
     assert A.n_heavy_narrow is None and A.thresholds == (5, 60)
     X = torch.from_numpy(c.x()).cuda()
-    for blk in A.column_blocks(3):
+    for blk in R.column_blocks(A, 3):
         assert blk.thresholds == (5, 60) and blk.n_heavy_narrow is None
         deg = (blk.row_end - blk.indptr)[blk.order.long()]
         assert blk.n_hub == int((deg > 60).sum()) and blk.n_hub + blk.n_heavy == int((deg > 5).sum())
-    for part in A.column_blocks(3)[0].split_whole() or ():
+    for part in R.split_whole(R.column_blocks(A, 3)[0]) or ():
         assert part.n_heavy_narrow is None
+    P = NativePlan(A, 16, hops=4, col_blocks=3, split_block0=True)
+    plan_py, _ = R.hop_plan(A, 16, 3, compact=False, split=True)
+    for (L, _), (Ab, _, _) in zip(P.launches(16), plan_py):
+        assert (L.n_hub, L.n_heavy) == (Ab.n_hub, Ab.heavy(16))     # d = 16: the narrow count is n_heavy
+    P.close()
     auto = _csr(c, (None, None))
-    assert all(b.n_heavy_narrow is not None for b in auto.column_blocks(3))
+    assert all(b.n_heavy_narrow is not None for b in R.column_blocks(auto, 3))
     y = hop(A, X, torch.empty_like(X), col_blocks=3, agg=(torch.zeros_like(X), 1.0, True))
     torch.cuda.synchronize()
     c.check_hop(1, y.cpu().numpy())
@@ -750,7 +758,9 @@ def test_blocked_hop_hub_rows_chained_or_forked_bit_exact(oracle_mod, mode):
     from srgnn import synth
     from srgnn.csr import DeviceCSR
     from srgnn.normalize import sym_norm_binary
-    from srgnn.spmm import _same_hub_rows, hop, spmm
+    import plan_layout_ref as R
+    from srgnn.plan import cached
+    from srgnn.spmm import hop, spmm
     n = 30000
     u, v = synth.rmat_undirected_t(n, 400000, seed=51, device="cuda")
     ip, ix = synth.symmetric_csr_t(n, u, v)
@@ -761,16 +771,17 @@ def test_blocked_hop_hub_rows_chained_or_forked_bit_exact(oracle_mod, mode):
     thr = 150 if mode == "mixed" else 300
     A = DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, hub_threshold=thr, device="cuda")
     want = spmm(A, x)
-    blocks = A.column_blocks(3)
+    blocks = R.column_blocks(A, 3)
     assert any(b.n_hub for b in blocks)
-    assert _same_hub_rows(A, 3, blocks) == (mode == "same")
+    assert R._same_hub_rows([R.split_whole(blocks[0])[0]] + blocks[1:]) == (mode == "same")
     y = torch.empty_like(x)
     for _ in range(3):
         hop(A, x, y, col_blocks=3)
         torch.cuda.synchronize()
         assert torch.equal(y, want), mode
+    # the native plan chains exactly when the restatement does
+    assert cached(A, 128).hub_chain == (mode == "same")
     # with the aggregation step fused (the split block 0 and the aggregating last block in the chain)
-    assert _same_hub_rows(A, 3, [blocks[0].split_whole()[0]] + blocks[1:], agg=True) == (mode == "same")
     agg = torch.empty_like(x)
     for _ in range(2):
         hop(A, x, y, col_blocks=3, agg=(agg, 0.5, True))
@@ -782,25 +793,25 @@ def test_propagate_plan_entry_rejects_bad_launches():
     """srg_propagate_plan_f32 (the native blocked hop loop) validates every launch before the first
     kernel: a schedule with hub / heavy rows but no row_order, a null panel, negative K."""
     import ctypes
+    import plan_layout_ref as R
     from srgnn import _lib
-    from srgnn import spmm as spmm_mod
     c = G.Case("rand_d128_r05")
     A = _csr(c, (None, None))
     X = torch.from_numpy(c.x()).cuda()
     Y = torch.empty_like(X)
     d = X.shape[1]
-    plan, join = spmm_mod._hop_plan(A, d, 2)
-    arr = spmm_mod._plan_array(plan, d)
+    plan, join = R.hop_plan(A, d, 2, compact=False, split=True)
+    arr = R.launch_array(plan, d)
     panels = (ctypes.c_void_p * 2)(X.data_ptr(), Y.data_ptr())
     _lib.call(X.device, "srg_propagate_plan_f32", arr, len(plan), int(join), panels, d, d, 1, _lib.stream(X.device))
     torch.cuda.synchronize()
     c.check_hop(1, Y.cpu().numpy())
-    bad = spmm_mod._plan_array(plan, d)
+    bad = R.launch_array(plan, d)
     bad[0].n_heavy, bad[0].row_order = max(1, bad[0].n_heavy), None
     with pytest.raises(RuntimeError):
         _lib.call(X.device, "srg_propagate_plan_f32", bad, len(plan), int(join), panels, d, d, 1, _lib.stream(X.device))
     if any(Ab.is_span for Ab, _, _ in plan):
-        half = spmm_mod._plan_array(plan, d)
+        half = R.launch_array(plan, d)
         i = next(j for j, (Ab, _, _) in enumerate(plan) if Ab.is_span)
         half[i].slot_end = None                   # slot spans come in pairs
         with pytest.raises(RuntimeError):
@@ -815,7 +826,7 @@ def test_propagate_plan_entry_rejects_bad_launches():
     Ah = _csr(c, (16, 64))
     hplan = [(Ah, _lib.SRG_SPMM_HUB_NOJOIN, "plain")]
     assert Ah.n_hub > 0
-    nj = spmm_mod._plan_array(hplan, d)
+    nj = R.launch_array(hplan, d)
     Z = torch.empty_like(X)
     three = (ctypes.c_void_p * 3)(X.data_ptr(), Y.data_ptr(), Z.data_ptr())
     with pytest.raises(RuntimeError, match="join_hub"):
@@ -828,24 +839,26 @@ def test_propagate_plan_entry_rejects_bad_launches():
 
 @pytest.mark.parametrize("native", [True, False])
 @pytest.mark.parametrize("name", ["rand_d128_r05", "rand_d36_ppr", "cora_sym_k3"])
-def test_schedule_ordered_one_launch_bit_exact(monkeypatch, name, native):
-    """A long-lived one-launch operator's launch-ordered copy (made by spmm.prepare for runs of >=
-    MIN_HOPS_TO_COMPACT hops: the native plan's compact copy, or DeviceCSR.schedule_ordered in the
-    torch formulation): propagate and hop through it == the reference, bit for bit."""
+def test_schedule_ordered_one_launch_bit_exact(name, native):
+    """A long-lived one-launch operator's launch-ordered copy (spmm.prepare for runs of >=
+    SRG_PLAN_MIN_HOPS_TO_COMPACT hops: the native plan's compact copy; or the test restatement's
+    schedule_ordered, run through the plan loop): propagate and hop through it == the reference, bit
+    for bit."""
+    import plan_layout_ref as R
     from srgnn import spmm as spmm_mod
     from srgnn.plan import cached
-    monkeypatch.setattr(spmm_mod, "NATIVE_PLAN", native)
     c = G.Case(name)
     A = _csr(c, (None, None))
     X = torch.from_numpy(c.x()).cuda()
-    assert spmm_mod.prepare(A, X.shape[1], hops=1000) == 1
     if native:
+        assert spmm_mod.prepare(A, X.shape[1], hops=1000) == 1
         P = cached(A, X.shape[1])
         assert P.compact and P.n_launch == 1 and P.col_blocks == 1
+        hops = spmm_mod.propagate(A, X, c.k)
     else:
-        S = A._blocks["sched"]
+        S = R.schedule_ordered(A)
         assert S.is_span and S.nnz == A.nnz and S.indices.data_ptr() != A.indices.data_ptr()
-    hops = spmm_mod.propagate(A, X, c.k)
+        hops = R.propagate(A, X, c.k, 1, compact=True)
     torch.cuda.synchronize()
     for k in range(1, c.k + 1):
         c.check_hop(k, hops[k].cpu().numpy())

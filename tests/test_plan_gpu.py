@@ -1,7 +1,7 @@
 """The native one-GPU planner (srg_plan_build / srg_plan_propagate_f32, csrc/srg_plan.hip) against the
-torch formulation of the same layout (DeviceCSR.column_blocks / compact_column_blocks / split_whole +
-spmm._hop_plan) launch by launch -- schedules, hub / slice-wave counts, flags, the entries every slot
-span points at -- and its hops against the reference's (golden fixtures) bit for bit."""
+test-side torch restatement of the same layout (tests/plan_layout_ref.py: column blocks, compact copies,
+block 0's split, the hop plan's flags) launch by launch -- schedules, hub / slice-wave counts, flags, the
+entries every slot span points at -- and its hops against the reference's (golden fixtures) bit for bit."""
 import ctypes
 
 import numpy as np
@@ -58,19 +58,15 @@ def _spans(beg, end):
     return start + torch.arange(tot, dtype=torch.int64, device=beg.device) - off
 
 
-def _python_layout(A, d, B, compact, split, monkeypatch):
-    """spmm._hop_plan's launches for a forced layout: [(operator, flags)], join."""
-    from srgnn import spmm as S
-    monkeypatch.setattr(S, "SPLIT_BLOCK0", split)
+def _python_layout(A, d, B, compact, split, monkeypatch=None):
+    """The restatement's launches for a forced layout: [(operator, flags)], join (split None: the
+    planner's automatic choice for these small panels, split)."""
+    import plan_layout_ref as R
     if B > 1:
-        if compact:
-            A.compact_column_blocks(B)
-        else:
-            A.column_blocks(B)
-        plan, join = S._hop_plan(A, d, B)
+        plan, join = R.hop_plan(A, d, B, compact, True if split is None else bool(split))
         return [(Ab, f) for Ab, f, _ in plan], join
     if compact:
-        return [(A.schedule_ordered(), 0)], False
+        return [(R.schedule_ordered(A), 0)], False
     return [(A, 0)], False
 
 
@@ -304,8 +300,9 @@ def test_native_plan_edge_cases():
 
 
 def test_native_plan_automatic_choices_match_prepare(monkeypatch):
-    """At a size where the automatic rules cut (a 600 MB panel): the native plan's block count, split
-    and launches are those of the torch formulation's prepare(); propagate() runs through it."""
+    """At a size where the automatic rules cut (a 600 MB panel): prepare() lays the operator out with the
+    native plan (12 compact blocks, block 0 split, 13 launches, launch for launch the test restatement's
+    layout); propagate() runs through it."""
     from srgnn import spmm as S
     from srgnn.plan import NativePlan, cached
     rng = np.random.default_rng(2)
@@ -323,14 +320,12 @@ def test_native_plan_automatic_choices_match_prepare(monkeypatch):
     P = cached(A, d)
     assert P is not None and B == P.col_blocks == 12 and P.split_block0 and P.compact
     assert S.launches_per_hop(A, B, d) == B + 1
-    # the torch formulation of the same layout on a second operator over the same arrays
+    # the test restatement of the same layout on a second operator over the same arrays
+    import plan_layout_ref as R
     from srgnn.csr import DeviceCSR
     A2 = DeviceCSR.from_tensors(A.indptr, A.indices, A.values, n_cols=n, device="cuda")
-    monkeypatch.setattr(S, "NATIVE_PLAN", False)
-    assert S.prepare(A2, d, hops=40) == B
-    plan_py, join = S._hop_plan(A2, d, B)
+    plan_py, join = R.hop_plan(A2, d, B, compact=True, split=True)
     _check_layout(A, P, d, [(Ab, f) for Ab, f, _ in plan_py], join)
-    monkeypatch.setattr(S, "NATIVE_PLAN", True)
     X = torch.randn(n, d, device="cuda")
     out = S.propagate(A, X, 1, col_blocks=B)
     ref = S.spmm(A, X)
@@ -416,9 +411,8 @@ def test_plan_hop_strided_and_aggregating(B, compact, split, d):
 
 def test_aggregation_loop_runs_the_native_plan(monkeypatch):
     """spmm.prepare lays the operator out with the native plan; propagate_aggregate's fused hops then
-    run through it (srg_plan_hop_f32), with the same bits as the torch-formulated layout (NATIVE_PLAN
-    off)."""
-    from srgnn import spmm as S
+    run through it (srg_plan_hop_f32, the aggregation in the epilogue): the same bits as the
+    aggregation over one-launch hops."""
     from srgnn.aggregate import combine_plan, combine_steps, propagate_aggregate
     from srgnn.plan import cached
     ip, ix, v, n = _power_law(seed=17)
@@ -434,16 +428,15 @@ def test_aggregation_loop_runs_the_native_plan(monkeypatch):
     orig = PL.NativePlan.hop
 
     def spy(self, *a, **k):
-        calls.append(a[4] if len(a) > 4 else k.get("agg"))
+        calls.append((self.col_blocks, a[4] if len(a) > 4 else k.get("agg")))
         return orig(self, *a, **k)
     monkeypatch.setattr(PL.NativePlan, "hop", spy)
-    for native in (True, False):
-        monkeypatch.setattr(S, "NATIVE_PLAN", native)
+    for B in (3, 1):
         A = _csr(ip, ix, v, n)
-        outs.append(propagate_aggregate(A, X, K, steps, col_blocks=3))
-        assert (cached(A, d) is not None) == native
+        outs.append(propagate_aggregate(A, X, K, steps, col_blocks=B))
+        assert cached(A, d) is not None and cached(A, d).col_blocks == B
     assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
-    assert len(calls) == K and any(c is not None for c in calls)
+    assert len(calls) == 2 * K and any(agg is not None for B, agg in calls if B == 3)
 
 
 @pytest.mark.parametrize("d", [64, 128, 256])

@@ -157,9 +157,10 @@ def test_split_path_column_blocked_bit_identical(monkeypatch, B):
     L = W.laplacian_from_adj(a)
     f = W.HeatWaveletFilter(L, [-0.5, 0.5], order=3, lmax=None, dtype=torch.float32, device="cuda",
                             heavy_threshold=40, hub_threshold=400)
-    assert f._csr(f.fvals).column_blocks(int(B)) is not None
+    from srgnn.plan import cached
     S = torch.from_numpy(np.random.default_rng(9).standard_normal((a.shape[0], 128)).astype(np.float32)).cuda()
     assert torch.equal(f.apply(S, split=False), f.apply(S, split=True, col_block=64))
+    assert cached(f._csr(f.fvals), 64).col_blocks == B
 
 
 def test_split_path_runs_the_native_plan(monkeypatch):
@@ -178,24 +179,26 @@ def test_split_path_runs_the_native_plan(monkeypatch):
     assert torch.equal(f.apply(S, split=False), f.apply(S, split=True, col_block=64))
 
 
-def test_split_path_torch_blocks_fallback(monkeypatch):
-    """prepare_column_blocks(native=False) (bench.py's fallback when the plans crowd out the work
-    panels): the torch formulation of the same blocks, no native plan, bit for bit the fused kernel;
-    drop_layouts frees every cached layout, plans included."""
+def test_split_path_plans_in_torch_memory(monkeypatch):
+    """The filter's plans hold their memory as torch allocations (srg_plan_build_in: what the RMAT-26
+    filter bank needs, whose graph build leaves torch's cache full of reusable blocks); bit for bit the
+    fused kernel; drop_layouts frees every cached plan and returns the memory to torch."""
     from srgnn import spmm as S_, wavelet as W
-    from srgnn.plan import cached, plan_for
+    from srgnn.plan import cached
     monkeypatch.setattr(S_, "FORCE_COL_BLOCKS", 3)
     a = graphs()["rmat3000"]
     L = W.laplacian_from_adj(a)
     f = W.HeatWaveletFilter(L, [-0.5, 0.5], order=4, lmax=None, dtype=torch.float32, device="cuda")
-    assert f.prepare_column_blocks(64, hops=8, native=False) == 3
+    before = torch.cuda.memory_allocated()
+    assert f.prepare_column_blocks(64, hops=8) == 3
     Fm = f._csr(f.fvals)
-    assert cached(Fm, 64) is None and 3 in Fm._blocks
+    P = cached(Fm, 64)
+    assert P is not None and P._keep is not None and P._keep.numel() >= P.device_bytes
+    assert torch.cuda.memory_allocated() - before >= P.device_bytes
     S = torch.from_numpy(np.random.default_rng(6).standard_normal((a.shape[0], 128)).astype(np.float32)).cuda()
     assert torch.equal(f.apply(S, split=False), f.apply(S, split=True, col_block=64))
-    P = plan_for(Fm, 64, 8)
     f.drop_layouts()
-    assert not Fm._blocks and P._p is None
+    assert not Fm._blocks and P._p is None and P._keep is None
 
 
 def test_spmm_cheby_in_place_and_argument_checks():

@@ -15,6 +15,7 @@ import sys
 
 HERE = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(HERE, "scalable-roubust-gnn_amd"))
+sys.path.insert(0, os.path.join(HERE, "tests"))
 
 import torch  # noqa: E402
 
@@ -22,7 +23,7 @@ from srgnn import csr as _csr, graphs, synth  # noqa: E402
 from srgnn.csr import DeviceCSR  # noqa: E402
 from srgnn.spmm import hop  # noqa: E402
 
-_csr.BLOCK_WHOLE_MAX = 0      # every row cut (the probe's round-2 setting)
+
 
 B = 8
 LR = 4
@@ -35,7 +36,8 @@ cfg = sys.argv[1] if len(sys.argv) > 1 else "products"
 ip, ix, vals, n, d, _ = graphs.build(cfg, dev)
 A = DeviceCSR.from_tensors(ip, ix, vals, n_cols=n, device=dev)
 X = synth.uniform_features_t(n, d, device=dev)
-blocks = A.compact_column_blocks(B)
+import plan_layout_ref as R  # noqa: E402  (tests/: the torch restatement of the layout)
+blocks = R.compact_column_blocks(A, B, whole_max=0)   # every row cut (the probe's round-2 setting)
 n_slices = d // 32
 desc, Ys, info = [], [], []
 for blk in blocks:
