@@ -91,7 +91,7 @@ def hop(A: DeviceCSR, X: torch.Tensor, out: torch.Tensor, nt_store: bool = False
         _check_panel(agg[0], A.out_rows, "agg", d)
     if out.device != A.device or X.device != A.device:
         raise ValueError("A, X and out must be on the same device")
-    if X.data_ptr() == out.data_ptr():
+    if X.numel() and X.data_ptr() == out.data_ptr():
         raise ValueError("out must not alias X (its rows are gathered)")
     _no_spans(A, "hop")
     if A.n_rows != A.n_cols:
