@@ -142,9 +142,10 @@ int srg_spmm_csr_f32(const int64_t* indptr, const int32_t* indices, const float*
  * GraphOp.propagate, SSRG/operators/base_operator.py:32-35 (with the per-hop host round trips of
  * utils.py:38-47 removed).  A square (n_rows == rows of X).  Given no schedule (row_order NULL,
  * n_hub = n_heavy = 0) and flags within NT_STORE | FAST, the hops run through a plan built for them
- * (srg_plan_build with automatic choices, released in stream order after the hops; the call then
- * synchronises `stream` twice while it plans and takes the plan's memory for its duration); with a
- * schedule, or other flags, every hop is one launch over the caller's CSR. */
+ * (srg_plan_build with automatic choices -- no hub rows under FAST, so FAST changes no bit there, as
+ * before the planner -- released after the hops; the call then synchronises `stream` while it plans
+ * and releases, and allocates the plan's memory for its duration, so it cannot be captured into a HIP
+ * graph); with a schedule, or other flags, every hop is one launch over the caller's CSR (capturable). */
 int srg_propagate_khop_f32(const int64_t* indptr, const int32_t* indices, const float* values,
                            int64_t n_rows, const int32_t* row_order, int64_t n_hub,
                            int64_t n_heavy, float* const* panels,

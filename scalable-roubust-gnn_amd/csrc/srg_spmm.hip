@@ -2190,9 +2190,12 @@ int srg_propagate_khop_f32(const int64_t* indptr, const int32_t* indices, const 
     const uint32_t f = flags & ~SRG_SPMM_ACCUMULATE;
     if (!row_order && n_hub == 0 && n_heavy == 0 && K > 0 && n_rows > 0 && d > 0 &&
         !(f & ~(SRG_SPMM_NT_STORE | SRG_SPMM_FAST))) {
-        // no schedule: the hops run through a plan made for them (srg_plan.hip), freed after them
+        // no schedule: the hops run through a plan made for them (srg_plan.hip), freed after them.  Without
+        // a schedule there were never hub rows here, so FAST (which only re-associates hub rows) changed
+        // nothing: the implicit plan then has no hub rows either, and the bits stay exact
         srg_plan* P = nullptr;
-        rc = srg_plan_build(indptr, indices, values, n_rows, d, K, 0, SRG_PLAN_AUTO, SRG_PLAN_AUTO, 0, stream, &P);
+        const int64_t hub_t = (f & SRG_SPMM_FAST) ? SRG_PLAN_NONE : SRG_PLAN_AUTO;
+        rc = srg_plan_build(indptr, indices, values, n_rows, d, K, 0, hub_t, SRG_PLAN_AUTO, 0, stream, &P);
         if (rc) return rc;
         rc = srg_plan_propagate_f32(P, panels, ld, d, K, f, stream);
         const int rc2 = srg_plan_destroy(P, stream);

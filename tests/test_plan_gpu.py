@@ -235,6 +235,26 @@ def test_khop_without_schedule_plans_itself():
             assert torch.equal(outs[0][k].view(torch.int32), outs[1][k].view(torch.int32))
 
 
+def test_khop_without_schedule_fast_stays_exact():
+    """srg_propagate_khop_f32 without a schedule never had hub rows, so SRG_SPMM_FAST (which
+    re-associates hub rows only) changed no bit; its implicit plan is built without hub rows under
+    FAST, so the call stays exact -- bitwise the unscheduled exact call, on a graph with long rows."""
+    from srgnn import _lib
+    ip, ix, v, n = _power_law(seed=23)
+    A = _csr(ip, ix, v, n)
+    X = torch.randn(n, 64, device="cuda")
+    outs = []
+    for flags in (0, _lib.SRG_SPMM_FAST):
+        panels = [X] + [torch.empty_like(X) for _ in range(3)]
+        arr = (ctypes.c_void_p * 4)(*[p.data_ptr() for p in panels])
+        _lib.call(X.device, "srg_propagate_khop_f32", A.indptr.data_ptr(), A.indices.data_ptr(), A.values.data_ptr(),
+                  n, None, 0, 0, arr, 64, 64, 3, flags, _lib.stream(X.device))
+        outs.append(panels)
+    torch.cuda.synchronize()
+    for k in range(1, 4):
+        assert torch.equal(outs[0][k].view(torch.int32), outs[1][k].view(torch.int32)), k
+
+
 def test_native_plan_edge_cases():
     """No entries; every row whole (the cut launches are empty); a hub in one block only (no chain)."""
     from srgnn.plan import NativePlan
