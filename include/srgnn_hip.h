@@ -222,19 +222,21 @@ typedef struct {
     int32_t n_launch;                /* k_spmm launches per hop */
     int32_t compact, split_block0, hub_chain;
     int32_t device;
+    int32_t hub_rows_whole;          /* rows of the whole hub rows' launch (first in the hop; 0: none) */
 } srg_plan_desc;
 int srg_plan_build(const int64_t* indptr, const int32_t* indices, const float* values, int64_t n_rows,
                    int32_t d, int32_t hops, int32_t col_blocks, int64_t hub_threshold, int64_t heavy_threshold,
                    uint32_t opts, void* stream, srg_plan** plan);
-/* The device memory srg_plan_build would take for these arguments -- keep_bytes for the plan's life,
+/* The device memory srg_plan_build would take for these arguments (the ids and values are not read) --
+ * keep_bytes for the plan's life,
  * scratch_bytes during the build -- and the choices it would make (resolved_opts: SRG_PLAN_COMPACT or
  * SPANS | SPLIT_BLOCK0 or WHOLE_BLOCK0; resolved_col_blocks).  One pass over indptr (synchronises
  * `stream`); nothing is allocated.  With srg_plan_build_in, a host puts the plan in memory of its own
  * allocator (srgnn: torch's caching allocator, so a plan competes for the same cached blocks as the
  * panels instead of beside them). */
 int srg_plan_query(const int64_t* indptr, int64_t n_rows, int32_t d, int32_t hops, int32_t col_blocks,
-                   uint32_t opts, void* stream, size_t* keep_bytes, size_t* scratch_bytes, uint32_t* resolved_opts,
-                   int32_t* resolved_col_blocks);
+                   int64_t hub_threshold, int64_t heavy_threshold, uint32_t opts, void* stream, size_t* keep_bytes,
+                   size_t* scratch_bytes, uint32_t* resolved_opts, int32_t* resolved_col_blocks);
 /* srg_plan_build into the caller's memory: `keep` (>= keep_bytes of srg_plan_query for the same
  * arguments and the resolved opts / col_blocks, 256-byte aligned) holds the plan until srg_plan_destroy
  * returns; `scratch` (>= scratch_bytes) only until this call returns.  The plan never frees either. */

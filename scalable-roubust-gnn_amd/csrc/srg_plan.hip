@@ -52,11 +52,14 @@ struct srg_plan {
         const int64_t* slot_end = nullptr;
         int64_t item0 = 0;                   // the launch's first item (slot 0) among all the plan's items
         bool whole_rows = false;             // block 0's whole rows (not in the hub chain)
+        bool hub_whole = false;              // the whole hub rows' launch (hub workgroups only)
     };
     int device = 0;
     int64_t n = 0, nnz = 0, n_items = 0;
     int32_t d = 0, B = 1;
     bool split0 = false, compact = false, same_hubs = false;
+    bool block_hubs = false;                 // some launch over cut rows has hub rows
+    int64_t n_hub_whole = 0;                 // rows in the whole hub rows' launch
     // compact plans: whether the row-indexed spans hold every scheduled row (the light-row paths of
     // panels other than 64 / 128 / 256 columns read them) or only the hub and slice-wave rows (the
     // packed light rows read the spans by slot); completed on first need (complete_rows)
@@ -134,17 +137,30 @@ constexpr int kMaxLaunch = kMaxBlocks + 1;
 constexpr int kHubPrefix = 256;                // hub rows compared for the chain (more: no chain)
 constexpr int64_t kCopyChunk = 4096;           // entries of the copy per wave task
 
-// rows of a launch: every row, block 0's cut rows / whole rows
-enum RowSet { kAll = 0, kCut = 1, kWhole = 2 };
+// rows of a launch: every row, block 0's cut rows / whole rows, the whole hub rows (round 6)
+enum RowSet { kAll = 0, kCut = 1, kWhole = 2, kHubWhole = 3 };
+
+// Whole hub rows (round 6).  In a column-blocked hop a row longer than the one-launch
+// hop's hub threshold, max(2048, nnz / 1024) entries, used to be a hub row of every block: twelve chained
+// k_spmm_hub launches on the side stream per products hop, each queued behind a full-chip block launch
+// (4.5 ms of the 5.15 ms hop from the first fork to the last join).  Such a row is now cut nowhere: it is
+// the hub workgroups of one launch of its own, first in the hop, forked onto the side stream and joined at
+// the end of the hop -- its whole chain, in CSR order, in one k_spmm_hub launch (the chained spans
+// continued the same fma chain from the fp32 value stored between blocks: the same bits).  Only for
+// automatic hub thresholds and column-blocked plans.
+constexpr int kMaxLaunchTotal = kMaxLaunch + 1;
 
 struct LaunchTable {
     int n_launch;
     int lbits;                                 // launch id bits above the length bits
     int lenbits;
     int whole_rule;                            // 1: the one-launch hop's heavy threshold (nnz / 100000)
+    int base;                                  // 1: launch 0 is the whole hub rows' launch
     int64_t hub_t, heavy_t;                    // row lengths, or SRG_PLAN_AUTO / SRG_PLAN_NONE
-    int64_t off[kMaxLaunch + 1];               // item offsets of the launches
-    int64_t rows_lim[kMaxLaunch];              // compact: items of launch L below off[L] + rows_lim[L] get row-indexed spans
+    int64_t hubw_t;                            // rows longer than this are whole hub rows (INT64_MAX: none)
+    int64_t off[kMaxLaunchTotal + 1];          // item offsets of the launches
+    int64_t rows_lim[kMaxLaunchTotal];         // compact: items of launch L below off[L] + rows_lim[L] get row-indexed spans
+    int32_t blk[kMaxLaunchTotal];              // the column block each launch's spans belong to
 };
 
 // Bump allocation out of one device allocation (256-byte aligned pieces): a plan makes two
@@ -192,11 +208,24 @@ __global__ void __launch_bounds__(256) k_plan_stats(const int64_t* __restrict__ 
     }
 }
 
+// rows longer than t (the whole hub rows: a handful)
+__global__ void __launch_bounds__(256) k_plan_count_above(const int64_t* __restrict__ ip, int64_t n, int64_t t,
+                                                          unsigned long long* __restrict__ count)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    unsigned long long c = 0;
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += stride) c += ip[r + 1] - ip[r] > t ? 1 : 0;
+    for (int o = 32; o > 0; o >>= 1) c += (unsigned long long)__shfl_xor((long long)c, o);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(count, c);
+}
+
 // split points of the column blocks (srg_csr_col_splits' lower bounds) for the cut rows; the whole rows
 // end in block 0 (only block 0's end is ever read for them), and the cut-row flags
+// (the whole hub rows too: their one launch reads block 0's end).  flag[r]: 1 for a cut row, 1 << 32 for a
+// whole hub row, 0 for a whole row -- one exclusive scan then gives both positions (low / high words)
 __global__ void __launch_bounds__(256) k_plan_splits(const int64_t* __restrict__ ip, const int32_t* __restrict__ ix,
-                                                     int64_t n, int B, int64_t* __restrict__ splits,
-                                                     int32_t* __restrict__ cut)
+                                                     int64_t n, int B, int64_t hubw_t, int64_t* __restrict__ splits,
+                                                     int64_t* __restrict__ flag)
 {
     // grid-stride over the n (B - 1) (row, boundary) pairs: the grid is capped, so an operator of any
     // size (n (B - 1) past 2^32 work-items: 1.4e9 rows at B = 4) launches
@@ -206,8 +235,9 @@ __global__ void __launch_bounds__(256) k_plan_splits(const int64_t* __restrict__
         const int64_t r = t % n;
         const int64_t beg = ip[r], end = ip[r + 1];
         const bool whole = end - beg <= kWholeMax;
-        if (b == 1) cut[r] = whole ? 0 : 1;
-        if (whole) {
+        const bool hubw = end - beg > hubw_t;
+        if (b == 1) flag[r] = hubw ? (int64_t(1) << 32) : whole ? 0 : 1;
+        if (whole || hubw) {
             if (b == 1) splits[t] = end;
             continue;
         }
@@ -227,34 +257,39 @@ __device__ __forceinline__ int64_t bound_of(const int64_t* __restrict__ ip, cons
     return b == 0 ? ip[r] : (b == B ? ip[r + 1] : splits[(int64_t)(b - 1) * n + r]);
 }
 
-__device__ __forceinline__ int block_of(int L, bool split0) { return split0 ? (L <= 1 ? 0 : L - 1) : L; }
 
 // the sort items: one (launch, span length) key and the row id per (launch, row of it), the launch's
 // rows in ascending order (the stable sort keeps that order among equal lengths, as torch.sort does)
 __global__ void __launch_bounds__(256) k_plan_items(const int64_t* __restrict__ ip, const int64_t* __restrict__ splits,
-                                                    const int32_t* __restrict__ cutpos, int64_t n, int B, int split0,
+                                                    const int64_t* __restrict__ pos, int64_t n, int B, int split0,
                                                     LaunchTable T, uint64_t* __restrict__ keys,
                                                     int32_t* __restrict__ vals)
 {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     const uint64_t lmask = (1ull << T.lenbits) - 1;
+    const int L0 = T.base;                     // block 0's (first) launch
     for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += stride) {
         const int64_t deg = ip[r + 1] - ip[r];
-        auto put = [&](int L, int64_t pos, int64_t len) {
-            const int64_t i = T.off[L] + pos;
+        auto put = [&](int L, int64_t p, int64_t len) {
+            const int64_t i = T.off[L] + p;
             keys[i] = ((uint64_t)L << T.lenbits) | (lmask - (uint64_t)len);
             vals[i] = (int32_t)r;
         };
         if (B == 1) {
             put(0, r, deg);
+            continue;
+        }
+        // the cut rows before r, the whole hub rows before r
+        const int64_t cp = pos[r] & 0xffffffffll, hp = pos[r] >> 32;
+        if (deg > T.hubw_t) {
+            put(0, hp, deg);                   // the whole hub rows' launch: the whole row
         } else if (deg > kWholeMax) {
-            const int64_t cp = cutpos[r];
-            put(0, split0 ? cp : r, bound_of(ip, splits, n, B, 1, r) - ip[r]);
+            put(L0, split0 ? cp : r - hp, bound_of(ip, splits, n, B, 1, r) - ip[r]);
             for (int b = 1; b < B; ++b)
-                put(split0 ? b + 1 : b, cp,
+                put(L0 + (split0 ? b + 1 : b), cp,
                     bound_of(ip, splits, n, B, b + 1, r) - bound_of(ip, splits, n, B, b, r));
         } else {
-            put(split0 ? 1 : 0, split0 ? r - cutpos[r] : r, deg);
+            put(L0 + (split0 ? 1 : 0), split0 ? r - cp - hp : r - hp, deg);
         }
     }
 }
@@ -299,6 +334,15 @@ __global__ void k_plan_counts(const uint64_t* __restrict__ keys, const int32_t* 
     };
     // automatic thresholds from the launch's nnz; a caller's thresholds hold for every launch (the
     // narrow panels' slice waves then follow the heavy threshold too: DeviceCSR.heavy)
+    if (T.base && L == 0) {
+        // the whole hub rows' launch: every row is a hub row (hub workgroups only, no main launch)
+        counts[4 * L + 0] = nnz;
+        counts[4 * L + 1] = m;
+        counts[4 * L + 2] = 0;
+        counts[4 * L + 3] = 0;
+        for (int64_t j = 0; j < min<int64_t>(m, kHubPrefix); ++j) hubs[(int64_t)L * kHubPrefix + j] = vals[o + j];
+        return;
+    }
     const int64_t hub_t = T.hub_t == SRG_PLAN_AUTO ? max<int64_t>(2048, nnz / 1024) : T.hub_t;
     const int64_t heavy_t = T.heavy_t == SRG_PLAN_AUTO ? max<int64_t>(96, nnz / (T.whole_rule ? 100000 : kBlockHeavyPer))
                                                        : T.heavy_t;
@@ -323,7 +367,7 @@ __global__ void __launch_bounds__(256) k_plan_spans(const int64_t* __restrict__ 
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_items; i += stride) {
         const int L = (int)(keys[i] >> T.lenbits);
-        const int b = block_of(L, split0 != 0);
+        const int b = T.blk[L];
         const int64_t len = pos[i + 1] - pos[i];
         if (compact) {
             const int64_t p = pos[i];
@@ -351,7 +395,7 @@ __global__ void __launch_bounds__(256) k_plan_spans(const int64_t* __restrict__ 
 // pieces and took 1.3 ms; tools/plan_probe).
 __global__ void __launch_bounds__(256) k_plan_copy(const int64_t* __restrict__ ip, const int64_t* __restrict__ splits,
                                                    const int32_t* __restrict__ ix, const float* __restrict__ v,
-                                                   int64_t n, int B, int split0, int lenbits,
+                                                   int64_t n, int B, const LaunchTable T, int lenbits,
                                                    const uint64_t* __restrict__ keys, const int32_t* __restrict__ vals,
                                                    const int64_t* __restrict__ pos, int64_t n_items, int64_t nnz,
                                                    int32_t* __restrict__ oix, float* __restrict__ ov)
@@ -376,7 +420,7 @@ __global__ void __launch_bounds__(256) k_plan_copy(const int64_t* __restrict__ i
             if (i < n_items) {
                 p = pos[i];
                 const int L = (int)(keys[i] >> lenbits);
-                src = bound_of(ip, splits, n, B, block_of(L, split0 != 0), vals[i]);
+                src = bound_of(ip, splits, n, B, T.blk[L], vals[i]);
             }
             // the batch's items cover [pos[ibase], pos[ibase + 64])
             const int64_t pend = ibase + 64 < n_items ? pos[ibase + 64] : nnz;
@@ -643,6 +687,7 @@ static int build_impl(const int64_t* indptr, const int32_t* indices, const float
     }
     const int64_t max_deg = (int64_t)hs[0], n_whole_rows = (int64_t)hs[1];
     const int64_t nnz = (int64_t)hs[3] - (int64_t)hs[2];
+    unsigned long long* dstat = nullptr;     // (reused below for the whole hub rows' count)
     if (nnz < 0) return bail(pfail(SRG_ERR_INVALID, "indptr[n] < indptr[0]"));
     if (nnz > 0 && !mem.query() && (!indices || !values)) return bail(pfail(SRG_ERR_INVALID, "null indices / values"));
     P->nnz = nnz;
@@ -668,25 +713,48 @@ static int build_impl(const int64_t* indptr, const int32_t* indices, const float
     }
     P->compact = compact;
     const bool split0 = P->split0;
-    const int64_t n_cut = B > 1 ? n - n_whole_rows : 0;
+    // whole hub rows (column-blocked plans with automatic hub rows): longer than the one-launch hop's hub
+    // threshold; counted only when the longest row is (one more host sync)
+    int64_t hubw_t = INT64_MAX, n_hubw = 0;
+    if (B > 1 && hub_threshold == SRG_PLAN_AUTO && max_deg > std::max<int64_t>(2048, nnz / 1024)) {
+        hubw_t = std::max<int64_t>(2048, nnz / 1024);
+        DevBuf st;
+        st.s = s;
+        unsigned long long hc = 0;
+        if (hipMalloc(&st.p, sizeof(unsigned long long)) != hipSuccess) { (void)hipGetLastError(); return bail(pfail(SRG_ERR_ALLOC, "plan: statistics")); }
+        dstat = (unsigned long long*)st.p;
+        if (hipMemsetAsync(dstat, 0, sizeof(unsigned long long), s) != hipSuccess) return bail(pfail(SRG_ERR_HIP, "memset"));
+        hipLaunchKernelGGL(k_plan_count_above, dim3(grid_for(n, 256, 512)), dim3(256), 0, s, indptr, n, hubw_t, dstat);
+        if (hipMemcpyAsync(&hc, dstat, sizeof(hc), hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+            return bail(pfail(SRG_ERR_HIP, "plan: hub rows: %s", hipGetErrorString(hipGetLastError())));
+        n_hubw = (int64_t)hc;
+        if (!n_hubw) hubw_t = INT64_MAX;
+    }
+    const int64_t n_cut = B > 1 ? n - n_whole_rows - n_hubw : 0;
     std::vector<int> sets;     // row set per launch
     std::vector<int> blocks;
     if (B == 1) { sets = {kAll}; blocks = {0}; }
     else {
-        if (split0) { sets = {kCut, kWhole}; blocks = {0, 0}; }
-        else { sets = {kAll}; blocks = {0}; }
+        if (n_hubw) { sets = {kHubWhole}; blocks = {0}; }
+        if (split0) { sets.push_back(kCut); sets.push_back(kWhole); blocks.push_back(0); blocks.push_back(0); }
+        else { sets.push_back(kAll); blocks.push_back(0); }
         for (int b = 1; b < B; ++b) { sets.push_back(kCut); blocks.push_back(b); }
     }
     LaunchTable T{};
     T.n_launch = (int)sets.size();
     T.whole_rule = B == 1 ? 1 : 0;
+    T.base = n_hubw ? 1 : 0;
     T.hub_t = hub_threshold;
     T.heavy_t = heavy_threshold;
+    T.hubw_t = hubw_t;
     T.lenbits = bits_for((uint64_t)max_deg);
     T.lbits = bits_for((uint64_t)std::max(0, T.n_launch - 1));
     T.off[0] = 0;
-    for (int L = 0; L < T.n_launch; ++L)
-        T.off[L + 1] = T.off[L] + (sets[L] == kAll ? n : sets[L] == kCut ? n_cut : n_whole_rows);
+    for (int L = 0; L < T.n_launch; ++L) {
+        T.blk[L] = blocks[L];
+        T.off[L + 1] = T.off[L] + (sets[L] == kAll ? n - n_hubw : sets[L] == kCut ? n_cut
+                                   : sets[L] == kWhole ? n_whole_rows : n_hubw);
+    }
     const int64_t n_items = T.off[T.n_launch];
     P->n_items = n_items;
     if (T.lenbits + T.lbits > 64) return bail(pfail(SRG_ERR_INVALID, "row lengths too long to plan"));
@@ -714,7 +782,7 @@ static int build_impl(const int64_t* indptr, const int32_t* indices, const float
         KeyLen op{(1ull << T.lenbits) - 1};
         hipcub::TransformInputIterator<int64_t, KeyLen, const uint64_t*> lens((const uint64_t*)nullptr, op);
         if (B > 1) {
-            SRG_PLAN_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (const int32_t*)nullptr, (int32_t*)nullptr, n, s));
+            SRG_PLAN_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (const int64_t*)nullptr, (int64_t*)nullptr, n, s));
             cub_bytes = std::max(cub_bytes, tb);
         }
         SRG_PLAN_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (const uint64_t*)nullptr, (uint64_t*)nullptr,
@@ -725,7 +793,8 @@ static int build_impl(const int64_t* indptr, const int32_t* indices, const float
         cub_bytes = std::max(cub_bytes, tb);
     }
     int64_t *splits = nullptr, *slot_beg = nullptr, *slot_end = nullptr, *pos = nullptr, *dcounts = nullptr;
-    int32_t *cut = nullptr, *cutpos = nullptr, *vals = nullptr, *order = nullptr, *dhubs = nullptr, *oix = nullptr;
+    int64_t *cut = nullptr, *cutpos = nullptr;
+    int32_t *vals = nullptr, *order = nullptr, *dhubs = nullptr, *oix = nullptr;
     uint64_t *keys = nullptr, *skeys = nullptr;
     float* ov = nullptr;
     void* cub_tmp = nullptr;
@@ -748,8 +817,8 @@ static int build_impl(const int64_t* indptr, const int32_t* indices, const float
             P->blk_end = keep.take<int64_t>((size_t)B * n);
         }
         if (B > 1) {
-            cut = tmp.take<int32_t>((size_t)n);
-            cutpos = tmp.take<int32_t>((size_t)n);
+            cut = tmp.take<int64_t>((size_t)n);
+            cutpos = tmp.take<int64_t>((size_t)n);
         }
         keys = tmp.take<uint64_t>((size_t)n_items);
         skeys = tmp.take<uint64_t>((size_t)n_items);
@@ -795,7 +864,7 @@ static int build_impl(const int64_t* indptr, const int32_t* indices, const float
     // split points and the cut rows' positions
     if (B > 1) {
         hipLaunchKernelGGL(k_plan_splits, dim3(grid_for(n * (B - 1), 256, 1u << 20)), dim3(256), 0, s, indptr, indices,
-                           n, B, splits, cut);
+                           n, B, T.hubw_t, splits, cut);
         size_t tb = cub_bytes;
         SRG_PLAN_HIP(hipcub::DeviceScan::ExclusiveSum(cub_tmp, tb, cut, cutpos, n, s));
     }
@@ -847,7 +916,7 @@ static int build_impl(const int64_t* indptr, const int32_t* indices, const float
                            P->blk_beg, P->blk_end);
     if (compact)
         hipLaunchKernelGGL(k_plan_copy, dim3(grid_for((nnz + kCopyChunk - 1) / kCopyChunk, 4, 1u << 16)), dim3(256), 0, s,
-                           indptr, splits, indices, values, n, B, split0 ? 1 : 0, T.lenbits, skeys, order, pos, n_items,
+                           indptr, splits, indices, values, n, B, T, T.lenbits, skeys, order, pos, n_items,
                            nnz, oix, ov);
     {
         const hipError_t e = hipGetLastError();
@@ -866,6 +935,7 @@ static int build_impl(const int64_t* indptr, const int32_t* indices, const float
         D.n_heavy = counts[4 * L + 2];
         D.n_narrow = counts[4 * L + 3];
         D.whole_rows = sets[L] == kWhole;
+        D.hub_whole = sets[L] == kHubWhole;
         if (compact) {
             D.row_beg = P->blk_beg + (int64_t)b * n;
             D.row_end = P->blk_end + (int64_t)b * n;
@@ -889,7 +959,7 @@ static int build_impl(const int64_t* indptr, const int32_t* indices, const float
         std::vector<int32_t> ref;
         bool first = true;
         for (int L = 0; L < T.n_launch && same; ++L) {
-            if (sets[L] == kWhole) continue;
+            if (sets[L] == kWhole || sets[L] == kHubWhole) continue;
             const int64_t h = counts[4 * L + 1];
             if (h > kHubPrefix) { same = false; break; }
             std::vector<int32_t> set(hubs.begin() + (size_t)L * kHubPrefix, hubs.begin() + (size_t)L * kHubPrefix + h);
@@ -898,6 +968,9 @@ static int build_impl(const int64_t* indptr, const int32_t* indices, const float
             else same = set == ref;
         }
         P->same_hubs = same;
+        for (int L = 0; L < T.n_launch; ++L)
+            if (sets[L] == kCut || sets[L] == kAll) P->block_hubs |= counts[4 * L + 1] > 0;
+        P->n_hub_whole = n_hubw;
     }
     // after the build's kernels (one more wait on the stream: the copy); the caller's scratch may go
     // once the call returns
@@ -923,8 +996,8 @@ int srg_plan_build(const int64_t* indptr, const int32_t* indices, const float* v
 }
 
 int srg_plan_query(const int64_t* indptr, int64_t n_rows, int32_t d, int32_t hops, int32_t col_blocks,
-                   uint32_t opts, void* stream, size_t* keep_bytes, size_t* scratch_bytes, uint32_t* resolved_opts,
-                   int32_t* resolved_col_blocks)
+                   int64_t hub_threshold, int64_t heavy_threshold, uint32_t opts, void* stream, size_t* keep_bytes,
+                   size_t* scratch_bytes, uint32_t* resolved_opts, int32_t* resolved_col_blocks)
 {
     if (!keep_bytes || !scratch_bytes || !resolved_opts || !resolved_col_blocks)
         return pfail(SRG_ERR_INVALID, "null output");
@@ -933,9 +1006,9 @@ int srg_plan_query(const int64_t* indptr, int64_t n_rows, int32_t d, int32_t hop
     m.q_scratch = scratch_bytes;
     m.q_opts = resolved_opts;
     m.q_blocks = resolved_col_blocks;
-    // the sizes do not depend on the ids / values, only on indptr (lengths and split counts) and the
-    // thresholds (which only pick rows inside the sized arrays)
-    return build_impl(indptr, nullptr, nullptr, n_rows, d, hops, col_blocks, SRG_PLAN_AUTO, SRG_PLAN_AUTO, opts,
+    // the sizes do not depend on the ids / values, only on indptr (lengths and split counts) and the hub
+    // threshold (automatic hub rows may be whole hub rows: one item each instead of one per block)
+    return build_impl(indptr, nullptr, nullptr, n_rows, d, hops, col_blocks, hub_threshold, heavy_threshold, opts,
                       stream, nullptr, m);
 }
 
@@ -978,7 +1051,8 @@ int srg_plan_describe(const srg_plan* plan, srg_plan_desc* desc)
     desc->n_launch = (int32_t)plan->launches.size();
     desc->compact = plan->compact ? 1 : 0;
     desc->split_block0 = plan->split0 ? 1 : 0;
-    desc->hub_chain = (plan->B > 1 && plan->same_hubs) ? 1 : 0;
+    desc->hub_chain = (plan->B > 1 && plan->same_hubs && plan->block_hubs) ? 1 : 0;
+    desc->hub_rows_whole = (int32_t)plan->n_hub_whole;
     desc->device = plan->device;
     srg_clear_error();
     return SRG_OK;
@@ -1019,7 +1093,11 @@ static int plan_launches(const srg_plan* P, int32_t d, uint32_t flags, std::vect
         L.slot_beg = D.slot_beg;
         L.slot_end = D.slot_end;
         uint32_t f = base | (D.block > 0 ? SRG_SPMM_ACCUMULATE : 0u);
-        if (chain && D.n_hub > 0) {
+        if (D.hub_whole) {
+            // the whole hub rows: forked first, joined at the end of the hop (FAST: their segments)
+            f |= SRG_SPMM_HUB_NOJOIN | (fast ? SRG_SPMM_FAST : 0u);
+            forked = true;
+        } else if (chain && D.n_hub > 0) {
             f |= SRG_SPMM_HUB_NOJOIN | (forked ? SRG_SPMM_HUB_CONTINUE : 0u);
             forked = true;
         } else if (fast) {
@@ -1170,7 +1248,7 @@ int srg_plan_hop_f32(const srg_plan* plan, const float* X, int64_t ldx, float* Y
     if (agg) {
         if (plan->B == 1) on[0] = 1;
         else if (plan->split0) {
-            for (size_t i = 0; i < L.size(); ++i) on[i] = plan->launches[i].whole_rows ? 1 : 0;
+            for (size_t i = 0; i < L.size(); ++i) on[i] = (plan->launches[i].whole_rows || plan->launches[i].hub_whole) ? 1 : 0;
             on.back() = 1;
         } else fused = false;
     }

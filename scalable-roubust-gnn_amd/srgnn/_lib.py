@@ -149,7 +149,7 @@ def _declare(lib):
     lib.srg_propagate_plan_f32.argtypes = [_p, _i32, _i32, _p, _i64, _i32, _i32, _p]
     lib.srg_propagate_plan_f32.restype = ctypes.c_int
     lib.srg_plan_build.argtypes = [_p, _p, _p, _i64, _i32, _i32, _i32, _i64, _i64, _u32, _p, ctypes.POINTER(_p)]
-    lib.srg_plan_query.argtypes = [_p, _i64, _i32, _i32, _i32, _u32, _p, ctypes.POINTER(ctypes.c_size_t),
+    lib.srg_plan_query.argtypes = [_p, _i64, _i32, _i32, _i32, _i64, _i64, _u32, _p, ctypes.POINTER(ctypes.c_size_t),
                                    ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(_u32), ctypes.POINTER(_i32)]
     lib.srg_plan_build_in.argtypes = [_p, _p, _p, _i64, _i32, _i32, _i32, _i64, _i64, _u32, _p, ctypes.c_size_t, _p,
                                       ctypes.c_size_t, _p, ctypes.POINTER(_p)]

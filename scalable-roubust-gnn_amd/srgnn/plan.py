@@ -25,7 +25,7 @@ class PlanDesc(ctypes.Structure):
     _fields_ = [("n_rows", ctypes.c_int64), ("nnz", ctypes.c_int64), ("device_bytes", ctypes.c_int64),
                 ("d", ctypes.c_int32), ("col_blocks", ctypes.c_int32), ("n_launch", ctypes.c_int32),
                 ("compact", ctypes.c_int32), ("split_block0", ctypes.c_int32), ("hub_chain", ctypes.c_int32),
-                ("device", ctypes.c_int32)]
+                ("device", ctypes.c_int32), ("hub_rows_whole", ctypes.c_int32)]
 
 
 class HopLaunch(ctypes.Structure):
@@ -45,14 +45,22 @@ def _opts(compact, split_block0) -> int:
     return opts
 
 
+def _thresholds(A):
+    """A's (hub, heavy) thresholds as the planner takes them (None: automatic per launch; negative: no
+    such rows)."""
+    return tuple(_lib.SRG_PLAN_AUTO if t is None else _lib.SRG_PLAN_NONE if int(t) < 0 else int(t)
+                 for t in (A.thresholds[1], A.thresholds[0]))
+
+
 def query(A, d: int, hops: int, col_blocks: int = 0, compact=None, split_block0=None):
     """(keep_bytes, scratch_bytes, resolved opts, resolved column blocks) of a plan for these arguments
     (srg_plan_query: one pass over indptr, nothing allocated)."""
     kb, sb = ctypes.c_size_t(), ctypes.c_size_t()
     ro, rb = ctypes.c_uint32(), ctypes.c_int32()
-    _lib.call(A.device, "srg_plan_query", A.indptr.data_ptr(), A.n_rows, int(d), int(hops), int(col_blocks),
-              _opts(compact, split_block0), _lib.stream(A.device), ctypes.byref(kb), ctypes.byref(sb), ctypes.byref(ro),
-              ctypes.byref(rb))
+    hub_t, heavy_t = _thresholds(A)
+    _lib.call(A.device, "srg_plan_query", A.indptr.data_ptr(), A.n_rows, int(d), int(hops), int(col_blocks), hub_t,
+              heavy_t, _opts(compact, split_block0), _lib.stream(A.device), ctypes.byref(kb), ctypes.byref(sb),
+              ctypes.byref(ro), ctypes.byref(rb))
     return int(kb.value), int(sb.value), int(ro.value), int(rb.value)
 
 
@@ -81,9 +89,8 @@ class NativePlan:
         self._p = None
         self._keep = None
         n = A.n_rows
-        # A's thresholds (None: automatic per launch; negative: no such rows), for every launch
-        hub_t, heavy_t = (_lib.SRG_PLAN_AUTO if t is None else _lib.SRG_PLAN_NONE if int(t) < 0 else int(t)
-                          for t in (A.thresholds[1], A.thresholds[0]))
+        # A's thresholds, for every launch
+        hub_t, heavy_t = _thresholds(A)
         if compact is None and hops >= _lib.SRG_PLAN_MIN_HOPS_TO_COMPACT:
             # the library's rule (the copies and the build's keys / ids / positions, < 32 B per entry, in a
             # quarter of the free memory) over the memory torch can hand out, cached blocks included
@@ -122,6 +129,9 @@ class NativePlan:
         self.compact = bool(desc.compact)
         self.split_block0 = bool(desc.split_block0)
         self.hub_chain = bool(desc.hub_chain)
+        self.hub_rows_whole = int(desc.hub_rows_whole)
+        # k_spmm launches per hop: the whole hub rows' launch is hub workgroups only
+        self.spmm_launches = self.n_launch - (1 if self.hub_rows_whole else 0)
         self.device_bytes = int(desc.device_bytes)
 
     def _alloc(self, keep_bytes: int, scratch_bytes: int):

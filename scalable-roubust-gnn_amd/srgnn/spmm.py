@@ -61,14 +61,14 @@ def col_blocks_of(A: DeviceCSR, d: int) -> int:
 
 
 def launches_per_hop(A: DeviceCSR, B: int, d: int, agg: bool = False) -> int:
-    """k_spmm launches of one hop of A over a d-column panel in B column blocks: the cached plan's,
-    else what a plan with B blocks would run (B, plus one when block 0 runs as its cut spans and its
-    whole rows).  agg: the aggregation epilogue needs no launch of its own where block 0 is split, and
+    """k_spmm launches of one hop of A over a d-column panel in B column blocks: the cached plan's (its
+    whole hub rows' launch is hub workgroups only, not counted), else what a plan with B blocks would
+    run (B, plus one when block 0 runs as its cut spans and its whole rows).  agg: the aggregation epilogue needs no launch of its own where block 0 is split, and
     a separate accumulation pass (not a k_spmm launch) where it is not."""
     from .plan import cached, query
     P = cached(A, d)
     if P is not None and P.col_blocks == B:
-        return P.n_launch
+        return P.spmm_launches
     if B <= 1:
         return 1
     _, _, ro, rb = query(A, d, _lib.SRG_PLAN_MIN_HOPS_TO_CUT, B, None, SPLIT_BLOCK0)

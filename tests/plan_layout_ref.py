@@ -52,9 +52,39 @@ def _cache(A):
     return A._blocks.setdefault("layout_ref", {})
 
 
+def hub_whole_rows(A: DeviceCSR):
+    """The whole hub rows of a column-blocked plan (round 6): with an automatic hub threshold, the rows
+    longer than the one-launch hop's hub threshold max(2048, nnz / 1024) are cut nowhere -- one launch of
+    hub workgroups over their whole rows, first in the hop.  A bool mask, or None."""
+    if A.thresholds[1] is not None:
+        return None
+    deg = A.indptr[1:] - A.indptr[:-1]
+    mask = deg > max(2048, A.nnz // 1024)
+    return mask if bool(mask.any()) else None
+
+
+def hub_whole_launch(A: DeviceCSR):
+    """The whole hub rows' launch: their full spans, by decreasing length, every row a hub row."""
+    c = _cache(A)
+    if "hubw" not in c:
+        mask = hub_whole_rows(A)
+        if mask is None:
+            c["hubw"] = None
+        else:
+            ip = A.indptr
+            rows = torch.nonzero(mask).squeeze(1)
+            deg = (ip[1:] - ip[:-1])[rows]
+            order = rows[torch.sort(deg, descending=True, stable=True).indices].to(torch.int32).contiguous()
+            c["hubw"] = Block(ip[:-1], A.indices, A.values, int(rows.numel()), A.n_cols, order, 0, int(rows.numel()),
+                              0 if A.n_heavy_narrow is not None else None, row_end=ip[1:], row_space=A.n_rows,
+                              thresholds=A.thresholds)
+    return c["hubw"]
+
+
 def column_blocks(A: DeviceCSR, B: int, whole_max: int = WHOLE_MAX):
     """B span operators over A's rows (None for B < 2 or an empty operator); block 0 carries
-    `whole_rows` (rows of <= whole_max entries, computed whole in block 0 and not scheduled later)."""
+    `whole_rows` (rows of <= whole_max entries, computed whole in block 0 and not scheduled later).
+    The whole hub rows (hub_whole_rows) are in no block."""
     key = ("blocks", int(B), int(whole_max))
     c = _cache(A)
     if key in c:
@@ -67,26 +97,30 @@ def column_blocks(A: DeviceCSR, B: int, whole_max: int = WHOLE_MAX):
     splits = torch.empty((B - 1, A.n_rows), dtype=torch.int64, device=dev)
     _lib.call(dev, "srg_csr_col_splits", ip.data_ptr(), A.indices.data_ptr(), A.n_rows, n, B, splits.data_ptr(),
               _lib.stream(dev))
-    whole = (ip[1:] - ip[:-1]) <= whole_max if whole_max > 0 else None
-    if whole is not None:
-        splits = torch.where(whole.unsqueeze(0), ip[1:].unsqueeze(0), splits)
-        later = torch.nonzero(~whole).squeeze(1)
+    deg_all = ip[1:] - ip[:-1]
+    whole = deg_all <= whole_max if whole_max > 0 else torch.zeros_like(deg_all, dtype=torch.bool)
+    hubw = hub_whole_rows(A)
+    if hubw is None:
+        hubw = torch.zeros_like(whole)
+    # whole rows and whole hub rows end in block 0 (their later spans empty)
+    splits = torch.where((whole | hubw).unsqueeze(0), ip[1:].unsqueeze(0), splits)
+    first = torch.nonzero(~hubw).squeeze(1)              # block 0's rows
+    later = torch.nonzero(~whole & ~hubw).squeeze(1)     # the cut rows: blocks 1..
     bounds = [ip[:-1]] + [splits[b] for b in range(B - 1)] + [ip[1:]]
     heavy_t, hub_t = A.thresholds
     auto_narrow = A.n_heavy_narrow is not None
     out = []
     for b in range(B):
         beg, end = bounds[b], bounds[b + 1]
-        deg = end - beg
-        nnz_b = int(deg.sum().item())
-        sel = deg[later] if (b > 0 and whole is not None) else deg
-        order, n_heavy, n_hub = _schedule(sel, nnz_b, heavy_t, hub_t)
-        if b > 0 and whole is not None:
-            order = later[order.to(torch.int64)].to(torch.int32)
+        rows = first if b == 0 else later
+        sel = (end - beg)[rows]
+        order, n_heavy, n_hub = _schedule(sel, int(sel.sum().item()), heavy_t, hub_t)
+        order = rows[order.to(torch.int64)].to(torch.int32)
         narrow = narrow_heavy_degrees(sel, n_hub) if auto_narrow else None
         blk = Block(beg, A.indices, A.values, int(sel.numel()), n, order, n_heavy, n_hub, narrow, row_end=end,
                     row_space=A.n_rows, thresholds=A.thresholds)
-        blk.whole_rows = whole if b == 0 else None
+        blk.whole_rows = (whole & ~hubw) if (b == 0 and whole_max > 0) else None
+        blk.cut_rows = ~whole & ~hubw
         out.append(blk)
     c[key] = out
     return out
@@ -99,7 +133,7 @@ def split_whole(blk: Block):
     c = _cache(blk)
     if "split" not in c:
         parts = []
-        for sel in (~blk.whole_rows, blk.whole_rows):
+        for sel in (blk.cut_rows, blk.whole_rows):
             rows = torch.nonzero(sel).squeeze(1)
             deg = (blk.row_end - blk.indptr)[rows]
             heavy_t, hub_t = blk.thresholds
@@ -153,6 +187,20 @@ def schedule_ordered(A: DeviceCSR) -> Block:
     return c["sched"]
 
 
+def compact_hub_whole_launch(A: DeviceCSR):
+    """hub_whole_launch with its entries copied in its schedule's order."""
+    c = _cache(A)
+    if "hubw_compact" not in c:
+        h = hub_whole_launch(A)
+        if h is None:
+            c["hubw_compact"] = None
+        else:
+            beg, end, ix, v = _copy_in_order(h, h.order.to(torch.int64))
+            c["hubw_compact"] = Block(beg, ix, v, h.n_rows, A.n_cols, h.order, 0, h.n_hub, h.n_heavy_narrow,
+                                      row_end=end, row_space=A.n_rows, thresholds=A.thresholds)
+    return c["hubw_compact"]
+
+
 def compact_column_blocks(A: DeviceCSR, B: int, whole_max: int = WHOLE_MAX):
     """column_blocks with each block's entries copied in the order its launches take the rows (block
     0: its cut rows' schedule, then its whole rows')."""
@@ -172,6 +220,7 @@ def compact_column_blocks(A: DeviceCSR, B: int, whole_max: int = WHOLE_MAX):
         nb = Block(beg, ix, v, blk.n_rows, A.n_cols, blk.order, blk.n_heavy, blk.n_hub, blk.n_heavy_narrow,
                    row_end=end, row_space=blk.row_space, thresholds=blk.thresholds)
         nb.whole_rows = blk.whole_rows
+        nb.cut_rows = blk.cut_rows
         if parts:
             _cache(nb)["split"] = tuple(
                 Block(beg, ix, v, p.n_rows, A.n_cols, p.order, p.n_heavy, p.n_hub, p.n_heavy_narrow, row_end=end,
@@ -195,8 +244,11 @@ def hop_plan(A: DeviceCSR, d: int, B: int, compact: bool, split: bool, whole_max
         blocks = (compact_column_blocks if compact else column_blocks)(A, B, whole_max)
     else:
         blocks = None
+    hubw = None
     if not blocks:
         blocks = [schedule_ordered(A) if compact else A]
+    else:
+        hubw = (compact_hub_whole_launch if compact else hub_whole_launch)(A)
     u2 = len(blocks) > 1 and d >= 128
     parts = split_whole(blocks[0]) if (split or agg) and len(blocks) > 1 else None
     cut_launches = ([parts[0]] + blocks[1:]) if parts is not None else blocks
@@ -204,12 +256,17 @@ def hop_plan(A: DeviceCSR, d: int, B: int, compact: bool, split: bool, whole_max
     base = (_lib.SRG_SPMM_PACKED_U2 if u2 else 0) | \
         (_lib.SRG_SPMM_CAP_WAVES if len(blocks) > 1 and A.n_cols * d * 4 >= CAP_WAVES_MIN_PANEL else 0)
     seq = []
+    plan, forked = [], False
+    if hubw is not None:
+        # forked first, joined at the end of the hop; its rows end their chains there (the aggregation)
+        plan.append((hubw, base | _lib.SRG_SPMM_HUB_NOJOIN | (_lib.SRG_SPMM_FAST if fast else 0),
+                     "agg" if agg else "plain"))
+        forked = True
     for b, Ab in enumerate(blocks):
         if parts is not None and b == 0:
             seq += [(parts[0], False, "plain"), (parts[1], False, "agg" if agg else "plain")]
         else:
             seq.append((Ab, b > 0, "agg" if agg and b == len(blocks) - 1 else "plain"))
-    plan, forked = [], False
     for Ab, acc, kind in seq:
         f = base | (_lib.SRG_SPMM_ACCUMULATE if acc else 0)
         if chain and Ab.n_hub > 0:

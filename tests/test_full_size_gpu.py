@@ -64,10 +64,11 @@ def test_products_timed_layout_every_hop_bit_exact(oracle_mod):
     assert auto_col_blocks(A, d, hops=hops) == 12
     assert prepare(A, d, hops) == 12                # bench.py's call: the native plan
     P = cached(A, d)
-    assert P.compact and P.split_block0 and P.hub_chain and P.n_launch == 13
+    # the top row (155,868 entries) is a whole hub row: one hub launch forked first, then 13 k_spmm launches
+    assert P.compact and P.split_block0 and P.hub_rows_whole >= 1 and P.n_launch == 14
     assert spmm_mod.launches_per_hop(A, 12, d) == 13
     launches = P.launches(d)
-    assert sum(L.n_hub for L, _ in launches) >= 12  # the top row is a hub row of every cut launch
+    assert launches[0][0].n_hub == P.hub_rows_whole and launches[0][1]
     x = synth.uniform_features_t(n, d, seed=synth.FEATURE_SEED, device="cuda")
     panels = propagate(A, x, K)                     # through the cached plan
     torch.cuda.synchronize()

@@ -120,7 +120,8 @@ def test_native_layout_matches_torch_formulation(monkeypatch, B, compact, split,
     A = _csr(ip, ix, v, n)
     P = NativePlan(A, d, hops=3, col_blocks=B, compact=compact, split_block0=split)
     assert P.col_blocks == B and P.compact == compact
-    assert P.n_launch == (B + 1 if (B > 1 and split) else B)
+    # B launches, one more for block 0's split, one more for the whole hub rows (blocked plans)
+    assert P.n_launch == (B + 1 if (B > 1 and split) else B) + (1 if B > 1 else 0)
     # the hops first (a compact plan at 64 / 128 columns has row-indexed spans for its hub and
     # slice-wave rows only until srg_plan_launch completes them): the one-launch hops, bit for bit
     from srgnn.spmm import spmm
@@ -134,7 +135,10 @@ def test_native_layout_matches_torch_formulation(monkeypatch, B, compact, split,
     py, join = _python_layout(A, d, B, compact, split, monkeypatch)
     _check_layout(A, P, d, py, join)
     if B > 1:
-        assert P.hub_chain and join            # the two hubs are hubs of every cut launch
+        # the two hubs are longer than max(2048, nnz / 1024): the whole hub rows' launch, first, forked
+        assert P.hub_rows_whole == 2 and not P.hub_chain and join
+        L0, _ = P.launches(d)[0]
+        assert L0.n_rows == L0.n_hub == 2 and L0.n_heavy == 0
     P.close()
 
 
@@ -301,22 +305,30 @@ def test_native_plan_edge_cases():
         ref = spmm(A, spmm(A, X))
         assert torch.equal(panels[2].view(torch.int32), ref.view(torch.int32))
     # a hub row whose entries all lie in block 0: block 0's launch has a hub the others lack -> no chain
+    # (an explicit hub threshold: automatic ones would make this row a whole hub row, below)
+    from srgnn.csr import DeviceCSR
     ip2, ix2, v2, n2 = _power_law(hubs=(), seed=11)
     deg = np.diff(ip2)
     deg[5] = 6000
     ip2 = np.concatenate([[0], np.cumsum(deg)]).astype(np.int64)
     rows = [np.sort(rng.choice(n2, k, replace=False)) if r != 5 else np.arange(6000) for r, k in enumerate(deg)]
     ix2 = np.concatenate(rows).astype(np.int32)
-    A = _csr(ip2, ix2, rng.standard_normal(ix2.size).astype(np.float32), n2)
+    vv2 = rng.standard_normal(ix2.size).astype(np.float32)
+    # automatic: the 6000-entry row is a whole hub row (> max(2048, nnz / 1024)): its own launch, first
+    Aa = _csr(ip2, ix2, vv2, n2)
+    Pa = NativePlan(Aa, 64, hops=2, col_blocks=4, split_block0=True)
+    assert Pa.hub_rows_whole == 1 and not Pa.hub_chain and Pa.n_launch == 6
+    A = DeviceCSR.from_tensors(ip2, ix2, vv2, n_cols=n2, hub_threshold=2048, device="cuda")
     P = NativePlan(A, 64, hops=2, col_blocks=4, split_block0=True)
-    assert not P.hub_chain
+    assert not P.hub_chain and P.hub_rows_whole == 0
     Ls = P.launches(64)
     assert Ls[0][0].n_hub == 1 and all(L.n_hub == 0 for L, _ in Ls[2:])
     X = torch.randn(n2, 64, device="cuda")
-    panels = [X, torch.empty_like(X), torch.empty_like(X)]
-    P.propagate(panels, 64, 64, 2)
-    ref = spmm(A, spmm(A, X))
-    assert torch.equal(panels[2].view(torch.int32), ref.view(torch.int32))
+    for plan in (P, Pa):
+        panels = [X, torch.empty_like(X), torch.empty_like(X)]
+        plan.propagate(panels, 64, 64, 2)
+        ref = spmm(A, spmm(A, X))
+        assert torch.equal(panels[2].view(torch.int32), ref.view(torch.int32))
 
 
 def test_native_plan_automatic_choices_match_prepare(monkeypatch):

@@ -43,15 +43,16 @@ def case(oracle_mod):
     return dict(lib=_lib, n=n, d=d, K=K, x=torch.from_numpy(x).to(dev), want=want, arrays=arrays, dev=dev)
 
 
-def _build(c, stream, hops=20, col_blocks=4, opts=None):
+def _build(c, stream, hops=20, col_blocks=4, opts=None, hub=1000):
     L = c["lib"]
     ip, ix, v = c["arrays"]
     p = ctypes.c_void_p()
     if opts is None:
         opts = L.SRG_PLAN_COMPACT | L.SRG_PLAN_SPLIT_BLOCK0
-    # hub rows: > 1000 entries in a launch -> both hubs, in every block (a chained hub side stream)
+    # hub rows: > 1000 entries in a launch -> both hubs, in every block (a chained hub side stream); automatic
+    # (SRG_PLAN_AUTO): both are whole hub rows, one launch of their own forked first in every hop
     L.call(c["dev"], "srg_plan_build", ip.data_ptr(), ix.data_ptr(), v.data_ptr(), c["n"], c["d"], hops, col_blocks,
-           1000, L.SRG_PLAN_AUTO, opts, stream.cuda_stream, ctypes.byref(p))
+           hub, L.SRG_PLAN_AUTO, opts, stream.cuda_stream, ctypes.byref(p))
     return p.value
 
 
@@ -83,20 +84,25 @@ def _check(c, panels, what):
         assert np.array_equal(got.view(np.int32), c["want"][k].view(np.int32)), f"{what}: hop {k} differs"
 
 
-def test_build_hop_release_build_hop_bitwise(case):
+@pytest.mark.parametrize("hub", ["chained", "whole"])
+def test_build_hop_release_build_hop_bitwise(case, hub):
     c = case
+    L = c["lib"]
+    ht = 1000 if hub == "chained" else L.SRG_PLAN_AUTO
     s1 = torch.cuda.Stream(device=c["dev"])
     s1.wait_stream(torch.cuda.current_stream())
     A, B = _panels(c), _panels(c)
-    # 1. chained hub spans, eager then captured and replayed; released right behind the replay
-    p1 = _build(c, s1)
+    # 1. chained hub spans (or the whole hub rows' launch), eager then captured and replayed; released
+    # right behind the replay
+    p1 = _build(c, s1, hub=ht)
     d1 = _desc(c, p1)
-    assert d1.col_blocks == 4 and d1.compact == 1 and d1.split_block0 == 1 and d1.hub_chain == 1
+    assert d1.col_blocks == 4 and d1.compact == 1 and d1.split_block0 == 1
+    assert (d1.hub_chain, d1.hub_rows_whole) == ((1, 0) if hub == "chained" else (0, 2))
     for _ in range(3):                   # call 1 eager, call 2 captured + replayed, call 3 replayed
         _propagate(c, p1, A, s1)
     _destroy(c, p1, s1)                  # no host synchronisation before: destroy must order itself
     # 2. a new plan over (most likely) the same memory, its hops into other panels
-    p2 = _build(c, s1)
+    p2 = _build(c, s1, hub=ht)
     _propagate(c, p2, B, s1)
     _destroy(c, p2, s1)
     _check(c, A, "first plan (graph replay, released in flight)")
@@ -163,7 +169,8 @@ def test_plan_in_caller_memory(case):
     s1.wait_stream(torch.cuda.current_stream())
     kb, sb = ctypes.c_size_t(), ctypes.c_size_t()
     ro, rb = ctypes.c_uint32(), ctypes.c_int32()
-    L.call(c["dev"], "srg_plan_query", ip.data_ptr(), c["n"], c["d"], 20, 4, L.SRG_PLAN_SPLIT_BLOCK0, s1.cuda_stream,
+    L.call(c["dev"], "srg_plan_query", ip.data_ptr(), c["n"], c["d"], 20, 4, 1000, L.SRG_PLAN_AUTO,
+           L.SRG_PLAN_SPLIT_BLOCK0, s1.cuda_stream,
            ctypes.byref(kb), ctypes.byref(sb), ctypes.byref(ro), ctypes.byref(rb))
     assert rb.value == 4 and (ro.value & L.SRG_PLAN_SPLIT_BLOCK0)
     keep = torch.empty(kb.value, dtype=torch.uint8, device=c["dev"])
