@@ -268,7 +268,10 @@ def test_column_block_spans_are_lower_bounds(whole_max):
     shuffled = ix.copy()
     shuffled[ip[5]:ip[6]] = shuffled[ip[5]:ip[6]][::-1]
     for ids, sorted_rows in ((ix, True), (shuffled, False)):
-        A = DeviceCSR.from_tensors(ip, ids, np.ones(ids.size, np.float32), n_cols=n, device="cuda")
+        # an explicit hub threshold: the 3000-entry row stays a cut row (automatic hub rows this long would
+        # be whole hub rows, cut nowhere)
+        A = DeviceCSR.from_tensors(ip, ids, np.ones(ids.size, np.float32), n_cols=n, hub_threshold=100000,
+                                   device="cuda")
         for B in (2, 3, 7):
             blocks = R.column_blocks(A, B, whole_max)
             starts = [b.indptr.cpu().numpy() for b in blocks] + [blocks[-1].row_end.cpu().numpy()]
