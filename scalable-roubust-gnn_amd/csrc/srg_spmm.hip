@@ -21,7 +21,6 @@
 // The Chebyshev (wavelet) kernels reuse the same row-wave gather and add a fused epilogue that
 // forms the next Chebyshev term and accumulates every scale's filter output in the same pass.
 #include <hip/hip_runtime.h>
-#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <cstdarg>
@@ -1546,21 +1545,6 @@ constexpr int spmm_lds_bytes(uint32_t flags) { return (flags & SRG_SPMM_CAP_WAVE
 // the single-wave delay after a hub fork (10 us: 0 and 5 stay bimodal, 20 is 1-3 % slower,
 // profiles/r01_dispatch_delay_sweep.txt)
 constexpr int kHubDelayUs = 10;
-// Hub rows of a launch that joins them at its end (the one-launch hop): the hub workgroups go on the
-// launch stream ahead of the main launch, which is enqueued with hipExtAnyOrderLaunch (no AQL barrier
-// bit, so it starts while they run) -- instead of a side-stream fork, a dispatch delay and a join.
-#ifndef SRG_HUB_ANY_ORDER
-#define SRG_HUB_ANY_ORDER 0
-#endif
-constexpr bool kHubAnyOrder = SRG_HUB_ANY_ORDER != 0;
-// a k_spmm launch, in any order after the hub workgroups ahead of it when ao_flags says so
-#define SRG_KLAUNCH(K, G, B, SHM, S, ...)                                                       \
-    do {                                                                                        \
-        if (ao_flags)                                                                           \
-            hipExtLaunchKernelGGL(K, G, B, SHM, S, nullptr, nullptr, ao_flags, __VA_ARGS__);    \
-        else                                                                                    \
-            hipLaunchKernelGGL(K, G, B, SHM, S, __VA_ARGS__);                                   \
-    } while (0)
 
 // Hub side streams.  One per (device, caller stream), created on first use, each with its own
 // fork / join events: callers on different streams never share events.  The whole fork sequence
@@ -1597,8 +1581,8 @@ int hub_attrs()
     return SRG_OK;
 }
 
-// The hub kernels' LDS attribute on the current device (once); the caller holds g_side_mu.
-int hub_attrs_locked()
+// The side stream of (current device, caller); the caller holds g_side_mu.
+int side_stream_locked(hipStream_t caller, SideStream** out)
 {
     int dev = 0;
     SRG_HIP_CHECK(hipGetDevice(&dev));
@@ -1609,15 +1593,6 @@ int hub_attrs_locked()
         if (rc) return rc;
         g_side_attr[dev] = true;
     }
-    return SRG_OK;
-}
-
-// The side stream of (current device, caller); the caller holds g_side_mu.
-int side_stream_locked(hipStream_t caller, SideStream** out)
-{
-    int dev = 0;
-    SRG_HIP_CHECK(hipGetDevice(&dev));
-    if (int rc = hub_attrs_locked()) return rc;
     const auto key = std::make_pair(dev, caller);
     if (g_side.find(key) == g_side.end()) {
         int live = 0;
@@ -1752,9 +1727,6 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
     SideStream* ss = nullptr;
     std::unique_lock<std::mutex> side_lock(g_side_mu, std::defer_lock);
     const bool fast = (flags & SRG_SPMM_FAST) && (EX == kEpiPlain || EX == kEpiSpan) && !epi.agg;
-    // hub rows joined at the end of this launch: ahead of it on `s`, the main launch in any order
-    const bool any_order = kHubAnyOrder && !fast && !(flags & (SRG_SPMM_HUB_NOJOIN | SRG_SPMM_HUB_CONTINUE));
-    uint32_t ao_flags = 0;
     if (n_hub > 0 && fast) {   // fork: the hub rows' segments, then their sums, beside the main launch
         side_lock.lock();
         int rc = side_stream_locked(s, &ss);
@@ -1790,28 +1762,6 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
         SRG_HIP_CHECK(hipFreeAsync(buf, ss->stream));
         SRG_HIP_CHECK(hipEventRecord(ss->join, ss->stream));
         ss->pending = (flags & SRG_SPMM_HUB_NOJOIN) != 0;
-    } else if (n_hub > 0 && any_order) {
-        // the hub workgroups on `s` itself, ahead of the main launch, which is then enqueued in any order
-        // (no AQL barrier: it starts while the hub workgroups run, after everything before them): no
-        // fork / join events, no dispatch delay; the next operation on `s` waits for both
-        side_lock.lock();
-        if (int rc = hub_attrs_locked()) return rc;
-        side_lock.unlock();
-        const dim3 hgrid((unsigned)(n_hub * n_slices));
-        const bool w256 = n_hub * n_slices > kHubWideLaunch || (flags & SRG_SPMM_HUB_W256);
-#define SRG_LAUNCH_HUB_S(SF, WW)                                                                             \
-    hipLaunchKernelGGL((k_spmm_hub<SF, IP, EX, WW>), hgrid, dim3(kHubThreads), (HubGeom<WW>::LDS_BYTES), s, \
-                       indptr, indices, vals, order, n_slices, X, ldx, Y, ldy, d, acc, nt, epi)
-        if (sfull) {
-            if (w256) SRG_LAUNCH_HUB_S(true, kHubWideW);
-            else SRG_LAUNCH_HUB_S(true, 512);
-        } else {
-            if (w256) SRG_LAUNCH_HUB_S(false, kHubWideW);
-            else SRG_LAUNCH_HUB_S(false, 512);
-        }
-#undef SRG_LAUNCH_HUB_S
-        SRG_HIP_CHECK(hipGetLastError());
-        ao_flags = hipExtAnyOrderLaunch;
     } else if (n_hub > 0) {   // fork: hub blocks run beside the main launch
         side_lock.lock();
         int rc = side_stream_locked(s, &ss);
@@ -1891,22 +1841,22 @@ int launch_spmm(const IP* indptr, const int32_t* indices, const float* vals, int
         const dim3 grid((unsigned)std::min<int64_t>(kMaxLaunchBlocks, blocks - b0));
         const int bb = (int)b0;
 #define SRG_LAUNCH_SPMM(V, F, SF)                                                               \
-    SRG_KLAUNCH((k_spmm<V, kUnroll, kUnrollHeavy, F, SF, IP, 0, EX>), grid, dim3(kBlock), shm, s,   \
+    hipLaunchKernelGGL((k_spmm<V, kUnroll, kUnrollHeavy, F, SF, IP, 0, EX>), grid, dim3(kBlock), shm, s,   \
                        indptr, indices, vals, morder, nr, nh, n_slices, nb_heavy, X, ldx, Y, ldy, \
                        d, acc, nt, bb, epi)
         const bool full = d % (64 * vec) == 0;        // implies d % 32 == 0
 #define SRG_LAUNCH_NARROW(NSV, SF)                                                                 \
-    SRG_KLAUNCH((k_spmm<1, kUnroll, kUnrollHeavy, false, SF, IP, NSV, EX>), grid, dim3(kBlock), shm, s, \
+    hipLaunchKernelGGL((k_spmm<1, kUnroll, kUnrollHeavy, false, SF, IP, NSV, EX>), grid, dim3(kBlock), shm, s, \
                        indptr, indices, vals, morder, nr, nh, n_slices, nb_heavy, X, ldx, Y, ldy,     \
                        d, acc, nt, bb, epi)
 #define SRG_LAUNCH_PACKED(LRV, LQV, UV)                                                              \
     do {                                                                                              \
         if (xh)                                                                                       \
-            SRG_KLAUNCH((k_spmm<1, UV, (LRV < 8 ? kUnrollHeavyWide : kUnrollHeavy), false, true, IP, 0, EX, LRV, LQV, true>), grid, dim3(kBlock), \
+            hipLaunchKernelGGL((k_spmm<1, UV, (LRV < 8 ? kUnrollHeavyWide : kUnrollHeavy), false, true, IP, 0, EX, LRV, LQV, true>), grid, dim3(kBlock), \
                                shm, s, indptr, indices, vals, morder, nr, nh, n_slices, nb_heavy_launch, X, ldx, Y, ldy, \
                                d, acc, nt, bb, epi);                                                  \
         else                                                                                          \
-            SRG_KLAUNCH((k_spmm<1, UV, (LRV < 8 ? kUnrollHeavyWide : kUnrollHeavy), false, true, IP, 0, EX, LRV, LQV>), grid, dim3(kBlock), shm, s, \
+            hipLaunchKernelGGL((k_spmm<1, UV, (LRV < 8 ? kUnrollHeavyWide : kUnrollHeavy), false, true, IP, 0, EX, LRV, LQV>), grid, dim3(kBlock), shm, s, \
                                indptr, indices, vals, morder, nr, nh, n_slices, nb_heavy, X, ldx, Y, ldy, \
                                d, acc, nt, bb, epi);                                                  \
     } while (0)
