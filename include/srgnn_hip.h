@@ -296,6 +296,17 @@ int srg_cheby_step_f64(const int64_t* indptr, const int32_t* indices, const doub
                        const double* To, double* Tn, int64_t ld, int32_t d, int mode, double a1,
                        double a2, const double* coef_prev, const double* coef, int32_t n_scales,
                        double* R, int64_t r_stride, void* stream);
+/* srg_cheby_step_f64 with the first n_hub rows of row_order (its longest rows) as hub rows: each runs
+ * as workgroups of 16-column slices, 8 waves gathering the row's X pieces into LDS for one wave's
+ * chains, on the hub side stream beside the row waves of the other rows (srg_spmm_csr_f32's hub
+ * fork; joined into `stream` before the call returns).  Bitwise srg_cheby_step_f64: the same chains
+ * in the same order, the same epilogue.  Hub rows need an even d and ld and a 16-byte aligned Tc
+ * (otherwise every row is a row wave). */
+int srg_cheby_step_hub_f64(const int64_t* indptr, const int32_t* indices, const double* values,
+                           int64_t n_rows, const int32_t* row_order, int64_t n_hub, const double* Tc,
+                           const double* To, double* Tn, int64_t ld, int32_t d, int mode, double a1,
+                           double a2, const double* coef_prev, const double* coef, int32_t n_scales,
+                           double* R, int64_t r_stride, void* stream);
 int srg_cheby_step_f32(const int64_t* indptr, const int32_t* indices, const float* values,
                        int64_t n_rows, const int32_t* row_order, const float* Tc, const float* To,
                        float* Tn, int64_t ld, int32_t d, int mode, float a1, float a2,

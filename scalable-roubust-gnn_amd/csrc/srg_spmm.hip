@@ -1141,6 +1141,185 @@ k_cheby(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// fp64 Chebyshev step, hub rows: one workgroup per (hub row, 16-column slice)
+//
+// A row wave keeps U gathers of its row in flight, so a row of degree D costs ~D/U load latencies:
+// in fp64 the products top row (155,868 entries) is one wave's chain beside the whole step.  As in
+// k_spmm_hub, kHub64Producers waves gather windows of kHub64W entries into LDS (two tiles, one
+// barrier per window; each window's gathers are issued two windows ahead) and one consumer wave
+// runs the slice's 16 column chains out of LDS: link k of column c is acc = acc + a_k * x_k[c], the
+// product and the sum rounded separately (scipy's csr_matvecs order, as row_gather), then k_cheby's
+// epilogue for the row's 16 columns -- the same operations, so the same bits.
+//   * producer lane (g, q) gathers the 16-byte chunk q (columns 2q, 2q + 1 of the slice) of entry g
+//     of a group of 8: one dwordx4 instruction brings 8 entries' 128-byte slices;
+//   * the tile is column-major, [16 columns][kHub64LD]: the consumer's lane c reads links k, k + 1
+//     of its column with one ds_read_b128, their values with one broadcast ds_read_b128;
+//   * the consumer keeps three 8-link register sets in flight (reads issued ~16 links ahead).
+// ------------------------------------------------------------------------------------------------
+constexpr int kHub64Cols = 16;
+constexpr int kHub64W = 512;
+constexpr int kHub64Producers = 8;
+constexpr int kHub64Threads = 64 * (kHub64Producers + 1);
+constexpr int kHub64UW = kHub64W / (kHub64Producers * 8);     // gathers per producer lane per window
+constexpr int kHub64LD = kHub64W + 4;                         // doubles per tile column (16-byte rows)
+constexpr int kHub64Tile = kHub64Cols * kHub64LD;
+constexpr int kHub64Slack = 32;                               // the ring's reads past the last window
+constexpr size_t kHub64LdsBytes = (size_t)(2 * kHub64Tile + 2 * kHub64W + kHub64Slack) * sizeof(double);
+static_assert(kHub64LdsBytes <= 160 * 1024, "k_cheby_hub64's LDS");
+
+__global__ void __launch_bounds__(kHub64Threads)
+k_cheby_hub64(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
+              const double* __restrict__ vals, const int32_t* __restrict__ hub_rows, int n_slices,
+              const double* __restrict__ Tc, const double* __restrict__ To, double* __restrict__ Tn, int64_t ld,
+              int d, int mode, double a1, double a2, ChebyCoef<double> cf, int n_scales, double* __restrict__ R,
+              int64_t r_stride)
+{
+    typedef typename Vec<double, 2>::type V2;
+    constexpr int W = kHub64W, UW = kHub64UW, LD = kHub64LD;
+    extern __shared__ __attribute__((aligned(16))) double h64_lds[];
+    double* aval_base = h64_lds + 2 * kHub64Tile;
+    const int row = hub_rows[blockIdx.x / n_slices];
+    const int slice = blockIdx.x % n_slices;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int lane = threadIdx.x & 63;
+    const int64_t beg = indptr[row];
+    const int64_t end = indptr[row + 1];
+    const int n_win = (int)((end - beg + W - 1) / W);
+
+    if (wave == 0) {   // ---------------- consumer: 16 column chains ----------------
+        const int c = lane & (kHub64Cols - 1);
+        const int col = slice * kHub64Cols + c;
+        const bool act = lane < kHub64Cols && col < d;
+        double acc = 0.0;
+        for (int h = 0; h < n_win; ++h) {
+            __syncthreads();                      // window h is in tile h & 1
+            if (lane < kHub64Cols) {
+                const double* tcol = h64_lds + (h & 1) * kHub64Tile + c * LD;
+                const double* av = aval_base + (h & 1) * W;
+                const int64_t sb = beg + (int64_t)h * W;
+                const int nb = (end - sb) < W ? (int)(end - sb) : W;
+                const int nc = nb / 8;            // full 8-link sets
+                V2 tA[4], aA[4], tB[4], aB[4], tC[4], aC[4];
+                // set k: links 8k .. 8k + 7 (reads past nb stay inside the LDS block: kHub64Slack)
+                auto ld = [&](int k, V2 (&t)[4], V2 (&a)[4]) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        t[i] = *reinterpret_cast<const V2*>(tcol + 8 * k + 2 * i);
+                        a[i] = *reinterpret_cast<const V2*>(av + 8 * k + 2 * i);   // broadcast
+                    }
+                };
+                auto run = [&](const V2 (&t)[4], const V2 (&a)[4]) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        acc = link(a[i][0], t[i][0], acc);
+                        acc = link(a[i][1], t[i][1], acc);
+                    }
+                };
+                ld(0, tA, aA);
+                __builtin_amdgcn_sched_barrier(0);
+                ld(1, tB, aB);
+                __builtin_amdgcn_sched_barrier(0);
+                int k = 0;
+                for (; k + 3 <= nc; k += 3) {
+                    ld(k + 2, tC, aC);
+                    __builtin_amdgcn_sched_barrier(0);
+                    run(tA, aA);
+                    __builtin_amdgcn_sched_barrier(0);
+                    ld(k + 3, tA, aA);
+                    __builtin_amdgcn_sched_barrier(0);
+                    run(tB, aB);
+                    __builtin_amdgcn_sched_barrier(0);
+                    ld(k + 4, tB, aB);
+                    __builtin_amdgcn_sched_barrier(0);
+                    run(tC, aC);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                // the loop leaves at most two full sets, k and k + 1 (already read), then < 8 links
+                if (k < nc) run(tA, aA);
+                if (k + 1 < nc) run(tB, aB);
+                for (int q = nc * 8; q < nb; ++q) acc = link(av[q], tcol[q], acc);
+            }
+        }
+        if (act) {
+            const int64_t off = (int64_t)row * ld + col;
+            double tn;
+            if (mode == SRG_CHEBY_INIT) {
+                const double tc = Tc[off];
+                tn = e_div(e_sub(acc, e_mul(a2, tc)), a1);
+                for (int s = 0; s < n_scales; ++s)
+                    R[s * r_stride + off] = e_add(e_mul(cf.prev[s], tc), e_mul(cf.cur[s], tn));
+            } else {
+                tn = e_sub(acc, To[off]);
+                for (int s = 0; s < n_scales; ++s)
+                    R[s * r_stride + off] = e_add(R[s * r_stride + off], e_mul(cf.cur[s], tn));
+            }
+            Tn[off] = tn;
+        }
+        return;
+    }
+
+    // ---------------- producers ----------------
+    const int p = wave - 1;
+    const int g = lane >> 3;          // entry within a gather's group of 8
+    const int qq = lane & 7;          // 16-byte chunk: columns 2qq, 2qq + 1 of the slice
+    const int qcol = slice * kHub64Cols + qq * 2;
+    const bool gact = qcol < d;       // d even (the launch's condition): both columns or neither
+    V2 x0[UW], x1[UW];
+    double a0[UW], a1v[UW];
+    int cn[UW];
+    double an[UW];
+    auto load_ids = [&](int w) {
+        const int64_t sb = beg + (int64_t)w * W;
+#pragma unroll
+        for (int b = 0; b < UW; ++b) {
+            int64_t jj = sb + (p * UW + b) * 8 + g;
+            jj = jj < end ? jj : end - 1;
+            cn[b] = indices[jj];
+            an[b] = vals[jj];
+        }
+    };
+    auto gather = [&](V2 (&x)[UW], double (&a)[UW]) {
+#pragma unroll
+        for (int b = 0; b < UW; ++b) {
+            x[b] = gact ? gload<double, 2>(Tc + (int64_t)cn[b] * ld + qcol) : vzero<double, 2>();
+            a[b] = an[b];
+        }
+    };
+    auto put = [&](int w, const V2 (&x)[UW], const double (&a)[UW]) {
+        double* tile = h64_lds + (w & 1) * kHub64Tile;
+        double* av = aval_base + (w & 1) * W;
+#pragma unroll
+        for (int b = 0; b < UW; ++b) {
+            const int nl = (p * UW + b) * 8 + g;   // entry within the window
+            tile[(2 * qq) * LD + nl] = x[b][0];
+            tile[(2 * qq + 1) * LD + nl] = x[b][1];
+            if (qq == 0) av[nl] = a[b];
+        }
+    };
+    // prologue: windows 0 and 1 in flight, window 0 published, window 2 in flight
+    if (n_win > 0) {
+        load_ids(0);
+        __builtin_amdgcn_sched_barrier(0);
+        gather(x0, a0);
+        if (n_win > 1) { load_ids(1); gather(x1, a1v); }
+        if (n_win > 2) load_ids(2);
+        put(0, x0, a0);
+        if (n_win > 2) { gather(x0, a0); if (n_win > 3) load_ids(3); }
+    }
+    __syncthreads();                              // window 0 published
+    for (int h = 0; h + 1 < n_win; h += 2) {
+        put(h + 1, x1, a1v);
+        if (h + 3 < n_win) { gather(x1, a1v); if (h + 4 < n_win) load_ids(h + 4); }
+        __syncthreads();
+        if (h + 2 >= n_win) break;
+        put(h + 2, x0, a0);
+        if (h + 4 < n_win) { gather(x0, a0); if (h + 5 < n_win) load_ids(h + 5); }
+        __syncthreads();
+    }
+    // barrier count: 1 (prologue) + (n_win - 1) in the loop == the consumer's n_win
+}
+
 // Chebyshev epilogue after a load-balanced SpMM (fp32, large graphs): Tn holds acc = A*Tc (the
 // same fma chain k_cheby forms, so results are bit-identical to the fused kernel) and becomes
 // Tn; every panel has its own leading dimension, so column blocks of S and R need no copies.
@@ -1591,6 +1770,8 @@ int side_stream_locked(hipStream_t caller, SideStream** out)
         int rc = hub_attrs<int>();
         if (!rc) rc = hub_attrs<int64_t>();
         if (rc) return rc;
+        SRG_HIP_CHECK(hipFuncSetAttribute((const void*)k_cheby_hub64, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          (int)kHub64LdsBytes));
         g_side_attr[dev] = true;
     }
     const auto key = std::make_pair(dev, caller);
@@ -1923,11 +2104,13 @@ int check_spmm_args(const void* indptr, const void* indices, const void* vals, i
     return SRG_OK;
 }
 
+// n_hub (fp64 only): the first n_hub rows of `order` run as k_cheby_hub64 workgroups on the hub side
+// stream beside the row waves of the others (joined before the call returns to the stream's order)
 template <typename T>
 int launch_cheby(const int64_t* indptr, const int32_t* indices, const T* vals, int64_t n_rows,
                  const int32_t* order, const T* Tc, const T* To, T* Tn, int64_t ld, int d, int mode,
                  T a1, T a2, const T* coef_prev, const T* coef, int n_scales, T* R, int64_t r_stride,
-                 hipStream_t s)
+                 hipStream_t s, int64_t n_hub = 0)
 {
     if (mode != SRG_CHEBY_INIT && mode != SRG_CHEBY_STEP)
         return fail(SRG_ERR_INVALID, "cheby mode %d", mode);
@@ -1944,7 +2127,33 @@ int launch_cheby(const int64_t* indptr, const int32_t* indices, const T* vals, i
         cf.prev[i] = (mode == SRG_CHEBY_INIT && i < n_scales) ? T(0.5) * coef_prev[i] : T(0);
         cf.cur[i] = i < n_scales ? coef[i] : T(0);
     }
+    if (n_hub < 0 || n_hub > n_rows || (n_hub > 0 && !order))
+        return fail(SRG_ERR_INVALID, "n_hub=%lld needs a row_order and <= n_rows", (long long)n_hub);
     if (n_rows == 0 || d == 0) return ok();
+    // hub workgroups gather 16-byte pieces (two columns) of Tc's rows
+    if (sizeof(T) != 8 || d % 2 || ld % 2 || !aligned(Tc, 16)) n_hub = 0;
+    const int n_slices = (d + kHub64Cols - 1) / kHub64Cols;
+    if (n_hub * n_slices > INT32_MAX - 64) return fail(SRG_ERR_INVALID, "too many hub slices");
+    SideStream* ss = nullptr;
+    std::unique_lock<std::mutex> side_lock(g_side_mu, std::defer_lock);
+    if constexpr (sizeof(T) == 8) {
+        if (n_hub > 0) {   // fork: the hub rows' workgroups beside the row waves
+            side_lock.lock();
+            int rc = side_stream_locked(s, &ss);
+            if (rc) return rc;
+            SRG_HIP_CHECK(hipEventRecord(ss->fork, s));
+            SRG_HIP_CHECK(hipStreamWaitEvent(ss->stream, ss->fork, 0));
+            hipLaunchKernelGGL(k_cheby_hub64, dim3((unsigned)(n_hub * n_slices)), dim3(kHub64Threads), kHub64LdsBytes,
+                               ss->stream, indptr, indices, vals, order, n_slices, Tc, To, Tn, ld, d, mode, a1, a2, cf,
+                               n_scales, R, r_stride);
+            SRG_HIP_CHECK(hipGetLastError());
+            SRG_HIP_CHECK(hipEventRecord(ss->join, ss->stream));
+            hipLaunchKernelGGL(k_dispatch_delay, dim3(1), dim3(64), 0, s, kHubDelayUs);
+            SRG_HIP_CHECK(hipGetLastError());
+        }
+    }
+    order = order ? order + n_hub : nullptr;
+    n_rows -= n_hub;
     const int64_t blocks = (n_rows + kWavesPerBlock - 1) / kWavesPerBlock;
     const int vec = pick_vec(d, ld, ld, Tc, Tn, sizeof(T)) >= 2 && aligned(R, 2 * sizeof(T)) &&
                             (r_stride % 2 == 0) && (To == nullptr || aligned(To, 2 * sizeof(T)))
@@ -1964,6 +2173,7 @@ int launch_cheby(const int64_t* indptr, const int32_t* indices, const T* vals, i
         SRG_HIP_CHECK(hipGetLastError());
     }
     SRG_HIP_CHECK(hipGetLastError());
+    if (ss) SRG_HIP_CHECK(hipStreamWaitEvent(s, ss->join, 0));   // join
     return ok();
 }
 
@@ -2321,6 +2531,18 @@ int srg_cheby_step_f64(const int64_t* indptr, const int32_t* indices, const doub
     return launch_cheby<double>(indptr, indices, values, n_rows, row_order, Tc, To, Tn, ld, d, mode,
                                 a1, a2, coef_prev, coef, n_scales, R, r_stride,
                                 static_cast<hipStream_t>(stream));
+}
+
+int srg_cheby_step_hub_f64(const int64_t* indptr, const int32_t* indices, const double* values,
+                           int64_t n_rows, const int32_t* row_order, int64_t n_hub, const double* Tc,
+                           const double* To, double* Tn, int64_t ld, int32_t d, int mode, double a1,
+                           double a2, const double* coef_prev, const double* coef, int32_t n_scales,
+                           double* R, int64_t r_stride, void* stream)
+{
+    SRG_DEVICE_GUARD(stream);
+    return launch_cheby<double>(indptr, indices, values, n_rows, row_order, Tc, To, Tn, ld, d, mode,
+                                a1, a2, coef_prev, coef, n_scales, R, r_stride,
+                                static_cast<hipStream_t>(stream), n_hub);
 }
 
 int srg_cheby_step_f32(const int64_t* indptr, const int32_t* indices, const float* values,

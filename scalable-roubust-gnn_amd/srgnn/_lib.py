@@ -82,6 +82,7 @@ EXPORTED_SYMBOLS = (
     "srg_plan_propagate_f32",
     "srg_plan_hop_f32",
     "srg_cheby_step_f64",
+    "srg_cheby_step_hub_f64",
     "srg_cheby_step_f32",
     "srg_cheby_epilogue_f32",
     "srg_hop_accumulate_f32",
@@ -164,6 +165,9 @@ def _declare(lib):
     lib.srg_cheby_step_f64.argtypes = [_p, _p, _p, _i64, _p, _p, _p, _p, _i64, _i32, ctypes.c_int,
                                        _f64, _f64, _p, _p, _i32, _p, _i64, _p]
     lib.srg_cheby_step_f64.restype = ctypes.c_int
+    lib.srg_cheby_step_hub_f64.argtypes = [_p, _p, _p, _i64, _p, _i64, _p, _p, _p, _i64, _i32, ctypes.c_int,
+                                           _f64, _f64, _p, _p, _i32, _p, _i64, _p]
+    lib.srg_cheby_step_hub_f64.restype = ctypes.c_int
     lib.srg_cheby_step_f32.argtypes = [_p, _p, _p, _i64, _p, _p, _p, _p, _i64, _i32, ctypes.c_int,
                                        _f32, _f32, _p, _p, _i32, _p, _i64, _p]
     lib.srg_cheby_step_f32.restype = ctypes.c_int

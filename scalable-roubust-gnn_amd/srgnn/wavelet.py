@@ -218,13 +218,15 @@ class HeatWaveletFilter:
         ns, nc = self.coeffs.shape
         f64 = self.dtype == torch.float64
         ct = ctypes.c_double if f64 else ctypes.c_float
-        name = "srg_cheby_step_f64" if f64 else "srg_cheby_step_f32"
         stream = _lib.stream(S.device)
+        # fp64: the schedule's hub rows as hub workgroups beside the row waves (srg_cheby_step_hub_f64)
+        sched = (self.n_hub,) if f64 else ()
+        name = "srg_cheby_step_hub_f64" if f64 else "srg_cheby_step_f32"
 
         def launch(vals, Tc, To, Tn, mode, coef_prev, coef):
             cp = self._coef(ct, coef_prev) if coef_prev is not None else None
             _lib.call(S.device, name, self.indptr.data_ptr(), self.indices.data_ptr(), vals.data_ptr(), n,
-                      self.order.data_ptr(), Tc.data_ptr(), To.data_ptr() if To is not None else None,
+                      self.order.data_ptr(), *sched, Tc.data_ptr(), To.data_ptr() if To is not None else None,
                       Tn.data_ptr(), d, d, mode, self.a1, self.a2, cp, self._coef(ct, coef), ns,
                       R.data_ptr(), n * d, stream)
 

@@ -40,6 +40,41 @@ def test_heat_filter_f64_bit_exact(oracle_mod, gname, d):
     np.testing.assert_array_equal(R, want)
 
 
+def _hub_graph():
+    """rmat3000 plus three hub nodes: node 7 joined to every node (a ~3,000-entry row: six 512-entry
+    windows, the last partial), node 11 to 1,100 nodes, node 13 to 520."""
+    a = graphs()["rmat3000"].tolil()
+    n = a.shape[0]
+    rng = np.random.default_rng(4)
+    for hub, k in ((7, n), (11, 1100), (13, 520)):
+        for j in (np.arange(n) if k >= n else rng.choice(n, k, replace=False)):
+            if j != hub:
+                a[hub, j] = a[j, hub] = 1.0
+    return sp.csr_matrix(a)
+
+
+@pytest.mark.parametrize("hub", [500, 0, 6])
+@pytest.mark.parametrize("d", [5, 16, 64, 100, 128, 130])
+def test_heat_filter_f64_hub_rows_bit_exact(oracle_mod, hub, d):
+    """srg_cheby_step_hub_f64: the schedule's hub rows (> hub entries) as hub workgroups on the side
+    stream, the other rows as row waves -- bit for bit the oracle's cheby_op and the all-row-wave
+    step.  hub = 0: every non-empty row a hub row (one short window each); d = 5: odd, every row a row
+    wave; d = 100 / 130: a partial last slice."""
+    from srgnn import wavelet as W
+    a = _hub_graph()
+    L = W.laplacian_from_adj(a)
+    n = a.shape[0]
+    f = W.HeatWaveletFilter(L, [-0.5, 0.5], order=3, lmax=None, device="cuda", hub_threshold=hub)
+    g = W.HeatWaveletFilter(L, [-0.5, 0.5], order=3, lmax=f.lmax, device="cuda", hub_threshold=-1)
+    assert f.n_hub == (int((np.diff(L.indptr) > hub).sum())) and f.n_hub >= 3 and g.n_hub == 0
+    S = np.random.default_rng(d).standard_normal((n, d))
+    St = torch.from_numpy(S).cuda()
+    R = f.apply(St).cpu().numpy()
+    want = oracle_mod.cheby_op((L.indptr, L.indices, L.data), f.coeffs, S, f.lmax)
+    np.testing.assert_array_equal(R.view(np.uint64), want.view(np.uint64))
+    np.testing.assert_array_equal(g.apply(St).cpu().numpy().view(np.uint64), R.view(np.uint64))
+
+
 @pytest.mark.parametrize("order", [1, 2, 5])
 def test_heat_filter_orders(oracle_mod, order):
     from srgnn import wavelet as W
