@@ -92,7 +92,8 @@ def parse():
     ap.add_argument("--col-block", type=int, default=None, help="wavelet: column block width")
     ap.add_argument("--dtype", default="f32", choices=["f32", "f64"],
                     help="wavelet: f64 = the reference's precision (pygsp cheby_op in fp64, base_model.py:236-265): "
-                         "one srg_cheby_step_f64 launch per order, bit-exact vs the oracle; f32 = the reduced-"
+                         "each order the fp64 Chebyshev step (column-blocked with hub workgroups where the panel "
+                         "outgrows the caches), bit-exact vs the oracle; f32 = the reduced-"
                          "precision variant (load-balanced SpMM + epilogue)")
     ap.add_argument("--fused-epilogue", action="store_true",
                     help="wavelet: one srg_spmm_cheby_f32 launch per order (two work panels) instead of the "
@@ -307,7 +308,8 @@ def measure_pmc(a):
     probe = None
     sums = {}
     # the kernel whose traffic is the roofline's: the hop's k_spmm launches, or the fp64 Chebyshev step
-    kern = "k_cheby<double" if (a.op == "wavelet" and a.dtype == "f64") else "k_spmm<"
+    # (fp64 step: the block launches k_cheby_blk64, the hub workgroups k_cheby_hub64, or one k_cheby<double>)
+    kern = "k_cheby" if (a.op == "wavelet" and a.dtype == "f64") else "k_spmm<"
     try:
         for counter in ("FETCH_SIZE", "WRITE_SIZE"):
             d = os.path.join(out, counter)
@@ -723,8 +725,11 @@ def run_wavelet(a, dev, world=1, rank=0, pmc=None):
 def run_wavelet_f64(a, dev, pmc=None):
     """The filter bank at the reference's precision: pygsp cheby_op is fp64 (SSRG/models/base_scalable/
     base_model.py:236-265, :243), R_s = sum_k c_{s,k} T_k(L~) S for tau = -0.5, +0.5, order 3.  Each order
-    is one srg_cheby_step_f64 launch (the row-wave gather with the recurrence and every scale's output
-    fused, scipy's operation order: bit-exact vs the oracle's restatement of cheby_op).  The panel is the
+    is HeatWaveletFilter.order_step: the row-wave gather with the recurrence and every scale's output fused,
+    scipy's operation order (bit-exact vs the oracle's restatement of cheby_op) -- over the filter's
+    column-blocked plan (srg_plan_cheby_step_f64: one launch per column block, the whole hub rows as hub
+    workgroups on the side stream) where the fp64 panel outgrows the caches, else one srg_cheby_step_hub_f64
+    launch.  The panel is the
     config's d columns, or -- where five fp64 panels of that width (S, two T work panels, the two scales'
     R) do not fit -- the widest power-of-two column block that does (RMAT-26): a step then filters that
     block, and `config.col_block` says so.  value = order * nnz(L) * steps / time.  Parity after the
@@ -761,20 +766,19 @@ def run_wavelet_f64(a, dev, pmc=None):
         step()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    # roofline: one Chebyshev STEP launch (F T_k - T_{k-1}, both scales' R updated), HIP events on the
-    # launch stream, over work panels of the block's width
+    # roofline: one Chebyshev STEP order (F T_k - T_{k-1}, both scales' R updated: every block launch and the
+    # hub workgroups, joined back), HIP events on the launch stream, over work panels of the block's width
+    P64 = filt._plan64(cb)
+    step_launches = P64.n_launch if P64 is not None else 1
     from srgnn import _lib
     stream = torch.cuda.current_stream(dev)
     t_cur, t_old = torch.empty_like(S), torch.empty_like(S)
     t_cur.copy_(S)
     t_old.zero_()
-    coef = (ctypes.c_double * ns)(*[float(c) for c in filt.coeffs[:, 2]])
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * a.roofline_reps)]
     for r in range(a.roofline_reps):
         ev[2 * r].record(stream)
-        _lib.call(dev, "srg_cheby_step_f64", filt.indptr.data_ptr(), filt.indices.data_ptr(), filt.fvals.data_ptr(), n,
-                  filt.order.data_ptr(), S.data_ptr(), t_old.data_ptr(), t_cur.data_ptr(), cb, cb,
-                  _lib.SRG_CHEBY_STEP, filt.a1, filt.a2, None, coef, ns, R.data_ptr(), n * cb, _lib.stream(dev))
+        filt.order_step(filt.fvals, S, t_old, t_cur, _lib.SRG_CHEBY_STEP, None, filt.coeffs[:, 2], R)
         ev[2 * r + 1].record(stream)
     torch.cuda.synchronize()
     kern_s = float(np.mean([ev[2 * r].elapsed_time(ev[2 * r + 1]) * 1e-3 for r in range(a.roofline_reps)]))
@@ -808,7 +812,10 @@ def run_wavelet_f64(a, dev, pmc=None):
                    "n_nodes": n, "nnz_L": nnz, "d": d, "col_block": cb,
                    "columns_per_step": cb, "chebyshev_order": order, "scales": taus, "lmax": lmax,
                    "parallelism": "x1",
-                   "mode": "fp64, one srg_cheby_step_f64 launch per order (SpMM + recurrence + both scales fused)"
+                   "mode": ("fp64, per order %d column-block launches of srg_plan_cheby_step_f64 + %d whole hub rows "
+                            "as hub workgroups beside them (SpMM + recurrence + both scales fused)"
+                            % (P64.col_blocks, P64.hub_rows_whole) if P64 is not None else
+                            "fp64, one srg_cheby_step_hub_f64 launch per order (SpMM + recurrence + both scales fused)")
                            + ("" if cb == d else f"; a step filters one {cb}-column block of the {d}-column "
                                                  "panel (the widest whose five fp64 panels fit)")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
@@ -818,8 +825,10 @@ def run_wavelet_f64(a, dev, pmc=None):
                                         else "compulsory bytes / the launch's time (no counter run: a lower bound)"),
                      "traffic_source": pmc["source"] if traffic else None,
                      "unit_of_work": f"one Chebyshev STEP order over a {cb}-column fp64 panel",
-                     "kernel": "k_cheby<double> (srg_cheby_step_f64, SRG_CHEBY_STEP)",
-                     "kernel_ms": kern_s * 1e3,
+                     "kernel": ("k_cheby_blk64 (+ k_cheby_hub64 beside it): one STEP order = %d launches "
+                                "(srg_plan_cheby_step_f64)" % step_launches if P64 is not None
+                                else "k_cheby<double> (+ k_cheby_hub64 beside it; srg_cheby_step_hub_f64, SRG_CHEBY_STEP)"),
+                     "kernel_ms": kern_s * 1e3, "launches_per_step": step_launches,
                      "frac_no_reuse": b_alg / kern_s / 1e9 / peak, "frac_compulsory": b_comp / kern_s / 1e9 / peak,
                      "algorithmic_bytes_per_launch": b_alg, "compulsory_bytes_per_launch": b_comp,
                      "traffic_over_compulsory": (traffic / b_comp) if traffic else None},

@@ -212,6 +212,9 @@ typedef struct srg_plan srg_plan;
 #define SRG_PLAN_SPANS 0x2u          /* never copy: spans of the caller's arrays */
 #define SRG_PLAN_SPLIT_BLOCK0 0x4u   /* block 0 as two launches (default: panels < 16 GiB) */
 #define SRG_PLAN_WHOLE_BLOCK0 0x8u   /* block 0 as one launch */
+#define SRG_PLAN_WHOLE_HUBS 0x10u    /* with an explicit hub_threshold (column-blocked plans): rows longer than it
+                                        are whole hub rows -- cut nowhere, one launch of their own first in the
+                                        hop -- as SRG_PLAN_AUTO does for rows > max(2048, nnz / 1024) */
 #define SRG_PLAN_AUTO (-1)
 #define SRG_PLAN_NONE (-2)
 typedef struct {
@@ -280,6 +283,20 @@ int srg_plan_propagate_f32(const srg_plan* plan, float* const* panels, int64_t l
  * into the hops as they are produced. */
 int srg_plan_hop_f32(const srg_plan* plan, const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t d,
                      uint32_t flags, float* agg, int64_t lda, float w, int32_t agg_init, void* stream);
+/* One fp64 Chebyshev order through the plan: srg_cheby_step_f64's recurrence and epilogue (below), bitwise,
+ * with the plan's column blocks -- each block's launch gathers from one column block of Tc and continues
+ * every row's chain from the fp64 partial sum the block before stored in Tn; the epilogue runs where the
+ * chain ends (block 0's whole rows, the last block) -- and its whole hub rows as hub workgroups on the
+ * hub side stream (joined before the call returns to `stream`'s order).  `values`: the operator's fp64
+ * values (L for INIT, F for STEP: one plan serves both, the layout depends on indptr / indices only).  The
+ * plan must read spans of the caller's arrays (SRG_PLAN_SPANS; its fp32 values may be NULL, the fp32
+ * entry points then refuse it) with block 0 as two launches (SRG_PLAN_SPLIT_BLOCK0) when blocked; build it
+ * for twice the panel width (the layout is sized by panel bytes).  Replaces pygsp cheby_op's per-order
+ * L.dot (SSRG/models/base_scalable/base_model.py:236-265) for graphs whose fp64 panels outgrow the
+ * Infinity Cache. */
+int srg_plan_cheby_step_f64(const srg_plan* plan, const double* values, const double* Tc, const double* To, double* Tn,
+                            int64_t ld, int32_t d, int mode, double a1, double a2, const double* coef_prev,
+                            const double* coef, int32_t n_scales, double* R, int64_t r_stride, void* stream);
 
 /* Chebyshev heat-kernel filter bank (wavelet basis), SSRG/models/base_scalable/base_model.py:
  * 184-191, 236-265 via pygsp cheby_op.  One fused launch per Chebyshev order:

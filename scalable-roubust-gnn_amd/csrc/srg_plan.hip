@@ -33,11 +33,7 @@
 
 #include "srgnn_hip.h"
 
-extern "C" void srg_set_error(int code, const char* msg);   // srg_spmm.hip: thread-local srg_last_error
-extern "C" void srg_clear_error(void);
-extern "C" int srg_run_plan_hop(const srg_hop_launch* launches, int32_t n_launch, int32_t join_hub, const float* X,
-                                int64_t ldx, float* Y, int64_t ldy, int32_t d, const uint8_t* agg_on, float* agg,
-                                int64_t lda, float w, int32_t agg_init, void* stream);   // srg_spmm.hip
+#include "srg_plan_internal.h"
 
 struct srg_plan {
     struct Launch {
@@ -59,6 +55,7 @@ struct srg_plan {
     int32_t d = 0, B = 1;
     bool split0 = false, compact = false, same_hubs = false;
     bool block_hubs = false;                 // some launch over cut rows has hub rows
+    bool no_values = false;                  // built without fp32 values (SRG_PLAN_SPANS): fp64 steps only
     int64_t n_hub_whole = 0;                 // rows in the whole hub rows' launch
     // compact plans: whether the row-indexed spans hold every scheduled row (the light-row paths of
     // panels other than 64 / 128 / 256 columns read them) or only the hub and slice-wave rows (the
@@ -654,7 +651,8 @@ static int build_impl(const int64_t* indptr, const int32_t* indices, const float
     if (hub_threshold < SRG_PLAN_NONE || heavy_threshold < SRG_PLAN_NONE)
         return pfail(SRG_ERR_INVALID, "hub_threshold=%lld, heavy_threshold=%lld: a row length, SRG_PLAN_AUTO or SRG_PLAN_NONE",
                      (long long)hub_threshold, (long long)heavy_threshold);
-    const uint32_t known = SRG_PLAN_COMPACT | SRG_PLAN_SPANS | SRG_PLAN_SPLIT_BLOCK0 | SRG_PLAN_WHOLE_BLOCK0;
+    const uint32_t known = SRG_PLAN_COMPACT | SRG_PLAN_SPANS | SRG_PLAN_SPLIT_BLOCK0 | SRG_PLAN_WHOLE_BLOCK0 |
+                           SRG_PLAN_WHOLE_HUBS;
     if ((opts & ~known) || ((opts & SRG_PLAN_COMPACT) && (opts & SRG_PLAN_SPANS)) ||
         ((opts & SRG_PLAN_SPLIT_BLOCK0) && (opts & SRG_PLAN_WHOLE_BLOCK0)))
         return pfail(SRG_ERR_INVALID, "opts=0x%x: unknown or conflicting options", opts);
@@ -689,8 +687,11 @@ static int build_impl(const int64_t* indptr, const int32_t* indices, const float
     const int64_t nnz = (int64_t)hs[3] - (int64_t)hs[2];
     unsigned long long* dstat = nullptr;     // (reused below for the whole hub rows' count)
     if (nnz < 0) return bail(pfail(SRG_ERR_INVALID, "indptr[n] < indptr[0]"));
-    if (nnz > 0 && !mem.query() && (!indices || !values)) return bail(pfail(SRG_ERR_INVALID, "null indices / values"));
+    // values may be NULL for a SPANS plan (fp64 Chebyshev steps bring their own values: srg_plan_cheby_step_f64)
+    if (nnz > 0 && !mem.query() && (!indices || (!values && !(opts & SRG_PLAN_SPANS))))
+        return bail(pfail(SRG_ERR_INVALID, "null indices / values"));
     P->nnz = nnz;
+    P->no_values = nnz > 0 && !values;
     // ---- 2: the layout: blocks, launches, copies ----
     const int64_t panel = n * (int64_t)d * 4;
     int B = col_blocks;
@@ -716,8 +717,13 @@ static int build_impl(const int64_t* indptr, const int32_t* indices, const float
     // whole hub rows (column-blocked plans with automatic hub rows): longer than the one-launch hop's hub
     // threshold; counted only when the longest row is (one more host sync)
     int64_t hubw_t = INT64_MAX, n_hubw = 0;
-    if (B > 1 && hub_threshold == SRG_PLAN_AUTO && max_deg > std::max<int64_t>(2048, nnz / 1024)) {
-        hubw_t = std::max<int64_t>(2048, nnz / 1024);
+    // (SRG_PLAN_WHOLE_HUBS: longer than an explicit hub threshold -- and than a whole row, which is cut nowhere
+    // already)
+    const bool whole_hubs = (opts & SRG_PLAN_WHOLE_HUBS) && hub_threshold >= 0;
+    const int64_t hubw_rule = hub_threshold == SRG_PLAN_AUTO ? std::max<int64_t>(2048, nnz / 1024)
+                              : whole_hubs ? std::max<int64_t>(hub_threshold, kWholeMax) : INT64_MAX;
+    if (B > 1 && hubw_rule != INT64_MAX && max_deg > hubw_rule) {
+        hubw_t = hubw_rule;
         DevBuf st;
         st.s = s;
         unsigned long long hc = 0;
@@ -744,7 +750,8 @@ static int build_impl(const int64_t* indptr, const int32_t* indices, const float
     T.n_launch = (int)sets.size();
     T.whole_rule = B == 1 ? 1 : 0;
     T.base = n_hubw ? 1 : 0;
-    T.hub_t = hub_threshold;
+    // explicit whole hub rows: no launch over cut rows has hub rows of its own
+    T.hub_t = B > 1 && whole_hubs ? SRG_PLAN_NONE : hub_threshold;
     T.heavy_t = heavy_threshold;
     T.hubw_t = hubw_t;
     T.lenbits = bits_for((uint64_t)max_deg);
@@ -759,7 +766,8 @@ static int build_impl(const int64_t* indptr, const int32_t* indices, const float
     P->n_items = n_items;
     if (T.lenbits + T.lbits > 64) return bail(pfail(SRG_ERR_INVALID, "row lengths too long to plan"));
     if (mem.query()) {
-        *mem.q_opts = (compact ? SRG_PLAN_COMPACT : SRG_PLAN_SPANS) | (split0 ? SRG_PLAN_SPLIT_BLOCK0 : SRG_PLAN_WHOLE_BLOCK0);
+        *mem.q_opts = (compact ? SRG_PLAN_COMPACT : SRG_PLAN_SPANS) | (split0 ? SRG_PLAN_SPLIT_BLOCK0 : SRG_PLAN_WHOLE_BLOCK0) |
+                      (opts & SRG_PLAN_WHOLE_HUBS);
         *mem.q_blocks = B;
         if (n == 0) {
             *mem.q_keep = 0;
@@ -1135,6 +1143,9 @@ int srg_plan_propagate_f32(const srg_plan* plan, float* const* panels, int64_t l
     if (!plan) return pfail(SRG_ERR_INVALID, "null plan");
     if (flags & ~(SRG_SPMM_NT_STORE | SRG_SPMM_FAST))
         return pfail(SRG_ERR_INVALID, "flags=0x%x: a plan's hops take NT_STORE and FAST only", flags);
+    if (plan->no_values)
+        return pfail(SRG_ERR_INVALID, "the plan was built without fp32 values (SRG_PLAN_SPANS, values NULL): it serves "
+                     "srg_plan_cheby_step_f64 only");
     if (d <= 0 || K < 0) return pfail(SRG_ERR_INVALID, "d=%d, K=%d", d, K);
     if (K == 0 || plan->launches.empty()) { srg_clear_error(); return SRG_OK; }
     DevGuard g(static_cast<hipStream_t>(stream));
@@ -1213,6 +1224,9 @@ int srg_plan_hop_f32(const srg_plan* plan, const float* X, int64_t ldx, float* Y
     if (!plan) return pfail(SRG_ERR_INVALID, "null plan");
     if (flags & ~(SRG_SPMM_NT_STORE | SRG_SPMM_FAST))
         return pfail(SRG_ERR_INVALID, "flags=0x%x: a plan's hops take NT_STORE and FAST only", flags);
+    if (plan->no_values)
+        return pfail(SRG_ERR_INVALID, "the plan was built without fp32 values (SRG_PLAN_SPANS, values NULL): it serves "
+                     "srg_plan_cheby_step_f64 only");
     if ((flags & SRG_SPMM_FAST) && agg)
         return pfail(SRG_ERR_INVALID, "FAST takes no aggregation epilogue");
     if (d <= 0 || ldx < d || ldy < d) return pfail(SRG_ERR_INVALID, "d=%d, ldx=%lld, ldy=%lld", d, (long long)ldx, (long long)ldy);
@@ -1260,6 +1274,41 @@ int srg_plan_hop_f32(const srg_plan* plan, const float* X, int64_t ldx, float* Y
         rc = srg_hop_accumulate_f32(agg, lda, Y, ldy, plan->n, d, w, agg_init ? SRG_ACC_INIT : SRG_ACC_ADD, stream);
         if (rc) return rc;
     }
+    srg_clear_error();
+    return SRG_OK;
+}
+
+int srg_plan_cheby_step_f64(const srg_plan* plan, const double* values, const double* Tc, const double* To, double* Tn,
+                            int64_t ld, int32_t d, int mode, double a1, double a2, const double* coef_prev,
+                            const double* coef, int32_t n_scales, double* R, int64_t r_stride, void* stream)
+{
+    if (!plan) return pfail(SRG_ERR_INVALID, "null plan");
+    if (plan->compact)
+        return pfail(SRG_ERR_INVALID, "an fp64 step reads spans of the caller's arrays: build the plan with SRG_PLAN_SPANS");
+    if (plan->B > 1 && !plan->split0)
+        return pfail(SRG_ERR_INVALID, "an fp64 step needs block 0 as two launches: build the plan with SRG_PLAN_SPLIT_BLOCK0");
+    if (plan->launches.empty()) { srg_clear_error(); return SRG_OK; }
+    if (!values && plan->nnz > 0) return pfail(SRG_ERR_INVALID, "null values");
+    DevGuard g(static_cast<hipStream_t>(stream));
+    if (g.rc) return g.rc;
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess || dev != plan->device)
+        return pfail(SRG_ERR_INVALID, "the plan lives on device %d, the stream on %d", plan->device, dev);
+    std::vector<srg_hop_launch> L;
+    (void)plan_launches(plan, d, 0, L);
+    std::vector<uint8_t> roles(L.size(), 0);
+    for (size_t i = 0; i < L.size(); ++i) {
+        const srg_plan::Launch& D = plan->launches[i];
+        if (D.hub_whole) roles[i] = SRG_CHEBY64_HUBS;
+        else roles[i] = (D.block == 0 ? SRG_CHEBY64_FIRST : 0) |
+                        (D.whole_rows || plan->B == 1 || D.block == plan->B - 1 ? SRG_CHEBY64_LAST : 0);
+    }
+    const int64_t* indptr = plan->launches[0].row_beg;   // block 0 of a spans plan: the caller's indptr
+    const int32_t* indices = plan->launches[0].indices;
+    const int rc = srg_run_plan_cheby_f64(L.data(), roles.data(), (int32_t)L.size(), indptr, indices, values, Tc, To, Tn,
+                                          ld, d, mode, a1, a2, coef_prev, coef, n_scales, R, r_stride, stream);
+    if (rc) return rc;
+    note_use(const_cast<srg_plan*>(plan), static_cast<hipStream_t>(stream));
     srg_clear_error();
     return SRG_OK;
 }

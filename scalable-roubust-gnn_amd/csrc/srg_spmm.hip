@@ -34,6 +34,7 @@
 #include <vector>
 
 #include "srgnn_hip.h"
+#include "srg_plan_internal.h"
 
 #ifndef SRG_GIT_REV
 #define SRG_GIT_REV "dev"
@@ -1146,28 +1147,33 @@ k_cheby(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
 //
 // A row wave keeps U gathers of its row in flight, so a row of degree D costs ~D/U load latencies:
 // in fp64 the products top row (155,868 entries) is one wave's chain beside the whole step.  As in
-// k_spmm_hub, kHub64Producers waves gather windows of kHub64W entries into LDS (two tiles, one
+// k_spmm_hub, kHub64Producers waves gather windows of W entries into LDS (two tiles, one
 // barrier per window; each window's gathers are issued two windows ahead) and one consumer wave
 // runs the slice's 16 column chains out of LDS: link k of column c is acc = acc + a_k * x_k[c], the
 // product and the sum rounded separately (scipy's csr_matvecs order, as row_gather), then k_cheby's
 // epilogue for the row's 16 columns -- the same operations, so the same bits.
 //   * producer lane (g, q) gathers the 16-byte chunk q (columns 2q, 2q + 1 of the slice) of entry g
 //     of a group of 8: one dwordx4 instruction brings 8 entries' 128-byte slices;
-//   * the tile is column-major, [16 columns][kHub64LD]: the consumer's lane c reads links k, k + 1
+//   * the tile is column-major, [16 columns][W + 4]: the consumer's lane c reads links k, k + 1
 //     of its column with one ds_read_b128, their values with one broadcast ds_read_b128;
 //   * the consumer keeps three 8-link register sets in flight (reads issued ~16 links ahead).
 // ------------------------------------------------------------------------------------------------
 constexpr int kHub64Cols = 16;
-constexpr int kHub64W = 512;
 constexpr int kHub64Producers = 8;
 constexpr int kHub64Threads = 64 * (kHub64Producers + 1);
-constexpr int kHub64UW = kHub64W / (kHub64Producers * 8);     // gathers per producer lane per window
-constexpr int kHub64LD = kHub64W + 4;                         // doubles per tile column (16-byte rows)
-constexpr int kHub64Tile = kHub64Cols * kHub64LD;
 constexpr int kHub64Slack = 32;                               // the ring's reads past the last window
-constexpr size_t kHub64LdsBytes = (size_t)(2 * kHub64Tile + 2 * kHub64W + kHub64Slack) * sizeof(double);
-static_assert(kHub64LdsBytes <= 160 * 1024, "k_cheby_hub64's LDS");
+// W entries per window: 512 (141 KB of LDS, one workgroup per CU) for a few hub rows beside the row waves,
+// 256 (72 KB, two per CU) once a launch has more hub workgroups than CUs (as k_spmm_hub's kHubWideW)
+template <int W>
+struct Hub64Geom {
+    static constexpr int UW = W / (kHub64Producers * 8);      // gathers per producer lane per window
+    static constexpr int LD = W + 4;                          // doubles per tile column (16-byte rows)
+    static constexpr int TILE = kHub64Cols * LD;
+    static constexpr size_t LDS_BYTES = (size_t)(2 * TILE + 2 * W + kHub64Slack) * sizeof(double);
+    static_assert(LDS_BYTES <= 160 * 1024, "k_cheby_hub64's LDS");
+};
 
+template <int W>
 __global__ void __launch_bounds__(kHub64Threads)
 k_cheby_hub64(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
               const double* __restrict__ vals, const int32_t* __restrict__ hub_rows, int n_slices,
@@ -1176,9 +1182,9 @@ k_cheby_hub64(const int64_t* __restrict__ indptr, const int32_t* __restrict__ in
               int64_t r_stride)
 {
     typedef typename Vec<double, 2>::type V2;
-    constexpr int W = kHub64W, UW = kHub64UW, LD = kHub64LD;
+    constexpr int UW = Hub64Geom<W>::UW, LD = Hub64Geom<W>::LD, TILE = Hub64Geom<W>::TILE;
     extern __shared__ __attribute__((aligned(16))) double h64_lds[];
-    double* aval_base = h64_lds + 2 * kHub64Tile;
+    double* aval_base = h64_lds + 2 * TILE;
     const int row = hub_rows[blockIdx.x / n_slices];
     const int slice = blockIdx.x % n_slices;
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -1195,7 +1201,7 @@ k_cheby_hub64(const int64_t* __restrict__ indptr, const int32_t* __restrict__ in
         for (int h = 0; h < n_win; ++h) {
             __syncthreads();                      // window h is in tile h & 1
             if (lane < kHub64Cols) {
-                const double* tcol = h64_lds + (h & 1) * kHub64Tile + c * LD;
+                const double* tcol = h64_lds + (h & 1) * TILE + c * LD;
                 const double* av = aval_base + (h & 1) * W;
                 const int64_t sb = beg + (int64_t)h * W;
                 const int nb = (end - sb) < W ? (int)(end - sb) : W;
@@ -1287,7 +1293,7 @@ k_cheby_hub64(const int64_t* __restrict__ indptr, const int32_t* __restrict__ in
         }
     };
     auto put = [&](int w, const V2 (&x)[UW], const double (&a)[UW]) {
-        double* tile = h64_lds + (w & 1) * kHub64Tile;
+        double* tile = h64_lds + (w & 1) * TILE;
         double* av = aval_base + (w & 1) * W;
 #pragma unroll
         for (int b = 0; b < UW; ++b) {
@@ -1318,6 +1324,86 @@ k_cheby_hub64(const int64_t* __restrict__ indptr, const int32_t* __restrict__ in
         __syncthreads();
     }
     // barrier count: 1 (prologue) + (n_win - 1) in the loop == the consumer's n_win
+}
+
+// the hub workgroups of n_items (row, slice) pairs on `s` (the window size by the launch's width)
+void launch_hub64(int64_t n_items, hipStream_t s, const int64_t* indptr, const int32_t* indices, const double* vals,
+                  const int32_t* rows, int n_slices, const double* Tc, const double* To, double* Tn, int64_t ld, int d,
+                  int mode, double a1, double a2, const ChebyCoef<double>& cf, int n_scales, double* R, int64_t r_stride)
+{
+    if (n_items > kHubWideLaunch)
+        hipLaunchKernelGGL(k_cheby_hub64<256>, dim3((unsigned)n_items), dim3(kHub64Threads), Hub64Geom<256>::LDS_BYTES, s,
+                           indptr, indices, vals, rows, n_slices, Tc, To, Tn, ld, d, mode, a1, a2, cf, n_scales, R, r_stride);
+    else
+        hipLaunchKernelGGL(k_cheby_hub64<512>, dim3((unsigned)n_items), dim3(kHub64Threads), Hub64Geom<512>::LDS_BYTES, s,
+                           indptr, indices, vals, rows, n_slices, Tc, To, Tn, ld, d, mode, a1, a2, cf, n_scales, R, r_stride);
+}
+
+// ------------------------------------------------------------------------------------------------
+// fp64 Chebyshev step over a column-blocked plan (srg_plan_cheby_step_f64): one launch per block of
+// the plan, the row waves of k_cheby over the launch's schedule, row w's entries the span
+// [slot_beg[w], slot_end[w]) of the caller's arrays.  A row's chain starts at 0 in block 0 (FIRST),
+// continues from the fp64 partial sum the block before stored in Tn (exact: the stored value is the
+// chain's value), and ends -- k_cheby's epilogue, the same operations -- in block 0 for the whole rows
+// and in the last block for the cut rows (LAST).  So bitwise srg_cheby_step_f64, with each launch
+// gathering from one column block of Tc (1/B of the panel: the L2 / Infinity Cache keep it).
+// ------------------------------------------------------------------------------------------------
+template <int VEC, int U, bool FIRST, bool LAST>
+__global__ void __launch_bounds__(kBlock)
+k_cheby_blk64(const int64_t* __restrict__ slot_beg, const int64_t* __restrict__ slot_end,
+              const int32_t* __restrict__ order, int n_rows, const int32_t* __restrict__ indices,
+              const double* __restrict__ vals, const double* __restrict__ Tc, const double* __restrict__ To,
+              double* __restrict__ Tn, int64_t ld, int d, int mode, double a1, double a2, ChebyCoef<double> cf,
+              int n_scales, double* __restrict__ R, int64_t r_stride, int block_base)
+{
+    typedef typename Vec<double, VEC>::type V;
+    const int w = wave_slot(block_base);
+    if (w >= n_rows) return;
+    if constexpr (!FIRST && !LAST) {
+        if (slot_beg[w] >= slot_end[w]) return;   // nothing in this block: the partial sum stays
+    }
+    const int row = order[w];
+    const int lane = threadIdx.x & 63;
+    const int64_t roff = (int64_t)row * ld;
+    for (int c0 = 0; c0 < d; c0 += 64 * VEC) {
+        const int col = c0 + lane * VEC;
+        const bool act = col < d;
+        V acc = vzero<double, VEC>();
+        if constexpr (!FIRST) {
+            if (act) acc = vload<double, VEC>(Tn + roff + col);
+        }
+        row_gather<double, VEC, U, false, int64_t, true>(acc, slot_beg, indices, vals, w, Tc, ld, col, act, slot_end);
+        if (!act) continue;
+        if constexpr (!LAST) {
+            vstore<double, VEC>(Tn + roff + col, acc, false);
+        } else {
+            V tn;
+            if (mode == SRG_CHEBY_INIT) {
+                const V tc = vload<double, VEC>(Tc + roff + col);
+#pragma unroll
+                for (int i = 0; i < VEC; ++i) elem(tn, i) = e_div(e_sub(elem(acc, i), e_mul(a2, elem(tc, i))), a1);
+                for (int s = 0; s < n_scales; ++s) {
+                    V r;
+#pragma unroll
+                    for (int i = 0; i < VEC; ++i)
+                        elem(r, i) = e_add(e_mul(cf.prev[s], elem(tc, i)), e_mul(cf.cur[s], elem(tn, i)));
+                    vstore<double, VEC>(R + s * r_stride + roff + col, r, false);
+                }
+            } else {
+                const V to = vload<double, VEC>(To + roff + col);
+#pragma unroll
+                for (int i = 0; i < VEC; ++i) elem(tn, i) = e_sub(elem(acc, i), elem(to, i));
+                for (int s = 0; s < n_scales; ++s) {
+                    double* rp = R + s * r_stride + roff + col;
+                    V r = vload<double, VEC>(rp);
+#pragma unroll
+                    for (int i = 0; i < VEC; ++i) elem(r, i) = e_add(elem(r, i), e_mul(cf.cur[s], elem(tn, i)));
+                    vstore<double, VEC>(rp, r, false);
+                }
+            }
+            vstore<double, VEC>(Tn + roff + col, tn, false);
+        }
+    }
 }
 
 // Chebyshev epilogue after a load-balanced SpMM (fp32, large graphs): Tn holds acc = A*Tc (the
@@ -1770,8 +1856,10 @@ int side_stream_locked(hipStream_t caller, SideStream** out)
         int rc = hub_attrs<int>();
         if (!rc) rc = hub_attrs<int64_t>();
         if (rc) return rc;
-        SRG_HIP_CHECK(hipFuncSetAttribute((const void*)k_cheby_hub64, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                          (int)kHub64LdsBytes));
+        SRG_HIP_CHECK(hipFuncSetAttribute((const void*)k_cheby_hub64<512>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          (int)Hub64Geom<512>::LDS_BYTES));
+        SRG_HIP_CHECK(hipFuncSetAttribute((const void*)k_cheby_hub64<256>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          (int)Hub64Geom<256>::LDS_BYTES));
         g_side_attr[dev] = true;
     }
     const auto key = std::make_pair(dev, caller);
@@ -2143,9 +2231,8 @@ int launch_cheby(const int64_t* indptr, const int32_t* indices, const T* vals, i
             if (rc) return rc;
             SRG_HIP_CHECK(hipEventRecord(ss->fork, s));
             SRG_HIP_CHECK(hipStreamWaitEvent(ss->stream, ss->fork, 0));
-            hipLaunchKernelGGL(k_cheby_hub64, dim3((unsigned)(n_hub * n_slices)), dim3(kHub64Threads), kHub64LdsBytes,
-                               ss->stream, indptr, indices, vals, order, n_slices, Tc, To, Tn, ld, d, mode, a1, a2, cf,
-                               n_scales, R, r_stride);
+            launch_hub64(n_hub * n_slices, ss->stream, indptr, indices, vals, order, n_slices, Tc, To, Tn, ld, d, mode,
+                         a1, a2, cf, n_scales, R, r_stride);
             SRG_HIP_CHECK(hipGetLastError());
             SRG_HIP_CHECK(hipEventRecord(ss->join, ss->stream));
             hipLaunchKernelGGL(k_dispatch_delay, dim3(1), dim3(64), 0, s, kHubDelayUs);
@@ -2543,6 +2630,99 @@ int srg_cheby_step_hub_f64(const int64_t* indptr, const int32_t* indices, const 
     return launch_cheby<double>(indptr, indices, values, n_rows, row_order, Tc, To, Tn, ld, d, mode,
                                 a1, a2, coef_prev, coef, n_scales, R, r_stride,
                                 static_cast<hipStream_t>(stream), n_hub);
+}
+
+// Library-internal (srg_plan.hip's srg_plan_cheby_step_f64): one fp64 Chebyshev step over a plan's
+// launches.  roles[i]: SRG_CHEBY64_FIRST / _LAST bits (the block where launch i's rows' chains start /
+// end), or SRG_CHEBY64_HUBS (the whole hub rows: k_cheby_hub64 on the hub side stream, joined at the
+// end of the step).  A launch without spans by slot is the one-launch plan's CSR launch: srg_cheby_
+// step_hub_f64 over its schedule.  `values` are the fp64 values at the plan's entry positions.
+__attribute__((visibility("hidden"))) int srg_run_plan_cheby_f64(const srg_hop_launch* launches, const uint8_t* roles, int32_t n_launch, const int64_t* indptr,
+                           const int32_t* indices, const double* values, const double* Tc, const double* To,
+                           double* Tn, int64_t ld, int32_t d, int mode, double a1, double a2, const double* coef_prev,
+                           const double* coef, int32_t n_scales, double* R, int64_t r_stride, void* stream)
+{
+    SRG_DEVICE_GUARD(stream);
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    if (mode != SRG_CHEBY_INIT && mode != SRG_CHEBY_STEP) return fail(SRG_ERR_INVALID, "cheby mode %d", mode);
+    if (n_scales < 1 || n_scales > 8) return fail(SRG_ERR_INVALID, "n_scales=%d not in [1,8]", n_scales);
+    if (!coef || (mode == SRG_CHEBY_INIT && !coef_prev)) return fail(SRG_ERR_INVALID, "null coefficient array");
+    if (mode == SRG_CHEBY_STEP && !To) return fail(SRG_ERR_INVALID, "null To for a step");
+    if (d < 0 || ld < d) return fail(SRG_ERR_INVALID, "d=%d, ld=%lld", d, (long long)ld);
+    if (n_launch == 1 && !launches[0].slot_beg) {
+        const srg_hop_launch& L = launches[0];
+        return launch_cheby<double>(indptr, indices, values, L.n_rows, L.row_order, Tc, To, Tn, ld, d, mode, a1, a2,
+                                    coef_prev, coef, n_scales, R, r_stride, s, L.n_hub);
+    }
+    int64_t n_total = 0;
+    for (int i = 0; i < n_launch; ++i) {
+        const srg_hop_launch& L = launches[i];
+        if (!L.slot_beg || !L.slot_end || (L.n_rows > 0 && !L.row_order))
+            return fail(SRG_ERR_INVALID, "launch %d: a blocked fp64 step reads spans by slot", i);
+        if (roles[i] & (SRG_CHEBY64_LAST | SRG_CHEBY64_HUBS)) n_total += L.n_rows;
+    }
+    if (d == 0 || n_total == 0) return ok();
+    if (!Tc || !Tn || !R || !indices || !values) return fail(SRG_ERR_INVALID, "null panel or entry array");
+    if (r_stride < n_total * ld && n_scales > 1) return fail(SRG_ERR_INVALID, "r_stride too small for stacked scale panels");
+    ChebyCoef<double> cf;
+    for (int i = 0; i < 8; ++i) {
+        cf.prev[i] = (mode == SRG_CHEBY_INIT && i < n_scales) ? 0.5 * coef_prev[i] : 0.0;
+        cf.cur[i] = i < n_scales ? coef[i] : 0.0;
+        cf.mid[i] = 0.0;
+    }
+    const bool v2 = d % 2 == 0 && ld % 2 == 0 && aligned(Tc, 16) && aligned(Tn, 16) && aligned(R, 16) &&
+                    r_stride % 2 == 0 && (To == nullptr || aligned(To, 16));
+    const int n_slices = (d + kHub64Cols - 1) / kHub64Cols;
+    SideStream* ss = nullptr;
+    std::unique_lock<std::mutex> side_lock(g_side_mu, std::defer_lock);
+    for (int i = 0; i < n_launch; ++i) {
+        const srg_hop_launch& L = launches[i];
+        if (L.n_rows <= 0) continue;
+        int role = roles[i];
+        if (role == SRG_CHEBY64_HUBS) {
+            if (v2 && L.n_rows * n_slices <= INT32_MAX - 64) {   // fork: the hub workgroups beside the blocks
+                side_lock.lock();
+                int rc = side_stream_locked(s, &ss);
+                if (rc) return rc;
+                SRG_HIP_CHECK(hipEventRecord(ss->fork, s));
+                SRG_HIP_CHECK(hipStreamWaitEvent(ss->stream, ss->fork, 0));
+                launch_hub64(L.n_rows * n_slices, ss->stream, indptr, indices, values, L.row_order, n_slices, Tc, To,
+                             Tn, ld, d, mode, a1, a2, cf, n_scales, R, r_stride);
+                SRG_HIP_CHECK(hipGetLastError());
+                SRG_HIP_CHECK(hipEventRecord(ss->join, ss->stream));
+                hipLaunchKernelGGL(k_dispatch_delay, dim3(1), dim3(64), 0, s, kHubDelayUs);
+                SRG_HIP_CHECK(hipGetLastError());
+                continue;
+            }
+            role = SRG_CHEBY64_FIRST | SRG_CHEBY64_LAST;   // row waves over their whole spans
+        }
+        const int64_t blocks = (L.n_rows + kWavesPerBlock - 1) / kWavesPerBlock;
+        const int nr = (int)L.n_rows;
+        // (uncapped: 4 or 6 waves per SIMD measured 0.5-3 % slower, profiles/r06i_cheby64_plan_sweep.txt)
+        for (int64_t b0 = 0; b0 < blocks; b0 += kMaxLaunchBlocks) {
+            const dim3 grid((unsigned)std::min<int64_t>(kMaxLaunchBlocks, blocks - b0));
+#define SRG_LAUNCH_BLK64(V, F, LA)                                                                                \
+    hipLaunchKernelGGL((k_cheby_blk64<V, kUnroll, F, LA>), grid, dim3(kBlock), 0, s, L.slot_beg, L.slot_end,     \
+                       L.row_order, nr, indices, values, Tc, To, Tn, ld, d, mode, a1, a2, cf, n_scales, R, r_stride, \
+                       (int)b0)
+#define SRG_LAUNCH_BLK64_V(F, LA)                  \
+    do {                                           \
+        if (v2) SRG_LAUNCH_BLK64(2, F, LA);        \
+        else SRG_LAUNCH_BLK64(1, F, LA);           \
+    } while (0)
+            switch (role & (SRG_CHEBY64_FIRST | SRG_CHEBY64_LAST)) {
+            case SRG_CHEBY64_FIRST | SRG_CHEBY64_LAST: SRG_LAUNCH_BLK64_V(true, true); break;
+            case SRG_CHEBY64_FIRST: SRG_LAUNCH_BLK64_V(true, false); break;
+            case SRG_CHEBY64_LAST: SRG_LAUNCH_BLK64_V(false, true); break;
+            default: SRG_LAUNCH_BLK64_V(false, false); break;
+            }
+#undef SRG_LAUNCH_BLK64_V
+#undef SRG_LAUNCH_BLK64
+            SRG_HIP_CHECK(hipGetLastError());
+        }
+    }
+    if (ss) SRG_HIP_CHECK(hipStreamWaitEvent(s, ss->join, 0));   // join
+    return ok();
 }
 
 int srg_cheby_step_f32(const int64_t* indptr, const int32_t* indices, const float* values,

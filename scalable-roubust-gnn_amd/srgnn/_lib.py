@@ -48,6 +48,7 @@ SRG_PLAN_COMPACT = 0x1
 SRG_PLAN_SPANS = 0x2
 SRG_PLAN_SPLIT_BLOCK0 = 0x4
 SRG_PLAN_WHOLE_BLOCK0 = 0x8
+SRG_PLAN_WHOLE_HUBS = 0x10
 SRG_PLAN_AUTO = -1
 SRG_PLAN_NONE = -2
 
@@ -81,6 +82,7 @@ EXPORTED_SYMBOLS = (
     "srg_plan_launch",
     "srg_plan_propagate_f32",
     "srg_plan_hop_f32",
+    "srg_plan_cheby_step_f64",
     "srg_cheby_step_f64",
     "srg_cheby_step_hub_f64",
     "srg_cheby_step_f32",
@@ -159,8 +161,10 @@ def _declare(lib):
     lib.srg_plan_launch.argtypes = [_p, _i32, _i32, _p, _p, _p]
     lib.srg_plan_propagate_f32.argtypes = [_p, _p, _i64, _i32, _i32, _u32, _p]
     lib.srg_plan_hop_f32.argtypes = [_p, _p, _i64, _p, _i64, _i32, _u32, _p, _i64, _f32, _i32, _p]
+    lib.srg_plan_cheby_step_f64.argtypes = [_p, _p, _p, _p, _p, _i64, _i32, ctypes.c_int, _f64, _f64, _p, _p, _i32, _p,
+                                            _i64, _p]
     for name in ("srg_plan_build", "srg_plan_query", "srg_plan_build_in", "srg_plan_destroy", "srg_plan_describe", "srg_plan_launch", "srg_plan_propagate_f32",
-                 "srg_plan_hop_f32"):
+                 "srg_plan_hop_f32", "srg_plan_cheby_step_f64"):
         getattr(lib, name).restype = ctypes.c_int
     lib.srg_cheby_step_f64.argtypes = [_p, _p, _p, _i64, _p, _p, _p, _p, _i64, _i32, ctypes.c_int,
                                        _f64, _f64, _p, _p, _i32, _p, _i64, _p]

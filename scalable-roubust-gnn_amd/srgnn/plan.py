@@ -52,15 +52,17 @@ def _thresholds(A):
                  for t in (A.thresholds[1], A.thresholds[0]))
 
 
-def query(A, d: int, hops: int, col_blocks: int = 0, compact=None, split_block0=None):
+def query(A, d: int, hops: int, col_blocks: int = 0, compact=None, split_block0=None, extra_opts: int = 0,
+          thresholds=None):
     """(keep_bytes, scratch_bytes, resolved opts, resolved column blocks) of a plan for these arguments
-    (srg_plan_query: one pass over indptr, nothing allocated)."""
+    (srg_plan_query: one pass over indptr, nothing allocated); thresholds: (hub, heavy) as the planner takes
+    them (default: A's)."""
     kb, sb = ctypes.c_size_t(), ctypes.c_size_t()
     ro, rb = ctypes.c_uint32(), ctypes.c_int32()
-    hub_t, heavy_t = _thresholds(A)
+    hub_t, heavy_t = _thresholds(A) if thresholds is None else thresholds
     _lib.call(A.device, "srg_plan_query", A.indptr.data_ptr(), A.n_rows, int(d), int(hops), int(col_blocks), hub_t,
-              heavy_t, _opts(compact, split_block0), _lib.stream(A.device), ctypes.byref(kb), ctypes.byref(sb),
-              ctypes.byref(ro), ctypes.byref(rb))
+              heavy_t, _opts(compact, split_block0) | int(extra_opts), _lib.stream(A.device), ctypes.byref(kb),
+              ctypes.byref(sb), ctypes.byref(ro), ctypes.byref(rb))
     return int(kb.value), int(sb.value), int(ro.value), int(rb.value)
 
 
@@ -81,7 +83,8 @@ class NativePlan:
     give it that memory (after emptying its cache once), an automatic layout steps down: compact copies
     -> spans of A's arrays -> one launch per hop (the same bits every time)."""
 
-    def __init__(self, A, d: int, hops: int, col_blocks: int = 0, compact=None, split_block0=None):
+    def __init__(self, A, d: int, hops: int, col_blocks: int = 0, compact=None, split_block0=None, fp64: bool = False,
+                 hub_threshold=None):
         if A.is_span or A.n_rows != A.n_cols:
             raise ValueError("a plan takes a whole square operator")
         self.device = A.device
@@ -91,6 +94,16 @@ class NativePlan:
         n = A.n_rows
         # A's thresholds, for every launch
         hub_t, heavy_t = _thresholds(A)
+        self.fp64 = bool(fp64)
+        extra = 0
+        if fp64:
+            # fp64 Chebyshev steps (cheby_step_f64): spans of A's arrays (the values come with each step), block
+            # 0 as two launches, the layout sized for the fp64 panel's bytes; hub rows above an explicit
+            # threshold are whole hub rows (automatic: the planner's rule)
+            d, compact, split_block0 = 2 * int(d), False, True
+            hub_t = _lib.SRG_PLAN_AUTO if hub_threshold is None else int(hub_threshold)
+            heavy_t = _lib.SRG_PLAN_NONE
+            extra = _lib.SRG_PLAN_WHOLE_HUBS if hub_t >= 0 else 0
         if compact is None and hops >= _lib.SRG_PLAN_MIN_HOPS_TO_COMPACT:
             # the library's rule (the copies and the build's keys / ids / positions, < 32 B per entry, in a
             # quarter of the free memory) over the memory torch can hand out, cached blocks included
@@ -102,7 +115,7 @@ class NativePlan:
             tries.append((1, False))
         last = None
         for cb, cp in tries:
-            kb, sb, ro, rb = query(A, d, hops, cb, cp, split_block0)
+            kb, sb, ro, rb = query(A, d, hops, cb, cp, split_block0, extra, (hub_t, heavy_t))
             try:
                 keep, scratch = self._alloc(kb, sb)
             except torch.cuda.OutOfMemoryError as e:     # a smaller layout, the same bits
@@ -111,7 +124,8 @@ class NativePlan:
             p = ctypes.c_void_p()
             _lib.call(self.device, "srg_plan_build_in", A.indptr.data_ptr(),
                       A.indices.data_ptr() if A.indices.numel() else None,
-                      A.values.data_ptr() if A.values.numel() else None, n, int(d), int(hops), rb, hub_t, heavy_t,
+                      A.values.data_ptr() if A.values.numel() and not fp64 else None, n, int(d), int(hops), rb, hub_t,
+                      heavy_t,
                       ro, keep.data_ptr() if kb else _dummy(self.device), kb,
                       scratch.data_ptr() if sb else _dummy(self.device), sb, _lib.stream(self.device), ctypes.byref(p))
             del scratch                 # the build has returned (and synchronised): the scratch goes back
@@ -175,6 +189,19 @@ class NativePlan:
         _lib.call(self.device, "srg_plan_hop_f32", self._p, X.data_ptr(), X.stride(0), Y.data_ptr(), Y.stride(0),
                   int(d), int(flags), agg.data_ptr() if agg is not None else None,
                   agg.stride(0) if agg is not None else 0, float(w), 1 if init else 0, _lib.stream(self.device))
+
+    def cheby_step_f64(self, values, Tc, To, Tn, ld: int, d: int, mode: int, a1: float, a2: float, coef_prev, coef,
+                       n_scales: int, R, r_stride: int) -> None:
+        """One fp64 Chebyshev order through the plan (srg_plan_cheby_step_f64): `values` the operator's fp64
+        values, Tc / To / Tn / R device tensors (row stride ld), coef_prev / coef ctypes double arrays."""
+        if self._p is None:
+            raise ValueError("the plan is closed")
+        if not self.fp64:
+            raise ValueError("an fp32 plan: build it with fp64=True")
+        _lib.call(self.device, "srg_plan_cheby_step_f64", self._p, values.data_ptr() if values.numel() else None,
+                  Tc.data_ptr(), To.data_ptr() if To is not None else None, Tn.data_ptr(), int(ld), int(d), int(mode),
+                  float(a1), float(a2), coef_prev, coef, int(n_scales), R.data_ptr(), int(r_stride),
+                  _lib.stream(self.device))
 
     def close(self) -> None:
         """Releases the plan: srg_plan_destroy orders itself after every stream the plan's work went to

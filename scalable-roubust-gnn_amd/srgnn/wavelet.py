@@ -9,7 +9,10 @@ then L1-normalises each phi row (sklearn normalize).  cheby_op is the Chebyshev 
     R = c0/2 T0 + sum_k c_k T_k
 Here every Chebyshev order is ONE fused launch of srg_cheby_step_{f64,f32}: the SpMM row-wave
 gather plus an epilogue that forms T_{k+1} and accumulates every scale's output R_s in the same
-pass (all scales share the T_k panels, so two scales cost one recurrence, not two).  For fp32 on
+pass (all scales share the T_k panels, so two scales cost one recurrence, not two).  In fp64 (the
+reference's precision) the longest rows run as LDS-fed hub workgroups beside the row waves, and panels
+that outgrow the Infinity Cache run each order over a column-blocked plan (srg_plan_cheby_step_f64:
+one launch per column block, the chains continued through Tn, the same bits).  For fp32 on
 large power-law graphs (`split=True`, the default for fp32) each order is instead the
 load-balanced SpMM (slice waves, hub workgroups) plus srg_cheby_epilogue_f32 -- bit-identical to
 the fused kernel -- and the panel can be filtered in column blocks (`col_block`) so that
@@ -213,22 +216,67 @@ class HeatWaveletFilter:
                               [t.view(-1)[: n * w].view(n, w) for t in work], fused_epilogue)
         return R
 
-    def _apply_fused(self, S, R):
-        n, d = S.shape
-        ns, nc = self.coeffs.shape
+    # fp64 steps over column blocks (srg_plan_cheby_step_f64): None = the planner's rule for the fp64 panel's
+    # bytes (blocked from ~512 MiB panels), else forced; whole hub rows of the blocked steps: None = rows
+    # longer than hub64_rule(nnz), else an explicit row length (SRG_PLAN_WHOLE_HUBS)
+    col_blocks64 = None
+    hub64_threshold = None
+
+    @staticmethod
+    def hub64_rule(nnz: int) -> int:
+        """Whole hub rows of the blocked fp64 steps: rows longer than max(2048, nnz / 4096) entries, four times
+        as many as the fp32 hops' rule.  An fp64 row wave keeps 8 KiB of 1 KiB rows in flight, so its chain
+        is the longer one; products, 16 blocks, one STEP order (profiles/r06i_cheby64_plan_sweep.txt): 17.7 ms
+        with the fp32 rule's one hub row, 13.8 with 23 (> 32,768 entries), 14.0 with 252 (> 16,384)."""
+        return max(2048, int(nnz) // 4096)
+
+    def _plan64(self, d: int):
+        """The column-blocked layout of the fp64 steps over d-column panels (srgnn.plan.NativePlan with
+        fp64=True: one plan for L and F, whose entries share positions), or None where the panel stays one
+        launch per order."""
+        key = (int(d), self.col_blocks64, self.hub64_threshold)
+        cache = self.__dict__.setdefault("_plans64", {})
+        if key not in cache:
+            from .plan import NativePlan, query
+            A = self._csr(self.fvals)
+            cb = int(self.col_blocks64 or 0)
+            ht = self.hub64_rule(int(self.indices.numel())) if self.hub64_threshold is None else int(self.hub64_threshold)
+            # the run a filter serves: every order of every apply (bench / basis batches reuse it)
+            hops = 1 << 20
+            _, _, _, B = query(A, 2 * d, hops, cb, False, True, _lib.SRG_PLAN_WHOLE_HUBS if ht >= 0 else 0,
+                               (ht, _lib.SRG_PLAN_NONE))
+            cache[key] = NativePlan(A, d, hops, col_blocks=cb, fp64=True, hub_threshold=ht) if B > 1 else None
+        return cache[key]
+
+    def order_step(self, vals, Tc, To, Tn, mode, coef_prev, coef, R) -> None:
+        """One Chebyshev order over contiguous [n, d] panels (R: [n_scales, n, d]): srg_cheby_step_f32, or in
+        fp64 srg_plan_cheby_step_f64 over the filter's column-blocked plan where the panel is blocked, else
+        srg_cheby_step_hub_f64 with the schedule's hub rows as hub workgroups -- the same bits every way."""
+        n, d = Tc.shape
+        ns = self.coeffs.shape[0]
         f64 = self.dtype == torch.float64
         ct = ctypes.c_double if f64 else ctypes.c_float
-        stream = _lib.stream(S.device)
-        # fp64: the schedule's hub rows as hub workgroups beside the row waves (srg_cheby_step_hub_f64)
-        sched = (self.n_hub,) if f64 else ()
-        name = "srg_cheby_step_hub_f64" if f64 else "srg_cheby_step_f32"
+        cp = self._coef(ct, coef_prev) if coef_prev is not None else None
+        cc = self._coef(ct, coef)
+        To_p = To.data_ptr() if To is not None else None
+        if f64:
+            P = self._plan64(d)
+            if P is not None:
+                P.cheby_step_f64(vals, Tc, To, Tn, d, d, mode, self.a1, self.a2, cp, cc, ns, R, n * d)
+                return
+            _lib.call(Tc.device, "srg_cheby_step_hub_f64", self.indptr.data_ptr(), self.indices.data_ptr(),
+                      vals.data_ptr(), n, self.order.data_ptr(), self.n_hub, Tc.data_ptr(), To_p, Tn.data_ptr(), d, d,
+                      mode, self.a1, self.a2, cp, cc, ns, R.data_ptr(), n * d, _lib.stream(Tc.device))
+            return
+        _lib.call(Tc.device, "srg_cheby_step_f32", self.indptr.data_ptr(), self.indices.data_ptr(), vals.data_ptr(), n,
+                  self.order.data_ptr(), Tc.data_ptr(), To_p, Tn.data_ptr(), d, d, mode, self.a1, self.a2, cp, cc, ns,
+                  R.data_ptr(), n * d, _lib.stream(Tc.device))
+
+    def _apply_fused(self, S, R):
+        nc = self.coeffs.shape[1]
 
         def launch(vals, Tc, To, Tn, mode, coef_prev, coef):
-            cp = self._coef(ct, coef_prev) if coef_prev is not None else None
-            _lib.call(S.device, name, self.indptr.data_ptr(), self.indices.data_ptr(), vals.data_ptr(), n,
-                      self.order.data_ptr(), *sched, Tc.data_ptr(), To.data_ptr() if To is not None else None,
-                      Tn.data_ptr(), d, d, mode, self.a1, self.a2, cp, self._coef(ct, coef), ns,
-                      R.data_ptr(), n * d, stream)
+            self.order_step(vals, Tc, To, Tn, mode, coef_prev, coef, R)
 
         # T_{k-1}, T_k and the free panel rotate through three buffers (S itself is never written)
         t_old, t_cur = S, torch.empty_like(S)
@@ -263,9 +311,12 @@ class HeatWaveletFilter:
         return B
 
     def drop_layouts(self) -> None:
-        """Frees L's and F's cached layouts (native plans, column blocks)."""
+        """Frees L's and F's cached layouts (native plans, column blocks) and the fp64 steps' plans."""
         for vals in (self.lvals, self.fvals):
             self._csr(vals).drop_blocks()
+        for P in self.__dict__.pop("_plans64", {}).values():
+            if P is not None:
+                P.close()
 
     def work_panels(self, fused_epilogue: bool = False) -> int:
         """[n, column block] work panels the split path needs: T_1 alone for order 1; T_{k-1} and

@@ -8,7 +8,9 @@ Times, with HIP events around `reps` launches each:
   cb<B>     the step over B column-block CSRs of F, one launch each (INIT mode, 1 scale: the same
             row-wave gather per block with only X's column range touched; the epilogue's panel passes
             repeat per block, so this over-counts them) -- what column locality would buy.
-  hub<h>    srg_cheby_step_hub_f64 with the h longest rows as hub workgroups beside the row waves.
+  hub<h>    srg_cheby_step_hub_f64 with the h longest rows as hub workgroups beside the row waves,
+  --plan    the blocked steps (srg_plan_cheby_step_f64) over B column blocks and hub thresholds, each
+            checked bitwise against the one-launch step.
 Results are not combined with the oracle (timing only).
 """
 import ctypes
@@ -69,6 +71,33 @@ def step_hub(h):
               filt.a2, None, coef, 2, R.data_ptr(), n * d, _lib.stream(dev))
 
 
+if "--plan" in sys.argv:
+    # the blocked steps (srg_plan_cheby_step_f64 through HeatWaveletFilter.order_step), bitwise against the
+    # one-launch step with the automatic hub rows
+    import time
+    R.zero_()
+    step_hub(filt.n_hub)
+    torch.cuda.synchronize()
+    ref_T, ref_R = Tn.clone(), R.clone()
+    cf = filt.coeffs[:, 2]
+    for B, ht in ((0, None), (16, None), (16, 32768), (16, 16384), (24, 16384), (16, 12288), (32, 16384)):
+        filt.col_blocks64, filt.hub64_threshold = (B or None), ht
+        t0 = time.perf_counter()
+        P = filt._plan64(d)
+        torch.cuda.synchronize()
+        tb = time.perf_counter() - t0
+        R.zero_()
+        filt.order_step(filt.fvals, S, To, Tn, _lib.SRG_CHEBY_STEP, None, cf, R)
+        torch.cuda.synchronize()
+        same = bool(torch.equal(Tn, ref_T) and torch.equal(R, ref_R))
+        ms = timed(lambda: filt.order_step(filt.fvals, S, To, Tn, _lib.SRG_CHEBY_STEP, None, cf, R))
+        print(json.dumps({"waves": os.environ.get("SRG_CHEBY64_WAVES", "0"), "col_blocks": P.col_blocks if P else 1,
+                          "hub64_threshold": ht,
+                          "hub_rows_whole": P.hub_rows_whole if P else filt.n_hub, "launches": P.n_launch if P else 1,
+                          "plan_mb": (P.device_bytes >> 20) if P else 0, "build_s": round(tb, 3), "step_ms": ms,
+                          "bitwise_vs_one_launch": same}), flush=True)
+        filt.drop_layouts()
+    sys.exit(0)
 for h in (1, 4, 16, 64, 256, 1024):
     out[f"hub{h}_ms"] = timed(lambda: step_hub(h))
 print(json.dumps(out), flush=True)

@@ -44,9 +44,9 @@ ap.add_argument("--col-block", type=int, default=None,
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 if a.op == "wavelet64":
-    # bench.py --op wavelet --dtype f64's roofline launch: one fp64 Chebyshev STEP (srg_cheby_step_f64)
+    # bench.py --op wavelet --dtype f64's roofline step: one fp64 Chebyshev STEP order (HeatWaveletFilter.
+    # order_step: srg_plan_cheby_step_f64 over the column-blocked plan, or one srg_cheby_step_hub_f64 launch)
     # over the block width bench.py picks (the widest whose five fp64 panels fit), `reps` times
-    import ctypes
     from srgnn import _lib
     from srgnn import wavelet as W
     ip, ix, lv, n, d, lmax = graphs.build_laplacian(a.config, dev, d=a.d)
@@ -61,16 +61,15 @@ if a.op == "wavelet64":
     S = synth.uniform_features_t(n, cb, device=dev).to(torch.float64)
     R = torch.zeros((2, n, cb), dtype=torch.float64, device=dev)
     To, Tn = torch.zeros_like(S), torch.empty_like(S)
-    coef = (ctypes.c_double * 2)(*[float(c) for c in filt.coeffs[:, 2]])
+    P = filt._plan64(cb)          # the blocked layout bench.py's steps run (None: one launch per order)
     torch.cuda.synchronize()
     for _ in range(a.reps):
-        _lib.call(dev, "srg_cheby_step_f64", filt.indptr.data_ptr(), filt.indices.data_ptr(), filt.fvals.data_ptr(), n,
-                  filt.order.data_ptr(), S.data_ptr(), To.data_ptr(), Tn.data_ptr(), cb, cb, _lib.SRG_CHEBY_STEP,
-                  filt.a1, filt.a2, None, coef, 2, R.data_ptr(), n * cb, _lib.stream(dev))
+        filt.order_step(filt.fvals, S, To, Tn, _lib.SRG_CHEBY_STEP, None, filt.coeffs[:, 2], R)
     torch.cuda.synchronize()
     nnz = int(ix.numel())
     print(json.dumps({"config": a.config, "op": "wavelet64", "n": n, "nnz": nnz, "d": cb, "reps": a.reps,
-                      "launches_per_hop": 1, "column_blocks": 1, "n_heavy": filt.n_heavy, "n_hub": filt.n_hub,
+                      "launches_per_hop": P.n_launch if P else 1, "column_blocks": P.col_blocks if P else 1,
+                      "n_heavy": filt.n_heavy, "n_hub": P.hub_rows_whole if P else filt.n_hub,
                       "algorithmic_bytes": roofline.cheby_step_bytes_no_reuse_f64(n, nnz, cb, 2),
                       "compulsory_bytes": roofline.cheby_step_bytes_compulsory_f64(n, nnz, cb, 2)}))
     sys.exit(0)
