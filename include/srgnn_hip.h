@@ -305,7 +305,10 @@ int srg_plan_cheby_step_f64(const srg_plan* plan, const double* values, const do
  * with A = L (combinatorial Laplacian) for INIT and A = F = (2/a1)(L - a2 I) for STEP (the caller
  * builds F's values).  R holds n_scales stacked panels: R + s*r_stride.  coef_prev (c0 per scale,
  * INIT only) and coef (c1 or ck per scale) are HOST arrays of n_scales <= 8 values.  fp64 follows
- * scipy's operation order (separate multiply and add, no fma); fp32 uses fma chains. */
+ * scipy's operation order (separate multiply and add, no fma); fp32 uses fma chains.  The fused steps
+ * (srg_cheby_step_*, srg_cheby_step_hub_f64, srg_plan_cheby_step_f64) also take the epilogue's lean modes
+ * below (SRG_CHEBY_INIT_T, SRG_CHEBY_STEP_FIRST with coef_prev = c0 then c1 per scale, | SRG_CHEBY_NO_T):
+ * the same bits, four panel passes less per order-3 filter. */
 #define SRG_CHEBY_INIT 0
 #define SRG_CHEBY_STEP 1
 int srg_cheby_step_f64(const int64_t* indptr, const int32_t* indices, const double* values,

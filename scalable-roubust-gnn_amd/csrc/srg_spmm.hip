@@ -1092,6 +1092,63 @@ constexpr size_t kHubLdsBytes = HubGeom<kHubW>::LDS_BYTES;
 // ------------------------------------------------------------------------------------------------
 // Chebyshev step with fused epilogue (wavelet basis)
 // ------------------------------------------------------------------------------------------------
+// The fused step's epilogue at VEC consecutive elements of row-offset `off`: acc = (A Tc) there becomes
+// T_{k+1}, every scale's output updated -- k_cheby_epilogue's modes and operations:
+//   INIT:       Tn = (acc - a2 Tc) / a1;  R_s = (c0_s/2) Tc + c1_s Tn
+//   INIT_T:     Tn = (acc - a2 Tc) / a1   (R formed by the first step)
+//   STEP_FIRST: Tn = acc - To (To = T0, Tc = T1);  R_s = ((c0_s/2) T0 + c1_s T1) + c2_s Tn
+//   STEP:       Tn = acc - To;  R_s += ck_s Tn
+// with SRG_CHEBY_NO_T leaving Tn unstored (the last order).  The lean sequence INIT_T, STEP_FIRST, ...,
+// STEP | NO_T forms every R with the same operations in the same order as INIT, STEP, ..., STEP: the
+// same bits with four panel passes less per order-3 filter.
+template <typename T, int VEC>
+__device__ __forceinline__ void cheby_epi_at(int mode, const typename Vec<T, VEC>::type& acc, const T* __restrict__ Tc,
+                                             const T* __restrict__ To, T* __restrict__ Tn, T* __restrict__ R,
+                                             int64_t off, int64_t r_stride, T a1, T a2, const ChebyCoef<T>& cf,
+                                             int n_scales)
+{
+    typedef typename Vec<T, VEC>::type V;
+    const int m = mode & 0xf;
+    V tn;
+    if (m == SRG_CHEBY_INIT || m == SRG_CHEBY_INIT_T) {
+        const V tc = vload<T, VEC>(Tc + off);
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) elem(tn, i) = e_div(e_sub(elem(acc, i), e_mul(a2, elem(tc, i))), a1);
+        if (m == SRG_CHEBY_INIT)
+            for (int s = 0; s < n_scales; ++s) {
+                V r;
+#pragma unroll
+                for (int i = 0; i < VEC; ++i)
+                    elem(r, i) = e_add(e_mul(cf.prev[s], elem(tc, i)), e_mul(cf.cur[s], elem(tn, i)));
+                vstore<T, VEC>(R + s * r_stride + off, r, false);
+            }
+    } else if (m == SRG_CHEBY_STEP_FIRST) {
+        const V t0 = vload<T, VEC>(To + off), t1 = vload<T, VEC>(Tc + off);
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) elem(tn, i) = e_sub(elem(acc, i), elem(t0, i));
+        for (int s = 0; s < n_scales; ++s) {
+            V r;
+#pragma unroll
+            for (int i = 0; i < VEC; ++i)
+                elem(r, i) = e_add(e_add(e_mul(cf.prev[s], elem(t0, i)), e_mul(cf.mid[s], elem(t1, i))),
+                                   e_mul(cf.cur[s], elem(tn, i)));
+            vstore<T, VEC>(R + s * r_stride + off, r, false);
+        }
+    } else {
+        const V to = vload<T, VEC>(To + off);
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) elem(tn, i) = e_sub(elem(acc, i), elem(to, i));
+        for (int s = 0; s < n_scales; ++s) {
+            T* rp = R + s * r_stride + off;
+            V r = vload<T, VEC>(rp);
+#pragma unroll
+            for (int i = 0; i < VEC; ++i) elem(r, i) = e_add(elem(r, i), e_mul(cf.cur[s], elem(tn, i)));
+            vstore<T, VEC>(rp, r, false);
+        }
+    }
+    if (!(mode & SRG_CHEBY_NO_T)) vstore<T, VEC>(Tn + off, tn, false);
+}
+
 template <typename T, int VEC, int U>
 __global__ void __launch_bounds__(kBlock)
 k_cheby(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
@@ -1112,33 +1169,7 @@ k_cheby(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
         V acc = vzero<T, VEC>();
         row_gather<T, VEC, U, false, int64_t>(acc, indptr, indices, vals, row, Tc, ld, col, act);
         if (!act) continue;
-        V tn;
-        if (mode == SRG_CHEBY_INIT) {
-            // Tn = (L Tc - a2 Tc) / a1 ;  R_s = (c0_s / 2) Tc + c1_s Tn
-            const V tc = vload<T, VEC>(Tc + roff + col);
-#pragma unroll
-            for (int i = 0; i < VEC; ++i) elem(tn, i) = e_div(e_sub(elem(acc, i), e_mul(a2, elem(tc, i))), a1);
-            for (int s = 0; s < n_scales; ++s) {
-                V r;
-#pragma unroll
-                for (int i = 0; i < VEC; ++i)
-                    elem(r, i) = e_add(e_mul(cf.prev[s], elem(tc, i)), e_mul(cf.cur[s], elem(tn, i)));
-                vstore<T, VEC>(R + s * r_stride + roff + col, r, false);
-            }
-        } else {
-            // Tn = F Tc - To ;  R_s += ck_s Tn
-            const V to = vload<T, VEC>(To + roff + col);
-#pragma unroll
-            for (int i = 0; i < VEC; ++i) elem(tn, i) = e_sub(elem(acc, i), elem(to, i));
-            for (int s = 0; s < n_scales; ++s) {
-                T* rp = R + s * r_stride + roff + col;
-                V r = vload<T, VEC>(rp);
-#pragma unroll
-                for (int i = 0; i < VEC; ++i) elem(r, i) = e_add(elem(r, i), e_mul(cf.cur[s], elem(tn, i)));
-                vstore<T, VEC>(rp, r, false);
-            }
-        }
-        vstore<T, VEC>(Tn + roff + col, tn, false);
+        cheby_epi_at<T, VEC>(mode, acc, Tc, To, Tn, R, roff + col, r_stride, a1, a2, cf, n_scales);
     }
 }
 
@@ -1247,21 +1278,7 @@ k_cheby_hub64(const int64_t* __restrict__ indptr, const int32_t* __restrict__ in
                 for (int q = nc * 8; q < nb; ++q) acc = link(av[q], tcol[q], acc);
             }
         }
-        if (act) {
-            const int64_t off = (int64_t)row * ld + col;
-            double tn;
-            if (mode == SRG_CHEBY_INIT) {
-                const double tc = Tc[off];
-                tn = e_div(e_sub(acc, e_mul(a2, tc)), a1);
-                for (int s = 0; s < n_scales; ++s)
-                    R[s * r_stride + off] = e_add(e_mul(cf.prev[s], tc), e_mul(cf.cur[s], tn));
-            } else {
-                tn = e_sub(acc, To[off]);
-                for (int s = 0; s < n_scales; ++s)
-                    R[s * r_stride + off] = e_add(R[s * r_stride + off], e_mul(cf.cur[s], tn));
-            }
-            Tn[off] = tn;
-        }
+        if (act) cheby_epi_at<double, 1>(mode, acc, Tc, To, Tn, R, (int64_t)row * ld + col, r_stride, a1, a2, cf, n_scales);
         return;
     }
 
@@ -1374,35 +1391,10 @@ k_cheby_blk64(const int64_t* __restrict__ slot_beg, const int64_t* __restrict__ 
         }
         row_gather<double, VEC, U, false, int64_t, true>(acc, slot_beg, indices, vals, w, Tc, ld, col, act, slot_end);
         if (!act) continue;
-        if constexpr (!LAST) {
+        if constexpr (!LAST)
             vstore<double, VEC>(Tn + roff + col, acc, false);
-        } else {
-            V tn;
-            if (mode == SRG_CHEBY_INIT) {
-                const V tc = vload<double, VEC>(Tc + roff + col);
-#pragma unroll
-                for (int i = 0; i < VEC; ++i) elem(tn, i) = e_div(e_sub(elem(acc, i), e_mul(a2, elem(tc, i))), a1);
-                for (int s = 0; s < n_scales; ++s) {
-                    V r;
-#pragma unroll
-                    for (int i = 0; i < VEC; ++i)
-                        elem(r, i) = e_add(e_mul(cf.prev[s], elem(tc, i)), e_mul(cf.cur[s], elem(tn, i)));
-                    vstore<double, VEC>(R + s * r_stride + roff + col, r, false);
-                }
-            } else {
-                const V to = vload<double, VEC>(To + roff + col);
-#pragma unroll
-                for (int i = 0; i < VEC; ++i) elem(tn, i) = e_sub(elem(acc, i), elem(to, i));
-                for (int s = 0; s < n_scales; ++s) {
-                    double* rp = R + s * r_stride + roff + col;
-                    V r = vload<double, VEC>(rp);
-#pragma unroll
-                    for (int i = 0; i < VEC; ++i) elem(r, i) = e_add(elem(r, i), e_mul(cf.cur[s], elem(tn, i)));
-                    vstore<double, VEC>(rp, r, false);
-                }
-            }
-            vstore<double, VEC>(Tn + roff + col, tn, false);
-        }
+        else
+            cheby_epi_at<double, VEC>(mode, acc, Tc, To, Tn, R, roff + col, r_stride, a1, a2, cf, n_scales);
     }
 }
 
@@ -2192,6 +2184,28 @@ int check_spmm_args(const void* indptr, const void* indices, const void* vals, i
     return SRG_OK;
 }
 
+// The fused step's mode and coefficients (cheby_epi_at): coef_prev holds c0 per scale (INIT) or c0 then c1
+// per scale (STEP_FIRST), coef c1 (INIT) or ck (STEP, STEP_FIRST); INIT_T takes neither; | SRG_CHEBY_NO_T.
+template <typename T>
+int cheby_setup(int mode, const T* coef_prev, const T* coef, int n_scales, const void* To, ChebyCoef<T>& cf)
+{
+    const int m = mode & ~SRG_CHEBY_NO_T;
+    if (m != SRG_CHEBY_INIT && m != SRG_CHEBY_STEP && m != SRG_CHEBY_INIT_T && m != SRG_CHEBY_STEP_FIRST)
+        return fail(SRG_ERR_INVALID, "cheby mode %d", mode);
+    if (n_scales < 1 || n_scales > 8) return fail(SRG_ERR_INVALID, "n_scales=%d not in [1,8]", n_scales);
+    const bool needs_r = m != SRG_CHEBY_INIT_T;
+    if ((needs_r && !coef) || ((m == SRG_CHEBY_INIT || m == SRG_CHEBY_STEP_FIRST) && !coef_prev))
+        return fail(SRG_ERR_INVALID, "null coefficient array");
+    if ((m == SRG_CHEBY_STEP || m == SRG_CHEBY_STEP_FIRST) && !To) return fail(SRG_ERR_INVALID, "null To for a step");
+    for (int i = 0; i < 8; ++i) {
+        const bool on = i < n_scales;
+        cf.prev[i] = ((m == SRG_CHEBY_INIT || m == SRG_CHEBY_STEP_FIRST) && on) ? T(0.5) * coef_prev[i] : T(0);
+        cf.mid[i] = (m == SRG_CHEBY_STEP_FIRST && on) ? coef_prev[n_scales + i] : T(0);
+        cf.cur[i] = (needs_r && on) ? coef[i] : T(0);
+    }
+    return SRG_OK;
+}
+
 // n_hub (fp64 only): the first n_hub rows of `order` run as k_cheby_hub64 workgroups on the hub side
 // stream beside the row waves of the others (joined before the call returns to the stream's order)
 template <typename T>
@@ -2200,21 +2214,13 @@ int launch_cheby(const int64_t* indptr, const int32_t* indices, const T* vals, i
                  T a1, T a2, const T* coef_prev, const T* coef, int n_scales, T* R, int64_t r_stride,
                  hipStream_t s, int64_t n_hub = 0)
 {
-    if (mode != SRG_CHEBY_INIT && mode != SRG_CHEBY_STEP)
-        return fail(SRG_ERR_INVALID, "cheby mode %d", mode);
-    if (n_scales < 1 || n_scales > 8) return fail(SRG_ERR_INVALID, "n_scales=%d not in [1,8]", n_scales);
-    if (!coef || (mode == SRG_CHEBY_INIT && !coef_prev))
-        return fail(SRG_ERR_INVALID, "null coefficient array");
-    if (mode == SRG_CHEBY_STEP && !To) return fail(SRG_ERR_INVALID, "null To for a step");
-    int rc = check_spmm_args(indptr, indices, vals, n_rows, Tc, ld, Tn, ld, d);
+    ChebyCoef<T> cf;
+    int rc = cheby_setup<T>(mode, coef_prev, coef, n_scales, To, cf);
+    if (rc) return rc;
+    rc = check_spmm_args(indptr, indices, vals, n_rows, Tc, ld, Tn, ld, d);
     if (rc) return rc;
     if (r_stride < n_rows * ld && n_scales > 1)
         return fail(SRG_ERR_INVALID, "r_stride too small for stacked scale panels");
-    ChebyCoef<T> cf;
-    for (int i = 0; i < 8; ++i) {
-        cf.prev[i] = (mode == SRG_CHEBY_INIT && i < n_scales) ? T(0.5) * coef_prev[i] : T(0);
-        cf.cur[i] = i < n_scales ? coef[i] : T(0);
-    }
     if (n_hub < 0 || n_hub > n_rows || (n_hub > 0 && !order))
         return fail(SRG_ERR_INVALID, "n_hub=%lld needs a row_order and <= n_rows", (long long)n_hub);
     if (n_rows == 0 || d == 0) return ok();
@@ -2644,10 +2650,9 @@ __attribute__((visibility("hidden"))) int srg_run_plan_cheby_f64(const srg_hop_l
 {
     SRG_DEVICE_GUARD(stream);
     const hipStream_t s = static_cast<hipStream_t>(stream);
-    if (mode != SRG_CHEBY_INIT && mode != SRG_CHEBY_STEP) return fail(SRG_ERR_INVALID, "cheby mode %d", mode);
-    if (n_scales < 1 || n_scales > 8) return fail(SRG_ERR_INVALID, "n_scales=%d not in [1,8]", n_scales);
-    if (!coef || (mode == SRG_CHEBY_INIT && !coef_prev)) return fail(SRG_ERR_INVALID, "null coefficient array");
-    if (mode == SRG_CHEBY_STEP && !To) return fail(SRG_ERR_INVALID, "null To for a step");
+    ChebyCoef<double> cf;
+    int rc0 = cheby_setup<double>(mode, coef_prev, coef, n_scales, To, cf);
+    if (rc0) return rc0;
     if (d < 0 || ld < d) return fail(SRG_ERR_INVALID, "d=%d, ld=%lld", d, (long long)ld);
     if (n_launch == 1 && !launches[0].slot_beg) {
         const srg_hop_launch& L = launches[0];
@@ -2664,12 +2669,6 @@ __attribute__((visibility("hidden"))) int srg_run_plan_cheby_f64(const srg_hop_l
     if (d == 0 || n_total == 0) return ok();
     if (!Tc || !Tn || !R || !indices || !values) return fail(SRG_ERR_INVALID, "null panel or entry array");
     if (r_stride < n_total * ld && n_scales > 1) return fail(SRG_ERR_INVALID, "r_stride too small for stacked scale panels");
-    ChebyCoef<double> cf;
-    for (int i = 0; i < 8; ++i) {
-        cf.prev[i] = (mode == SRG_CHEBY_INIT && i < n_scales) ? 0.5 * coef_prev[i] : 0.0;
-        cf.cur[i] = i < n_scales ? coef[i] : 0.0;
-        cf.mid[i] = 0.0;
-    }
     const bool v2 = d % 2 == 0 && ld % 2 == 0 && aligned(Tc, 16) && aligned(Tn, 16) && aligned(R, 16) &&
                     r_stride % 2 == 0 && (To == nullptr || aligned(To, 16));
     const int n_slices = (d + kHub64Cols - 1) / kHub64Cols;

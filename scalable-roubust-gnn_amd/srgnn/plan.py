@@ -75,6 +75,9 @@ def _torch_free(device) -> int:
 class NativePlan:
     """A srg_plan over the arrays of square DeviceCSR `A` for a run of `hops` hops of d-column panels.
 
+    fp64: the layout of fp64 Chebyshev steps (cheby_step_f64): spans of A's arrays without fp32 values, block 0
+    split, sized for the fp64 panel; hub_threshold: whole hub rows above this length (SRG_PLAN_WHOLE_HUBS;
+    None: A's thresholds, or for fp64 the planner's automatic rule).
     col_blocks: 0 = automatic (srg_plan_build's rule), else forced; compact: None = automatic (runs of
     >= SRG_PLAN_MIN_HOPS_TO_COMPACT hops, when the copies and the build's temporaries fit in a quarter
     of the memory torch can still hand out), True / False = always / never; split_block0: None =
@@ -104,6 +107,10 @@ class NativePlan:
             hub_t = _lib.SRG_PLAN_AUTO if hub_threshold is None else int(hub_threshold)
             heavy_t = _lib.SRG_PLAN_NONE
             extra = _lib.SRG_PLAN_WHOLE_HUBS if hub_t >= 0 else 0
+        elif hub_threshold is not None:
+            # whole hub rows above an explicit length (SRG_PLAN_WHOLE_HUBS) instead of A's per-launch hub rows
+            hub_t = int(hub_threshold)
+            extra = _lib.SRG_PLAN_WHOLE_HUBS
         if compact is None and hops >= _lib.SRG_PLAN_MIN_HOPS_TO_COMPACT:
             # the library's rule (the copies and the build's keys / ids / positions, < 32 B per entry, in a
             # quarter of the free memory) over the memory torch can hand out, cached blocks included

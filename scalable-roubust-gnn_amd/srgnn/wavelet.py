@@ -170,8 +170,8 @@ class HeatWaveletFilter:
         self.fvals = ((2.0 / self.a1) * torch.where(diag, l64 - self.a2, l64)).to(dtype)
         del diag, l64
         self.lvals = lvals.to(dtype)
-        # split path: the lean epilogue sequence (SRG_CHEBY_INIT_T / STEP_FIRST / NO_T); False runs
-        # INIT + STEP epilogues (same bits; set the attribute for A/B runs)
+        # the lean epilogue sequence (SRG_CHEBY_INIT_T / STEP_FIRST / NO_T) of the split path and of the fused
+        # steps; False runs INIT + STEP epilogues (same bits; set the attribute for A/B runs)
         self.lean_epilogue = True
         self.order, self.n_heavy, self.n_hub = make_schedule(self.indptr, heavy_threshold, hub_threshold)
         self.thresholds = (heavy_threshold, hub_threshold)
@@ -257,7 +257,7 @@ class HeatWaveletFilter:
         f64 = self.dtype == torch.float64
         ct = ctypes.c_double if f64 else ctypes.c_float
         cp = self._coef(ct, coef_prev) if coef_prev is not None else None
-        cc = self._coef(ct, coef)
+        cc = self._coef(ct, coef) if coef is not None else None
         To_p = To.data_ptr() if To is not None else None
         if f64:
             P = self._plan64(d)
@@ -274,17 +274,29 @@ class HeatWaveletFilter:
 
     def _apply_fused(self, S, R):
         nc = self.coeffs.shape[1]
+        c = self.coeffs
 
         def launch(vals, Tc, To, Tn, mode, coef_prev, coef):
             self.order_step(vals, Tc, To, Tn, mode, coef_prev, coef, R)
 
+        # the lean sequence (order >= 2): order 1 stores T1 only, order 2 forms R from T0, T1, T2, the last
+        # order stores no T -- the same operations in the same order as INIT + STEP..., four panel passes less
+        lean = self.lean_epilogue and nc > 2
         # T_{k-1}, T_k and the free panel rotate through three buffers (S itself is never written)
         t_old, t_cur = S, torch.empty_like(S)
         free = [torch.empty_like(S)] if nc > 2 else []
-        launch(self.lvals, S, None, t_cur, _lib.SRG_CHEBY_INIT, self.coeffs[:, 0], self.coeffs[:, 1])
+        if lean:
+            launch(self.lvals, S, None, t_cur, _lib.SRG_CHEBY_INIT_T, None, None)
+        else:
+            launch(self.lvals, S, None, t_cur, _lib.SRG_CHEBY_INIT, c[:, 0], c[:, 1])
         for k in range(2, nc):
             t_new = free.pop() if free else torch.empty_like(S)
-            launch(self.fvals, t_cur, t_old, t_new, _lib.SRG_CHEBY_STEP, None, self.coeffs[:, k])
+            last = _lib.SRG_CHEBY_NO_T if lean and k == nc - 1 else 0
+            if lean and k == 2:
+                launch(self.fvals, t_cur, t_old, t_new, _lib.SRG_CHEBY_STEP_FIRST | last, np.concatenate([c[:, 0], c[:, 1]]),
+                       c[:, 2])
+            else:
+                launch(self.fvals, t_cur, t_old, t_new, _lib.SRG_CHEBY_STEP | last, None, c[:, k])
             if t_old is not S:
                 free.append(t_old)
             t_old, t_cur = t_cur, t_new

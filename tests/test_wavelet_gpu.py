@@ -107,6 +107,29 @@ def test_heat_filter_f64_column_blocked_bit_exact(oracle_mod, B, hub, d):
     f.drop_layouts()
 
 
+@pytest.mark.parametrize("order", [1, 2, 3, 5])
+@pytest.mark.parametrize("B", [None, 5])
+def test_fp64_lean_sequence_bit_identical(oracle_mod, order, B):
+    """The fused fp64 steps' lean epilogue sequence (INIT_T, STEP_FIRST, ..., STEP | NO_T) == INIT + STEP ...
+    == the oracle, bit for bit, one launch per order (with its hub rows) or over a 5-block plan."""
+    from srgnn import wavelet as W
+    a = _hub_graph()
+    L = W.laplacian_from_adj(a)
+    n = a.shape[0]
+    f = W.HeatWaveletFilter(L, [-1.0, 0.3, 2.0], order=order, lmax=None, device="cuda", hub_threshold=500)
+    f.col_blocks64, f.hub64_threshold = B, (500 if B else None)
+    S = np.random.default_rng(order).standard_normal((n, 64))
+    St = torch.from_numpy(S).cuda()
+    lean = f.apply(St).cpu().numpy()
+    f.lean_epilogue = False
+    full = f.apply(St).cpu().numpy()
+    assert (f._plan64(64) is not None) == bool(B)
+    want = oracle_mod.cheby_op((L.indptr, L.indices, L.data), f.coeffs, S, f.lmax)
+    np.testing.assert_array_equal(lean.view(np.uint64), want.view(np.uint64))
+    np.testing.assert_array_equal(full.view(np.uint64), want.view(np.uint64))
+    f.drop_layouts()
+
+
 def test_fp64_plan_refuses_fp32_hops():
     """A plan built without fp32 values (the fp64 steps' layout) is refused by the fp32 entry points."""
     from srgnn import _lib
