@@ -215,6 +215,10 @@ typedef struct srg_plan srg_plan;
 #define SRG_PLAN_WHOLE_HUBS 0x10u    /* with an explicit hub_threshold (column-blocked plans): rows longer than it
                                         are whole hub rows -- cut nowhere, one launch of their own first in the
                                         hop -- as SRG_PLAN_AUTO does for rows > max(2048, nnz / 1024) */
+#define SRG_PLAN_WHOLE_MAX_SHIFT 16
+#define SRG_PLAN_WHOLE_MAX(n) ((uint32_t)(n) << SRG_PLAN_WHOLE_MAX_SHIFT)   /* block 0's whole rows: at most n
+                                        entries (1..65535; 0 = the default 48) -- the fp64 steps' partial sums are
+                                        1 KB per row per block, so their break-even row length differs */
 #define SRG_PLAN_AUTO (-1)
 #define SRG_PLAN_NONE (-2)
 typedef struct {

@@ -155,6 +155,7 @@ struct LaunchTable {
     int base;                                  // 1: launch 0 is the whole hub rows' launch
     int64_t hub_t, heavy_t;                    // row lengths, or SRG_PLAN_AUTO / SRG_PLAN_NONE
     int64_t hubw_t;                            // rows longer than this are whole hub rows (INT64_MAX: none)
+    int64_t whole_max;                         // rows this short run whole in block 0 (kWholeMax or the opts')
     int64_t off[kMaxLaunchTotal + 1];          // item offsets of the launches
     int64_t rows_lim[kMaxLaunchTotal];         // compact: items of launch L below off[L] + rows_lim[L] get row-indexed spans
     int32_t blk[kMaxLaunchTotal];              // the column block each launch's spans belong to
@@ -175,8 +176,8 @@ struct Arena {
     }
 };
 
-// stats[0] = the longest row, stats[1] = rows of <= kWholeMax entries; stats[2], [3] = indptr[0], indptr[n]
-__global__ void __launch_bounds__(256) k_plan_stats(const int64_t* __restrict__ ip, int64_t n,
+// stats[0] = the longest row, stats[1] = rows of <= whole_max entries; stats[2], [3] = indptr[0], indptr[n]
+__global__ void __launch_bounds__(256) k_plan_stats(const int64_t* __restrict__ ip, int64_t n, int64_t whole_max,
                                                     unsigned long long* __restrict__ stats)
 {
     __shared__ unsigned long long smx[4], swh[4];
@@ -185,7 +186,7 @@ __global__ void __launch_bounds__(256) k_plan_stats(const int64_t* __restrict__ 
     for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += stride) {
         const int64_t deg = ip[r + 1] - ip[r];
         mx = max(mx, (unsigned long long)max<int64_t>(deg, 0));
-        whole += deg <= kWholeMax ? 1 : 0;
+        whole += deg <= whole_max ? 1 : 0;
     }
     for (int o = 32; o > 0; o >>= 1) {
         mx = max(mx, (unsigned long long)__shfl_xor((long long)mx, o));
@@ -221,8 +222,8 @@ __global__ void __launch_bounds__(256) k_plan_count_above(const int64_t* __restr
 // (the whole hub rows too: their one launch reads block 0's end).  flag[r]: 1 for a cut row, 1 << 32 for a
 // whole hub row, 0 for a whole row -- one exclusive scan then gives both positions (low / high words)
 __global__ void __launch_bounds__(256) k_plan_splits(const int64_t* __restrict__ ip, const int32_t* __restrict__ ix,
-                                                     int64_t n, int B, int64_t hubw_t, int64_t* __restrict__ splits,
-                                                     int64_t* __restrict__ flag)
+                                                     int64_t n, int B, int64_t hubw_t, int64_t whole_max,
+                                                     int64_t* __restrict__ splits, int64_t* __restrict__ flag)
 {
     // grid-stride over the n (B - 1) (row, boundary) pairs: the grid is capped, so an operator of any
     // size (n (B - 1) past 2^32 work-items: 1.4e9 rows at B = 4) launches
@@ -231,7 +232,7 @@ __global__ void __launch_bounds__(256) k_plan_splits(const int64_t* __restrict__
         const int b = (int)(t / n) + 1;
         const int64_t r = t % n;
         const int64_t beg = ip[r], end = ip[r + 1];
-        const bool whole = end - beg <= kWholeMax;
+        const bool whole = end - beg <= whole_max;
         const bool hubw = end - beg > hubw_t;
         if (b == 1) flag[r] = hubw ? (int64_t(1) << 32) : whole ? 0 : 1;
         if (whole || hubw) {
@@ -280,7 +281,7 @@ __global__ void __launch_bounds__(256) k_plan_items(const int64_t* __restrict__ 
         const int64_t cp = pos[r] & 0xffffffffll, hp = pos[r] >> 32;
         if (deg > T.hubw_t) {
             put(0, hp, deg);                   // the whole hub rows' launch: the whole row
-        } else if (deg > kWholeMax) {
+        } else if (deg > T.whole_max) {
             put(L0, split0 ? cp : r - hp, bound_of(ip, splits, n, B, 1, r) - ip[r]);
             for (int b = 1; b < B; ++b)
                 put(L0 + (split0 ? b + 1 : b), cp,
@@ -652,7 +653,9 @@ static int build_impl(const int64_t* indptr, const int32_t* indices, const float
         return pfail(SRG_ERR_INVALID, "hub_threshold=%lld, heavy_threshold=%lld: a row length, SRG_PLAN_AUTO or SRG_PLAN_NONE",
                      (long long)hub_threshold, (long long)heavy_threshold);
     const uint32_t known = SRG_PLAN_COMPACT | SRG_PLAN_SPANS | SRG_PLAN_SPLIT_BLOCK0 | SRG_PLAN_WHOLE_BLOCK0 |
-                           SRG_PLAN_WHOLE_HUBS;
+                           SRG_PLAN_WHOLE_HUBS | (0xffffu << SRG_PLAN_WHOLE_MAX_SHIFT);
+    // block 0's whole rows: at most this many entries (SRG_PLAN_WHOLE_MAX(n); 0: kWholeMax)
+    const int64_t whole_max = (opts >> SRG_PLAN_WHOLE_MAX_SHIFT) ? (int64_t)(opts >> SRG_PLAN_WHOLE_MAX_SHIFT) : kWholeMax;
     if ((opts & ~known) || ((opts & SRG_PLAN_COMPACT) && (opts & SRG_PLAN_SPANS)) ||
         ((opts & SRG_PLAN_SPLIT_BLOCK0) && (opts & SRG_PLAN_WHOLE_BLOCK0)))
         return pfail(SRG_ERR_INVALID, "opts=0x%x: unknown or conflicting options", opts);
@@ -679,7 +682,8 @@ static int build_impl(const int64_t* indptr, const int32_t* indices, const float
         if (hipMalloc(&st.p, 4 * sizeof(unsigned long long)) != hipSuccess) { (void)hipGetLastError(); return bail(pfail(SRG_ERR_ALLOC, "plan: statistics")); }
         unsigned long long* dstats = (unsigned long long*)st.p;
         if (hipMemsetAsync(dstats, 0, 4 * sizeof(unsigned long long), s) != hipSuccess) return bail(pfail(SRG_ERR_HIP, "memset"));
-        hipLaunchKernelGGL(k_plan_stats, dim3(grid_for(std::max<int64_t>(n, 1), 256, 512)), dim3(256), 0, s, indptr, n, dstats);
+        hipLaunchKernelGGL(k_plan_stats, dim3(grid_for(std::max<int64_t>(n, 1), 256, 512)), dim3(256), 0, s, indptr, n, whole_max,
+                           dstats);
         if (hipMemcpyAsync(hs, dstats, sizeof(hs), hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
             return bail(pfail(SRG_ERR_HIP, "plan: degree statistics: %s", hipGetErrorString(hipGetLastError())));
     }
@@ -721,7 +725,7 @@ static int build_impl(const int64_t* indptr, const int32_t* indices, const float
     // already)
     const bool whole_hubs = (opts & SRG_PLAN_WHOLE_HUBS) && hub_threshold >= 0;
     const int64_t hubw_rule = hub_threshold == SRG_PLAN_AUTO ? std::max<int64_t>(2048, nnz / 1024)
-                              : whole_hubs ? std::max<int64_t>(hub_threshold, kWholeMax) : INT64_MAX;
+                              : whole_hubs ? std::max<int64_t>(hub_threshold, whole_max) : INT64_MAX;
     if (B > 1 && hubw_rule != INT64_MAX && max_deg > hubw_rule) {
         hubw_t = hubw_rule;
         DevBuf st;
@@ -754,6 +758,7 @@ static int build_impl(const int64_t* indptr, const int32_t* indices, const float
     T.hub_t = B > 1 && whole_hubs ? SRG_PLAN_NONE : hub_threshold;
     T.heavy_t = heavy_threshold;
     T.hubw_t = hubw_t;
+    T.whole_max = whole_max;
     T.lenbits = bits_for((uint64_t)max_deg);
     T.lbits = bits_for((uint64_t)std::max(0, T.n_launch - 1));
     T.off[0] = 0;
@@ -767,7 +772,7 @@ static int build_impl(const int64_t* indptr, const int32_t* indices, const float
     if (T.lenbits + T.lbits > 64) return bail(pfail(SRG_ERR_INVALID, "row lengths too long to plan"));
     if (mem.query()) {
         *mem.q_opts = (compact ? SRG_PLAN_COMPACT : SRG_PLAN_SPANS) | (split0 ? SRG_PLAN_SPLIT_BLOCK0 : SRG_PLAN_WHOLE_BLOCK0) |
-                      (opts & SRG_PLAN_WHOLE_HUBS);
+                      (opts & (SRG_PLAN_WHOLE_HUBS | (0xffffu << SRG_PLAN_WHOLE_MAX_SHIFT)));
         *mem.q_blocks = B;
         if (n == 0) {
             *mem.q_keep = 0;
@@ -872,7 +877,7 @@ static int build_impl(const int64_t* indptr, const int32_t* indices, const float
     // split points and the cut rows' positions
     if (B > 1) {
         hipLaunchKernelGGL(k_plan_splits, dim3(grid_for(n * (B - 1), 256, 1u << 20)), dim3(256), 0, s, indptr, indices,
-                           n, B, T.hubw_t, splits, cut);
+                           n, B, T.hubw_t, T.whole_max, splits, cut);
         size_t tb = cub_bytes;
         SRG_PLAN_HIP(hipcub::DeviceScan::ExclusiveSum(cub_tmp, tb, cut, cutpos, n, s));
     }

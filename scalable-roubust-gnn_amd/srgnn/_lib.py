@@ -49,6 +49,7 @@ SRG_PLAN_SPANS = 0x2
 SRG_PLAN_SPLIT_BLOCK0 = 0x4
 SRG_PLAN_WHOLE_BLOCK0 = 0x8
 SRG_PLAN_WHOLE_HUBS = 0x10
+SRG_PLAN_WHOLE_MAX_SHIFT = 16
 SRG_PLAN_AUTO = -1
 SRG_PLAN_NONE = -2
 

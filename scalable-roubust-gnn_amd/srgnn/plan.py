@@ -77,7 +77,8 @@ class NativePlan:
 
     fp64: the layout of fp64 Chebyshev steps (cheby_step_f64): spans of A's arrays without fp32 values, block 0
     split, sized for the fp64 panel; hub_threshold: whole hub rows above this length (SRG_PLAN_WHOLE_HUBS;
-    None: A's thresholds, or for fp64 the planner's automatic rule).
+    None: A's thresholds, or for fp64 the planner's automatic rule); whole_max: block 0's whole rows at most
+    this long (None: the planner's 48).
     col_blocks: 0 = automatic (srg_plan_build's rule), else forced; compact: None = automatic (runs of
     >= SRG_PLAN_MIN_HOPS_TO_COMPACT hops, when the copies and the build's temporaries fit in a quarter
     of the memory torch can still hand out), True / False = always / never; split_block0: None =
@@ -87,7 +88,7 @@ class NativePlan:
     -> spans of A's arrays -> one launch per hop (the same bits every time)."""
 
     def __init__(self, A, d: int, hops: int, col_blocks: int = 0, compact=None, split_block0=None, fp64: bool = False,
-                 hub_threshold=None):
+                 hub_threshold=None, whole_max=None):
         if A.is_span or A.n_rows != A.n_cols:
             raise ValueError("a plan takes a whole square operator")
         self.device = A.device
@@ -111,6 +112,9 @@ class NativePlan:
             # whole hub rows above an explicit length (SRG_PLAN_WHOLE_HUBS) instead of A's per-launch hub rows
             hub_t = int(hub_threshold)
             extra = _lib.SRG_PLAN_WHOLE_HUBS
+        if whole_max is not None:
+            # block 0's whole rows: at most whole_max entries (SRG_PLAN_WHOLE_MAX; the planner's default 48)
+            extra |= int(whole_max) << _lib.SRG_PLAN_WHOLE_MAX_SHIFT
         if compact is None and hops >= _lib.SRG_PLAN_MIN_HOPS_TO_COMPACT:
             # the library's rule (the copies and the build's keys / ids / positions, < 32 B per entry, in a
             # quarter of the free memory) over the memory torch can hand out, cached blocks included

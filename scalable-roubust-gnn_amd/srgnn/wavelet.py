@@ -221,6 +221,8 @@ class HeatWaveletFilter:
     # longer than hub64_rule(nnz), else an explicit row length (SRG_PLAN_WHOLE_HUBS)
     col_blocks64 = None
     hub64_threshold = None
+    # block 0's whole rows of the blocked fp64 steps (None: the planner's 48 entries)
+    whole64_max = None
 
     @staticmethod
     def hub64_rule(nnz: int) -> int:
@@ -234,7 +236,7 @@ class HeatWaveletFilter:
         """The column-blocked layout of the fp64 steps over d-column panels (srgnn.plan.NativePlan with
         fp64=True: one plan for L and F, whose entries share positions), or None where the panel stays one
         launch per order."""
-        key = (int(d), self.col_blocks64, self.hub64_threshold)
+        key = (int(d), self.col_blocks64, self.hub64_threshold, self.whole64_max)
         cache = self.__dict__.setdefault("_plans64", {})
         if key not in cache:
             from .plan import NativePlan, query
@@ -243,9 +245,11 @@ class HeatWaveletFilter:
             ht = self.hub64_rule(int(self.indices.numel())) if self.hub64_threshold is None else int(self.hub64_threshold)
             # the run a filter serves: every order of every apply (bench / basis batches reuse it)
             hops = 1 << 20
-            _, _, _, B = query(A, 2 * d, hops, cb, False, True, _lib.SRG_PLAN_WHOLE_HUBS if ht >= 0 else 0,
+            wm = (int(self.whole64_max) << _lib.SRG_PLAN_WHOLE_MAX_SHIFT) if self.whole64_max else 0
+            _, _, _, B = query(A, 2 * d, hops, cb, False, True, (_lib.SRG_PLAN_WHOLE_HUBS if ht >= 0 else 0) | wm,
                                (ht, _lib.SRG_PLAN_NONE))
-            cache[key] = NativePlan(A, d, hops, col_blocks=cb, fp64=True, hub_threshold=ht) if B > 1 else None
+            cache[key] = (NativePlan(A, d, hops, col_blocks=cb, fp64=True, hub_threshold=ht, whole_max=self.whole64_max)
+                          if B > 1 else None)
         return cache[key]
 
     def order_step(self, vals, Tc, To, Tn, mode, coef_prev, coef, R) -> None:

@@ -75,21 +75,23 @@ def test_heat_filter_f64_hub_rows_bit_exact(oracle_mod, hub, d):
     np.testing.assert_array_equal(g.apply(St).cpu().numpy().view(np.uint64), R.view(np.uint64))
 
 
-@pytest.mark.parametrize("B,hub", [(2, None), (4, None), (7, 500), (4, 0), (16, 40)])
+@pytest.mark.parametrize("B,hub,wm", [(2, None, None), (4, None, None), (7, 500, None), (4, 0, None), (16, 40, None),
+                                      (4, None, 100), (6, 500, 12)])
 @pytest.mark.parametrize("d", [5, 64, 100, 128])
-def test_heat_filter_f64_column_blocked_bit_exact(oracle_mod, B, hub, d):
+def test_heat_filter_f64_column_blocked_bit_exact(oracle_mod, B, hub, wm, d):
     """srg_plan_cheby_step_f64: the fp64 orders through a column-blocked plan (spans of the filter's arrays,
     block 0's cut rows and whole rows, blocks 1.. continuing every chain from the fp64 partial sum in Tn,
     the epilogue where the chain ends, whole hub rows as hub workgroups on the side stream) == the oracle's
     cheby_op == the one-launch steps, bit for bit.  hub None: the fp64 rule (node 7's ~3,000 entries >
     2,048: one whole hub row); 500: explicit (SRG_PLAN_WHOLE_HUBS, three rows); 0 / 40: every row of more
-    than 48 entries a whole hub row (no cut rows at all); d = 5: 1-wide lanes and the hub rows as row waves."""
+    than 48 entries a whole hub row (no cut rows at all); wm: block 0's whole-row limit (SRG_PLAN_WHOLE_MAX);
+    d = 5: 1-wide lanes and the hub rows as row waves."""
     from srgnn import wavelet as W
     a = _hub_graph()
     L = W.laplacian_from_adj(a)
     n = a.shape[0]
     f = W.HeatWaveletFilter(L, [-0.5, 0.5], order=3, lmax=None, device="cuda")
-    f.col_blocks64, f.hub64_threshold = B, hub
+    f.col_blocks64, f.hub64_threshold, f.whole64_max = B, hub, wm
     S = np.random.default_rng(d + B).standard_normal((n, d))
     St = torch.from_numpy(S).cuda()
     R = f.apply(St).cpu().numpy()
@@ -97,7 +99,7 @@ def test_heat_filter_f64_column_blocked_bit_exact(oracle_mod, B, hub, d):
     assert P is not None and P.col_blocks == B and P.fp64
     deg = np.diff(L.indptr)
     t = W.HeatWaveletFilter.hub64_rule(L.nnz) if hub is None else hub
-    whole = int((deg > max(t, 48)).sum())                  # rows of <= 48 entries run whole anyway
+    whole = int((deg > max(t, wm or 48)).sum())            # block 0's whole rows (<= 48 entries) run whole anyway
     assert P.hub_rows_whole == whole and whole >= 1
     want = oracle_mod.cheby_op((L.indptr, L.indices, L.data), f.coeffs, S, f.lmax)
     np.testing.assert_array_equal(R.view(np.uint64), want.view(np.uint64))

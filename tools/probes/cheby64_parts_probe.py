@@ -29,7 +29,12 @@ from srgnn import wavelet as W  # noqa: E402
 cfg = sys.argv[1] if len(sys.argv) > 1 and not sys.argv[1].startswith("--") else "products"
 reps = 3
 dev = torch.device("cuda", 0)
-ip, ix, lv, n, d, lmax = graphs.build_laplacian(cfg, dev)
+def _arg(name, default=None):
+    return sys.argv[sys.argv.index(name) + 1] if name in sys.argv else default
+
+
+d_arg = _arg("--d")
+ip, ix, lv, n, d, lmax = graphs.build_laplacian(cfg, dev, d=int(d_arg) if d_arg else None)
 filt = W.HeatWaveletFilter.from_device(ip, ix, lv, n, [-0.5, 0.5], order=3, lmax=lmax, dtype=torch.float64)
 S = synth.uniform_features_t(n, d, device=dev).to(torch.float64)
 R = torch.zeros((2, n, d), dtype=torch.float64, device=dev)
@@ -61,7 +66,8 @@ def timed(fn):
 
 out = {"config": cfg, "n": n, "nnz": int(ix.numel()), "d": d,
        "top_degrees": [int(x) for x in deg[order[:4].long()].tolist()]}
-out["full_ms"] = timed(lambda: step(filt.indptr, filt.indices, filt.fvals, order, n))
+if "--no-ref" not in sys.argv:
+    out["full_ms"] = timed(lambda: step(filt.indptr, filt.indices, filt.fvals, order, n))
 out["n_hub_auto"] = filt.n_hub
 
 
@@ -75,13 +81,20 @@ if "--plan" in sys.argv:
     # the blocked steps (srg_plan_cheby_step_f64 through HeatWaveletFilter.order_step), bitwise against the
     # one-launch step with the automatic hub rows
     import time
-    R.zero_()
-    step_hub(filt.n_hub)
-    torch.cuda.synchronize()
-    ref_T, ref_R = Tn.clone(), R.clone()
+    ref = "--no-ref" not in sys.argv
+    if ref:
+        R.zero_()
+        step_hub(filt.n_hub)
+        torch.cuda.synchronize()
+        ref_T, ref_R = Tn.clone(), R.clone()
     cf = filt.coeffs[:, 2]
-    for B, ht in ((0, None), (16, None), (16, 32768), (16, 16384), (24, 16384), (16, 12288), (32, 16384)):
-        filt.col_blocks64, filt.hub64_threshold = (B or None), ht
+    configs = ((0, None), (16, None), (16, 32768), (16, 16384), (24, 16384), (16, 12288), (32, 16384))
+    if _arg("--configs"):    # B:hub[:whole],... (hub empty: the fp64 rule; whole: block 0's whole-row limit)
+        configs = tuple(tuple(int(x) if x else None for x in (c.split(":") + [""])[:3])
+                        for c in _arg("--configs").split(","))
+    for cfg_ in configs:
+        B, ht, wm = (tuple(cfg_) + (None,))[:3]
+        filt.col_blocks64, filt.hub64_threshold, filt.whole64_max = (B or None), ht, wm
         t0 = time.perf_counter()
         P = filt._plan64(d)
         torch.cuda.synchronize()
@@ -89,10 +102,10 @@ if "--plan" in sys.argv:
         R.zero_()
         filt.order_step(filt.fvals, S, To, Tn, _lib.SRG_CHEBY_STEP, None, cf, R)
         torch.cuda.synchronize()
-        same = bool(torch.equal(Tn, ref_T) and torch.equal(R, ref_R))
+        same = bool(torch.equal(Tn, ref_T) and torch.equal(R, ref_R)) if ref else None
         ms = timed(lambda: filt.order_step(filt.fvals, S, To, Tn, _lib.SRG_CHEBY_STEP, None, cf, R))
         print(json.dumps({"waves": os.environ.get("SRG_CHEBY64_WAVES", "0"), "col_blocks": P.col_blocks if P else 1,
-                          "hub64_threshold": ht,
+                          "hub64_threshold": ht, "whole_max": wm,
                           "hub_rows_whole": P.hub_rows_whole if P else filt.n_hub, "launches": P.n_launch if P else 1,
                           "plan_mb": (P.device_bytes >> 20) if P else 0, "build_s": round(tb, 3), "step_ms": ms,
                           "bitwise_vs_one_launch": same}), flush=True)
