@@ -253,12 +253,19 @@ class HeatWaveletFilter:
         return cache[key]
 
     def order_step(self, vals, Tc, To, Tn, mode, coef_prev, coef, R) -> None:
-        """One Chebyshev order over contiguous [n, d] panels (R: [n_scales, n, d]): srg_cheby_step_f32, or in
-        fp64 srg_plan_cheby_step_f64 over the filter's column-blocked plan where the panel is blocked, else
-        srg_cheby_step_hub_f64 with the schedule's hub rows as hub workgroups -- the same bits every way."""
+        """One Chebyshev order over [n, d] panels sharing one row stride (R: [n_scales, n, d] with that row
+        stride): srg_cheby_step_f32, or in fp64 srg_plan_cheby_step_f64 over the filter's column-blocked plan
+        where the panel is blocked, else srg_cheby_step_hub_f64 with the schedule's hub rows as hub
+        workgroups -- the same bits every way.  (Feature chunks of 64 / 32 columns, each its own blocked step,
+        measured 9-15 % / 85 % slower: profiles/r06p_products_cheby64_feature_chunks_negative.txt.)"""
         n, d = Tc.shape
-        ns = self.coeffs.shape[0]
         f64 = self.dtype == torch.float64
+        ld = Tc.stride(0)
+        if any(t is not None and (t.stride(0) != ld or t.stride(1) != 1) for t in (Tc, To, Tn)) or \
+                R.stride(1) != ld or R.stride(2) != 1:
+            raise ValueError("the step's panels share one row stride")
+        ns = self.coeffs.shape[0]
+        rs = R.stride(0)
         ct = ctypes.c_double if f64 else ctypes.c_float
         cp = self._coef(ct, coef_prev) if coef_prev is not None else None
         cc = self._coef(ct, coef) if coef is not None else None
@@ -266,15 +273,15 @@ class HeatWaveletFilter:
         if f64:
             P = self._plan64(d)
             if P is not None:
-                P.cheby_step_f64(vals, Tc, To, Tn, d, d, mode, self.a1, self.a2, cp, cc, ns, R, n * d)
+                P.cheby_step_f64(vals, Tc, To, Tn, ld, d, mode, self.a1, self.a2, cp, cc, ns, R, rs)
                 return
             _lib.call(Tc.device, "srg_cheby_step_hub_f64", self.indptr.data_ptr(), self.indices.data_ptr(),
-                      vals.data_ptr(), n, self.order.data_ptr(), self.n_hub, Tc.data_ptr(), To_p, Tn.data_ptr(), d, d,
-                      mode, self.a1, self.a2, cp, cc, ns, R.data_ptr(), n * d, _lib.stream(Tc.device))
+                      vals.data_ptr(), n, self.order.data_ptr(), self.n_hub, Tc.data_ptr(), To_p, Tn.data_ptr(), ld, d,
+                      mode, self.a1, self.a2, cp, cc, ns, R.data_ptr(), rs, _lib.stream(Tc.device))
             return
         _lib.call(Tc.device, "srg_cheby_step_f32", self.indptr.data_ptr(), self.indices.data_ptr(), vals.data_ptr(), n,
-                  self.order.data_ptr(), Tc.data_ptr(), To_p, Tn.data_ptr(), d, d, mode, self.a1, self.a2, cp, cc, ns,
-                  R.data_ptr(), n * d, _lib.stream(Tc.device))
+                  self.order.data_ptr(), Tc.data_ptr(), To_p, Tn.data_ptr(), ld, d, mode, self.a1, self.a2, cp, cc, ns,
+                  R.data_ptr(), rs, _lib.stream(Tc.device))
 
     def _apply_fused(self, S, R):
         nc = self.coeffs.shape[1]
