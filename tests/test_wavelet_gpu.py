@@ -132,6 +132,71 @@ def test_fp64_lean_sequence_bit_identical(oracle_mod, order, B):
     f.drop_layouts()
 
 
+@pytest.mark.parametrize("case", ["no_edges", "d1", "d2", "one_hub_only"])
+def test_fp64_blocked_edge_cases(oracle_mod, case):
+    """Blocked fp64 steps on degenerate layouts: a Laplacian without edges (every row a 1-entry whole row,
+    the cut launches empty), 1- and 2-column panels, and a star whose centre is the only cut row (a whole
+    hub row; every other row whole) -- the oracle's bits."""
+    from srgnn import wavelet as W
+    if case == "no_edges":
+        a = sp.csr_matrix((500, 500))
+    elif case == "one_hub_only":
+        n0 = 3000
+        a = sp.csr_matrix((np.ones(n0 - 1), (np.zeros(n0 - 1, dtype=np.int64), np.arange(1, n0))), shape=(n0, n0))
+        a = a + a.T
+    else:
+        a = _hub_graph()
+    d = {"d1": 1, "d2": 2}.get(case, 8)
+    L = W.laplacian_from_adj(a)
+    n = a.shape[0]
+    f = W.HeatWaveletFilter(L, [-0.5, 0.5], order=3, lmax=None if case != "no_edges" else 2.0, device="cuda")
+    f.col_blocks64 = 3
+    S = np.random.default_rng(3).standard_normal((n, d))
+    R = f.apply(torch.from_numpy(S).cuda()).cpu().numpy()
+    P = f._plan64(d)
+    assert P is not None and P.col_blocks == 3
+    if case == "one_hub_only":
+        assert P.hub_rows_whole == 1
+    want = oracle_mod.cheby_op((L.indptr, L.indices, L.data), f.coeffs, S, f.lmax)
+    np.testing.assert_array_equal(R.view(np.uint64), want.view(np.uint64))
+    f.drop_layouts()
+
+
+def test_plan_cheby_step_argument_checks():
+    """srg_plan_cheby_step_f64 refuses a compact plan (its ids are copies, the fp64 values are not), a
+    blocked plan with block 0 as one launch, null values and unknown modes; nothing runs."""
+    import ctypes as C
+    from srgnn import _lib
+    from srgnn.plan import NativePlan
+    from srgnn.csr import DeviceCSR
+    a = _hub_graph()
+    n = a.shape[0]
+    A = DeviceCSR.from_scipy(sp.csr_matrix(a, dtype=np.float32), device="cuda")
+    T = torch.zeros((n, 64), dtype=torch.float64, device="cuda")
+    R = torch.zeros((2, n, 64), dtype=torch.float64, device="cuda")
+    v = torch.ones(A.nnz, dtype=torch.float64, device="cuda")
+    coef = (C.c_double * 2)(1.0, 1.0)
+
+    def step(P, vals=v, mode=_lib.SRG_CHEBY_STEP):
+        _lib.call(P.device, "srg_plan_cheby_step_f64", P._p, vals.data_ptr() if vals is not None else None,
+                  T.data_ptr(), T.data_ptr(), T.data_ptr(), 64, 64, mode, 1.0, 1.0, None, coef, 2, R.data_ptr(), n * 64,
+                  _lib.stream(P.device))
+    P = NativePlan(A, 64, 20, col_blocks=3, compact=True, split_block0=True)
+    with pytest.raises(_lib.SrgError, match="SRG_PLAN_SPANS"):
+        step(P)
+    P.close()
+    P = NativePlan(A, 64, 20, col_blocks=3, compact=False, split_block0=False)
+    with pytest.raises(_lib.SrgError, match="SPLIT_BLOCK0"):
+        step(P)
+    P.close()
+    P = NativePlan(A, 64, 20, col_blocks=3, fp64=True)
+    with pytest.raises(_lib.SrgError, match="null values"):
+        step(P, vals=None)
+    with pytest.raises(_lib.SrgError, match="cheby mode"):
+        step(P, mode=9)
+    P.close()
+
+
 def test_fp64_plan_refuses_fp32_hops():
     """A plan built without fp32 values (the fp64 steps' layout) is refused by the fp32 entry points."""
     from srgnn import _lib
