@@ -252,6 +252,17 @@ class HeatWaveletFilter:
                           if B > 1 else None)
         return cache[key]
 
+    def _n_hub64(self) -> int:
+        """Hub rows of the one-launch fp64 step: the schedule's first rows longer than hub64_rule(nnz) (the
+        fp64 rule; an explicit hub_threshold keeps the schedule's own n_hub).  The schedule lists rows by
+        decreasing length, so these are its first n rows."""
+        if self.thresholds[1] is not None:
+            return self.n_hub
+        if "_nh64" not in self.__dict__:
+            deg = self.indptr[1:] - self.indptr[:-1]
+            self._nh64 = int((deg > self.hub64_rule(int(self.indices.numel()))).sum().item()) if self.n else 0
+        return self._nh64
+
     def order_step(self, vals, Tc, To, Tn, mode, coef_prev, coef, R) -> None:
         """One Chebyshev order over [n, d] panels sharing one row stride (R: [n_scales, n, d] with that row
         stride): srg_cheby_step_f32, or in fp64 srg_plan_cheby_step_f64 over the filter's column-blocked plan
@@ -276,7 +287,7 @@ class HeatWaveletFilter:
                 P.cheby_step_f64(vals, Tc, To, Tn, ld, d, mode, self.a1, self.a2, cp, cc, ns, R, rs)
                 return
             _lib.call(Tc.device, "srg_cheby_step_hub_f64", self.indptr.data_ptr(), self.indices.data_ptr(),
-                      vals.data_ptr(), n, self.order.data_ptr(), self.n_hub, Tc.data_ptr(), To_p, Tn.data_ptr(), ld, d,
+                      vals.data_ptr(), n, self.order.data_ptr(), self._n_hub64(), Tc.data_ptr(), To_p, Tn.data_ptr(), ld, d,
                       mode, self.a1, self.a2, cp, cc, ns, R.data_ptr(), rs, _lib.stream(Tc.device))
             return
         _lib.call(Tc.device, "srg_cheby_step_f32", self.indptr.data_ptr(), self.indices.data_ptr(), vals.data_ptr(), n,
