@@ -199,7 +199,8 @@ int srg_propagate_plan_f32(const srg_hop_launch* launches, int32_t n_launch, int
  * Unlike the other (B) entries the plan allocates device memory (hipMalloc: the schedules, the spans
  * by slot, the copies -- srg_plan_describe's device_bytes -- and a scratch arena freed before it
  * returns) and synchronises `stream` while it builds.  The plan BORROWS indptr / indices / values (span
- * layouts read them every hop): they must outlive it.  indptr[n_rows + 1], indices / values
+ * layouts read them every hop): they must outlive it.  values may be NULL with SRG_PLAN_SPANS: such a
+ * plan serves srg_plan_cheby_step_f64 only (which brings its fp64 values per call).  indptr[n_rows + 1], indices / values
  * [indptr[n_rows] - indptr[0]], column ids in [0, n_rows) (not validated here: srg_csr_validate).
  * hub_threshold / heavy_threshold: SRG_PLAN_AUTO (per launch, from its nnz: hub rows > max(2048,
  * nnz / 1024) entries, slice-wave rows > max(96, nnz / 100000) for the one-launch hop, nnz / 30000 for
