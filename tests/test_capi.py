@@ -131,6 +131,41 @@ def test_planner_rejects_bad_arguments_before_the_device():
 
 
 @pytest.mark.gpu
+def test_plain_c_host_runs_the_fp64_steps(tmp_path):
+    """examples/cheby64_plan.c: a plain C program plans an operator for the fp64 Chebyshev steps (no fp32
+    values, whole hub rows) and runs an order-3 two-scale filter through srg_plan_cheby_step_f64 (lean
+    epilogue) and through srg_cheby_step_f64 (one launch per order): bit for bit the same, blocked (4 blocks)
+    and automatic (one launch on this small panel)."""
+    import json
+    import subprocess
+
+    import numpy as np
+    exe = os.path.join(REPO, "examples", "cheby64_plan")
+    assert os.path.exists(exe), "build it with `make -C examples` (__graft_entry__.build() does)"
+    rng = np.random.default_rng(9)
+    n = 30000
+    deg = np.minimum(rng.zipf(1.8, n), 3000).astype(np.int64)
+    deg[7] = 20000
+    ip = np.concatenate([[0], np.cumsum(deg)]).astype(np.int64)
+    ix = np.concatenate([np.sort(rng.choice(n, k, replace=False)) for k in deg]).astype(np.int32)
+    v = (rng.standard_normal(ix.size) * 0.1).astype(np.float32)
+    path = tmp_path / "g.csr"
+    with open(path, "wb") as f:
+        f.write(b"SRGCSR1\0")
+        f.write(np.array([n, ix.size], dtype=np.int64).tobytes())
+        f.write(ip.tobytes())
+        f.write(ix.tobytes())
+        f.write(v.tobytes())
+    for d, blocks, want_blocks in (("64", "4", 4), ("100", "0", 1), ("128", "7", 7)):
+        r = subprocess.run([exe, str(path), d, blocks, "2"], capture_output=True, timeout=120)
+        assert r.returncode == 0, r.stdout.decode() + r.stderr.decode()
+        res = json.loads(r.stdout.decode())
+        assert res["bitwise_vs_one_launch"] is True and res["n"] == n and res["col_blocks"] == want_blocks
+        hubs = int((deg > max(2048, int(ix.size) // 4096)).sum())
+        assert hubs >= 1 and res["hub_rows_whole"] == (hubs if want_blocks > 1 else 0)
+
+
+@pytest.mark.gpu
 def test_plain_c_host_runs_the_planner(tmp_path):
     """examples/plan_propagate.c: a plain C program reads a CSR file, plans its hops on the device
     (srg_plan_build), checks the plans' launches on the host, times the one-shot and long-lived runs
