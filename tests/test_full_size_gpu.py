@@ -84,6 +84,33 @@ def test_products_timed_layout_every_hop_bit_exact(oracle_mod):
         prev = got
 
 
+@pytest.mark.timeout(600)
+def test_products_wavelet_f64_blocked_two_columns_every_row(oracle_mod):
+    """The fp64 filter bank bench.py --op wavelet --dtype f64 times (pygsp cheby_op's precision): the
+    products-shaped Laplacian (126 M entries), d = 128, order 3, two scales, through the automatic
+    column-blocked plan (16 blocks, the whole hub rows above max(2048, nnz / 4096) entries as hub
+    workgroups, the lean epilogue sequence) -- every row of both scales' outputs in two columns against
+    the oracle's cheby_op over the whole graph, bit for bit."""
+    from srgnn import graphs, synth
+    from srgnn import wavelet as W
+    ip, ix, lv, n, d, lmax = graphs.build_laplacian("products", torch.device("cuda"))
+    assert d == 128
+    filt = W.HeatWaveletFilter.from_device(ip, ix, lv, n, [-0.5, 0.5], order=3, lmax=lmax, dtype=torch.float64)
+    S = synth.uniform_features_t(n, d, seed=synth.FEATURE_SEED, device="cuda").to(torch.float64)
+    R = filt.apply(S)
+    P = filt._plan64(d)
+    assert P is not None and P.col_blocks == 16 and P.hub_rows_whole >= 1 and not P.compact
+    torch.cuda.synchronize()
+    cols = [0, d - 1]
+    want = oracle_mod.cheby_op((ip.cpu().numpy(), ix.cpu().numpy(), lv.to(torch.float64).cpu().numpy()), filt.coeffs,
+                               S[:, cols].cpu().numpy(), lmax)
+    got = R[:, :, cols].cpu().numpy()
+    for s in range(2):
+        bad = np.flatnonzero((got[s].view(np.uint64) != want[s].view(np.uint64)).any(axis=1))
+        assert bad.size == 0, f"scale {s}: {bad.size} of {n} rows differ (first row {int(bad[0])})"
+    filt.drop_layouts()
+
+
 def test_arxiv_k5_every_row_bit_exact(oracle_mod):
     """arxiv-shaped graph (169 K nodes, 2.48 M nonzeros), K = 5, d = 128 (BASELINE configs[1]):
     every row of every hop equals the oracle's own 5-hop chain from X, bit for bit."""
