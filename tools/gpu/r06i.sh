@@ -1,5 +1,6 @@
 # round 6: fp64 blocked steps -- parity after the W=256 hub windows, then the products sweep over
-# column blocks, whole-hub thresholds and block-launch occupancy
+# column blocks, whole-hub thresholds and block-launch occupancy (SRG_CHEBY64_WAVES: an experiment knob of
+# that build, removed after the sweep -- profiles/r06i_cheby64_plan_sweep.txt)
 R=${GRAFT_REPO_ROOT:-.}
 O=$R/gpurun_out/r06i
 mkdir -p $O

@@ -104,7 +104,7 @@ if "--plan" in sys.argv:
         torch.cuda.synchronize()
         same = bool(torch.equal(Tn, ref_T) and torch.equal(R, ref_R)) if ref else None
         ms = timed(lambda: filt.order_step(filt.fvals, S, To, Tn, _lib.SRG_CHEBY_STEP, None, cf, R))
-        print(json.dumps({"waves": os.environ.get("SRG_CHEBY64_WAVES", "0"), "col_blocks": P.col_blocks if P else 1,
+        print(json.dumps({"col_blocks": P.col_blocks if P else 1,
                           "hub64_threshold": ht, "whole_max": wm,
                           "hub_rows_whole": P.hub_rows_whole if P else filt.n_hub, "launches": P.n_launch if P else 1,
                           "plan_mb": (P.device_bytes >> 20) if P else 0, "build_s": round(tb, 3), "step_ms": ms,
