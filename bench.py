@@ -871,18 +871,28 @@ def run_wavelet_dist(a, dev, world, rank):
     ip, ix, lv, n, d, lmax = graphs.build_laplacian(a.config, dev, d=a.d)
     nnz = int(ix.numel())
     order = 3
+    f64 = a.dtype == "f64"
+    tdt, esz = (torch.float64, 8) if f64 else (torch.float32, 4)
     f = HaloWaveletFilter(ip, ix, lv, n, [-0.5, 0.5], order=order, lmax=lmax, chunks=(a.chunks or (4 if world <= 2 else 6)),
-                          heavy_threshold=a.heavy_threshold, device=dev)
-    X = synth.uniform_features_t(n, d, seed=synth.FEATURE_SEED, device=dev)
+                          heavy_threshold=a.heavy_threshold, device=dev, dtype=tdt)
+    # fp64: the widest power-of-two column block whose five [rows + halo] panels fit (as one GPU's fp64 line)
+    cb = a.col_block or d
+    if f64 and not a.col_block:
+        torch.cuda.synchronize()
+        free, _ = torch.cuda.mem_get_info(dev)
+        while cb > 1 and 5 * (f.rows + f.opL.halo) * cb * esz > free - 8 * 2 ** 30:
+            cb //= 2
+    X = synth.uniform_features_t(n, cb, seed=synth.FEATURE_SEED, device=dev).to(tdt)
     S_local = X[f.r0:f.r1].contiguous()
     # this rank's rows of the one-GPU filter bank on the whole graph, checked after the timed steps
     ref = None
     free, _ = torch.cuda.mem_get_info(dev)
-    if 6 * n * d * 4 < 0.5 * free:
+    if 6 * n * cb * esz < 0.5 * free:
         from srgnn import wavelet as W
         one = W.HeatWaveletFilter.from_device(ip, ix, lv, n, [-0.5, 0.5], order=order, lmax=lmax,
-                                              dtype=torch.float32, heavy_threshold=a.heavy_threshold)
+                                              dtype=tdt, heavy_threshold=a.heavy_threshold)
         ref = one.apply(X)[:, f.r0:f.r1].clone()
+        one.drop_layouts()
         del one
     del X, ip, ix, lv
     torch.cuda.empty_cache()
@@ -910,11 +920,16 @@ def run_wavelet_dist(a, dev, world, rank):
     res = {"metric": "propagated edges/sec (wavelet-basis Chebyshev propagation)",
            "value": a.steps * order * nnz / dt, "unit": "propagated edges/s", "n_gpus": world,
            "steps": a.steps, "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True,
-           "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+           "scaling": "strong", "vs_baseline": None, "dtype": "f64" if f64 else "f32",
            "data": f"synthetic (R-MAT power-law graph with the {a.config} node/edge counts, U[-1,1) features)",
-           "config": {"workload": f"{a.config}-shaped heat-wavelet filter bank", "n_nodes": n, "nnz_L": nnz, "d": d,
+           "config": {"workload": f"{a.config}-shaped heat-wavelet filter bank" + (", fp64 (the reference's precision)"
+                                                                                   if f64 else ""),
+                      "n_nodes": n, "nnz_L": nnz, "d": d, "col_block": cb,
                       "chebyshev_order": order, "scales": [-0.5, 0.5], "lmax": lmax,
-                      "parallelism": f"row-partition x{world} (halo exchange per order)"},
+                      "parallelism": f"row-partition x{world} (halo exchange per order)",
+                      "mode": ("fp64: per order one fused srg_cheby_step_hub_f64 launch over each rank's rows, fp64 "
+                               "halo rows exchanged" if f64 else "fp32 split path per rank")
+                      + ("" if cb == d else f"; a step filters one {cb}-column block of the {d}-column panel")},
            "roofline": None, "cpu_baseline": None, "parity_vs_1gpu": parity,
            "devices": devices}
     if rank == 0:

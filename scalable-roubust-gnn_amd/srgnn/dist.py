@@ -20,6 +20,7 @@ GPU: the multi-GPU results are bitwise equal to the single-GPU ones.
 """
 from __future__ import annotations
 
+import ctypes
 
 import numpy as np
 import torch
@@ -484,7 +485,7 @@ class HaloPartitionedOperator:
             return None
         recv = panel[off:off + total_in]
         if self.send_cat[g].numel():
-            if self._hip:      # srg_gather_rows_f32: 16-byte row chunks, 12-15 % faster than index_select
+            if self._hip and panel.dtype == torch.float32:   # srg_gather_rows_f32: 16-byte row chunks, 12-15 % faster than index_select
                 from .spmm import gather_rows
                 send = gather_rows(panel[: self.rows], self.send_cat[g])
             else:
@@ -504,7 +505,7 @@ class HaloPartitionedOperator:
         off = self.rows + self.n_recv
         recv = panel[off:off + self.n_ghost]
         if self.ghost_send_cat.numel():
-            if self._hip:
+            if self._hip and panel.dtype == torch.float32:
                 from .spmm import gather_rows
                 send = gather_rows(panel[: self.rows], self.ghost_send_cat)
             else:
@@ -723,11 +724,15 @@ class HaloWaveletFilter:
     Chebyshev order is the local SpMM of this rank's rows (L for order 1, F = (2/a1)(L - a2 I)
     after), the element-wise epilogue on the own rows, and one halo exchange of the new T_k --
     the same arithmetic per element as one GPU, so the result is bitwise equal to it.
-    SpectralModel's operator at the RMAT-26 configuration (BASELINE.json) on P GPUs."""
+    SpectralModel's operator at the RMAT-26 configuration (BASELINE.json) on P GPUs.
+    dtype=torch.float64 (pygsp cheby_op's own precision, base_model.py:236-265): every order is one
+    fused srg_cheby_step_hub_f64 launch over this rank's rows (the longest as hub workgroups beside
+    the row waves, the lean epilogue sequence), its halo exchanged as fp64 rows -- bitwise the one-GPU
+    fp64 filter and the oracle's cheby_op."""
 
     def __init__(self, indptr, indices, lvals, n: int, taus, order: int = 3, lmax: float = None,
                  group=None, chunks: int = 4, heavy_threshold=None, hub_threshold=None, device=None,
-                 rank=None, world=None, local_spmm=None, epilogue=None):
+                 rank=None, world=None, local_spmm=None, epilogue=None, dtype=torch.float32):
         from .wavelet import heat_cheby_coeffs
         if lmax is None:
             raise ValueError("lmax is required")
@@ -751,9 +756,75 @@ class HaloWaveletFilter:
         self.rows, self.r0, self.r1 = self.opL.rows, self.opL.r0, self.opL.r1
         self._epi = epilogue or _epilogue_device
         self.overlap = True      # real GPU ranks: each order's exchange overlapped chunk by chunk
+        if dtype not in (torch.float32, torch.float64):
+            raise TypeError("dtype must be float32 or float64")
+        self.dtype = dtype
+        if dtype == torch.float64:
+            from .wavelet import HeatWaveletFilter
+            rows64 = torch.repeat_interleave(torch.arange(n, device=dev), ip[1:] - ip[:-1])
+            diag64 = indices.to(dev).to(torch.int64) == rows64
+            del rows64
+            # F in fp64 (the one-GPU filter's values, not rounded), both at the local entry positions
+            self._v64 = {"L": self.opL._local_values(lv64),
+                         "F": self.opL._local_values((2.0 / self.a1) * torch.where(diag64, lv64 - self.a2, lv64))}
+            del diag64
+            # own rows by decreasing length (stable), the longest as hub rows (the one-GPU fp64 rule on
+            # this rank's entries; an explicit hub_threshold holds as given)
+            lip = self.opL._lip
+            deg = lip[1:self.rows + 1] - lip[:self.rows]
+            self._sched64 = torch.sort(deg, descending=True, stable=True).indices.to(torch.int32).contiguous()
+            t = HeatWaveletFilter.hub64_rule(int(deg.sum().item())) if hub_threshold is None else int(hub_threshold)
+            self._n_hub64 = int((deg > t).sum().item()) if t >= 0 else 0
+        del lv64
 
     def new_panel(self, d):
+        if self.dtype == torch.float64:
+            return torch.zeros((self.rows + self.opL.halo, d), dtype=torch.float64, device=self.opL.device)
         return self.opL.new_panel(d)
+
+    def _order64(self, which, Tc, To, Tn, mode, coef_prev, coef, R):
+        """One fp64 order over this rank's rows: Tc gathered through the local operator (own rows and halo),
+        Tn and R written on the own rows."""
+        from . import _lib
+        op = self.opL
+        d = Tc.shape[1]
+        ns = self.coeffs.shape[0]
+        ct = ctypes.c_double
+        cp = (ct * len(coef_prev))(*coef_prev) if coef_prev is not None else None
+        cc = (ct * len(coef))(*coef) if coef is not None else None
+        _lib.call(op.device, "srg_cheby_step_hub_f64", op._lip.data_ptr(), op._lix.data_ptr() if op._lix.numel() else None,
+                  self._v64[which].data_ptr() if self._v64[which].numel() else None, self.rows, self._sched64.data_ptr(),
+                  self._n_hub64, Tc.data_ptr(), To.data_ptr() if To is not None else None, Tn.data_ptr(), d, d, mode,
+                  self.a1, self.a2, cp, cc, ns, R.data_ptr(), self.rows * d, _lib.stream(op.device))
+
+    def _steps64(self, S_panel, work, R):
+        """steps() in fp64: the lean sequence of fused one-launch orders; yields each T_k whose halo the
+        caller exchanges (all but the last order's)."""
+        from . import _lib
+        ns, nc = self.coeffs.shape
+        cf = self.coeffs
+        lean = nc > 2
+        t_old, t_cur = S_panel, work[0]
+        free = list(work[1:])
+        if lean:
+            self._order64("L", S_panel, None, t_cur, _lib.SRG_CHEBY_INIT_T, None, None, R)
+        else:
+            self._order64("L", S_panel, None, t_cur, _lib.SRG_CHEBY_INIT, cf[:, 0], cf[:, 1], R)
+        if nc > 2:
+            yield t_cur
+        for k in range(2, nc):
+            t_new = free.pop()
+            last = _lib.SRG_CHEBY_NO_T if k == nc - 1 else 0
+            if k == 2:
+                self._order64("F", t_cur, t_old, t_new, _lib.SRG_CHEBY_STEP_FIRST | last,
+                              np.concatenate([cf[:, 0], cf[:, 1]]), cf[:, 2], R)
+            else:
+                self._order64("F", t_cur, t_old, t_new, _lib.SRG_CHEBY_STEP | last, None, cf[:, k], R)
+            if t_old is not S_panel:
+                free.append(t_old)
+            t_old, t_cur = t_cur, t_new
+            if k + 1 < nc:
+                yield t_cur
 
     def _order(self, op, src, dst, epi, exchange: bool) -> bool:
         """One Chebyshev order: dst = op @ src on the own rows, finished by epi(a, b) over row
@@ -772,6 +843,9 @@ class HaloWaveletFilter:
         panel whose halo the caller must exchange next (on real GPU ranks the orders exchange
         their own halo, overlapped, and nothing is yielded).  S_panel's halo must already be
         filled; work = three [rows + halo, d] panels; R = [ns, rows, d]."""
+        if self.dtype == torch.float64:
+            yield from self._steps64(S_panel, work, R)
+            return
         ns, nc = self.coeffs.shape
         t_old, t_cur = S_panel, work[0]
         free = list(work[1:])
@@ -811,7 +885,7 @@ class HaloWaveletFilter:
         S_panel = self.new_panel(d)
         S_panel[: self.rows].copy_(S_local[: self.rows])
         self.opL.exchange(S_panel)
-        R = torch.empty((self.coeffs.shape[0], self.rows, d), dtype=torch.float32, device=S_panel.device)
+        R = torch.empty((self.coeffs.shape[0], self.rows, d), dtype=self.dtype, device=S_panel.device)
         work = [self.new_panel(d) for _ in range(3)]
         for panel in self.steps(S_panel, work, R):
             self.opL.exchange(panel)
@@ -819,18 +893,19 @@ class HaloWaveletFilter:
 
 
 def simulate_halo_wavelet(indptr, indices, lvals, n: int, S: torch.Tensor, taus, order: int, lmax: float,
-                          world: int, chunks: int = 3, heavy_threshold=None, hub_threshold=None, device=None):
+                          world: int, chunks: int = 3, heavy_threshold=None, hub_threshold=None, device=None,
+                          dtype=torch.float32):
     """P virtual HaloWaveletFilter ranks in one process; returns the full [n_scales, n, d] output."""
     shares = [HaloWaveletFilter(indptr, indices, lvals, n, taus, order, lmax, chunks=chunks,
                                 heavy_threshold=heavy_threshold, hub_threshold=hub_threshold, device=device,
-                                rank=q, world=world) for q in range(world)]
+                                rank=q, world=world, dtype=dtype) for q in range(world)]
     d = S.shape[1]
     ops = [f.opL for f in shares]
     S_p = [f.new_panel(d) for f in shares]
     for f, sp_ in zip(shares, S_p):
         sp_[: f.rows].copy_(S[f.r0:f.r1])
     _virtual_exchange(ops, S_p)
-    Rs = [torch.empty((len(taus), f.rows, d), dtype=torch.float32, device=S_p[0].device) for f in shares]
+    Rs = [torch.empty((len(taus), f.rows, d), dtype=dtype, device=S_p[0].device) for f in shares]
     gens = [f.steps(sp_, [f.new_panel(d) for _ in range(3)], R) for f, sp_, R in zip(shares, S_p, Rs)]
     while True:
         outs = [next(g, None) for g in gens]

@@ -438,6 +438,29 @@ def test_halo_wavelet_virtual_ranks_bitwise(world, chunks):
     assert torch.equal(got, want)
 
 
+@pytest.mark.parametrize("world,hub", [(2, None), (3, 100), (8, None), (4, 0)])
+def test_halo_wavelet_f64_virtual_ranks_bitwise(oracle_mod, world, hub):
+    """The fp64 filter bank (pygsp cheby_op's precision) over the halo partition: P virtual ranks on one GPU,
+    each order one fused srg_cheby_step_hub_f64 launch over the rank's rows (hub rows: the fp64 rule, or
+    rows > 100 entries, or every row) and one exchange of fp64 halo rows == the one-GPU fp64 filter == the
+    oracle's cheby_op, bit for bit."""
+    from srgnn import normalize, synth, wavelet as W
+    from srgnn.dist import simulate_halo_wavelet
+    n = 4000
+    u, v = synth.rmat_undirected_t(n, 40000, seed=17, device="cuda")
+    ip, ix, lv = normalize.sym_norm_edges_blocked(u.to(torch.int32), v.to(torch.int32), n, kind="laplacian")
+    S = synth.uniform_features_t(n, 64, seed=5, device="cuda").to(torch.float64)
+    lmax = 2.0 * float((ip[1:] - ip[:-1]).max())
+    one = W.HeatWaveletFilter.from_device(ip, ix, lv, n, [-0.5, 0.5], order=3, lmax=lmax, dtype=torch.float64)
+    want = one.apply(S)
+    got = simulate_halo_wavelet(ip, ix, lv, n, S, [-0.5, 0.5], 3, lmax, world, chunks=3, device="cuda",
+                                hub_threshold=hub, dtype=torch.float64)
+    assert got.dtype == torch.float64 and torch.equal(got, want)
+    ref = oracle_mod.cheby_op((ip.cpu().numpy(), ix.cpu().numpy(), lv.to(torch.float64).cpu().numpy()), one.coeffs,
+                              S.cpu().numpy(), lmax)
+    np.testing.assert_array_equal(got.cpu().numpy().view(np.uint64), ref.view(np.uint64))
+
+
 @pytest.mark.parametrize("name", ["wav_rand", "wav_cora"])
 def test_wavelet_basis_equals_reference_spectral_model(name):
     """The GPU wavelet basis against the REFERENCE's own SpectralModel.preprocess (golden wav_*,
