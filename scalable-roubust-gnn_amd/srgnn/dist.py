@@ -774,6 +774,7 @@ class HaloWaveletFilter:
             deg = lip[1:self.rows + 1] - lip[:self.rows]
             self._sched64 = torch.sort(deg, descending=True, stable=True).indices.to(torch.int32).contiguous()
             t = HeatWaveletFilter.hub64_rule(int(deg.sum().item())) if hub_threshold is None else int(hub_threshold)
+            self._hub64_t = t
             self._n_hub64 = int((deg > t).sum().item()) if t >= 0 else 0
         del lv64
 
@@ -782,9 +783,40 @@ class HaloWaveletFilter:
             return torch.zeros((self.rows + self.opL.halo, d), dtype=torch.float64, device=self.opL.device)
         return self.opL.new_panel(d)
 
+    # the local fp64 steps over column blocks: None = the planner's rule for the rank's [rows + halo] fp64 panel,
+    # 1 = one launch per order, else forced
+    col_blocks64 = None
+
+    def _plan64(self, d: int):
+        """The rank's column-blocked fp64 layout (srgnn.plan.NativePlan, fp64): a plan over the local operator as
+        a square one on the panel's rows -- own rows, then the halo's empty rows (their epilogue results land in
+        halo slots the exchange overwrites, and in rows of an internal R that are dropped) -- or None for one
+        launch per order."""
+        cache = self.__dict__.setdefault("_plans64", {})
+        key = (int(d), self.col_blocks64)
+        if key not in cache:
+            from . import _lib
+            from .csr import DeviceCSR
+            from .plan import NativePlan, query
+            op = self.opL
+            m = self.rows + op.halo
+            A = DeviceCSR.from_tensors(op._lip, op._lix, self._v64["F"], n_cols=m, device=op.device, validate=False)
+            cb = int(self.col_blocks64 or 0)
+            t = self._hub64_t
+            _, _, _, B = query(A, 2 * d, 1 << 20, cb, False, True, _lib.SRG_PLAN_WHOLE_HUBS if t >= 0 else 0,
+                               (t, _lib.SRG_PLAN_NONE))
+            cache[key] = NativePlan(A, d, 1 << 20, col_blocks=cb, fp64=True, hub_threshold=t) if B > 1 else None
+        return cache[key]
+
+    def drop_layouts(self) -> None:
+        for P in self.__dict__.pop("_plans64", {}).values():
+            if P is not None:
+                P.close()
+
     def _order64(self, which, Tc, To, Tn, mode, coef_prev, coef, R):
         """One fp64 order over this rank's rows: Tc gathered through the local operator (own rows and halo),
-        Tn and R written on the own rows."""
+        Tn and R written on the own rows (over the rank's column-blocked plan: every panel row, R then
+        [n_scales, rows + halo, d])."""
         from . import _lib
         op = self.opL
         d = Tc.shape[1]
@@ -792,6 +824,10 @@ class HaloWaveletFilter:
         ct = ctypes.c_double
         cp = (ct * len(coef_prev))(*coef_prev) if coef_prev is not None else None
         cc = (ct * len(coef))(*coef) if coef is not None else None
+        P = self._plan64(d)
+        if P is not None:
+            P.cheby_step_f64(self._v64[which], Tc, To, Tn, d, d, mode, self.a1, self.a2, cp, cc, ns, R, R.stride(0))
+            return
         _lib.call(op.device, "srg_cheby_step_hub_f64", op._lip.data_ptr(), op._lix.data_ptr() if op._lix.numel() else None,
                   self._v64[which].data_ptr() if self._v64[which].numel() else None, self.rows, self._sched64.data_ptr(),
                   self._n_hub64, Tc.data_ptr(), To.data_ptr() if To is not None else None, Tn.data_ptr(), d, d, mode,
@@ -804,6 +840,10 @@ class HaloWaveletFilter:
         ns, nc = self.coeffs.shape
         cf = self.coeffs
         lean = nc > 2
+        R_out = R
+        if self._plan64(S_panel.shape[1]) is not None:
+            # the plan's launches write every panel row: R over the panel's rows, the own rows copied out last
+            R = torch.empty((ns, self.rows + self.opL.halo, S_panel.shape[1]), dtype=torch.float64, device=R.device)
         t_old, t_cur = S_panel, work[0]
         free = list(work[1:])
         if lean:
@@ -825,6 +865,8 @@ class HaloWaveletFilter:
             t_old, t_cur = t_cur, t_new
             if k + 1 < nc:
                 yield t_cur
+        if R is not R_out:
+            R_out.copy_(R[:, :self.rows])
 
     def _order(self, op, src, dst, epi, exchange: bool) -> bool:
         """One Chebyshev order: dst = op @ src on the own rows, finished by epi(a, b) over row
@@ -894,11 +936,14 @@ class HaloWaveletFilter:
 
 def simulate_halo_wavelet(indptr, indices, lvals, n: int, S: torch.Tensor, taus, order: int, lmax: float,
                           world: int, chunks: int = 3, heavy_threshold=None, hub_threshold=None, device=None,
-                          dtype=torch.float32):
-    """P virtual HaloWaveletFilter ranks in one process; returns the full [n_scales, n, d] output."""
+                          dtype=torch.float32, col_blocks64=None):
+    """P virtual HaloWaveletFilter ranks in one process; returns the full [n_scales, n, d] output
+    (col_blocks64: each fp64 rank's column blocks, None = the planner's rule)."""
     shares = [HaloWaveletFilter(indptr, indices, lvals, n, taus, order, lmax, chunks=chunks,
                                 heavy_threshold=heavy_threshold, hub_threshold=hub_threshold, device=device,
                                 rank=q, world=world, dtype=dtype) for q in range(world)]
+    for f in shares:
+        f.col_blocks64 = col_blocks64
     d = S.shape[1]
     ops = [f.opL for f in shares]
     S_p = [f.new_panel(d) for f in shares]

@@ -438,12 +438,14 @@ def test_halo_wavelet_virtual_ranks_bitwise(world, chunks):
     assert torch.equal(got, want)
 
 
-@pytest.mark.parametrize("world,hub", [(2, None), (3, 100), (8, None), (4, 0)])
-def test_halo_wavelet_f64_virtual_ranks_bitwise(oracle_mod, world, hub):
+@pytest.mark.parametrize("world,hub,blocks", [(2, None, None), (3, 100, None), (8, None, None), (4, 0, None),
+                                               (2, None, 4), (3, 100, 3), (4, None, 7)])
+def test_halo_wavelet_f64_virtual_ranks_bitwise(oracle_mod, world, hub, blocks):
     """The fp64 filter bank (pygsp cheby_op's precision) over the halo partition: P virtual ranks on one GPU,
     each order one fused srg_cheby_step_hub_f64 launch over the rank's rows (hub rows: the fp64 rule, or
-    rows > 100 entries, or every row) and one exchange of fp64 halo rows == the one-GPU fp64 filter == the
-    oracle's cheby_op, bit for bit."""
+    rows > 100 entries, or every row) -- or, forced, the rank's column-blocked fp64 plan over its [rows + halo]
+    panel -- and one exchange of fp64 halo rows == the one-GPU fp64 filter == the oracle's cheby_op, bit for
+    bit."""
     from srgnn import normalize, synth, wavelet as W
     from srgnn.dist import simulate_halo_wavelet
     n = 4000
@@ -454,7 +456,7 @@ def test_halo_wavelet_f64_virtual_ranks_bitwise(oracle_mod, world, hub):
     one = W.HeatWaveletFilter.from_device(ip, ix, lv, n, [-0.5, 0.5], order=3, lmax=lmax, dtype=torch.float64)
     want = one.apply(S)
     got = simulate_halo_wavelet(ip, ix, lv, n, S, [-0.5, 0.5], 3, lmax, world, chunks=3, device="cuda",
-                                hub_threshold=hub, dtype=torch.float64)
+                                hub_threshold=hub, dtype=torch.float64, col_blocks64=blocks)
     assert got.dtype == torch.float64 and torch.equal(got, want)
     ref = oracle_mod.cheby_op((ip.cpu().numpy(), ix.cpu().numpy(), lv.to(torch.float64).cpu().numpy()), one.coeffs,
                               S.cpu().numpy(), lmax)

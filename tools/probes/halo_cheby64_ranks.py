@@ -26,6 +26,7 @@ ap.add_argument("--config", default="products")
 ap.add_argument("--world", type=int, default=8)
 ap.add_argument("--d", type=int, default=None)
 ap.add_argument("--reps", type=int, default=5)
+ap.add_argument("--blocks", type=int, default=None, help="each rank's fp64 column blocks (None: the planner's rule)")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 ip, ix, lv, n, d, lmax = graphs.build_laplacian(a.config, dev, d=a.d)
@@ -60,15 +61,19 @@ torch.cuda.empty_cache()
 for q in range(a.world):
     f = HaloWaveletFilter(ip, ix, lv, n, taus, order=3, lmax=lmax, device=dev, rank=q, world=a.world,
                           dtype=torch.float64)
+    f.col_blocks64 = a.blocks
     m = f.rows + f.opL.halo
     Tc = torch.rand((m, d), dtype=torch.float64, device=dev)
     To, Tn = torch.rand_like(Tc), torch.empty_like(Tc)
-    R = torch.zeros((2, f.rows, d), dtype=torch.float64, device=dev)
+    Pq = f._plan64(d)
+    R = torch.zeros((2, m if Pq is not None else f.rows, d), dtype=torch.float64, device=dev)
     ms = timed(lambda: f._order64("F", Tc, To, Tn, _lib.SRG_CHEBY_STEP, None, f.coeffs[:, 2], R), a.reps)
     out["ranks"].append({"rank": q, "rows": f.rows, "halo": f.opL.halo, "nnz": f.opL.nnz_local,
-                         "hub_rows": f._n_hub64, "ms_per_order": ms})
+                         "hub_rows": f._n_hub64, "col_blocks": Pq.col_blocks if Pq is not None else 1,
+                         "ms_per_order": ms})
     print(json.dumps(out["ranks"][-1]), flush=True)
-    del f, Tc, To, Tn, R
+    f.drop_layouts()
+    del f, Tc, To, Tn, R, Pq
     torch.cuda.empty_cache()
 mx = max(r["ms_per_order"] for r in out["ranks"])
 out["max_rank_ms"] = mx
