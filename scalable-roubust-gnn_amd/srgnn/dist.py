@@ -783,9 +783,10 @@ class HaloWaveletFilter:
             return torch.zeros((self.rows + self.opL.halo, d), dtype=torch.float64, device=self.opL.device)
         return self.opL.new_panel(d)
 
-    # the local fp64 steps over column blocks: None = the planner's rule for the rank's [rows + halo] fp64 panel,
-    # 1 = one launch per order, else forced
-    col_blocks64 = None
+    # the local fp64 steps over column blocks: 1 = one launch per order (the default: faster on every rank share
+    # measured -- products P=4 max 5.67 ms one launch vs 6.14 planner-blocked (15 blocks), P=8 2.73 vs 4.33 (12);
+    # profiles/r06ae_*, r06af_*), None = the planner's rule for the rank's [rows + halo] fp64 panel, else forced
+    col_blocks64 = 1
 
     def _plan64(self, d: int):
         """The rank's column-blocked fp64 layout (srgnn.plan.NativePlan, fp64): a plan over the local operator as
@@ -936,9 +937,9 @@ class HaloWaveletFilter:
 
 def simulate_halo_wavelet(indptr, indices, lvals, n: int, S: torch.Tensor, taus, order: int, lmax: float,
                           world: int, chunks: int = 3, heavy_threshold=None, hub_threshold=None, device=None,
-                          dtype=torch.float32, col_blocks64=None):
+                          dtype=torch.float32, col_blocks64=1):
     """P virtual HaloWaveletFilter ranks in one process; returns the full [n_scales, n, d] output
-    (col_blocks64: each fp64 rank's column blocks, None = the planner's rule)."""
+    (col_blocks64: each fp64 rank's column blocks, 1 = one launch per order, None = the planner's rule)."""
     shares = [HaloWaveletFilter(indptr, indices, lvals, n, taus, order, lmax, chunks=chunks,
                                 heavy_threshold=heavy_threshold, hub_threshold=hub_threshold, device=device,
                                 rank=q, world=world, dtype=dtype) for q in range(world)]

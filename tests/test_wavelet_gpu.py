@@ -438,8 +438,8 @@ def test_halo_wavelet_virtual_ranks_bitwise(world, chunks):
     assert torch.equal(got, want)
 
 
-@pytest.mark.parametrize("world,hub,blocks", [(2, None, None), (3, 100, None), (8, None, None), (4, 0, None),
-                                               (2, None, 4), (3, 100, 3), (4, None, 7)])
+@pytest.mark.parametrize("world,hub,blocks", [(2, None, 1), (3, 100, 1), (8, None, 1), (4, 0, 1),
+                                               (2, None, 4), (3, 100, 3), (4, None, 7), (2, None, None)])
 def test_halo_wavelet_f64_virtual_ranks_bitwise(oracle_mod, world, hub, blocks):
     """The fp64 filter bank (pygsp cheby_op's precision) over the halo partition: P virtual ranks on one GPU,
     each order one fused srg_cheby_step_hub_f64 launch over the rank's rows (hub rows: the fp64 rule, or

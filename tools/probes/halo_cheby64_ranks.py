@@ -26,7 +26,8 @@ ap.add_argument("--config", default="products")
 ap.add_argument("--world", type=int, default=8)
 ap.add_argument("--d", type=int, default=None)
 ap.add_argument("--reps", type=int, default=5)
-ap.add_argument("--blocks", type=int, default=None, help="each rank's fp64 column blocks (None: the planner's rule)")
+ap.add_argument("--blocks", type=int, default=1,
+                help="each rank's fp64 column blocks (1: one launch per order, 0: the planner's rule)")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 ip, ix, lv, n, d, lmax = graphs.build_laplacian(a.config, dev, d=a.d)
@@ -61,7 +62,7 @@ torch.cuda.empty_cache()
 for q in range(a.world):
     f = HaloWaveletFilter(ip, ix, lv, n, taus, order=3, lmax=lmax, device=dev, rank=q, world=a.world,
                           dtype=torch.float64)
-    f.col_blocks64 = a.blocks
+    f.col_blocks64 = a.blocks or None
     m = f.rows + f.opL.halo
     Tc = torch.rand((m, d), dtype=torch.float64, device=dev)
     To, Tn = torch.rand_like(Tc), torch.empty_like(Tc)
