@@ -463,6 +463,35 @@ def test_halo_wavelet_f64_virtual_ranks_bitwise(oracle_mod, world, hub, blocks):
     np.testing.assert_array_equal(got.cpu().numpy().view(np.uint64), ref.view(np.uint64))
 
 
+@pytest.mark.parametrize("world,d,order", [(8, 1, 1), (5, 3, 2), (8, 64, 5), (3, 7, 3), (7, 2, 4)])
+def test_halo_wavelet_f64_ragged_edge_cases(oracle_mod, world, d, order):
+    """The fp64 halo filter bank on a ragged operator: a third of the rows empty (no diagonal either), a few
+    ranks holding only a handful of rows, odd and one-column panels (the hub workgroups need an even d, so
+    those run as row waves only), orders 1 (no lean sequence) to 5 == the one-GPU fp64 filter == the
+    oracle's cheby_op, bit for bit."""
+    from srgnn import wavelet as W
+    from srgnn.dist import simulate_halo_wavelet
+    rng = np.random.default_rng(world * 100 + d)
+    n = 60
+    deg = rng.integers(0, 12, n)
+    deg[40:] = 0
+    deg[3] = 45
+    ip = np.concatenate([[0], np.cumsum(deg)]).astype(np.int64)
+    ix = np.concatenate([np.sort(rng.choice(n, k, replace=False)) for k in deg] + [np.zeros(0, np.int64)])
+    lv = rng.standard_normal(ix.size).astype(np.float32)
+    ip_t, ix_t, lv_t = (torch.from_numpy(a).cuda() for a in (ip, ix.astype(np.int32), lv))
+    S = torch.from_numpy(rng.standard_normal((n, d))).cuda()
+    lmax = 9.0
+    one = W.HeatWaveletFilter.from_device(ip_t, ix_t, lv_t, n, [-0.5, 0.5], order=order, lmax=lmax,
+                                          dtype=torch.float64)
+    want = one.apply(S)
+    got = simulate_halo_wavelet(ip_t, ix_t, lv_t, n, S, [-0.5, 0.5], order, lmax, world, chunks=2, device="cuda",
+                                hub_threshold=8, dtype=torch.float64)
+    assert got.shape == (2, n, d) and torch.equal(got, want)
+    ref = oracle_mod.cheby_op((ip, ix.astype(np.int32), lv.astype(np.float64)), one.coeffs, S.cpu().numpy(), lmax)
+    np.testing.assert_array_equal(got.cpu().numpy().view(np.uint64), ref.view(np.uint64))
+
+
 @pytest.mark.parametrize("name", ["wav_rand", "wav_cora"])
 def test_wavelet_basis_equals_reference_spectral_model(name):
     """The GPU wavelet basis against the REFERENCE's own SpectralModel.preprocess (golden wav_*,
