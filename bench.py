@@ -927,8 +927,9 @@ def run_wavelet_dist(a, dev, world, rank):
                       "n_nodes": n, "nnz_L": nnz, "d": d, "col_block": cb,
                       "chebyshev_order": order, "scales": [-0.5, 0.5], "lmax": lmax,
                       "parallelism": f"row-partition x{world} (halo exchange per order)",
-                      "mode": ("fp64: per order one fused srg_cheby_step_hub_f64 launch over each rank's rows, fp64 "
-                               "halo rows exchanged" if f64 else "fp32 split path per rank")
+                      "mode": ("fp64: per order one fused srg_cheby_step_hub_f64 launch per row chunk of each rank, "
+                               "each chunk's fp64 halo rows sent while the next chunks compute" if f64
+                               else "fp32 split path per rank")
                       + ("" if cb == d else f"; a step filters one {cb}-column block of the {d}-column panel")},
            "roofline": None, "cpu_baseline": None, "parity_vs_1gpu": parity,
            "devices": devices}

@@ -776,6 +776,13 @@ class HaloWaveletFilter:
             t = HeatWaveletFilter.hub64_rule(int(deg.sum().item())) if hub_threshold is None else int(hub_threshold)
             self._hub64_t = t
             self._n_hub64 = int((deg > t).sum().item()) if t >= 0 else 0
+            # the same per row chunk of the halo plan (chunk_ranges), for the orders overlapped with their
+            # exchange: chunk c's launch, then its group's all_to_all while the next chunks compute
+            self._sched64_chunks = []
+            for a, b in self.opL.chunk_ranges:
+                dc = deg[a:b]
+                oc = (torch.sort(dc, descending=True, stable=True).indices + a).to(torch.int32).contiguous()
+                self._sched64_chunks.append((oc, int((dc > t).sum().item()) if t >= 0 else 0))
         del lv64
 
     def new_panel(self, d):
@@ -814,10 +821,11 @@ class HaloWaveletFilter:
             if P is not None:
                 P.close()
 
-    def _order64(self, which, Tc, To, Tn, mode, coef_prev, coef, R):
+    def _order64(self, which, Tc, To, Tn, mode, coef_prev, coef, R, sched=None):
         """One fp64 order over this rank's rows: Tc gathered through the local operator (own rows and halo),
         Tn and R written on the own rows (over the rank's column-blocked plan: every panel row, R then
-        [n_scales, rows + halo, d])."""
+        [n_scales, rows + halo, d]).  sched = (rows by decreasing length, hub rows among them): one launch
+        over those rows only (a row chunk of the overlapped orders)."""
         from . import _lib
         op = self.opL
         d = Tc.shape[1]
@@ -825,18 +833,41 @@ class HaloWaveletFilter:
         ct = ctypes.c_double
         cp = (ct * len(coef_prev))(*coef_prev) if coef_prev is not None else None
         cc = (ct * len(coef))(*coef) if coef is not None else None
-        P = self._plan64(d)
+        P = self._plan64(d) if sched is None else None
         if P is not None:
             P.cheby_step_f64(self._v64[which], Tc, To, Tn, d, d, mode, self.a1, self.a2, cp, cc, ns, R, R.stride(0))
             return
+        order, n_hub = (self._sched64, self._n_hub64) if sched is None else sched
+        if order.numel() == 0:
+            return
         _lib.call(op.device, "srg_cheby_step_hub_f64", op._lip.data_ptr(), op._lix.data_ptr() if op._lix.numel() else None,
-                  self._v64[which].data_ptr() if self._v64[which].numel() else None, self.rows, self._sched64.data_ptr(),
-                  self._n_hub64, Tc.data_ptr(), To.data_ptr() if To is not None else None, Tn.data_ptr(), d, d, mode,
+                  self._v64[which].data_ptr() if self._v64[which].numel() else None, order.numel(), order.data_ptr(),
+                  n_hub, Tc.data_ptr(), To.data_ptr() if To is not None else None, Tn.data_ptr(), d, d, mode,
                   self.a1, self.a2, cp, cc, ns, R.data_ptr(), self.rows * d, _lib.stream(op.device))
+
+    def _order64_overlapped(self, which, Tc, To, Tn, mode, coef_prev, coef, R):
+        """One fp64 order on real GPU ranks with its exchange overlapped (HaloPartitionedOperator.
+        hop_with_epilogue's pattern): per row chunk its launch (the recurrence fused, so its rows of Tn are
+        final), then its group's rows packed and sent with an asynchronous all_to_all while the next chunks
+        compute; the hub group's rows (final once every chunk ran) last; the stream waits for all of them."""
+        op = self.opL
+        pending = []
+        for c, sched in enumerate(self._sched64_chunks):
+            self._order64(which, Tc, To, Tn, mode, coef_prev, coef, R, sched=sched)
+            pending.append(op._exchange_group(Tn, c, async_op=True))
+        pending.append(op._exchange_group(Tn, op.C, async_op=True))
+        for item in pending:
+            if item is not None:
+                item[0].wait()
+
+    def _overlap64(self, d: int) -> bool:
+        op = self.opL
+        return bool(self.overlap and op._hip and op.world > 1 and not op.virtual and self._plan64(d) is None)
 
     def _steps64(self, S_panel, work, R):
         """steps() in fp64: the lean sequence of fused one-launch orders; yields each T_k whose halo the
-        caller exchanges (all but the last order's)."""
+        caller exchanges (all but the last order's; real GPU ranks exchange their own, overlapped chunk by
+        chunk, and yield nothing)."""
         from . import _lib
         ns, nc = self.coeffs.shape
         cf = self.coeffs
@@ -847,24 +878,33 @@ class HaloWaveletFilter:
             R = torch.empty((ns, self.rows + self.opL.halo, S_panel.shape[1]), dtype=torch.float64, device=R.device)
         t_old, t_cur = S_panel, work[0]
         free = list(work[1:])
+        overlap = self._overlap64(S_panel.shape[1])
+
+        def order(exchange, *args):
+            """One order; whether the caller still has to exchange its T (not when it was overlapped)."""
+            if exchange and overlap:
+                self._order64_overlapped(*args)
+                return False
+            self._order64(*args)
+            return exchange
         if lean:
-            self._order64("L", S_panel, None, t_cur, _lib.SRG_CHEBY_INIT_T, None, None, R)
+            more = order(nc > 2, "L", S_panel, None, t_cur, _lib.SRG_CHEBY_INIT_T, None, None, R)
         else:
-            self._order64("L", S_panel, None, t_cur, _lib.SRG_CHEBY_INIT, cf[:, 0], cf[:, 1], R)
-        if nc > 2:
+            more = order(nc > 2, "L", S_panel, None, t_cur, _lib.SRG_CHEBY_INIT, cf[:, 0], cf[:, 1], R)
+        if more:
             yield t_cur
         for k in range(2, nc):
             t_new = free.pop()
             last = _lib.SRG_CHEBY_NO_T if k == nc - 1 else 0
             if k == 2:
-                self._order64("F", t_cur, t_old, t_new, _lib.SRG_CHEBY_STEP_FIRST | last,
-                              np.concatenate([cf[:, 0], cf[:, 1]]), cf[:, 2], R)
+                more = order(k + 1 < nc, "F", t_cur, t_old, t_new, _lib.SRG_CHEBY_STEP_FIRST | last,
+                             np.concatenate([cf[:, 0], cf[:, 1]]), cf[:, 2], R)
             else:
-                self._order64("F", t_cur, t_old, t_new, _lib.SRG_CHEBY_STEP | last, None, cf[:, k], R)
+                more = order(k + 1 < nc, "F", t_cur, t_old, t_new, _lib.SRG_CHEBY_STEP | last, None, cf[:, k], R)
             if t_old is not S_panel:
                 free.append(t_old)
             t_old, t_cur = t_cur, t_new
-            if k + 1 < nc:
+            if more:
                 yield t_cur
         if R is not R_out:
             R_out.copy_(R[:, :self.rows])

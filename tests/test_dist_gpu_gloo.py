@@ -76,7 +76,7 @@ def test_halo_hop_on_gpu_ranks_bitwise(tmp_path, world, ghost, whole_x, chunks, 
     assert flags.all(), f"ranks disagree with one GPU: {flags.tolist()}"
 
 
-def _wavelet_worker(rank, world, port, out_path, chunks):
+def _wavelet_worker(rank, world, port, out_path, chunks, f64=False):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path[:0] = [os.path.join(os.path.dirname(here), "scalable-roubust-gnn_amd")]
@@ -87,12 +87,18 @@ def _wavelet_worker(rank, world, port, out_path, chunks):
     lip, lix, lv, n, _, lmax = graphs.build_laplacian("arxiv", dev, n=20000, n_edges=160000, d=48)
     S = synth.uniform_features_t(n, 48, seed=9, device=dev)
     taus = [-0.5, 0.5]
-    f = HaloWaveletFilter(lip, lix, lv, n, taus, order=3, lmax=lmax, chunks=chunks, hub_threshold=300, device=dev)
+    dt = torch.float64 if f64 else torch.float32
+    S = S.to(dt)
+    f = HaloWaveletFilter(lip, lix, lv, n, taus, order=4 if f64 else 3, lmax=lmax, chunks=chunks, hub_threshold=300,
+                          device=dev, dtype=dt)
     R = f.apply(S[f.r0:f.r1].contiguous())              # orders overlapped with their exchange
-    want = simulate_halo_wavelet(lip, lix, lv, n, S, taus, 3, lmax, world=world, chunks=chunks,
-                                 hub_threshold=300, device=dev)
+    want = simulate_halo_wavelet(lip, lix, lv, n, S, taus, 4 if f64 else 3, lmax, world=world, chunks=chunks,
+                                 hub_threshold=300, device=dev, dtype=dt)
     torch.cuda.synchronize()
-    ok = bool(f.opL.views[f.opL.C][1] > 0) and torch.equal(R, want[:, f.r0:f.r1])
+    ok = bool(f.opL.views[f.opL.C][1] > 0) and R.dtype == dt and torch.equal(R, want[:, f.r0:f.r1])
+    if f64:
+        # the overlapped path ran (one launch per row chunk, its group sent right after), with hub rows in it
+        ok = ok and f._overlap64(48) and sum(h for _, h in f._sched64_chunks) == f._n_hub64 > 0
     flags = [None] * world
     dist.all_gather_object(flags, ok)
     if rank == 0:
@@ -101,12 +107,12 @@ def _wavelet_worker(rank, world, port, out_path, chunks):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,chunks", [(2, 3), (3, 2)])
-def test_halo_wavelet_on_gpu_ranks_bitwise(tmp_path, world, chunks):
+@pytest.mark.parametrize("world,chunks,f64", [(2, 3, False), (3, 2, False), (2, 3, True), (3, 4, True)])
+def test_halo_wavelet_on_gpu_ranks_bitwise(tmp_path, world, chunks, f64):
     """HaloWaveletFilter.apply on GPU ranks (each Chebyshev order's exchange overlapped chunk by
-    chunk, the recurrence applied per chunk range before its rows are sent) equals the
-    virtual-rank simulation, itself bitwise one GPU."""
+    chunk, the recurrence applied per chunk range before its rows are sent; fp64: one fused launch per
+    row chunk) equals the virtual-rank simulation, itself bitwise one GPU."""
     out = str(tmp_path / "flags.npy")
-    mp.spawn(_wavelet_worker, args=(world, _free_port(), out, chunks), nprocs=world, join=True)
+    mp.spawn(_wavelet_worker, args=(world, _free_port(), out, chunks, f64), nprocs=world, join=True)
     flags = np.load(out)
     assert flags.all(), f"ranks disagree: {flags.tolist()}"

@@ -1,0 +1,8 @@
+# round 6: fp64 halo orders overlapped with their exchange chunk by chunk -- GPU-rank gloo tests, the virtual
+# ranks, and the N=2 fp64 wavelet bench path (two ranks on one GPU over gloo)
+R=${GRAFT_REPO_ROOT:-.}
+O=$R/gpurun_out/r06ak
+mkdir -p $O
+cd $R
+timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu tests/test_dist_gpu_gloo.py tests/test_wavelet_gpu.py -k "wavelet" > $O/tests.log 2>&1 &&
+SRGNN_DIST_BACKEND=gloo timeout -k 10 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --op wavelet --dtype f64 --steps 2 --warmup 1 > $O/wav64_n2_gloo.json 2> $O/wav64_n2_gloo.err
