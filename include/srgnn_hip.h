@@ -326,7 +326,11 @@ int srg_cheby_step_f64(const int64_t* indptr, const int32_t* indices, const doub
  * chains, on the hub side stream beside the row waves of the other rows (srg_spmm_csr_f32's hub
  * fork; joined into `stream` before the call returns).  Bitwise srg_cheby_step_f64: the same chains
  * in the same order, the same epilogue.  Hub rows need an even d and ld and a 16-byte aligned Tc
- * (otherwise every row is a row wave). */
+ * (otherwise every row is a row wave).  mode | SRG_CHEBY_HUB_NOJOIN leaves the hub rows running (as
+ * SRG_SPMM_HUB_NOJOIN): later launches on `stream` run beside them until the caller's srg_hub_join
+ * (srgnn/dist.py forks a halo rank's hub group this way, then runs its row chunks).  Only this entry
+ * takes the flag. */
+#define SRG_CHEBY_HUB_NOJOIN 0x20
 int srg_cheby_step_hub_f64(const int64_t* indptr, const int32_t* indices, const double* values,
                            int64_t n_rows, const int32_t* row_order, int64_t n_hub, const double* Tc,
                            const double* To, double* Tn, int64_t ld, int32_t d, int mode, double a1,

@@ -2207,13 +2207,20 @@ int cheby_setup(int mode, const T* coef_prev, const T* coef, int n_scales, const
 }
 
 // n_hub (fp64 only): the first n_hub rows of `order` run as k_cheby_hub64 workgroups on the hub side
-// stream beside the row waves of the others (joined before the call returns to the stream's order)
+// stream beside the row waves of the others (joined before the call returns to the stream's order;
+// with SRG_CHEBY_HUB_NOJOIN in mode, left running for srg_hub_join: later launches on the stream run
+// beside them)
 template <typename T>
 int launch_cheby(const int64_t* indptr, const int32_t* indices, const T* vals, int64_t n_rows,
                  const int32_t* order, const T* Tc, const T* To, T* Tn, int64_t ld, int d, int mode,
                  T a1, T a2, const T* coef_prev, const T* coef, int n_scales, T* R, int64_t r_stride,
                  hipStream_t s, int64_t n_hub = 0)
 {
+    bool nojoin = false;
+    if constexpr (sizeof(T) == 8) {
+        nojoin = (mode & SRG_CHEBY_HUB_NOJOIN) != 0;
+        mode &= ~SRG_CHEBY_HUB_NOJOIN;
+    }
     ChebyCoef<T> cf;
     int rc = cheby_setup<T>(mode, coef_prev, coef, n_scales, To, cf);
     if (rc) return rc;
@@ -2241,6 +2248,7 @@ int launch_cheby(const int64_t* indptr, const int32_t* indices, const T* vals, i
                          a1, a2, cf, n_scales, R, r_stride);
             SRG_HIP_CHECK(hipGetLastError());
             SRG_HIP_CHECK(hipEventRecord(ss->join, ss->stream));
+            ss->pending = nojoin;
             hipLaunchKernelGGL(k_dispatch_delay, dim3(1), dim3(64), 0, s, kHubDelayUs);
             SRG_HIP_CHECK(hipGetLastError());
         }
@@ -2266,7 +2274,7 @@ int launch_cheby(const int64_t* indptr, const int32_t* indices, const T* vals, i
         SRG_HIP_CHECK(hipGetLastError());
     }
     SRG_HIP_CHECK(hipGetLastError());
-    if (ss) SRG_HIP_CHECK(hipStreamWaitEvent(s, ss->join, 0));   // join
+    if (ss && !nojoin) SRG_HIP_CHECK(hipStreamWaitEvent(s, ss->join, 0));   // join
     return ok();
 }
 
@@ -2620,6 +2628,7 @@ int srg_cheby_step_f64(const int64_t* indptr, const int32_t* indices, const doub
                        double a2, const double* coef_prev, const double* coef, int32_t n_scales,
                        double* R, int64_t r_stride, void* stream)
 {
+    if (mode & SRG_CHEBY_HUB_NOJOIN) return fail(SRG_ERR_INVALID, "cheby mode %d: HUB_NOJOIN needs the hub entry", mode);
     SRG_DEVICE_GUARD(stream);
     return launch_cheby<double>(indptr, indices, values, n_rows, row_order, Tc, To, Tn, ld, d, mode,
                                 a1, a2, coef_prev, coef, n_scales, R, r_stride,

@@ -34,6 +34,7 @@ SRG_CHEBY_STEP = 1
 SRG_CHEBY_INIT_T = 2
 SRG_CHEBY_STEP_FIRST = 3
 SRG_CHEBY_NO_T = 0x10
+SRG_CHEBY_HUB_NOJOIN = 0x20
 
 SRG_ACC_INIT = 0
 SRG_ACC_ADD = 1

@@ -776,13 +776,18 @@ class HaloWaveletFilter:
             t = HeatWaveletFilter.hub64_rule(int(deg.sum().item())) if hub_threshold is None else int(hub_threshold)
             self._hub64_t = t
             self._n_hub64 = int((deg > t).sum().item()) if t >= 0 else 0
-            # the same per row chunk of the halo plan (chunk_ranges), for the orders overlapped with their
-            # exchange: chunk c's launch, then its group's all_to_all while the next chunks compute
-            self._sched64_chunks = []
-            for a, b in self.opL.chunk_ranges:
-                dc = deg[a:b]
-                oc = (torch.sort(dc, descending=True, stable=True).indices + a).to(torch.int32).contiguous()
-                self._sched64_chunks.append((oc, int((dc > t).sum().item()) if t >= 0 else 0))
+            # the same per exchange group of the halo plan, for the orders overlapped with their exchange: the
+            # hub group's launch first, its fp64 hub rows left running on the hub side stream
+            # (SRG_CHEBY_HUB_NOJOIN: they carry every fp64 hub row), then each chunk's other rows beside them,
+            # every chunk's group sent right after its launch, the hub group's after the join
+            self._sched64_groups = []
+            C = self.opL.C
+            for g in [C] + list(range(C)):
+                order_g, n_g = self.opL.views[g][0], self.opL.views[g][1]
+                rows_g = order_g[:n_g].to(torch.int64)
+                dg = deg[rows_g]
+                og = rows_g[torch.sort(dg, descending=True, stable=True).indices].to(torch.int32).contiguous()
+                self._sched64_groups.append((g, (og, int((dg > t).sum().item()) if t >= 0 else 0)))
         del lv64
 
     def new_panel(self, d):
@@ -825,7 +830,7 @@ class HaloWaveletFilter:
         """One fp64 order over this rank's rows: Tc gathered through the local operator (own rows and halo),
         Tn and R written on the own rows (over the rank's column-blocked plan: every panel row, R then
         [n_scales, rows + halo, d]).  sched = (rows by decreasing length, hub rows among them): one launch
-        over those rows only (a row chunk of the overlapped orders)."""
+        over those rows only (an exchange group of the overlapped orders)."""
         from . import _lib
         op = self.opL
         d = Tc.shape[1]
@@ -845,17 +850,25 @@ class HaloWaveletFilter:
                   n_hub, Tc.data_ptr(), To.data_ptr() if To is not None else None, Tn.data_ptr(), d, d, mode,
                   self.a1, self.a2, cp, cc, ns, R.data_ptr(), self.rows * d, _lib.stream(op.device))
 
-    def _order64_overlapped(self, which, Tc, To, Tn, mode, coef_prev, coef, R):
+    def _order64_overlapped(self, which, Tc, To, Tn, mode, coef_prev, coef, R, exchange: bool = True):
         """One fp64 order on real GPU ranks with its exchange overlapped (HaloPartitionedOperator.
-        hop_with_epilogue's pattern): per row chunk its launch (the recurrence fused, so its rows of Tn are
-        final), then its group's rows packed and sent with an asynchronous all_to_all while the next chunks
-        compute; the hub group's rows (final once every chunk ran) last; the stream waits for all of them."""
+        hop_with_epilogue's pattern): per exchange group of the halo plan one launch over its rows (the
+        recurrence fused, so they are final) -- the hub group first with its hub rows left running beside
+        the row chunks, each chunk's rows packed and sent with an asynchronous all_to_all right after its
+        launch while the next chunks compute, the hub group's after the join; the stream waits for all of
+        them.  exchange=False: the launches alone (tools/probes/halo_cheby64_ranks.py times them)."""
+        from . import _lib
         op = self.opL
         pending = []
-        for c, sched in enumerate(self._sched64_chunks):
+        (gh, hub_sched), chunks = self._sched64_groups[0], self._sched64_groups[1:]
+        self._order64(which, Tc, To, Tn, mode | _lib.SRG_CHEBY_HUB_NOJOIN, coef_prev, coef, R, sched=hub_sched)
+        for g, sched in chunks:
             self._order64(which, Tc, To, Tn, mode, coef_prev, coef, R, sched=sched)
-            pending.append(op._exchange_group(Tn, c, async_op=True))
-        pending.append(op._exchange_group(Tn, op.C, async_op=True))
+            if exchange:
+                pending.append(op._exchange_group(Tn, g, async_op=True))
+        _lib.call(op.device, "srg_hub_join", _lib.stream(op.device))
+        if exchange:
+            pending.append(op._exchange_group(Tn, gh, async_op=True))
         for item in pending:
             if item is not None:
                 item[0].wait()

@@ -54,6 +54,9 @@ def test_invalid_arguments_fail_before_launch():
     rc = L.srg_cheby_step_f64(None, None, None, 4, None, None, None, None, 8, 8, 7, 1.0, 1.0,
                               None, None, 1, None, 32, None)
     assert rc == _lib.SRG_ERR_INVALID and "mode" in _lib.last_error()
+    rc = L.srg_cheby_step_f64(None, None, None, 4, None, None, None, None, 8, 8,
+                              _lib.SRG_CHEBY_STEP | _lib.SRG_CHEBY_HUB_NOJOIN, 1.0, 1.0, None, None, 1, None, 32, None)
+    assert rc == _lib.SRG_ERR_INVALID and "HUB_NOJOIN" in _lib.last_error()
     L.srg_clear_error()
     assert L.srg_last_error_code() == 0
 

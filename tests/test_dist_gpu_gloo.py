@@ -97,8 +97,11 @@ def _wavelet_worker(rank, world, port, out_path, chunks, f64=False):
     torch.cuda.synchronize()
     ok = bool(f.opL.views[f.opL.C][1] > 0) and R.dtype == dt and torch.equal(R, want[:, f.r0:f.r1])
     if f64:
-        # the overlapped path ran (one launch per row chunk, its group sent right after), with hub rows in it
-        ok = ok and f._overlap64(48) and sum(h for _, h in f._sched64_chunks) == f._n_hub64 > 0
+        # the overlapped path ran (one launch per exchange group, sent right after), with hub rows in it, and
+        # the groups' launches cover every own row once
+        rows = torch.cat([o for _, (o, _) in f._sched64_groups]).to(torch.int64)
+        ok = (ok and f._overlap64(48) and sum(h for _, (_, h) in f._sched64_groups) == f._n_hub64 > 0
+              and torch.equal(torch.sort(rows).values, torch.arange(f.rows, device=dev)))
     flags = [None] * world
     dist.all_gather_object(flags, ok)
     if rank == 0:
@@ -111,7 +114,7 @@ def _wavelet_worker(rank, world, port, out_path, chunks, f64=False):
 def test_halo_wavelet_on_gpu_ranks_bitwise(tmp_path, world, chunks, f64):
     """HaloWaveletFilter.apply on GPU ranks (each Chebyshev order's exchange overlapped chunk by
     chunk, the recurrence applied per chunk range before its rows are sent; fp64: one fused launch per
-    row chunk) equals the virtual-rank simulation, itself bitwise one GPU."""
+    exchange group, the hub group first) equals the virtual-rank simulation, itself bitwise one GPU."""
     out = str(tmp_path / "flags.npy")
     mp.spawn(_wavelet_worker, args=(world, _free_port(), out, chunks, f64), nprocs=world, join=True)
     flags = np.load(out)

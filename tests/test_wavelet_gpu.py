@@ -75,6 +75,38 @@ def test_heat_filter_f64_hub_rows_bit_exact(oracle_mod, hub, d):
     np.testing.assert_array_equal(g.apply(St).cpu().numpy().view(np.uint64), R.view(np.uint64))
 
 
+def test_fp64_hub_step_nojoin_then_rows_beside():
+    """srg_cheby_step_hub_f64 with SRG_CHEBY_HUB_NOJOIN: the hub rows' launch left running on the hub side
+    stream, the other rows as separate launches on the stream beside it, then srg_hub_join -- bit for bit the
+    one joined launch over every row (the halo ranks' overlapped orders)."""
+    import ctypes
+    from srgnn import _lib, wavelet as W
+    a = _hub_graph()
+    L = W.laplacian_from_adj(a)
+    n = a.shape[0]
+    f = W.HeatWaveletFilter(L, [-0.5, 0.5], order=3, lmax=None, device="cuda", hub_threshold=200)
+    assert f.n_hub >= 3
+    rng = np.random.default_rng(3)
+    Tc, To = (torch.from_numpy(rng.standard_normal((n, 64))).cuda() for _ in range(2))
+    cc = (ctypes.c_double * 2)(*f.coeffs[:, 2])
+    dev, st = Tc.device, _lib.stream(Tc.device)
+
+    def step(rows, n_hub, mode, Tn, R):
+        _lib.call(dev, "srg_cheby_step_hub_f64", f.indptr.data_ptr(), f.indices.data_ptr(), f.fvals.data_ptr(),
+                  rows.numel(), rows.data_ptr(), n_hub, Tc.data_ptr(), To.data_ptr(), Tn.data_ptr(), 64, 64, mode,
+                  f.a1, f.a2, None, cc, 2, R.data_ptr(), n * 64, st)
+    want_T, want_R = torch.empty_like(Tc), torch.zeros((2, n, 64), dtype=torch.float64, device="cuda")
+    step(f.order, f.n_hub, _lib.SRG_CHEBY_STEP, want_T, want_R)
+    got_T, got_R = torch.empty_like(Tc), torch.zeros_like(want_R)
+    hubs, rest = f.order[: f.n_hub].contiguous(), f.order[f.n_hub:]
+    step(hubs, f.n_hub, _lib.SRG_CHEBY_STEP | _lib.SRG_CHEBY_HUB_NOJOIN, got_T, got_R)
+    for part in torch.chunk(rest, 3):
+        step(part.contiguous(), 0, _lib.SRG_CHEBY_STEP, got_T, got_R)
+    _lib.call(dev, "srg_hub_join", st)
+    torch.cuda.synchronize()
+    assert torch.equal(got_T, want_T) and torch.equal(got_R, want_R)
+
+
 @pytest.mark.parametrize("B,hub,wm", [(2, None, None), (4, None, None), (7, 500, None), (4, 0, None), (16, 40, None),
                                       (4, None, 100), (6, 500, 12)])
 @pytest.mark.parametrize("d", [5, 64, 100, 128])

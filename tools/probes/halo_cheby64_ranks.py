@@ -26,6 +26,9 @@ ap.add_argument("--config", default="products")
 ap.add_argument("--world", type=int, default=8)
 ap.add_argument("--d", type=int, default=None)
 ap.add_argument("--reps", type=int, default=5)
+ap.add_argument("--chunks", type=int, default=0,
+                help="time the GPU ranks' overlapped order: one launch per exchange group of a C-chunk halo plan "
+                     "(no exchange); 0: one launch per order")
 ap.add_argument("--blocks", type=int, default=1,
                 help="each rank's fp64 column blocks (1: one launch per order, 0: the planner's rule)")
 a = ap.parse_args()
@@ -46,7 +49,8 @@ def timed(fn, reps):
     return e0.elapsed_time(e1) / reps
 
 
-out = {"config": a.config, "n": n, "nnz": int(ix.numel()), "d": d, "world": a.world, "ranks": []}
+out = {"config": a.config, "n": n, "nnz": int(ix.numel()), "d": d, "world": a.world, "chunks": a.chunks or None,
+       "ranks": []}
 # the one-GPU blocked step for scale
 one = W.HeatWaveletFilter.from_device(ip, ix, lv, n, taus, order=3, lmax=lmax, dtype=torch.float64)
 S = torch.rand((n, d), dtype=torch.float64, device=dev)
@@ -61,17 +65,31 @@ del one, S, To, Tn, R
 torch.cuda.empty_cache()
 for q in range(a.world):
     f = HaloWaveletFilter(ip, ix, lv, n, taus, order=3, lmax=lmax, device=dev, rank=q, world=a.world,
-                          dtype=torch.float64)
+                          dtype=torch.float64, **({"chunks": a.chunks} if a.chunks else {}))
     f.col_blocks64 = a.blocks or None
     m = f.rows + f.opL.halo
     Tc = torch.rand((m, d), dtype=torch.float64, device=dev)
     To, Tn = torch.rand_like(Tc), torch.empty_like(Tc)
     Pq = f._plan64(d)
     R = torch.zeros((2, m if Pq is not None else f.rows, d), dtype=torch.float64, device=dev)
-    ms = timed(lambda: f._order64("F", Tc, To, Tn, _lib.SRG_CHEBY_STEP, None, f.coeffs[:, 2], R), a.reps)
+    extra = {}
+    if a.chunks:
+        # the halo plan's exchange groups as launches (hub group, then each chunk's other rows), each timed
+        def order():   # as the GPU ranks run it: hub group unjoined, the chunks beside it, the join
+            f._order64_overlapped("F", Tc, To, Tn, _lib.SRG_CHEBY_STEP, None, f.coeffs[:, 2], R, exchange=False)
+        extra["group_ms"] = [timed(lambda sc=sc: f._order64("F", Tc, To, Tn, _lib.SRG_CHEBY_STEP, None, f.coeffs[:, 2], R,
+                                                             sched=sc), a.reps) for _, sc in f._sched64_groups]
+        extra["group_rows"] = [int(o.numel()) for _, (o, _) in f._sched64_groups]
+        extra["group_hubs"] = [h for _, (_, h) in f._sched64_groups]
+        extra["one_launch_ms"] = timed(lambda: f._order64("F", Tc, To, Tn, _lib.SRG_CHEBY_STEP, None, f.coeffs[:, 2], R),
+                                       a.reps)
+    else:
+        def order():
+            f._order64("F", Tc, To, Tn, _lib.SRG_CHEBY_STEP, None, f.coeffs[:, 2], R)
+    ms = timed(order, a.reps)
     out["ranks"].append({"rank": q, "rows": f.rows, "halo": f.opL.halo, "nnz": f.opL.nnz_local,
                          "hub_rows": f._n_hub64, "col_blocks": Pq.col_blocks if Pq is not None else 1,
-                         "ms_per_order": ms})
+                         "ms_per_order": ms, **extra})
     print(json.dumps(out["ranks"][-1]), flush=True)
     f.drop_layouts()
     del f, Tc, To, Tn, R, Pq
