@@ -719,6 +719,10 @@ def _epilogue_device(Tn, Tc, To, mode, a1, a2, coef_prev, coef, R):
               a1, a2, cp, cc, ns, R.data_ptr(), R.stride(1), R.stride(0), _lib.stream(Tn.device))
 
 
+# fp64 halo orders on GPU ranks: the hub group's rows above this many entries run as hub workgroups
+HUB_GROUP64_MIN = 8192
+
+
 class HaloWaveletFilter:
     """HeatWaveletFilter's fp32 split path (wavelet.py) over the halo-exchange partition: every
     Chebyshev order is the local SpMM of this rank's rows (L for order 1, F = (2/a1)(L - a2 I)
@@ -780,6 +784,11 @@ class HaloWaveletFilter:
             # hub group's launch first, its fp64 hub rows left running on the hub side stream
             # (SRG_CHEBY_HUB_NOJOIN: they carry every fp64 hub row), then each chunk's other rows beside them,
             # every chunk's group sent right after its launch, the hub group's after the join
+            # The hub group's rows above HUB_GROUP64_MIN entries run as hub workgroups too (the rank's longest
+            # rows: as row waves on the stream they would hold the chunks behind them -- RMAT-26 P = 8, 334
+            # such rows of up to 67 K entries: 32.2 ms per order against 24.8 for one launch, profiles/r06ap_*;
+            # every hub-group row, products P = 8's 1,070 of them (all > 2,048 entries): 3.16 against 2.51 with
+            # its 194 rows > 3,850 only, r06aq_*, r06ar_*).
             self._sched64_groups = []
             C = self.opL.C
             for g in [C] + list(range(C)):
@@ -787,7 +796,9 @@ class HaloWaveletFilter:
                 rows_g = order_g[:n_g].to(torch.int64)
                 dg = deg[rows_g]
                 og = rows_g[torch.sort(dg, descending=True, stable=True).indices].to(torch.int32).contiguous()
-                self._sched64_groups.append((g, (og, int((dg > t).sum().item()) if t >= 0 else 0)))
+                tg = min(t, HUB_GROUP64_MIN) if g == C else t
+                nh = int((dg > tg).sum().item()) if t >= 0 else 0
+                self._sched64_groups.append((g, (og, nh)))
         del lv64
 
     def new_panel(self, d):
