@@ -350,3 +350,31 @@ def test_bench_sampled_dist_parity_on_gloo_ranks(tmp_path, oracle_mod, corrupt):
     assert par["halo_equal_to_owners"] == (corrupt != "halo")
     assert rec["devices"]["world_size"] == 2 and rec["devices"]["backend"] == "gloo"
     assert [r["rank"] for r in rec["devices"]["ranks"]] == [0, 1]
+
+
+@pytest.mark.parametrize("world,chunks,hub", [(2, 2, 30), (3, 4, None), (4, 3, 0), (3, 2, -1)])
+def test_halo_wavelet_f64_group_schedules(world, chunks, hub):
+    """The fp64 halo filter's launch schedules (host logic, no device): one launch per exchange group of the
+    halo plan, the hub group first, every own row in exactly one launch, each launch's rows by decreasing
+    length with its hub rows first (the hub group's rows above min(rule, HUB_GROUP64_MIN), the chunks' above
+    the rule; none with hub_threshold < 0); the one-launch schedule is every own row once, longest first."""
+    from srgnn.dist import HUB_GROUP64_MIN, HaloWaveletFilter
+    from srgnn.wavelet import HeatWaveletFilter
+    ip, ix, lv, _, n = _wavelet_graph()
+    for q in range(world):
+        f = HaloWaveletFilter(ip, ix, lv, n, [-0.5, 0.5], order=3, lmax=40.0, chunks=chunks, hub_threshold=hub,
+                              device="cpu", rank=q, world=world, dtype=torch.float64)
+        deg = (f.opL._lip[1:f.rows + 1] - f.opL._lip[:f.rows]).to(torch.int64)
+        t = HeatWaveletFilter.hub64_rule(int(deg.sum())) if hub is None else hub
+        groups = f._sched64_groups
+        assert [g for g, _ in groups] == [f.opL.C] + list(range(f.opL.C))
+        rows = torch.cat([o.to(torch.int64) for _, (o, _) in groups])
+        assert torch.equal(torch.sort(rows).values, torch.arange(f.rows))
+        for g, (o, nh) in groups:
+            dg = deg[o.to(torch.int64)]
+            assert bool((dg[:-1] >= dg[1:]).all())
+            tg = min(t, HUB_GROUP64_MIN) if g == f.opL.C else t
+            assert nh == (int((dg > tg).sum()) if t >= 0 else 0)
+        assert torch.equal(torch.sort(f._sched64.to(torch.int64)).values, torch.arange(f.rows))
+        assert f._n_hub64 == (int((deg > t).sum()) if t >= 0 else 0)
+        assert f.new_panel(8).dtype == torch.float64 and f.new_panel(8).shape == (f.rows + f.opL.halo, 8)
